@@ -1,0 +1,255 @@
+// PyTorch bindings for the gfx950 kernels in csrc/kernels (extension `_C`).
+//
+// Every op: validates dtype/device/shape on the host (a mis-shaped launch of a
+// hand-written kernel can fault the GPU, so we refuse it here), then calls the
+// extern "C" launcher on the caller's current HIP stream, so ops are
+// hipGraph-capturable (no allocation, no synchronisation).
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime.h>
+
+extern "C" {
+int ft_rmsnorm(void* out, const void* x, const void* w, int rows, int hidden, int x_stride,
+               int out_stride, float eps, hipStream_t stream);
+int ft_fused_add_rmsnorm(void* out, const void* x, void* residual, const void* w, int rows,
+                         int hidden, int x_stride, int out_stride, float eps, hipStream_t stream);
+int ft_silu_mul(void* out, const void* gu, int rows, int inter, hipStream_t stream);
+int ft_rope_kv_write(void* qkv, int qkv_stride, const int* positions, const float* cos_sin,
+                     const int* slot_mapping, void* k_cache, void* v_cache, int tokens, int nq,
+                     int nkv, int head_dim, int block_size, hipStream_t stream);
+int ft_decode_partition_size();
+int ft_paged_decode_attention(void* out, int out_stride, float* tmp_out, float* tmp_ml,
+                              const void* q, int q_stride, const void* k_cache,
+                              const void* v_cache, const int* block_tables, int bt_stride,
+                              const int* seq_lens, int batch, int nq, int nkv, int head_dim,
+                              int block_size, int max_splits, float scale, hipStream_t stream);
+int ft_prefill_tile_tokens(int nq, int nkv);
+int ft_prefill_attention(void* out, int out_stride, const void* q, int q_stride,
+                         const void* k_cache, const void* v_cache, const int* block_tables,
+                         int bt_stride, const int* seq_lens, const int* q_start_loc,
+                         const int* tile_info, int num_tiles, int nq, int nkv, int head_dim,
+                         int block_size, float scale, hipStream_t stream);
+int ft_sample(int* out_tokens, const void* logits, int logits_is_bf16, long logit_stride,
+              int batch, int vocab, const float* temperature, const float* top_p,
+              const int* top_k, const long long* seeds, const int* steps,
+              const uint32_t* allow_mask, int mask_words, hipStream_t stream);
+int ft_kv_block_copy(void* k_cache, void* v_cache, const int* src_dst, int num_pairs,
+                     long block_elems, hipStream_t stream);
+}
+
+namespace {
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void check_dev(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+}
+void check_bf16(const at::Tensor& t, const char* name) {
+  check_dev(t, name);
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16, name, " must be bfloat16");
+}
+void check_i32(const at::Tensor& t, const char* name) {
+  check_dev(t, name);
+  TORCH_CHECK(t.scalar_type() == at::kInt, name, " must be int32");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+}
+void check_rc(int rc, const char* op) { TORCH_CHECK(rc == 0, op, " launch failed, code ", rc); }
+void check_rows(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.dim() == 2, name, " must be 2-D");
+  TORCH_CHECK(t.stride(1) == 1, name, " rows must be contiguous");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, name, " must be 16-B aligned");
+  TORCH_CHECK(t.stride(0) % 8 == 0, name, " row stride must be a multiple of 8 elements");
+}
+
+void rmsnorm(at::Tensor out, at::Tensor x, at::Tensor w, double eps) {
+  check_bf16(out, "out");
+  check_bf16(x, "x");
+  check_bf16(w, "weight");
+  check_rows(out, "out");
+  check_rows(x, "x");
+  TORCH_CHECK(w.is_contiguous() && w.numel() == x.size(1), "weight shape");
+  TORCH_CHECK(out.size(0) == x.size(0) && out.size(1) == x.size(1), "out shape");
+  check_rc(ft_rmsnorm(out.data_ptr(), x.data_ptr(), w.data_ptr(), (int)x.size(0), (int)x.size(1),
+                      (int)x.stride(0), (int)out.stride(0), (float)eps, cur_stream()),
+           "rmsnorm");
+}
+
+void fused_add_rmsnorm(at::Tensor out, at::Tensor x, at::Tensor residual, at::Tensor w,
+                       double eps) {
+  check_bf16(out, "out");
+  check_bf16(x, "x");
+  check_bf16(residual, "residual");
+  check_bf16(w, "weight");
+  check_rows(out, "out");
+  check_rows(x, "x");
+  TORCH_CHECK(residual.is_contiguous() && residual.sizes() == x.sizes(), "residual shape");
+  TORCH_CHECK(w.is_contiguous() && w.numel() == x.size(1), "weight shape");
+  TORCH_CHECK(out.size(0) == x.size(0) && out.size(1) == x.size(1), "out shape");
+  check_rc(ft_fused_add_rmsnorm(out.data_ptr(), x.data_ptr(), residual.data_ptr(), w.data_ptr(),
+                                (int)x.size(0), (int)x.size(1), (int)x.stride(0),
+                                (int)out.stride(0), (float)eps, cur_stream()),
+           "fused_add_rmsnorm");
+}
+
+void silu_mul(at::Tensor out, at::Tensor gu) {
+  check_bf16(out, "out");
+  check_bf16(gu, "gate_up");
+  TORCH_CHECK(gu.is_contiguous() && out.is_contiguous(), "contiguous tensors required");
+  TORCH_CHECK(gu.dim() == 2 && out.dim() == 2 && gu.size(0) == out.size(0) &&
+                  gu.size(1) == 2 * out.size(1),
+              "silu_mul shapes");
+  check_rc(ft_silu_mul(out.data_ptr(), gu.data_ptr(), (int)out.size(0), (int)out.size(1),
+                       cur_stream()),
+           "silu_mul");
+}
+
+void rope_kv_write(at::Tensor qkv, at::Tensor positions, at::Tensor cos_sin,
+                   at::Tensor slot_mapping, at::Tensor k_cache, at::Tensor v_cache, int64_t nq,
+                   int64_t nkv, int64_t head_dim) {
+  check_bf16(qkv, "qkv");
+  check_rows(qkv, "qkv");
+  check_i32(positions, "positions");
+  check_i32(slot_mapping, "slot_mapping");
+  check_dev(cos_sin, "cos_sin");
+  TORCH_CHECK(cos_sin.scalar_type() == at::kFloat && cos_sin.is_contiguous() &&
+                  cos_sin.size(1) == head_dim,
+              "cos_sin must be fp32 [max_pos, head_dim]");
+  check_bf16(k_cache, "k_cache");
+  check_bf16(v_cache, "v_cache");
+  TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(1) == nkv && k_cache.size(3) == head_dim,
+              "k_cache must be [blocks, nkv, block_size, head_dim]");
+  TORCH_CHECK(v_cache.sizes() == k_cache.sizes(), "v_cache shape");
+  TORCH_CHECK(qkv.size(1) >= (nq + 2 * nkv) * head_dim, "qkv width");
+  const int tokens = (int)qkv.size(0);
+  TORCH_CHECK(positions.numel() >= tokens && slot_mapping.numel() >= tokens, "metadata length");
+  check_rc(ft_rope_kv_write(qkv.data_ptr(), (int)qkv.stride(0), positions.data_ptr<int>(),
+                            cos_sin.data_ptr<float>(), slot_mapping.data_ptr<int>(),
+                            k_cache.data_ptr(), v_cache.data_ptr(), tokens, (int)nq, (int)nkv,
+                            (int)head_dim, (int)k_cache.size(2), cur_stream()),
+           "rope_kv_write");
+}
+
+void paged_decode_attention(at::Tensor out, at::Tensor q, at::Tensor k_cache, at::Tensor v_cache,
+                            at::Tensor block_tables, at::Tensor seq_lens, at::Tensor tmp_out,
+                            at::Tensor tmp_ml, int64_t nq, int64_t nkv, int64_t head_dim,
+                            int64_t max_splits, double scale) {
+  check_bf16(out, "out");
+  check_bf16(q, "q");
+  check_rows(out, "out");
+  check_rows(q, "q");
+  check_bf16(k_cache, "k_cache");
+  check_bf16(v_cache, "v_cache");
+  check_i32(block_tables, "block_tables");
+  check_i32(seq_lens, "seq_lens");
+  TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(1) == nkv && k_cache.size(3) == head_dim,
+              "k_cache shape");
+  const int batch = (int)q.size(0);
+  TORCH_CHECK(out.size(0) >= batch && seq_lens.numel() >= batch && block_tables.size(0) >= batch,
+              "batch sizes");
+  TORCH_CHECK(max_splits >= 1, "max_splits");
+  if (max_splits > 1) {
+    TORCH_CHECK(tmp_out.scalar_type() == at::kFloat && tmp_ml.scalar_type() == at::kFloat,
+                "tmp buffers fp32");
+    TORCH_CHECK(tmp_out.numel() >= (int64_t)batch * nq * max_splits * head_dim &&
+                    tmp_ml.numel() >= (int64_t)batch * nq * max_splits * 2,
+                "tmp buffers too small");
+  }
+  check_rc(ft_paged_decode_attention(out.data_ptr(), (int)out.stride(0),
+                                     max_splits > 1 ? tmp_out.data_ptr<float>() : nullptr,
+                                     max_splits > 1 ? tmp_ml.data_ptr<float>() : nullptr,
+                                     q.data_ptr(), (int)q.stride(0), k_cache.data_ptr(),
+                                     v_cache.data_ptr(), block_tables.data_ptr<int>(),
+                                     (int)block_tables.stride(0), seq_lens.data_ptr<int>(), batch,
+                                     (int)nq, (int)nkv, (int)head_dim, (int)k_cache.size(2),
+                                     (int)max_splits, (float)scale, cur_stream()),
+           "paged_decode_attention");
+}
+
+void prefill_attention(at::Tensor out, at::Tensor q, at::Tensor k_cache, at::Tensor v_cache,
+                       at::Tensor block_tables, at::Tensor seq_lens, at::Tensor q_start_loc,
+                       at::Tensor tile_info, int64_t num_tiles, int64_t nq, int64_t nkv,
+                       int64_t head_dim, double scale) {
+  check_bf16(out, "out");
+  check_bf16(q, "q");
+  check_rows(out, "out");
+  check_rows(q, "q");
+  check_bf16(k_cache, "k_cache");
+  check_bf16(v_cache, "v_cache");
+  check_i32(block_tables, "block_tables");
+  check_i32(seq_lens, "seq_lens");
+  check_i32(q_start_loc, "q_start_loc");
+  check_i32(tile_info, "tile_info");
+  TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(1) == nkv && k_cache.size(3) == head_dim,
+              "k_cache shape");
+  TORCH_CHECK(tile_info.numel() >= 2 * num_tiles, "tile_info too small");
+  check_rc(ft_prefill_attention(out.data_ptr(), (int)out.stride(0), q.data_ptr(),
+                                (int)q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
+                                block_tables.data_ptr<int>(), (int)block_tables.stride(0),
+                                seq_lens.data_ptr<int>(), q_start_loc.data_ptr<int>(),
+                                tile_info.data_ptr<int>(), (int)num_tiles, (int)nq, (int)nkv,
+                                (int)head_dim, (int)k_cache.size(2), (float)scale, cur_stream()),
+           "prefill_attention");
+}
+
+void sample(at::Tensor out_tokens, at::Tensor logits, at::Tensor temperature, at::Tensor top_p,
+            at::Tensor top_k, at::Tensor seeds, at::Tensor steps, c10::optional<at::Tensor> mask) {
+  check_i32(out_tokens, "out_tokens");
+  check_dev(logits, "logits");
+  TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "logits [B, V] with contiguous rows");
+  const bool is_bf16 = logits.scalar_type() == at::kBFloat16;
+  TORCH_CHECK(is_bf16 || logits.scalar_type() == at::kFloat, "logits fp32 or bf16");
+  const int batch = (int)logits.size(0), vocab = (int)logits.size(1);
+  TORCH_CHECK(out_tokens.numel() >= batch, "out_tokens too small");
+  TORCH_CHECK(temperature.scalar_type() == at::kFloat && top_p.scalar_type() == at::kFloat,
+              "temperature/top_p fp32");
+  check_i32(top_k, "top_k");
+  check_i32(steps, "steps");
+  TORCH_CHECK(seeds.scalar_type() == at::kLong && seeds.is_cuda(), "seeds int64");
+  TORCH_CHECK(temperature.numel() >= batch && top_p.numel() >= batch && top_k.numel() >= batch &&
+                  seeds.numel() >= batch && steps.numel() >= batch,
+              "sampling param length");
+  const uint32_t* mp = nullptr;
+  int words = 0;
+  if (mask.has_value() && mask->defined()) {
+    check_i32(*mask, "mask");
+    words = (int)mask->size(1);
+    TORCH_CHECK(mask->size(0) >= batch && words * 32 >= vocab, "mask shape");
+    mp = reinterpret_cast<const uint32_t*>(mask->data_ptr<int>());
+  }
+  check_rc(ft_sample(out_tokens.data_ptr<int>(), logits.data_ptr(), is_bf16 ? 1 : 0,
+                     (long)logits.stride(0), batch, vocab, temperature.data_ptr<float>(),
+                     top_p.data_ptr<float>(), top_k.data_ptr<int>(),
+                     reinterpret_cast<const long long*>(seeds.data_ptr<int64_t>()),
+                     steps.data_ptr<int>(), mp, words, cur_stream()),
+           "sample");
+}
+
+void kv_block_copy(at::Tensor k_cache, at::Tensor v_cache, at::Tensor src_dst) {
+  check_bf16(k_cache, "k_cache");
+  check_bf16(v_cache, "v_cache");
+  check_i32(src_dst, "src_dst");
+  TORCH_CHECK(k_cache.is_contiguous() && v_cache.is_contiguous(), "caches contiguous");
+  const long block_elems = (long)(k_cache.numel() / k_cache.size(0));
+  TORCH_CHECK(block_elems % 8 == 0, "block size");
+  check_rc(ft_kv_block_copy(k_cache.data_ptr(), v_cache.data_ptr(), src_dst.data_ptr<int>(),
+                            (int)(src_dst.numel() / 2), block_elems, cur_stream()),
+           "kv_block_copy");
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "FastTalk MI355X (gfx950) HIP kernels";
+  m.def("rmsnorm", &rmsnorm);
+  m.def("fused_add_rmsnorm", &fused_add_rmsnorm);
+  m.def("silu_mul", &silu_mul);
+  m.def("rope_kv_write", &rope_kv_write);
+  m.def("paged_decode_attention", &paged_decode_attention);
+  m.def("decode_partition_size", []() { return ft_decode_partition_size(); });
+  m.def("prefill_attention", &prefill_attention);
+  m.def("prefill_tile_tokens", [](int64_t nq, int64_t nkv) { return ft_prefill_tile_tokens((int)nq, (int)nkv); });
+  m.def("sample", &sample, py::arg("out_tokens"), py::arg("logits"), py::arg("temperature"),
+        py::arg("top_p"), py::arg("top_k"), py::arg("seeds"), py::arg("steps"),
+        py::arg("mask") = py::none());
+  m.def("kv_block_copy", &kv_block_copy);
+}

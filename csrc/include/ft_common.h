@@ -1,0 +1,97 @@
+// Shared device helpers for the FastTalk MI355X (gfx950 / CDNA4) kernels.
+//
+// Conventions used by every kernel in csrc/kernels:
+//   * wave64: lane = threadIdx.x & 63, block sizes are multiples of 64.
+//   * bf16 tensors are moved 16 B per lane (8 elements, `uint4`) and widened to
+//     fp32 with a shift (bf16 is the top half of an fp32), accumulation is fp32.
+//   * every launcher takes the hipStream_t of the caller so the launch can be
+//     captured into a hipGraph (no allocation / sync inside launchers).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ft {
+
+constexpr int kWave = 64;
+
+using bf16_raw = uint16_t;
+
+__device__ __forceinline__ float bf16_to_f32(uint16_t v) {
+  return __uint_as_float(static_cast<uint32_t>(v) << 16);
+}
+
+// round-to-nearest-even fp32 -> bf16 (NaN preserved as quiet NaN)
+__device__ __forceinline__ uint16_t f32_to_bf16(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return static_cast<uint16_t>((u >> 16) | 0x40u);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return static_cast<uint16_t>(u >> 16);
+}
+
+// unpack a 32-bit word holding two bf16 (low element first)
+__device__ __forceinline__ void unpack2(uint32_t w, float& lo, float& hi) {
+  lo = __uint_as_float(w << 16);
+  hi = __uint_as_float(w & 0xffff0000u);
+}
+
+__device__ __forceinline__ uint32_t pack2(float lo, float hi) {
+  return static_cast<uint32_t>(f32_to_bf16(lo)) | (static_cast<uint32_t>(f32_to_bf16(hi)) << 16);
+}
+
+// 8 x bf16 <-> 8 x fp32
+__device__ __forceinline__ void load8(const uint4& v, float (&f)[8]) {
+  unpack2(v.x, f[0], f[1]);
+  unpack2(v.y, f[2], f[3]);
+  unpack2(v.z, f[4], f[5]);
+  unpack2(v.w, f[6], f[7]);
+}
+
+__device__ __forceinline__ uint4 store8(const float (&f)[8]) {
+  uint4 v;
+  v.x = pack2(f[0], f[1]);
+  v.y = pack2(f[2], f[3]);
+  v.z = pack2(f[4], f[5]);
+  v.w = pack2(f[6], f[7]);
+  return v;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// reduce within aligned groups of `W` lanes (W power of two <= 64)
+template <int W>
+__device__ __forceinline__ float group_sum(float v) {
+#pragma unroll
+  for (int o = W / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <int W>
+__device__ __forceinline__ float group_max(float v) {
+#pragma unroll
+  for (int o = W / 2; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+__device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
+
+inline int ceil_div(int a, int b) { return (a + b - 1) / b; }
+
+}  // namespace ft
+
+#define FT_HIP_CHECK(expr)                                                   \
+  do {                                                                       \
+    hipError_t _e = (expr);                                                  \
+    if (_e != hipSuccess) return static_cast<int>(_e);                       \
+  } while (0)

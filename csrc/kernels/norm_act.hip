@@ -1,0 +1,156 @@
+// K2 (RMSNorm / fused residual-add + RMSNorm) and K9 (SiLU-and-mul) for gfx950.
+//
+// Both are HBM-bound streaming ops.  Layout decisions:
+//   * one wave64 per row, 4 rows per 256-thread workgroup; every lane moves
+//     16 B (8 x bf16) per access so one wave instruction covers 1 KiB of a row;
+//     the row stays in registers between the reduction and the scaled store
+//     (single HBM read + single write per tensor, no LDS round trip).
+//   * the fused variant writes the updated residual (bf16) and the normalised
+//     row in one pass, which is the "fuse elementwise into the producer" rule:
+//     the residual add never exists as a separate kernel.
+//   * SiLU-and-mul reads gate and up halves of the gate_up GEMM output with
+//     16-B loads and does the math in fp32 with a single rounding.
+#include "ft_common.h"
+
+namespace ft {
+
+// ----------------------------------------------------------------------------
+// RMSNorm: out[r] = bf16(bf16(x[r] * rsqrt(mean(x^2)+eps)) * w)   (HF Llama order)
+// If RESIDUAL: r = bf16(x + res); res <- r; out <- norm(r).
+// ----------------------------------------------------------------------------
+template <int NCHUNK, bool RESIDUAL>
+__global__ __launch_bounds__(256) void rmsnorm_kernel(uint16_t* __restrict__ out,
+                                                      const uint16_t* __restrict__ x,
+                                                      uint16_t* __restrict__ residual,
+                                                      const uint16_t* __restrict__ weight,
+                                                      int rows, int hidden, int x_stride,
+                                                      int out_stride, float eps) {
+  const int row = blockIdx.x * 4 + wave_id();
+  if (row >= rows) return;
+  const int lane = lane_id();
+  const uint4* xr = reinterpret_cast<const uint4*>(x + (size_t)row * x_stride);
+  uint4 v[NCHUNK];
+#pragma unroll
+  for (int c = 0; c < NCHUNK; ++c) v[c] = xr[c * 64 + lane];
+
+  if constexpr (RESIDUAL) {
+    uint4* rr = reinterpret_cast<uint4*>(residual + (size_t)row * hidden);
+#pragma unroll
+    for (int c = 0; c < NCHUNK; ++c) {
+      float a[8], b[8];
+      load8(v[c], a);
+      load8(rr[c * 64 + lane], b);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a[j] += b[j];
+      v[c] = store8(a);          // round the sum to bf16 (it is stored as bf16)
+      rr[c * 64 + lane] = v[c];
+    }
+  }
+
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCHUNK; ++c) {
+    float a[8];
+    load8(v[c], a);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ss += a[j] * a[j];
+  }
+  ss = wave_sum(ss);
+  const float inv = rsqrtf(ss / (float)hidden + eps);
+
+  const uint4* wr = reinterpret_cast<const uint4*>(weight);
+  uint4* orow = reinterpret_cast<uint4*>(out + (size_t)row * out_stride);
+#pragma unroll
+  for (int c = 0; c < NCHUNK; ++c) {
+    float a[8], w[8];
+    load8(v[c], a);
+    load8(wr[c * 64 + lane], w);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float n = bf16_to_f32(f32_to_bf16(a[j] * inv));
+      a[j] = n * w[j];
+    }
+    orow[c * 64 + lane] = store8(a);
+  }
+}
+
+template <bool RESIDUAL>
+static int launch_rmsnorm(uint16_t* out, const uint16_t* x, uint16_t* residual, const uint16_t* w,
+                          int rows, int hidden, int x_stride, int out_stride, float eps,
+                          hipStream_t stream) {
+  if (rows <= 0) return 0;
+  if (hidden % 512 != 0) return -1;
+  dim3 grid(ceil_div(rows, 4)), block(256);
+  const int nchunk = hidden / 512;
+#define FT_RMS_CASE(N)                                                                    \
+  case N:                                                                                 \
+    hipLaunchKernelGGL((rmsnorm_kernel<N, RESIDUAL>), grid, block, 0, stream, out, x,     \
+                       residual, w, rows, hidden, x_stride, out_stride, eps);             \
+    break;
+  switch (nchunk) {
+    FT_RMS_CASE(1)
+    FT_RMS_CASE(2)
+    FT_RMS_CASE(3)
+    FT_RMS_CASE(4)
+    FT_RMS_CASE(5)
+    FT_RMS_CASE(6)
+    FT_RMS_CASE(8)
+    FT_RMS_CASE(10)
+    FT_RMS_CASE(12)
+    FT_RMS_CASE(16)
+    default:
+      return -2;
+  }
+#undef FT_RMS_CASE
+  return static_cast<int>(hipGetLastError());
+}
+
+// ----------------------------------------------------------------------------
+// SiLU-and-mul: out[t, i] = silu(gu[t, i]) * gu[t, I + i]
+// ----------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void silu_mul_kernel(uint16_t* __restrict__ out,
+                                                       const uint16_t* __restrict__ gu, int rows,
+                                                       int inter) {
+  const int vec_per_row = inter / 8;
+  const long total = (long)rows * vec_per_row;
+  for (long idx = (long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (long)gridDim.x * blockDim.x) {
+    const long r = idx / vec_per_row;
+    const int c = (int)(idx - r * vec_per_row);
+    const uint4* g4 = reinterpret_cast<const uint4*>(gu + r * 2 * (long)inter);
+    float g[8], u[8];
+    load8(g4[c], g);
+    load8(g4[vec_per_row + c], u);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) g[j] = g[j] / (1.f + __expf(-g[j])) * u[j];
+    reinterpret_cast<uint4*>(out + r * (long)inter)[c] = store8(g);
+  }
+}
+
+}  // namespace ft
+
+extern "C" int ft_rmsnorm(void* out, const void* x, const void* w, int rows, int hidden,
+                          int x_stride, int out_stride, float eps, hipStream_t stream) {
+  return ft::launch_rmsnorm<false>((uint16_t*)out, (const uint16_t*)x, nullptr,
+                                   (const uint16_t*)w, rows, hidden, x_stride, out_stride, eps,
+                                   stream);
+}
+
+extern "C" int ft_fused_add_rmsnorm(void* out, const void* x, void* residual, const void* w,
+                                    int rows, int hidden, int x_stride, int out_stride,
+                                    float eps, hipStream_t stream) {
+  return ft::launch_rmsnorm<true>((uint16_t*)out, (const uint16_t*)x, (uint16_t*)residual,
+                                  (const uint16_t*)w, rows, hidden, x_stride, out_stride, eps,
+                                  stream);
+}
+
+extern "C" int ft_silu_mul(void* out, const void* gu, int rows, int inter, hipStream_t stream) {
+  if (rows <= 0) return 0;
+  if (inter % 8 != 0) return -1;
+  const long total = (long)rows * (inter / 8);
+  int grid = (int)((total + 255) / 256);
+  if (grid > 256 * 16) grid = 256 * 16;
+  hipLaunchKernelGGL(ft::silu_mul_kernel, dim3(grid), dim3(256), 0, stream, (uint16_t*)out,
+                     (const uint16_t*)gu, rows, inter);
+  return static_cast<int>(hipGetLastError());
+}

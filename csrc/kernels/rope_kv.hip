@@ -1,0 +1,102 @@
+// K4: fused rotary embedding + paged KV-cache write.
+//
+// Input is the fused QKV GEMM output [T, (nq + 2 nkv) * D].  One workgroup per
+// token; each lane handles 8 rotary pairs (element i and i + D/2, the Llama
+// "rotate_half" convention) with 16-B loads/stores.  Q is rotated in place (the
+// attention kernels read it with the QKV row stride, so there is no extra copy),
+// K is rotated and written straight into the paged cache, V is copied into the
+// paged cache.  The cos/sin table is precomputed on the host (llama3 rope
+// scaling included) as fp32 [max_pos, D] = [cos(D/2) | sin(D/2)], so the kernel
+// does no transcendental math (Appendix B "Element-wise": trig tables on host).
+//
+// Cache layout: [num_blocks, n_kv_heads, block_size, D] so that one (block,
+// head) tile is a contiguous block_size*D*2-byte run (decode/prefill attention
+// stream it with 16-B lane loads).
+#include "ft_common.h"
+
+namespace ft {
+
+template <int D>
+__global__ __launch_bounds__(256) void rope_kv_kernel(uint16_t* __restrict__ qkv, int qkv_stride,
+                                                      const int* __restrict__ positions,
+                                                      const float* __restrict__ cos_sin,
+                                                      const int* __restrict__ slot_mapping,
+                                                      uint16_t* __restrict__ k_cache,
+                                                      uint16_t* __restrict__ v_cache, int nq,
+                                                      int nkv, int block_size) {
+  constexpr int HALF = D / 2;
+  constexpr int CPH = HALF / 8;  // 8-pair chunks per head
+  const int t = blockIdx.x;
+  const int pos = positions[t];
+  const int slot = slot_mapping[t];
+  uint16_t* row = qkv + (size_t)t * qkv_stride;
+  const float* cs = cos_sin + (size_t)pos * D;
+
+  const int n_rot = (nq + nkv) * CPH;
+  for (int item = threadIdx.x; item < n_rot; item += blockDim.x) {
+    const int head = item / CPH;
+    const int c = item - head * CPH;
+    uint16_t* hp = row + head * D;  // q heads then k heads are contiguous
+    uint4* p1 = reinterpret_cast<uint4*>(hp + c * 8);
+    uint4* p2 = reinterpret_cast<uint4*>(hp + HALF + c * 8);
+    float x1[8], x2[8], co[8], si[8];
+    load8(*p1, x1);
+    load8(*p2, x2);
+    const float4* c4 = reinterpret_cast<const float4*>(cs + c * 8);
+    const float4* s4 = reinterpret_cast<const float4*>(cs + HALF + c * 8);
+    float4 ca = c4[0], cb = c4[1], sa = s4[0], sb = s4[1];
+    co[0] = ca.x; co[1] = ca.y; co[2] = ca.z; co[3] = ca.w;
+    co[4] = cb.x; co[5] = cb.y; co[6] = cb.z; co[7] = cb.w;
+    si[0] = sa.x; si[1] = sa.y; si[2] = sa.z; si[3] = sa.w;
+    si[4] = sb.x; si[5] = sb.y; si[6] = sb.z; si[7] = sb.w;
+    float y1[8], y2[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      y1[j] = x1[j] * co[j] - x2[j] * si[j];
+      y2[j] = x2[j] * co[j] + x1[j] * si[j];
+    }
+    const uint4 o1 = store8(y1), o2 = store8(y2);
+    if (head < nq) {
+      *p1 = o1;
+      *p2 = o2;
+    } else if (slot >= 0) {
+      const int kh = head - nq;
+      const int blk = slot / block_size, off = slot - blk * block_size;
+      uint16_t* kp = k_cache + (((size_t)blk * nkv + kh) * block_size + off) * D;
+      reinterpret_cast<uint4*>(kp + c * 8)[0] = o1;
+      reinterpret_cast<uint4*>(kp + HALF + c * 8)[0] = o2;
+    }
+  }
+  if (slot >= 0) {
+    const int blk = slot / block_size, off = slot - blk * block_size;
+    const int nv = nkv * (D / 8);
+    const uint4* vsrc = reinterpret_cast<const uint4*>(row + (nq + nkv) * D);
+    for (int item = threadIdx.x; item < nv; item += blockDim.x) {
+      const int kh = item / (D / 8), c = item - kh * (D / 8);
+      uint16_t* vp = v_cache + (((size_t)blk * nkv + kh) * block_size + off) * D;
+      reinterpret_cast<uint4*>(vp)[c] = vsrc[item];
+    }
+  }
+}
+
+}  // namespace ft
+
+extern "C" int ft_rope_kv_write(void* qkv, int qkv_stride, const int* positions,
+                                const float* cos_sin, const int* slot_mapping, void* k_cache,
+                                void* v_cache, int tokens, int nq, int nkv, int head_dim,
+                                int block_size, hipStream_t stream) {
+  if (tokens <= 0) return 0;
+  dim3 grid(tokens), block(256);
+  if (head_dim == 128) {
+    hipLaunchKernelGGL(ft::rope_kv_kernel<128>, grid, block, 0, stream, (uint16_t*)qkv,
+                       qkv_stride, positions, cos_sin, slot_mapping, (uint16_t*)k_cache,
+                       (uint16_t*)v_cache, nq, nkv, block_size);
+  } else if (head_dim == 64) {
+    hipLaunchKernelGGL(ft::rope_kv_kernel<64>, grid, block, 0, stream, (uint16_t*)qkv,
+                       qkv_stride, positions, cos_sin, slot_mapping, (uint16_t*)k_cache,
+                       (uint16_t*)v_cache, nq, nkv, block_size);
+  } else {
+    return -1;
+  }
+  return static_cast<int>(hipGetLastError());
+}

@@ -1,0 +1,179 @@
+"""Op dispatch: GPU tensors -> gfx950 HIP kernels (``_C``), CPU tensors -> the
+fp32 PyTorch references in :mod:`.reference`.
+
+There is deliberately no silent fallback for GPU tensors: if the native
+extension is missing or fails to load on a GPU host the first op raises, so a
+run can never pass on an eager PyTorch path while claiming the HIP kernels.
+"""
+from __future__ import annotations
+
+import os
+import threading
+from typing import Optional
+
+import torch
+
+from . import reference as ref
+
+_lock = threading.Lock()
+_C = None
+_C_err: Optional[BaseException] = None
+
+
+def native():
+    """Return the loaded ``_C`` extension (building it in-tree if allowed)."""
+    global _C, _C_err
+    if _C is not None:
+        return _C
+    with _lock:
+        if _C is not None:
+            return _C
+        try:
+            from .. import _C as mod  # type: ignore
+        except ImportError as e:  # pragma: no cover - depends on build state
+            if os.environ.get("FT_AUTOBUILD", "1") != "0":
+                from .build import build_kernels
+
+                build_kernels(verbose=True)
+                from .. import _C as mod  # type: ignore
+            else:
+                _C_err = e
+                raise RuntimeError(
+                    "fasttalk native extension _C is not built; run "
+                    "`python -m fasttalk_llm_microservice_amd.ops.build`") from e
+        _C = mod
+        return _C
+
+
+def native_available() -> bool:
+    try:
+        native()
+        return True
+    except Exception:
+        return False
+
+
+# ---------------------------------------------------------------------------------
+# norms / activations
+# ---------------------------------------------------------------------------------
+
+def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, out: Optional[torch.Tensor] = None):
+    if x.is_cuda:
+        if out is None:
+            out = torch.empty_like(x)
+        native().rmsnorm(out, x, w, eps)
+        return out
+    r = ref.rmsnorm(x, w, eps)
+    if out is not None:
+        out.copy_(r)
+        return out
+    return r
+
+
+def fused_add_rmsnorm(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, eps: float):
+    """residual <- x + residual;  x <- rmsnorm(residual) * w   (both in place)."""
+    if x.is_cuda:
+        native().fused_add_rmsnorm(x, x, residual, w, eps)
+        return x, residual
+    y, r = ref.fused_add_rmsnorm(x, residual, w, eps)
+    residual.copy_(r)
+    x.copy_(y)
+    return x, residual
+
+
+def silu_mul(gu: torch.Tensor, out: Optional[torch.Tensor] = None):
+    if gu.is_cuda:
+        if out is None:
+            out = torch.empty(gu.shape[0], gu.shape[1] // 2, dtype=gu.dtype, device=gu.device)
+        native().silu_mul(out, gu)
+        return out
+    r = ref.silu_mul(gu)
+    if out is not None:
+        out.copy_(r)
+        return out
+    return r
+
+
+# ---------------------------------------------------------------------------------
+# rotary + paged KV
+# ---------------------------------------------------------------------------------
+
+def rope_kv_write(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, nq, nkv, head_dim):
+    if qkv.is_cuda:
+        native().rope_kv_write(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, nq, nkv,
+                               head_dim)
+    else:
+        ref.rope_kv_write(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, nq, nkv,
+                          head_dim)
+
+
+def decode_partition_size() -> int:
+    return 256
+
+
+def prefill_tile_tokens(nq: int, nkv: int) -> int:
+    return 64 // (nq // nkv)
+
+
+def decode_attention(out, q, k_cache, v_cache, block_tables, seq_lens, tmp_out, tmp_ml, nq, nkv,
+                     head_dim, max_splits, scale):
+    """out[b] = attention of the single new query of sequence b (q: [B, >=nq*D] rows)."""
+    if q.is_cuda:
+        native().paged_decode_attention(out, q, k_cache, v_cache, block_tables, seq_lens, tmp_out,
+                                        tmp_ml, nq, nkv, head_dim, max_splits, scale)
+        return out
+    b = q.shape[0]
+    qq = q[:, : nq * head_dim].reshape(b, nq, head_dim)
+    qsl = torch.arange(b + 1, dtype=torch.int32)
+    o = ref.paged_attention(qq, k_cache, v_cache, block_tables, seq_lens[:b], qsl, scale)
+    out[:b, : nq * head_dim].copy_(o.reshape(b, nq * head_dim))
+    return out
+
+
+def prefill_attention(out, q, k_cache, v_cache, block_tables, seq_lens, q_start_loc, tile_info,
+                      num_tiles, nq, nkv, head_dim, scale):
+    if q.is_cuda:
+        native().prefill_attention(out, q, k_cache, v_cache, block_tables, seq_lens, q_start_loc,
+                                   tile_info, num_tiles, nq, nkv, head_dim, scale)
+        return out
+    t = q.shape[0]
+    qq = q[:, : nq * head_dim].reshape(t, nq, head_dim)
+    o = ref.paged_attention(qq, k_cache, v_cache, block_tables, seq_lens, q_start_loc, scale)
+    out[:t, : nq * head_dim].copy_(o.reshape(t, nq * head_dim))
+    return out
+
+
+def build_prefill_tiles(q_lens, tile_tokens: int):
+    """Host-side tile list [(seq, q_offset)] for the prefill kernel grid."""
+    tiles = []
+    for b, ql in enumerate(q_lens):
+        for s in range(0, int(ql), tile_tokens):
+            tiles.append((b, s))
+    return tiles
+
+
+# ---------------------------------------------------------------------------------
+# sampling
+# ---------------------------------------------------------------------------------
+
+def sample(logits, temperature, top_p, top_k, seeds, steps, out=None, mask=None):
+    if logits.is_cuda:
+        b = logits.shape[0]
+        if out is None:
+            out = torch.empty(b, dtype=torch.int32, device=logits.device)
+        native().sample(out, logits, temperature, top_p, top_k, seeds, steps, mask)
+        return out
+    r = ref.sample(logits, temperature, top_p, top_k, seeds, steps, mask)
+    if out is not None:
+        out[: r.shape[0]].copy_(r)
+        return out
+    return r
+
+
+def kv_block_copy(k_cache, v_cache, pairs: torch.Tensor):
+    if k_cache.is_cuda:
+        native().kv_block_copy(k_cache, v_cache, pairs)
+    else:
+        p = pairs.view(-1, 2).long()
+        k_cache[p[:, 1]] = k_cache[p[:, 0]]
+        v_cache[p[:, 1]] = v_cache[p[:, 0]]

@@ -1,0 +1,58 @@
+"""Tensor-parallel communicator (RCCL over xGMI via torch.distributed).
+
+``torch.distributed`` with ``backend="nccl"`` *is* RCCL on ROCm.  A TP group of
+one process per GPU issues exactly two collectives per transformer layer (after
+the row-parallel O and down projections) plus one
+all-gather of vocab-sharded logits per step (X4).  Small decode-size messages
+(≤ ``custom_max_bytes``) can go through :mod:`.custom_allreduce` (one-shot over
+xGMI peer mappings) when it is enabled and initialised; everything else uses
+RCCL.  On CPU (tests) the same code runs over ``gloo``.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+
+class TPComm:
+    def __init__(self, group: Optional["dist.ProcessGroup"] = None, rank: int = 0,
+                 world_size: int = 1):
+        self.group = group
+        self.rank = rank
+        self.world_size = world_size
+        self.custom = None  # CustomAllReduce, optional
+        self.custom_max_bytes = 8 << 20
+
+    @property
+    def enabled(self) -> bool:
+        return self.world_size > 1
+
+    def all_reduce(self, x: torch.Tensor) -> torch.Tensor:
+        if self.world_size == 1:
+            return x
+        if (self.custom is not None and x.is_cuda
+                and x.numel() * x.element_size() <= self.custom_max_bytes
+                and self.custom.can_handle(x)):
+            return self.custom.all_reduce(x)
+        dist.all_reduce(x, group=self.group)
+        return x
+
+    def all_gather_last(self, x: torch.Tensor) -> torch.Tensor:
+        """Concatenate rank shards along the last dim."""
+        if self.world_size == 1:
+            return x
+        parts = [torch.empty_like(x) for _ in range(self.world_size)]
+        dist.all_gather(parts, x.contiguous(), group=self.group)
+        return torch.cat(parts, dim=-1)
+
+    def broadcast_obj(self, obj, src: int = 0):
+        if self.world_size == 1:
+            return obj
+        lst = [obj]
+        dist.broadcast_object_list(lst, src=src, group=self.group)
+        return lst[0]
+
+
+SINGLE = TPComm()

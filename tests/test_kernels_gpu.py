@@ -1,0 +1,250 @@
+"""Numerics of every gfx950 HIP kernel against the fp32 PyTorch reference of the
+same op (fasttalk_llm_microservice_amd/ops/reference.py)."""
+import math
+
+import pytest
+import torch
+
+from fasttalk_llm_microservice_amd import ops
+from fasttalk_llm_microservice_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _close(a, b, atol, rtol=0.0, msg=""):
+    a = a.float().cpu()
+    b = b.float().cpu()
+    err = (a - b).abs()
+    tol = atol + rtol * b.abs()
+    bad = (err > tol).sum().item()
+    assert bad == 0, f"{msg}: {bad} elems out of tol, max err {err.max().item():.4g}"
+
+
+@pytest.fixture(autouse=True)
+def _native_loaded():
+    ops.native()  # fail loudly if the extension is missing
+    torch.manual_seed(0)
+
+
+@pytest.mark.parametrize("hidden", [2048, 3072, 4096, 8192])
+@pytest.mark.parametrize("rows", [1, 7, 130])
+def test_rmsnorm(hidden, rows):
+    x = torch.randn(rows, hidden, device=DEV).bfloat16()
+    w = (1 + 0.1 * torch.randn(hidden, device=DEV)).bfloat16()
+    out = ops.rmsnorm(x, w, 1e-5)
+    _close(out, ref.rmsnorm(x, w, 1e-5), atol=2e-2, rtol=1e-2, msg="rmsnorm")
+
+
+@pytest.mark.parametrize("hidden", [2048, 4096])
+def test_fused_add_rmsnorm(hidden):
+    x = torch.randn(33, hidden, device=DEV).bfloat16()
+    r = torch.randn(33, hidden, device=DEV).bfloat16()
+    w = (1 + 0.1 * torch.randn(hidden, device=DEV)).bfloat16()
+    ey, er = ref.fused_add_rmsnorm(x, r, w, 1e-5)
+    ops.fused_add_rmsnorm(x, r, w, 1e-5)
+    _close(r, er, atol=1e-2, rtol=1e-2, msg="residual")
+    _close(x, ey, atol=2e-2, rtol=1e-2, msg="normed")
+
+
+def test_silu_mul():
+    gu = torch.randn(37, 2 * 14336, device=DEV).bfloat16()
+    _close(ops.silu_mul(gu), ref.silu_mul(gu), atol=2e-2, rtol=1e-2, msg="silu_mul")
+
+
+def _alloc_cache(nblocks, nkv, bs, d):
+    k = torch.randn(nblocks, nkv, bs, d, device=DEV).bfloat16()
+    v = torch.randn(nblocks, nkv, bs, d, device=DEV).bfloat16()
+    return k, v
+
+
+@pytest.mark.parametrize("nq,nkv,d", [(32, 8, 128), (24, 8, 128), (32, 8, 64), (8, 1, 128)])
+def test_rope_kv_write(nq, nkv, d):
+    t, bs, nblocks = 45, 16, 20
+    qkv = torch.randn(t, (nq + 2 * nkv) * d, device=DEV).bfloat16()
+    pos = torch.randint(0, 4000, (t,), device=DEV, dtype=torch.int32)
+    cs = ref.rope_cos_sin(d, 8192, 500000.0, {"factor": 8.0, "low_freq_factor": 1.0,
+                                              "high_freq_factor": 4.0,
+                                              "original_max_position_embeddings": 8192}, DEV)
+    slots = torch.randperm(nblocks * bs, device=DEV)[:t].int()
+    slots[3] = -1
+    k1, v1 = _alloc_cache(nblocks, nkv, bs, d)
+    k2, v2 = k1.clone(), v1.clone()
+    q1 = qkv.clone()
+    q2 = qkv.clone()
+    ops.rope_kv_write(q1, pos, cs, slots, k1, v1, nq, nkv, d)
+    ref.rope_kv_write(q2, pos, cs, slots, k2, v2, nq, nkv, d)
+    _close(q1[:, : nq * d], q2[:, : nq * d], atol=2e-2, rtol=1e-2, msg="q")
+    _close(k1, k2, atol=2e-2, rtol=1e-2, msg="k cache")
+    assert torch.equal(v1, v2)
+
+
+def _random_tables(lens, bs, nblocks_total):
+    perm = torch.randperm(nblocks_total).int()
+    maxb = max((l + bs - 1) // bs for l in lens)
+    bt = torch.zeros(len(lens), maxb, dtype=torch.int32)
+    i = 0
+    for b, l in enumerate(lens):
+        n = (l + bs - 1) // bs
+        bt[b, :n] = perm[i: i + n]
+        i += n
+    return bt
+
+
+@pytest.mark.parametrize("nq,nkv,d", [(32, 8, 128), (64, 8, 128), (8, 8, 128), (24, 8, 128),
+                                      (32, 8, 64)])
+def test_decode_attention(nq, nkv, d):
+    bs = 16
+    lens = [1, 17, 255, 256, 257, 1000, 2100]
+    nblocks = sum((l + bs - 1) // bs for l in lens) + 4
+    k, v = _alloc_cache(nblocks, nkv, bs, d)
+    bt = _random_tables(lens, bs, nblocks).to(DEV)
+    sl = torch.tensor(lens, dtype=torch.int32, device=DEV)
+    b = len(lens)
+    q = torch.randn(b, nq * d, device=DEV).bfloat16()
+    part = ops.decode_partition_size()
+    max_splits = math.ceil(max(lens) / part)
+    tmp_out = torch.empty(b * nq * max_splits * d, device=DEV)
+    tmp_ml = torch.empty(b * nq * max_splits * 2, device=DEV)
+    out = torch.zeros(b, nq * d, device=DEV).bfloat16()
+    scale = d ** -0.5
+    ops.decode_attention(out, q, k, v, bt, sl, tmp_out, tmp_ml, nq, nkv, d, max_splits, scale)
+    expect = ref.paged_attention(q.view(b, nq, d), k, v, bt, sl,
+                                 torch.arange(b + 1, dtype=torch.int32), scale).view(b, nq * d)
+    _close(out, expect, atol=2e-2, rtol=2e-2, msg="decode attention")
+
+
+@pytest.mark.parametrize("nq,nkv,d", [(32, 8, 128), (24, 8, 128), (64, 8, 128), (32, 8, 64),
+                                      (8, 8, 128)])
+def test_prefill_attention(nq, nkv, d):
+    bs = 16
+    # (new tokens, cached prefix)
+    seqs = [(1, 0), (5, 0), (64, 0), (77, 33), (16, 300), (130, 1), (3, 500)]
+    lens = [a + p for a, p in seqs]
+    nblocks = sum((l + bs - 1) // bs for l in lens) + 4
+    k, v = _alloc_cache(nblocks, nkv, bs, d)
+    bt = _random_tables(lens, bs, nblocks).to(DEV)
+    sl = torch.tensor(lens, dtype=torch.int32, device=DEV)
+    qlens = [a for a, _ in seqs]
+    qsl = torch.tensor([0] + list(torch.tensor(qlens).cumsum(0)), dtype=torch.int32)
+    t = int(qsl[-1])
+    q = torch.randn(t, nq * d, device=DEV).bfloat16()
+    tiles = ops.build_prefill_tiles(qlens, ops.prefill_tile_tokens(nq, nkv))
+    ti = torch.tensor(tiles, dtype=torch.int32, device=DEV).flatten()
+    out = torch.zeros(t, nq * d, device=DEV).bfloat16()
+    scale = d ** -0.5
+    ops.prefill_attention(out, q, k, v, bt, sl, qsl.to(DEV), ti, len(tiles), nq, nkv, d, scale)
+    expect = ref.paged_attention(q.view(t, nq, d), k, v, bt, sl, qsl, scale).view(t, nq * d)
+    _close(out, expect, atol=2e-2, rtol=2e-2, msg="prefill attention")
+
+
+def test_prefill_attention_strided_q():
+    """q read straight out of the fused QKV buffer (row stride > nq*d)."""
+    nq, nkv, d, bs = 32, 8, 128, 16
+    lens = [40, 90]
+    nblocks = 16
+    k, v = _alloc_cache(nblocks, nkv, bs, d)
+    bt = _random_tables(lens, bs, nblocks).to(DEV)
+    sl = torch.tensor(lens, dtype=torch.int32, device=DEV)
+    qsl = torch.tensor([0, 40, 130], dtype=torch.int32)
+    qkv = torch.randn(130, (nq + 2 * nkv) * d, device=DEV).bfloat16()
+    tiles = ops.build_prefill_tiles([40, 90], ops.prefill_tile_tokens(nq, nkv))
+    ti = torch.tensor(tiles, dtype=torch.int32, device=DEV).flatten()
+    out = torch.zeros(130, nq * d, device=DEV).bfloat16()
+    ops.prefill_attention(out, qkv, k, v, bt, sl, qsl.to(DEV), ti, len(tiles), nq, nkv, d, 0.088)
+    expect = ref.paged_attention(qkv[:, : nq * d].reshape(130, nq, d), k, v, bt, sl, qsl,
+                                 0.088).view(130, nq * d)
+    _close(out, expect, atol=2e-2, rtol=2e-2, msg="strided q")
+
+
+def _sp(b, temp, top_p=1.0, top_k=0):
+    return (torch.full((b,), temp, device=DEV), torch.full((b,), top_p, device=DEV),
+            torch.full((b,), top_k, dtype=torch.int32, device=DEV),
+            torch.arange(b, dtype=torch.int64, device=DEV) * 7919,
+            torch.zeros(b, dtype=torch.int32, device=DEV))
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_sample_greedy(dtype):
+    logits = torch.randn(50, 128256, device=DEV).to(dtype)
+    t, p, k, s, st = _sp(50, 0.0)
+    out = ops.sample(logits, t, p, k, s, st)
+    assert torch.equal(out.long().cpu(), logits.float().argmax(-1).cpu())
+
+
+def test_sample_topk1_is_argmax():
+    logits = torch.randn(20, 128256, device=DEV)
+    t, p, k, s, st = _sp(20, 0.8, 1.0, 1)
+    out = ops.sample(logits, t, p, k, s, st)
+    assert torch.equal(out.long().cpu(), logits.argmax(-1).cpu())
+
+
+def test_sample_topk_membership():
+    logits = torch.randn(64, 128256, device=DEV)
+    t, p, k, s, st = _sp(64, 1.0, 1.0, 40)
+    out = ops.sample(logits, t, p, k, s, st).long().cpu()
+    topk = logits.topk(40, dim=-1).indices.cpu()
+    assert all(out[i].item() in set(topk[i].tolist()) for i in range(64))
+
+
+def test_sample_topp_membership():
+    logits = torch.randn(64, 32000, device=DEV) * 4
+    t, p, k, s, st = _sp(64, 0.7, 0.5, 0)
+    out = ops.sample(logits, t, p, k, s, st).long().cpu()
+    probs = torch.softmax(logits.cpu() / 0.7, -1)
+    for i in range(64):
+        sp, si = probs[i].sort(descending=True)
+        n = int((sp.cumsum(0) < 0.5).sum().item()) + 1
+        assert out[i].item() in set(si[: n + 1].tolist())
+
+
+def test_sample_distribution():
+    """Empirical frequencies of many independent draws match softmax(logits/T)."""
+    v = 64
+    base = torch.randn(v) * 1.5
+    rows = 4096
+    logits = base.to(DEV).repeat(rows, 1)
+    t = torch.full((rows,), 0.9, device=DEV)
+    p = torch.ones(rows, device=DEV)
+    k = torch.zeros(rows, dtype=torch.int32, device=DEV)
+    s = torch.arange(rows, dtype=torch.int64, device=DEV) * 104729 + 17
+    counts = torch.zeros(v)
+    for step in range(8):
+        st = torch.full((rows,), step, dtype=torch.int32, device=DEV)
+        out = ops.sample(logits, t, p, k, s, st).long().cpu()
+        counts += torch.bincount(out, minlength=v).float()
+    emp = counts / counts.sum()
+    expect = torch.softmax(base / 0.9, -1)
+    assert (emp - expect).abs().max().item() < 0.01
+
+
+def test_sample_mask():
+    v = 1000
+    logits = torch.randn(8, v, device=DEV)
+    mask = torch.zeros(8, (v + 31) // 32, dtype=torch.int32)
+    allowed = [5, 77, 999]
+    for a in allowed:
+        mask[:, a // 32] |= (1 << (a % 32)) if a % 32 < 31 else -(1 << 31)
+    t, p, k, s, st = _sp(8, 1.0)
+    out = ops.sample(logits, t, p, k, s, st, mask=mask.to(DEV)).cpu().tolist()
+    assert all(o in allowed for o in out)
+    t0, *_ = _sp(8, 0.0)
+    out = ops.sample(logits, t0, p, k, s, st, mask=mask.to(DEV)).cpu()
+    exp = torch.tensor(allowed)[logits.cpu()[:, allowed].argmax(-1)]
+    assert torch.equal(out.long(), exp)
+
+
+def test_sample_deterministic():
+    logits = torch.randn(16, 128256, device=DEV)
+    t, p, k, s, st = _sp(16, 0.7, 0.9, 0)
+    a = ops.sample(logits, t, p, k, s, st).cpu()
+    b = ops.sample(logits, t, p, k, s, st).cpu()
+    assert torch.equal(a, b)
+
+
+def test_kv_block_copy():
+    k, v = _alloc_cache(10, 8, 16, 128)
+    k0, v0 = k.clone(), v.clone()
+    pairs = torch.tensor([[1, 5], [2, 7]], dtype=torch.int32, device=DEV)
+    ops.kv_block_copy(k, v, pairs)
+    assert torch.equal(k[5], k0[1]) and torch.equal(v[7], v0[2]) and torch.equal(k[0], k0[0])
