@@ -1,0 +1,100 @@
+"""Engine configuration.
+
+Maps the vLLM engine flags the reference sets in ``docker-compose.vllm.yml:38-53``
+(``--max-num-seqs``, ``--max-num-batched-tokens``, ``--max-model-len``,
+``--gpu-memory-utilization``, ``--swap-space``, ``--tensor-parallel-size``,
+``--dtype``, ``--enforce-eager``) onto our in-process engine.  Existing
+``VLLM_*`` env files keep their meaning; ``ENGINE_*`` variables take precedence.
+Defaults are sized for one MI355X (288 GB HBM3E): 256 concurrent sequences
+instead of vLLM's 32 on a 24 GB card.
+"""
+from __future__ import annotations
+
+import dataclasses
+import os
+from typing import Optional, Tuple
+
+
+def _env(names, default, cast=str):
+    for n in names:
+        v = os.environ.get(n)
+        if v not in (None, ""):
+            try:
+                return cast(v)
+            except ValueError:
+                pass
+    return default
+
+
+def _bool(v: str) -> bool:
+    return str(v).lower() in ("1", "true", "yes", "on")
+
+
+@dataclasses.dataclass
+class EngineConfig:
+    model: str = "llama3.1-8b"
+    weights: str = "random"            # "random" or a safetensors checkpoint dir
+    tokenizer: Optional[str] = None    # tokenizer.json / dir; None -> synthetic Llama-3
+    seed: int = 0
+    dtype: str = "bfloat16"
+    device: str = "auto"               # auto | cuda | cpu
+    tp_size: int = 1
+    dp_size: int = 1
+    max_num_seqs: int = 256
+    max_num_batched_tokens: int = 8192
+    max_model_len: int = 8192
+    gpu_memory_utilization: float = 0.90
+    num_kv_blocks: Optional[int] = None
+    block_size: int = 16
+    swap_space_gb: float = 4.0
+    enable_prefix_caching: bool = True
+    enforce_eager: bool = False        # disable hipGraph decode capture
+    graph_batch_sizes: Tuple[int, ...] = (1, 2, 4, 8, 16, 24, 32, 48, 64, 80, 96, 128, 160, 192, 224, 256)
+    async_output: bool = True          # overlap detokenize/streaming with the next GPU step
+
+    def resolved_device(self) -> str:
+        if self.device != "auto":
+            return self.device
+        try:
+            import torch
+
+            return "cuda" if torch.cuda.is_available() else "cpu"
+        except Exception:
+            return "cpu"
+
+    def torch_dtype(self):
+        import torch
+
+        if self.resolved_device() == "cpu" and self.dtype in ("auto", "bfloat16") and \
+                os.environ.get("ENGINE_CPU_BF16", "0") != "1":
+            return torch.float32  # CPU backend computes in fp32
+        return {"bfloat16": torch.bfloat16, "bf16": torch.bfloat16, "float16": torch.bfloat16,
+                "half": torch.bfloat16, "auto": torch.bfloat16,
+                "float32": torch.float32}[self.dtype]
+
+    @classmethod
+    def from_env(cls, model: Optional[str] = None, **overrides) -> "EngineConfig":
+        c = cls(
+            model=model or _env(["ENGINE_MODEL", "VLLM_MODEL"], cls.model),
+            weights=_env(["ENGINE_WEIGHTS", "MODEL_WEIGHTS"], "random"),
+            tokenizer=_env(["ENGINE_TOKENIZER"], None),
+            seed=_env(["ENGINE_SEED"], 0, int),
+            dtype=_env(["ENGINE_DTYPE", "VLLM_DTYPE"], "bfloat16"),
+            device=_env(["ENGINE_DEVICE"], "auto"),
+            tp_size=_env(["ENGINE_TP_SIZE", "VLLM_TENSOR_PARALLEL_SIZE"], 1, int),
+            dp_size=_env(["ENGINE_DP_SIZE"], 1, int),
+            max_num_seqs=_env(["ENGINE_MAX_NUM_SEQS", "VLLM_MAX_NUM_SEQS"], 256, int),
+            max_num_batched_tokens=_env(["ENGINE_MAX_NUM_BATCHED_TOKENS",
+                                         "VLLM_MAX_NUM_BATCHED_TOKENS"], 8192, int),
+            max_model_len=_env(["ENGINE_MAX_MODEL_LEN", "VLLM_MAX_MODEL_LEN"], 8192, int),
+            gpu_memory_utilization=_env(["ENGINE_GPU_MEMORY_UTILIZATION",
+                                         "VLLM_GPU_MEMORY_UTILIZATION"], 0.90, float),
+            num_kv_blocks=_env(["ENGINE_NUM_KV_BLOCKS"], None, int),
+            block_size=_env(["ENGINE_BLOCK_SIZE"], 16, int),
+            swap_space_gb=_env(["ENGINE_SWAP_SPACE", "VLLM_SWAP_SPACE"], 4.0, float),
+            enable_prefix_caching=_env(["ENGINE_PREFIX_CACHING"], True, _bool),
+            enforce_eager=_env(["ENGINE_ENFORCE_EAGER", "VLLM_ENFORCE_EAGER"], False, _bool),
+        )
+        for k, v in overrides.items():
+            setattr(c, k, v)
+        return c

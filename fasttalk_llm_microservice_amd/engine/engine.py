@@ -1,0 +1,444 @@
+"""LLMEngine (synchronous step loop) and AsyncEngine (engine thread + asyncio
+streams).  Together they replace the vLLM server the reference reaches over
+HTTP/SSE (``app/core/vllm_handler.py:216-308``): ``AsyncEngine.generate`` is an
+async iterator of text deltas, ``abort`` is E12 (frees KV blocks mid-stream),
+``is_healthy`` / ``model_info`` are E13.
+"""
+from __future__ import annotations
+
+import asyncio
+import collections
+import itertools
+import logging
+import queue
+import threading
+import time
+import uuid
+from typing import Any, AsyncIterator, Callable, Dict, List, Optional, Sequence as Seq
+
+import numpy as np
+
+from ..models.config import resolve_model
+from ..parallel.comm import SINGLE, TPComm
+from ..runtime import rt
+from .chat_template import ChatTemplate
+from .config import EngineConfig
+from .sampling_params import SamplingParams
+from .scheduler import ScheduledBatch, Scheduler
+from .sequence import RequestOutput, SeqStatus, Sequence
+from .tokenizer import get_tokenizer
+
+log = logging.getLogger("fasttalk.engine")
+
+
+class EngineError(RuntimeError):
+    pass
+
+
+class LLMEngine:
+    def __init__(self, cfg: EngineConfig, comm: TPComm = SINGLE, runner=None):
+        self.cfg = cfg
+        self.model_cfg = resolve_model(cfg.weights if cfg.weights not in ("random", None, "")
+                                       else cfg.model)
+        tok_path = cfg.tokenizer
+        if tok_path is None and cfg.weights not in ("random", None, ""):
+            tok_path = cfg.weights
+        self.tokenizer = get_tokenizer(tok_path)
+        self.template = ChatTemplate(self.tokenizer)
+        if runner is None:
+            from .runner import ModelRunner
+
+            runner = ModelRunner(cfg, self.model_cfg, comm)
+        self.runner = runner
+        self.max_model_len = runner.max_model_len
+        R = rt()
+        self.bm = R.BlockManager(runner.num_blocks, cfg.block_size, cfg.enable_prefix_caching)
+        self.detok = R.Detokenizer(self.tokenizer.id_to_bytes)
+        self.scheduler = Scheduler(self.bm, cfg.block_size, cfg.max_num_seqs,
+                                   cfg.max_num_batched_tokens, self.max_model_len)
+        self.stop_ids = set(self.tokenizer.stop_ids) | set(self.model_cfg.eos_token_ids)
+        self._trie = None
+        self.stats = collections.Counter()
+        self.step_times = collections.deque(maxlen=512)
+        self.last_step_end = time.time()
+
+    # ------------------------------------------------------------------ requests
+    def add_request(self, request_id: str, prompt_ids: Seq[int], params: SamplingParams,
+                    on_output: Optional[Callable[[RequestOutput], None]] = None,
+                    meta: Any = None) -> Sequence:
+        prompt_ids = list(prompt_ids)
+        if not prompt_ids:
+            prompt_ids = [self.tokenizer.bos_id]
+        if len(prompt_ids) >= self.max_model_len:
+            raise EngineError(f"prompt of {len(prompt_ids)} tokens exceeds max_model_len "
+                              f"{self.max_model_len}")
+        seq = Sequence(request_id, prompt_ids, params, on_output, meta)
+        seq.detok_stream = self.detok.new_stream()
+        if params.guided is not None:
+            seq.grammar = params.guided.grammar(self)
+            seq.grammar_state = seq.grammar.initial()
+        self.scheduler.add(seq)
+        self.stats["requests"] += 1
+        return seq
+
+    def abort(self, request_id: str) -> bool:
+        seq = self.scheduler.abort(request_id)
+        if seq is None:
+            return False
+        self._finalize(seq, "abort", emit=True)
+        return True
+
+    def has_work(self) -> bool:
+        return self.scheduler.has_work()
+
+    # ------------------------------------------------------------------ helpers
+    def token_trie(self):
+        if self._trie is None:
+            self._trie = rt().TokenTrie(self.tokenizer.id_to_bytes)
+        return self._trie
+
+    def _masks_for(self, seqs: List[Sequence]) -> Optional[np.ndarray]:
+        if not any(s.grammar is not None for s in seqs):
+            return None
+        words = (self.runner.mcfg.vocab_size + 31) // 32
+        m = np.full((len(seqs), words), -1, dtype=np.int32)
+        for i, s in enumerate(seqs):
+            if s.grammar is not None and s.grammar_state >= 0:
+                raw = np.frombuffer(s.grammar.mask(s.grammar_state), dtype=np.int32)
+                m[i, : raw.shape[0]] = raw
+                m[i, raw.shape[0]:] = 0
+        return m
+
+    # ------------------------------------------------------------------ stepping
+    def step(self) -> List[RequestOutput]:
+        batch = self.scheduler.schedule()
+        if batch is None:
+            return []
+        t0 = time.perf_counter()
+        outs: List[RequestOutput] = []
+        # sequences the scheduler had to reject (cannot fit in the KV pool)
+        for s, n in zip(batch.seqs, batch.num_tokens):
+            if n == 0 and s.status == SeqStatus.FINISHED and s.finish_reason == "error":
+                self.scheduler.by_id.pop(s.request_id, None)
+                outs.append(self._finalize(s, "error", emit=True,
+                                           error="prompt does not fit in the KV cache"))
+        sampled_seqs = [s for s, n, sm in zip(batch.seqs, batch.num_tokens, batch.sample)
+                        if n > 0 and sm]
+        masks = self._masks_for(sampled_seqs)
+        toks = self.runner.execute(batch, masks)
+        self.scheduler.post_step(batch)
+        for seq, tok in zip(sampled_seqs, toks):
+            o = self._process_token(seq, int(tok))
+            if o is not None:
+                outs.append(o)
+        dt = time.perf_counter() - t0
+        self.step_times.append((batch.is_prefill, len(batch.seqs), batch.total_tokens, dt))
+        self.stats["prefill_steps" if batch.is_prefill else "decode_steps"] += 1
+        self.stats["generated_tokens"] += len(sampled_seqs)
+        if batch.is_prefill:
+            self.stats["prefill_tokens"] += batch.total_tokens
+        self.last_step_end = time.time()
+        return outs
+
+    def _process_token(self, seq: Sequence, tok: int) -> Optional[RequestOutput]:
+        if seq.status == SeqStatus.FINISHED:
+            return None
+        p = seq.params
+        now = time.perf_counter()
+        first = seq.first_token_time is None
+        if first:
+            seq.first_token_time = now
+        seq.append(tok)
+        n_out = seq.num_output
+        reason = None
+        is_stop_tok = (tok in self.stop_ids and not p.ignore_eos) or \
+            (p.stop_token_ids is not None and tok in p.stop_token_ids)
+        if seq.grammar is not None:
+            if seq.grammar.is_eos(tok) and seq.grammar.accepting(seq.grammar_state):
+                is_stop_tok = True
+            else:
+                seq.grammar_state = seq.grammar.advance_token(seq.grammar_state, tok)
+                if seq.grammar_state < 0:
+                    reason = "stop"
+        if is_stop_tok and n_out > p.min_tokens:
+            reason = "stop"
+            delta = ""
+        else:
+            delta = self.detok.push(seq.detok_stream, tok)
+        if reason is None:
+            if n_out >= p.max_tokens or seq.n_tokens >= self.max_model_len:
+                reason = "length"
+        if p.stop and delta:
+            delta, hit = self._apply_stop(seq, delta)
+            if hit:
+                reason = "stop"
+        elif p.stop and reason is not None:
+            pass
+        ids = [] if (is_stop_tok and reason == "stop") else [tok]
+        if reason is not None:
+            return self._finalize(seq, reason, emit=True, delta=delta, ids=ids)
+        if not delta and not first:
+            # nothing printable yet (partial UTF-8): still report progress
+            out = RequestOutput(seq.request_id, "", ids, num_output_tokens=n_out)
+        else:
+            out = RequestOutput(seq.request_id, delta, ids, num_output_tokens=n_out,
+                                num_prompt_tokens=seq.prompt_len,
+                                num_cached_tokens=seq.num_cached_tokens,
+                                ttft_s=(seq.first_token_time - seq.arrival) if first else None)
+        if seq.on_output is not None:
+            seq.on_output(out)
+        return out
+
+    def _apply_stop(self, seq: Sequence, delta: str):
+        """Hold back text that could be the start of a stop string."""
+        stops = seq.params.stop
+        buf = seq.stop_buf + delta
+        for s in stops:
+            i = buf.find(s)
+            if i >= 0:
+                seq.stop_buf = ""
+                return buf[:i], True
+        keep = max(len(s) for s in stops) - 1
+        if keep <= 0:
+            seq.stop_buf = ""
+            return buf, False
+        # emit all but the longest suffix that is a prefix of some stop string
+        hold = 0
+        for k in range(min(keep, len(buf)), 0, -1):
+            tail = buf[-k:]
+            if any(s.startswith(tail) for s in stops):
+                hold = k
+                break
+        seq.stop_buf = buf[len(buf) - hold:] if hold else ""
+        return buf[: len(buf) - hold], False
+
+    def _finalize(self, seq: Sequence, reason: str, emit: bool, delta: str = "",
+                  ids: Optional[List[int]] = None, error: Optional[str] = None) -> RequestOutput:
+        if seq.status != SeqStatus.FINISHED or seq.block_ids:
+            self.scheduler.finish(seq, reason)
+        seq.finish_reason = reason
+        tail = ""
+        if seq.detok_stream >= 0:
+            if reason != "abort":
+                tail = self.detok.flush(seq.detok_stream)
+            self.detok.release(seq.detok_stream)
+            seq.detok_stream = -1
+        text = delta + (seq.stop_buf if reason != "stop" else "") + tail
+        seq.stop_buf = ""
+        out = RequestOutput(seq.request_id, text, ids or [], finished=True, finish_reason=reason,
+                            num_prompt_tokens=seq.prompt_len,
+                            num_cached_tokens=seq.num_cached_tokens,
+                            num_output_tokens=seq.num_output, error=error)
+        self.stats["finished_" + reason] += 1
+        if emit and seq.on_output is not None:
+            seq.on_output(out)
+        return out
+
+    # ------------------------------------------------------------------ convenience
+    def generate(self, prompts: List[List[int]], params: SamplingParams) -> List[List[int]]:
+        """Blocking batch generation (tests / offline use)."""
+        ids = []
+        for i, p in enumerate(prompts):
+            rid = f"gen-{uuid.uuid4().hex[:8]}-{i}"
+            self.add_request(rid, p, SamplingParams(**{**params.__dict__}))
+            ids.append(rid)
+        results: Dict[str, List[int]] = {r: [] for r in ids}
+        done = set()
+        while len(done) < len(ids):
+            if not self.has_work():
+                break
+            for o in self.step():
+                if o.request_id in results:
+                    results[o.request_id].extend(o.token_ids)
+                    if o.finished:
+                        done.add(o.request_id)
+        return [results[r] for r in ids]
+
+    def kv_usage(self) -> float:
+        n = self.bm.num_blocks
+        return 1.0 - self.bm.num_free() / n if n else 0.0
+
+    def metrics(self) -> Dict[str, Any]:
+        st = list(self.step_times)
+        dec = [x for x in st if not x[0]]
+        pre = [x for x in st if x[0]]
+        return {
+            "running": len(self.scheduler.running),
+            "waiting": len(self.scheduler.waiting),
+            "kv_blocks_total": self.bm.num_blocks,
+            "kv_blocks_free": self.bm.num_free(),
+            "kv_blocks_cached": self.bm.num_cached(),
+            "kv_usage": self.kv_usage(),
+            "prefix_cache_hit_rate": (self.bm.hits / self.bm.queries) if self.bm.queries else 0.0,
+            "preemptions": self.scheduler.num_preemptions,
+            "decode_step_ms_avg": 1e3 * sum(x[3] for x in dec) / len(dec) if dec else 0.0,
+            "decode_batch_avg": sum(x[1] for x in dec) / len(dec) if dec else 0.0,
+            "prefill_step_ms_avg": 1e3 * sum(x[3] for x in pre) / len(pre) if pre else 0.0,
+            **{k: v for k, v in self.stats.items()},
+            "runner": dict(getattr(self.runner, "stats", {})),
+        }
+
+
+class AsyncEngine:
+    """Runs an :class:`LLMEngine` on a dedicated thread and multiplexes every
+    WebSocket session into its batched step loop (E16).  Outputs are handed to
+    the asyncio loop once per engine step (one ``call_soon_threadsafe`` per step,
+    not per token)."""
+
+    def __init__(self, engine: LLMEngine):
+        self.engine = engine
+        self._cmds: "queue.SimpleQueue" = queue.SimpleQueue()
+        self._wake = threading.Event()
+        self._stop = False
+        self._thread: Optional[threading.Thread] = None
+        self._streams: Dict[str, "asyncio.Queue"] = {}
+        self._loops: Dict[str, asyncio.AbstractEventLoop] = {}
+        self._pending: Dict[asyncio.AbstractEventLoop, list] = {}
+        self._ids = itertools.count()
+        self.error: Optional[BaseException] = None
+        self.heartbeat = time.time()
+
+    @classmethod
+    def from_config(cls, cfg: EngineConfig) -> "AsyncEngine":
+        return cls(LLMEngine(cfg))
+
+    # ------------------------------------------------------------------ lifecycle
+    def start(self):
+        if self._thread is None:
+            self._thread = threading.Thread(target=self._run, name="fasttalk-engine", daemon=True)
+            self._thread.start()
+        return self
+
+    def shutdown(self):
+        self._stop = True
+        self._wake.set()
+        if self._thread is not None:
+            self._thread.join(timeout=10)
+            self._thread = None
+
+    def is_healthy(self, stall_s: float = 120.0) -> bool:
+        """Watchdog: the step loop must be alive and, when busy, making progress."""
+        if self.error is not None or self._thread is None or not self._thread.is_alive():
+            return False
+        if self.engine.has_work() and time.time() - self.heartbeat > stall_s:
+            return False
+        return True
+
+    # ------------------------------------------------------------------ engine thread
+    def _deliver(self, out: RequestOutput):
+        loop = self._loops.get(out.request_id)
+        if loop is None:
+            return
+        self._pending.setdefault(loop, []).append(out)
+
+    def _flush(self):
+        for loop, items in self._pending.items():
+            if items:
+                try:
+                    loop.call_soon_threadsafe(self._dispatch, items)
+                except RuntimeError:
+                    pass
+        self._pending = {}
+
+    def _dispatch(self, items: List[RequestOutput]):
+        for o in items:
+            q = self._streams.get(o.request_id)
+            if q is not None:
+                q.put_nowait(o)
+
+    def _run(self):
+        eng = self.engine
+        while not self._stop:
+            self.heartbeat = time.time()
+            while True:
+                try:
+                    cmd = self._cmds.get_nowait()
+                except queue.Empty:
+                    break
+                self._handle(cmd)
+            if not eng.has_work():
+                self._flush()
+                self._wake.wait(0.05)
+                self._wake.clear()
+                continue
+            try:
+                eng.step()
+            except Exception as e:  # pragma: no cover - surfaced through health / streams
+                log.exception("engine step failed")
+                self.error = e
+                for seq in list(eng.scheduler.running) + list(eng.scheduler.waiting):
+                    eng._finalize(seq, "error", emit=True, error=str(e))
+                self._flush()
+                self.error = None if self._recoverable(e) else e
+                continue
+            self._flush()
+
+    @staticmethod
+    def _recoverable(e: BaseException) -> bool:
+        return not isinstance(e, (MemoryError,))
+
+    def _handle(self, cmd):
+        kind = cmd[0]
+        if kind == "add":
+            _, rid, prompt, params = cmd
+            try:
+                self.engine.add_request(rid, prompt, params, on_output=self._deliver)
+            except Exception as e:
+                self._deliver(RequestOutput(rid, "", [], finished=True, finish_reason="error",
+                                            error=str(e)))
+        elif kind == "abort":
+            self.engine.abort(cmd[1])
+
+    # ------------------------------------------------------------------ public API
+    def new_request_id(self) -> str:
+        return f"req-{next(self._ids)}-{uuid.uuid4().hex[:6]}"
+
+    async def generate(self, prompt_ids: Seq[int], params: SamplingParams,
+                       request_id: Optional[str] = None) -> AsyncIterator[RequestOutput]:
+        if self.error is not None:
+            raise EngineError(f"engine failed: {self.error}")
+        rid = request_id or self.new_request_id()
+        if rid in self._streams:
+            raise EngineError(f"duplicate request id {rid}")
+        q: asyncio.Queue = asyncio.Queue()
+        self._streams[rid] = q
+        self._loops[rid] = asyncio.get_running_loop()
+        self._cmds.put(("add", rid, list(prompt_ids), params))
+        self._wake.set()
+        finished = False
+        try:
+            while True:
+                o = await q.get()
+                if o.finished:
+                    finished = True
+                yield o
+                if finished:
+                    break
+        finally:
+            self._streams.pop(rid, None)
+            if not finished:
+                # consumer went away before the end: free the KV blocks
+                self._cmds.put(("abort", rid))
+                self._wake.set()
+            self._loops.pop(rid, None)
+
+    def abort(self, request_id: str) -> bool:
+        if request_id not in self._loops:
+            return False
+        self._cmds.put(("abort", request_id))
+        self._wake.set()
+        return True
+
+    def active_requests(self) -> List[str]:
+        return list(self._loops.keys())
+
+    def model_info(self) -> Dict[str, Any]:
+        e = self.engine
+        m = e.model_cfg
+        return {
+            "model": m.name, "num_layers": m.num_layers, "hidden_size": m.hidden_size,
+            "num_heads": m.num_heads, "num_kv_heads": m.num_kv_heads, "vocab_size": m.vocab_size,
+            "max_model_len": e.max_model_len, "dtype": str(e.runner.dtype).replace("torch.", ""),
+            "device": str(e.runner.device), "weights": e.cfg.weights,
+            "tensor_parallel_size": e.cfg.tp_size, "kv_cache_tokens": e.bm.num_blocks * e.cfg.block_size,
+        }

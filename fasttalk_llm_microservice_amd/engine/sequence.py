@@ -1,0 +1,95 @@
+"""Request / sequence state tracked by the scheduler."""
+from __future__ import annotations
+
+import dataclasses
+import enum
+import time
+from typing import Any, Callable, List, Optional
+
+import numpy as np
+
+from .sampling_params import SamplingParams
+
+
+class SeqStatus(enum.Enum):
+    WAITING = "waiting"
+    RUNNING = "running"
+    FINISHED = "finished"
+
+
+@dataclasses.dataclass
+class RequestOutput:
+    """One streamed event for a request (what the engine hands the API layer)."""
+    request_id: str
+    text: str                       # text delta (complete UTF-8 characters)
+    token_ids: List[int]            # new token ids in this delta
+    finished: bool = False
+    finish_reason: Optional[str] = None   # "stop" | "length" | "abort" | "error"
+    num_prompt_tokens: int = 0
+    num_cached_tokens: int = 0
+    num_output_tokens: int = 0
+    ttft_s: Optional[float] = None
+    error: Optional[str] = None
+
+
+class Sequence:
+    __slots__ = ("request_id", "params", "prompt_len", "_tok", "n_tokens", "status", "block_ids",
+                 "num_computed", "num_committed_blocks", "num_cached_tokens", "arrival",
+                 "first_token_time", "finish_reason", "detok_stream", "on_output", "grammar",
+                 "grammar_state", "stop_buf", "text_len", "aborted", "preemptions", "admit_order",
+                 "meta")
+
+    def __init__(self, request_id: str, prompt_ids: List[int], params: SamplingParams,
+                 on_output: Optional[Callable[[RequestOutput], None]] = None, meta: Any = None):
+        self.request_id = request_id
+        self.params = params
+        self.prompt_len = len(prompt_ids)
+        cap = max(64, len(prompt_ids) + min(params.max_tokens, 4096) + 1)
+        self._tok = np.zeros(cap, dtype=np.int32)
+        self._tok[: len(prompt_ids)] = prompt_ids
+        self.n_tokens = len(prompt_ids)
+        self.status = SeqStatus.WAITING
+        self.block_ids: List[int] = []
+        self.num_computed = 0
+        self.num_committed_blocks = 0
+        self.num_cached_tokens = 0
+        self.arrival = time.perf_counter()
+        self.first_token_time: Optional[float] = None
+        self.finish_reason: Optional[str] = None
+        self.detok_stream = -1
+        self.on_output = on_output
+        self.grammar = None
+        self.grammar_state = -1
+        self.stop_buf = ""
+        self.text_len = 0
+        self.aborted = False
+        self.preemptions = 0
+        self.admit_order = 0
+        self.meta = meta
+
+    # ---------------------------------------------------------------- tokens
+    @property
+    def tokens(self) -> np.ndarray:
+        return self._tok[: self.n_tokens]
+
+    def append(self, tok: int):
+        if self.n_tokens >= self._tok.shape[0]:
+            self._tok = np.concatenate([self._tok, np.zeros(self._tok.shape[0], dtype=np.int32)])
+        self._tok[self.n_tokens] = tok
+        self.n_tokens += 1
+
+    @property
+    def num_output(self) -> int:
+        return self.n_tokens - self.prompt_len
+
+    @property
+    def output_ids(self) -> List[int]:
+        return self._tok[self.prompt_len: self.n_tokens].tolist()
+
+    @property
+    def last_token(self) -> int:
+        return int(self._tok[self.n_tokens - 1])
+
+    @property
+    def is_finished(self) -> bool:
+        return self.status == SeqStatus.FINISHED
