@@ -1,0 +1,311 @@
+"""Voice agent with tool calling (E18) -- API of the reference
+``app/agents/voice_agent.py`` (``ConversationContext``, ``AgentConfig``,
+``VoiceAgent.generate_stream / generate / update_config / check_connection /
+get_model_info``).
+
+pydantic-ai is not installable offline, so the agent loop is native:
+  render messages + tool schemas (Llama-3.1 JSON tool calling) -> stream from the
+  backend -> a StreamingToolDetector decides from the first visible characters
+  whether the reply is a tool call (held back) or speech (streamed at once) ->
+  tool calls are parsed (llama3_json / hermes), executed, appended as assistant
+  tool-call + ``ipython`` result messages, and the model is re-prompted, up to
+  ``max_tool_rounds``.
+
+Differences from the reference (Appendix D): multi-turn history is passed as
+real chat messages to the native engine (prefix-cache friendly, Q18; the
+reference's flattened "Previous conversation:" prompt is still available as
+``_build_prompt_with_history`` and is used for remote backends); ``temperature
+= 0`` means greedy (Q5); with ``guided_tool_calls`` (or ``tool_choice=
+"required"``) the tool call is decoded under a JSON-schema token FSM, so even
+random-init weights produce a valid call (BASELINE config 5).
+"""
+from __future__ import annotations
+
+import json
+import logging
+import os
+import re
+from dataclasses import dataclass, field
+from datetime import datetime
+from typing import Any, AsyncGenerator, Dict, List, Optional
+
+from pydantic import BaseModel
+
+from app.agents.tools import Tool, make_search_tool, make_session_tool, make_time_tool
+
+logger = logging.getLogger(__name__)
+
+_TOOL_HINTS = re.compile(r"\b(search|look up|lookup|news|weather|latest|current|today|time|date|"
+                         r"session|google|find)\b", re.I)
+
+
+@dataclass
+class ConversationContext:
+    user_id: str
+    session_id: str
+    conversation_history: List[Dict[str, str]] = field(default_factory=list)
+    language: str = "en"
+    created_at: datetime = field(default_factory=datetime.now)
+    metadata: Dict[str, Any] = field(default_factory=dict)
+
+    def add_message(self, role: str, content: str):
+        self.conversation_history.append({"role": role, "content": content,
+                                          "timestamp": datetime.now().isoformat()})
+
+    def get_recent_messages(self, limit: int = 10) -> List[Dict[str, str]]:
+        return self.conversation_history[-limit:]
+
+
+class AgentConfig(BaseModel):
+    vllm_base_url: str = "http://vllm:8000/v1"
+    vllm_model: str = "hugging-quants/Meta-Llama-3.1-8B-Instruct-AWQ-INT4"
+    vllm_api_key: str = "not-needed"
+    temperature: float = 0.7
+    max_tokens: int = 2048
+    top_p: float = 0.9
+    enable_web_search: bool = True
+    enable_tools: bool = True
+    duckduckgo_rate_limit: float = 1.0
+    system_prompt: str = ("You are a helpful voice assistant for FastTalk. Keep your responses concise "
+                          "and conversational, suitable for speech synthesis. When asked about current "
+                          "events or facts you're unsure about, use web search. Avoid long lists or "
+                          "complex formatting - speak naturally as if in a conversation.")
+    guided_tool_calls: bool = False
+    max_tool_rounds: int = 3
+
+
+@dataclass
+class AgentEvent:
+    text: str = ""
+    num_tokens: int = 0
+    finish_reason: Optional[str] = None
+    prompt_tokens: int = 0
+    cached_tokens: int = 0
+    tool_call: Optional[Dict[str, Any]] = None
+    tool_result: Optional[str] = None
+
+
+class VoiceAgent:
+    def __init__(self, config: Optional[AgentConfig] = None, backend=None):
+        self.config = config or self._load_config_from_env()
+        self.backend = backend
+        self._tools: Optional[Dict[str, Tool]] = None
+        self._custom: Dict[str, Tool] = {}
+        self._active: Dict[str, str] = {}
+
+    def _load_config_from_env(self) -> AgentConfig:
+        e = os.getenv
+        return AgentConfig(
+            vllm_base_url=e("VLLM_BASE_URL", "http://vllm:8000/v1"),
+            vllm_model=e("VLLM_MODEL", AgentConfig().vllm_model),
+            vllm_api_key=e("VLLM_API_KEY", "not-needed"),
+            temperature=float(e("DEFAULT_TEMPERATURE", "0.7")),
+            max_tokens=int(e("DEFAULT_MAX_TOKENS", "2048")),
+            top_p=float(e("DEFAULT_TOP_P", "0.9")),
+            enable_web_search=e("ENABLE_WEB_SEARCH", "true").lower() == "true",
+            enable_tools=e("ENABLE_TOOLS", "true").lower() == "true",
+            duckduckgo_rate_limit=float(e("DUCKDUCKGO_RATE_LIMIT", "1.0")),
+            system_prompt=e("SYSTEM_PROMPT", AgentConfig().system_prompt),
+            guided_tool_calls=e("AGENT_GUIDED_TOOL_CALLS", "false").lower() == "true",
+        )
+
+    # ------------------------------------------------------------------ backend
+    def _get_backend(self):
+        if self.backend is None:
+            from app.core.vllm_handler import VLLMHandler
+
+            self.backend = VLLMHandler(self.config.vllm_base_url, self.config.vllm_model,
+                                       self.config.vllm_api_key)
+        return self.backend
+
+    @property
+    def is_native(self) -> bool:
+        return hasattr(self._get_backend(), "stream_events")
+
+    # ------------------------------------------------------------------ tools
+    def tool(self, fn=None, *, name: Optional[str] = None, description: Optional[str] = None,
+             parameters: Optional[Dict[str, Any]] = None):
+        """Decorator registering a custom tool ``fn(ctx, **kwargs)`` (sync or async)."""
+        def deco(f):
+            t = Tool(name or f.__name__, description or (f.__doc__ or "").strip(),
+                     parameters or {"type": "object", "properties": {}}, f)
+            self._custom[t.name] = t
+            self._tools = None
+            return f
+        return deco(fn) if fn is not None else deco
+
+    def tools(self) -> Dict[str, Tool]:
+        if self._tools is None:
+            tools: Dict[str, Tool] = {}
+            if self.config.enable_tools:
+                if self.config.enable_web_search:
+                    t = make_search_tool(self.config.duckduckgo_rate_limit)
+                    tools[t.name] = t
+                for t in (make_time_tool(), make_session_tool()):
+                    tools[t.name] = t
+                tools.update(self._custom)
+            self._tools = tools
+        return self._tools
+
+    def tool_schemas(self) -> List[Dict[str, Any]]:
+        return [t.schema() for t in self.tools().values()]
+
+    # ------------------------------------------------------------------ prompts
+    def _build_prompt_with_history(self, user_message: str, context: ConversationContext) -> str:
+        """Reference prompt format (last 10 messages flattened), kept for API fidelity."""
+        recent = context.get_recent_messages(limit=10)
+        if not recent:
+            return user_message
+        hist = "\n".join(f"{m['role'].capitalize()}: {m['content']}" for m in recent)
+        return f"Previous conversation:\n{hist}\n\nCurrent message from user: {user_message}"
+
+    def _messages(self, user_message: str, context: ConversationContext) -> List[Dict[str, Any]]:
+        hist = [dict(role=m["role"], content=m["content"]) for m in context.conversation_history]
+        if hist and hist[0]["role"] == "system":
+            system, hist = hist[0]["content"], hist[1:]
+        else:
+            system = self.config.system_prompt
+        return [{"role": "system", "content": system}] + hist + [{"role": "user", "content": user_message}]
+
+    def _wants_tool(self, user_message: str, tool_choice: Optional[str]) -> Optional[str]:
+        if not self.tools():
+            return None
+        if tool_choice in ("required",) or (tool_choice and tool_choice in self.tools()):
+            return tool_choice
+        if tool_choice in (None, "auto") and self.config.guided_tool_calls and \
+                _TOOL_HINTS.search(user_message or ""):
+            return "required"
+        return None
+
+    # ------------------------------------------------------------------ generation
+    async def generate_events(self, user_message: str, context: ConversationContext,
+                              temperature: Optional[float] = None, max_tokens: Optional[int] = None,
+                              top_p: Optional[float] = None, top_k: Optional[int] = None,
+                              stop=None, seed: Optional[int] = None, tool_choice: Optional[str] = None,
+                              ignore_eos: bool = False, min_tokens: int = 0
+                              ) -> AsyncGenerator[AgentEvent, None]:
+        temp = self.config.temperature if temperature is None else temperature
+        mt = self.config.max_tokens if max_tokens is None else max_tokens
+        tp = self.config.top_p if top_p is None else top_p
+        backend = self._get_backend()
+        if not self.is_native:
+            prompt = self._build_prompt_with_history(user_message, context)
+            msgs = [{"role": "system", "content": self.config.system_prompt},
+                    {"role": "user", "content": prompt}]
+            async for text in backend.generate_stream_async(messages=msgs, temperature=temp,
+                                                            max_tokens=mt, top_p=tp,
+                                                            request_id=context.session_id):
+                yield AgentEvent(text=text, num_tokens=1)
+            return
+
+        from fasttalk_llm_microservice_amd.engine.guided import GuidedSpec
+        from fasttalk_llm_microservice_amd.engine.tool_parser import StreamingToolDetector, parse_tool_calls
+
+        messages = self._messages(user_message, context)
+        schemas = self.tool_schemas()
+        force = self._wants_tool(user_message, tool_choice)
+        tools_by_name = self.tools()
+        for rnd in range(self.config.max_tool_rounds + 1):
+            guided = None
+            if force and rnd == 0:
+                pick = [s for s in schemas if force == "required" or s["function"]["name"] == force]
+                guided = GuidedSpec.tool_call(pick or schemas)
+            det = StreamingToolDetector() if (schemas and rnd < self.config.max_tool_rounds) else None
+            held: List[str] = []
+            held_tokens = 0
+            finish = None
+            sid = context.session_id
+            async for out in backend.stream_events(
+                    messages, temperature=temp, max_tokens=mt, top_p=tp, top_k=top_k, stop=stop,
+                    request_id=sid, session_id=sid if (rnd == 0 and guided is None) else None,
+                    tools=schemas or None, guided=guided, seed=seed,
+                    ignore_eos=ignore_eos and guided is None, min_tokens=min_tokens):
+                if out.finished:
+                    finish = out.finish_reason
+                n = len(out.token_ids)
+                if det is None:
+                    if out.text or n:
+                        yield AgentEvent(text=out.text, num_tokens=n,
+                                         prompt_tokens=out.num_prompt_tokens,
+                                         cached_tokens=out.num_cached_tokens)
+                    continue
+                mode, emit = det.feed(out.text)
+                if mode == "text":
+                    if held_tokens:
+                        n += held_tokens
+                        held_tokens = 0
+                    if emit or n:
+                        yield AgentEvent(text=emit, num_tokens=n, prompt_tokens=out.num_prompt_tokens,
+                                         cached_tokens=out.num_cached_tokens)
+                else:
+                    held.append(out.text)
+                    held_tokens += n
+            if det is not None and det.mode != "text":
+                text = det.buf
+                calls, rest = parse_tool_calls(text)
+                calls = [c for c in calls if c.name in tools_by_name]
+                if calls and finish != "abort":
+                    assistant = {"role": "assistant", "content": "",
+                                 "tool_calls": [c.to_openai() for c in calls]}
+                    messages.append(assistant)
+                    for c in calls:
+                        try:
+                            result = await tools_by_name[c.name](context, **c.arguments)
+                        except TypeError as e:
+                            result = f"[Error executing tool: {e}]"
+                        except Exception as e:
+                            result = f"[Error executing tool: {e}]"
+                        yield AgentEvent(num_tokens=held_tokens, tool_call={"name": c.name,
+                                                                            "arguments": c.arguments},
+                                         tool_result=result)
+                        held_tokens = 0
+                        messages.append({"role": "tool", "tool_call_id": c.id, "content": result})
+                    continue
+                # not a valid call: speak what was held back
+                if text or held_tokens:
+                    yield AgentEvent(text=text, num_tokens=held_tokens)
+            yield AgentEvent(finish_reason=finish or "stop")
+            return
+        yield AgentEvent(finish_reason="length")
+
+    async def generate_stream(self, user_message: str, context: ConversationContext,
+                              temperature: Optional[float] = None,
+                              max_tokens: Optional[int] = None) -> AsyncGenerator[str, None]:
+        async for ev in self.generate_events(user_message, context, temperature, max_tokens):
+            if ev.text:
+                yield ev.text
+
+    async def generate(self, user_message: str, context: ConversationContext,
+                       temperature: Optional[float] = None, max_tokens: Optional[int] = None) -> str:
+        return "".join([t async for t in self.generate_stream(user_message, context, temperature,
+                                                             max_tokens)])
+
+    def cancel(self, session_id: str) -> bool:
+        be = self._get_backend()
+        return bool(getattr(be, "cancel_generation", lambda _s: False)(session_id))
+
+    def update_config(self, **kwargs):
+        for k, v in kwargs.items():
+            if hasattr(self.config, k):
+                setattr(self.config, k, v)
+        self._tools = None
+
+    def check_connection(self) -> bool:
+        try:
+            return bool(self._get_backend().check_connection())
+        except Exception as e:
+            logger.error("agent backend check failed: %s", e)
+            return False
+
+    def get_model_info(self) -> Dict[str, Any]:
+        be = self._get_backend()
+        model = getattr(be, "model", self.config.vllm_model)
+        return {
+            "model": model,
+            "base_url": "in-process" if self.is_native else self.config.vllm_base_url,
+            "temperature": self.config.temperature,
+            "max_tokens": self.config.max_tokens,
+            "web_search_enabled": self.config.enable_web_search,
+            "tools_enabled": self.config.enable_tools,
+            "tools": list(self.tools()),
+        }

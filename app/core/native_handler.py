@@ -1,0 +1,268 @@
+"""In-process MI355X engine provider (``LLM_PROVIDER=native``).
+
+``NativeHandler`` exposes the same surface as the reference's ``VLLMHandler``
+(``app/core/vllm_handler.py:24-338``: ``check_connection``, ``get_model_info``,
+``generate_stream``, ``generate_stream_async``, ``cancel_generation``,
+``get_active_requests``) but instead of an HTTP/SSE round trip per token it
+submits to the :class:`AsyncEngine` that runs in this process.
+
+Extras the WS server uses:
+* ``stream_events`` yields engine ``RequestOutput`` objects (engine token
+  counts, time to first token, finish reason);
+* per-session token reuse: a follow-up turn is rendered as
+  ``previous prompt ids + generated ids + <|eot_id|> + new messages``, so the
+  engine's prefix cache matches the whole previous turn even though the
+  assistant text was detokenized (re-tokenizing it would not round-trip);
+* token-aware history truncation to ``max_model_len - max_tokens``
+  (Appendix D Q17): the oldest non-system messages are dropped first.
+"""
+from __future__ import annotations
+
+import asyncio
+import hashlib
+import logging
+import threading
+import time
+from typing import Any, AsyncIterator, Dict, Iterator, List, Optional
+
+from app.utils.error_handler import ErrorCategory, ErrorSeverity, LLMServiceError
+
+logger = logging.getLogger(__name__)
+
+_ENGINE_LOCK = threading.Lock()
+_ENGINES: Dict[str, Any] = {}
+
+
+def engine_config_from_service(config) -> "Any":
+    from fasttalk_llm_microservice_amd.engine.config import EngineConfig
+
+    model = config.resolved_engine_model() if hasattr(config, "resolved_engine_model") else None
+    dev = getattr(config, "compute_device", "auto")
+    device = "cuda" if dev == "cuda" else ("cpu" if dev in ("cpu", "mps") else "auto")
+    cfg = EngineConfig.from_env(model=model)
+    cfg.device = device if cfg.device == "auto" else cfg.device
+    if getattr(config, "engine_weights", None):
+        cfg.weights = config.engine_weights
+    if getattr(config, "engine_max_num_seqs", None):
+        cfg.max_num_seqs = config.engine_max_num_seqs
+    if getattr(config, "engine_max_model_len", None):
+        cfg.max_model_len = config.engine_max_model_len
+    if getattr(config, "engine_gpu_memory_utilization", None):
+        cfg.gpu_memory_utilization = config.engine_gpu_memory_utilization
+    if getattr(config, "engine_tp_size", None):
+        cfg.tp_size = config.engine_tp_size
+    if getattr(config, "engine_dp_size", None):
+        cfg.dp_size = config.engine_dp_size
+    return cfg
+
+
+def get_shared_engine(engine_cfg) -> "Any":
+    """One engine per (model, weights, device) per process."""
+    key = f"{engine_cfg.model}|{engine_cfg.weights}|{engine_cfg.resolved_device()}|{engine_cfg.tp_size}|{engine_cfg.dp_size}"
+    with _ENGINE_LOCK:
+        eng = _ENGINES.get(key)
+        if eng is None:
+            if engine_cfg.dp_size > 1 or engine_cfg.tp_size > 1:
+                from fasttalk_llm_microservice_amd.parallel.dp_router import MultiGPUEngine
+
+                eng = MultiGPUEngine(engine_cfg).start()
+            else:
+                from fasttalk_llm_microservice_amd.engine.engine import AsyncEngine
+
+                eng = AsyncEngine.from_config(engine_cfg).start()
+            _ENGINES[key] = eng
+        return eng
+
+
+def _fingerprint(messages: List[Dict[str, Any]]) -> List[str]:
+    out = []
+    for m in messages:
+        h = hashlib.blake2b(digest_size=12)
+        h.update(str(m.get("role", "")).encode())
+        h.update(b"\x00")
+        h.update(str(m.get("content", "")).encode())
+        out.append(h.hexdigest())
+    return out
+
+
+class _SessionTokens:
+    __slots__ = ("fps", "prompt_ids", "gen_ids", "reply_fp", "tools_fp")
+
+    def __init__(self):
+        self.fps: List[str] = []
+        self.prompt_ids: List[int] = []
+        self.gen_ids: List[int] = []
+        self.reply_fp: Optional[str] = None
+        self.tools_fp: str = ""
+
+
+def _tools_fp(tools) -> str:
+    if not tools:
+        return ""
+    import json as _json
+
+    return hashlib.blake2b(_json.dumps(tools, sort_keys=True, default=str).encode(),
+                           digest_size=12).hexdigest()
+
+
+class NativeHandler:
+    def __init__(self, config=None, engine=None, model: Optional[str] = None,
+                 default_max_tokens: int = 2048):
+        self.config = config
+        if engine is None:
+            engine = get_shared_engine(engine_config_from_service(config))
+        self.engine = engine
+        inner = getattr(engine, "engine", engine)
+        self.tokenizer = inner.tokenizer
+        self.template = inner.template
+        self.max_model_len = inner.max_model_len
+        self.model = model or getattr(inner.model_cfg, "name", "native")
+        self.default_max_tokens = default_max_tokens
+        self._active: Dict[str, str] = {}      # session/request key -> engine request id
+        self._sessions: Dict[str, _SessionTokens] = {}
+        self._lock = threading.Lock()
+        self._seq = 0
+
+    # ------------------------------------------------------------------ health / info
+    def check_connection(self) -> bool:
+        try:
+            return bool(self.engine.is_healthy())
+        except Exception as e:  # pragma: no cover
+            logger.error("engine health check failed: %s", e)
+            return False
+
+    def get_model_info(self) -> Dict[str, Any]:
+        info = dict(self.engine.model_info())
+        return {"models": [self.model], "current_model": self.model, "engine": info}
+
+    def get_active_requests(self) -> Dict[str, Dict[str, Any]]:
+        with self._lock:
+            return {k: {"engine_request_id": v} for k, v in self._active.items()}
+
+    def forget_session(self, session_id: str):
+        with self._lock:
+            self._sessions.pop(session_id, None)
+
+    # ------------------------------------------------------------------ prompt building
+    def build_prompt(self, messages: List[Dict[str, Any]], max_tokens: int,
+                     session_id: Optional[str] = None, tools=None) -> List[int]:
+        budget = max(16, self.max_model_len - max(1, max_tokens) - 1)
+        msgs = list(messages)
+        fps = _fingerprint(msgs)
+        tfp = _tools_fp(tools)
+        st = self._sessions.get(session_id) if session_id else None
+        ids: Optional[List[int]] = None
+        if st is not None and st.reply_fp is not None and st.tools_fp == tfp:
+            prev = st.fps + [st.reply_fp]
+            if len(fps) > len(prev) and fps[: len(prev)] == prev:
+                ids = st.prompt_ids + st.gen_ids + [self.tokenizer.eot_id]
+                for m in msgs[len(prev):]:
+                    ids += self.template.message_ids(m)
+                ids += self.template.generation_prompt()
+        if ids is None or len(ids) > budget:
+            ids = self.template.render(msgs, tools=tools)
+            # token-aware truncation: drop the oldest non-system messages
+            while len(ids) > budget and len(msgs) > 1:
+                drop = 1 if msgs[0].get("role") == "system" else 0
+                if drop >= len(msgs) - 1:
+                    break
+                msgs.pop(drop)
+                ids = self.template.render(msgs, tools=tools)
+            fps = _fingerprint(msgs)
+            if len(ids) > budget:
+                ids = ids[-budget:]
+        if session_id is not None:
+            st = self._sessions.setdefault(session_id, _SessionTokens())
+            st.fps, st.prompt_ids, st.gen_ids, st.reply_fp, st.tools_fp = fps, ids, [], None, tfp
+        return ids
+
+    def _remember_reply(self, session_id: Optional[str], gen_ids: List[int], text: str):
+        if not session_id:
+            return
+        st = self._sessions.get(session_id)
+        if st is None:
+            return
+        st.gen_ids = list(gen_ids)
+        st.reply_fp = _fingerprint([{"role": "assistant", "content": text}])[0]
+
+    # ------------------------------------------------------------------ generation
+    def _params(self, temperature, max_tokens, top_p, top_k=None, stop=None, seed=None,
+                guided=None, ignore_eos=False, min_tokens=0):
+        from fasttalk_llm_microservice_amd.engine.sampling_params import SamplingParams
+
+        return SamplingParams(
+            temperature=0.7 if temperature is None else float(temperature),
+            top_p=1.0 if top_p is None else float(top_p),
+            top_k=0 if top_k in (None, -1) else int(top_k),
+            max_tokens=int(max_tokens or self.default_max_tokens),
+            stop=stop, seed=seed, guided=guided, ignore_eos=ignore_eos, min_tokens=min_tokens)
+
+    async def stream_events(self, messages: List[Dict[str, Any]], temperature: Optional[float] = None,
+                            max_tokens: Optional[int] = None, top_p: Optional[float] = None,
+                            top_k: Optional[int] = None, stop: Optional[List[str]] = None,
+                            request_id: Optional[str] = None, session_id: Optional[str] = None,
+                            prompt_ids: Optional[List[int]] = None, tools=None, guided=None,
+                            seed: Optional[int] = None, ignore_eos: bool = False,
+                            min_tokens: int = 0) -> AsyncIterator[Any]:
+        mt = int(max_tokens or self.default_max_tokens)
+        params = self._params(temperature, mt, top_p, top_k, stop, seed, guided, ignore_eos,
+                              min_tokens)
+        if prompt_ids is None:
+            prompt_ids = self.build_prompt(messages, mt, session_id, tools)
+        key = request_id or session_id or f"native-{time.time_ns()}"
+        with self._lock:
+            self._seq += 1
+            rid = f"{key}#{self._seq}"
+            self._active[key] = rid
+        gen_ids: List[int] = []
+        text_parts: List[str] = []
+        try:
+            async for out in self.engine.generate(prompt_ids, params, request_id=rid):
+                gen_ids.extend(out.token_ids)
+                if out.text:
+                    text_parts.append(out.text)
+                if out.finished and out.finish_reason == "error":
+                    raise LLMServiceError(f"engine error: {out.error}", category=ErrorCategory.PROCESSING,
+                                          severity=ErrorSeverity.HIGH)
+                yield out
+            if session_id and not stop and guided is None:
+                self._remember_reply(session_id, gen_ids, "".join(text_parts))
+        finally:
+            with self._lock:
+                if self._active.get(key) == rid:
+                    del self._active[key]
+
+    async def generate_stream_async(self, messages: List[Dict[str, str]], temperature: Optional[float] = None,
+                                    max_tokens: Optional[int] = None, top_p: Optional[float] = None,
+                                    stop: Optional[List[str]] = None, tools=None,
+                                    request_id: Optional[str] = None, top_k: Optional[int] = None,
+                                    session_id: Optional[str] = None) -> AsyncIterator[str]:
+        async for out in self.stream_events(messages, temperature, max_tokens, top_p, top_k, stop,
+                                            request_id, session_id, tools=tools):
+            if out.text:
+                yield out.text
+
+    def generate_stream(self, messages: List[Dict[str, str]], temperature: Optional[float] = None,
+                        max_tokens: Optional[int] = None, top_p: Optional[float] = None,
+                        stop: Optional[List[str]] = None, tools=None,
+                        request_id: Optional[str] = None, top_k: Optional[int] = None) -> Iterator[str]:
+        """Synchronous iterator (drives a private event loop)."""
+        loop = asyncio.new_event_loop()
+        agen = self.generate_stream_async(messages, temperature, max_tokens, top_p, stop, tools,
+                                          request_id, top_k)
+        try:
+            while True:
+                try:
+                    yield loop.run_until_complete(agen.__anext__())
+                except StopAsyncIteration:
+                    break
+        finally:
+            loop.run_until_complete(agen.aclose())
+            loop.close()
+
+    def cancel_generation(self, request_id: str) -> bool:
+        with self._lock:
+            rid = self._active.get(request_id)
+        if rid is None:
+            return False
+        return bool(self.engine.abort(rid))

@@ -1,0 +1,197 @@
+"""Headline benchmark (BASELINE.json): output tokens/sec per node + p50 TTFT over
+WebSocket, Llama-3-8B, 50 concurrent sessions with conversation history.
+
+One process per GPU (``torchrun --nproc-per-node N``): every rank serves its own
+engine replica (data parallel, weak scaling: 50 sessions per GPU) behind the real
+service stack -- FastAPI ``/ws/llm`` on the aiohttp ASGI transport, the
+session/conversation managers, the native voice agent (default provider path),
+the in-process MI355X engine -- and a load-generator child process drives 50
+WebSocket sessions against it.  A *step* is one conversation turn of every
+session (user message -> streamed reply of ``--gen`` tokens, ``ignore_eos`` so
+every turn has fixed work); history accumulates across warmup and timed turns.
+
+Weights are random-init (no checkpoints offline) with the exact Llama-3-8B
+architecture; prompts are synthetic English.
+
+python bench.py [--gpus N] [--steps K] [--warmup W] [--sessions 50] [--gen 128]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import multiprocessing as mp
+import os
+import socket
+import sys
+import threading
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "bench"))
+
+
+def _free_port(base: int) -> int:
+    for p in range(base, base + 200):
+        with socket.socket() as s:
+            try:
+                s.bind(("127.0.0.1", p))
+                return p
+            except OSError:
+                continue
+    raise RuntimeError("no free port")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=4)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--sessions", type=int, default=50)
+    ap.add_argument("--gen", type=int, default=128)
+    ap.add_argument("--words", type=int, default=40)
+    ap.add_argument("--model", default="llama3-8b")
+    ap.add_argument("--temperature", type=float, default=0.7)
+    ap.add_argument("--top-p", type=float, default=0.9)
+    ap.add_argument("--no-agent", action="store_true", help="direct engine path instead of the agent")
+    ap.add_argument("--port", type=int, default=0)
+    a = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+
+    # ---- load generator child first (before this process touches the GPU) ----------
+    from ws_load import client_process, summarize
+
+    port = a.port or _free_port(18100 + 10 * local_rank)
+    sess_cfg = {"system_prompt": "You are a helpful voice assistant. Keep responses concise and "
+                                 "conversational.",
+                "temperature": a.temperature, "top_p": a.top_p, "max_tokens": a.gen,
+                "ignore_eos": True}
+    ctx = mp.get_context("spawn")
+    parent_conn, child_conn = ctx.Pipe()
+    client = ctx.Process(target=client_process, daemon=True,
+                         args=(child_conn, f"ws://127.0.0.1:{port}/ws/llm", a.sessions, sess_cfg,
+                               a.words, rank))
+    client.start()
+
+    # ---- service stack on this rank's GPU ------------------------------------------
+    os.environ.setdefault("LOG_LEVEL", "WARNING")
+    os.environ["LLM_PROVIDER"] = "native"
+    os.environ["ENGINE_MODEL"] = a.model
+    os.environ["ENABLE_PYDANTIC_AI"] = "false" if a.no_agent else "true"
+    os.environ.setdefault("LLM_MAX_CONNECTIONS", str(max(64, a.sessions + 8)))
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
+    from app.core.websocket_server_vllm import WebSocketLLMServer
+    from app.server.asgi_aiohttp import AiohttpASGIServer
+    from app.utils.config import Config
+
+    t_init = time.time()
+    cfg = Config()
+    cfg.port = port
+    server = WebSocketLLMServer(cfg)
+    engine = server.native_handler.engine
+    # capture the decode graphs the run will use before serving
+    for ml in (256, 512, 1024, 2048, 4096):
+        engine.engine.runner.warmup(batch_sizes=[a.sessions], max_len=ml)
+    import asyncio
+
+    asgi = AiohttpASGIServer(server.app, "127.0.0.1", port)
+    loop = asyncio.new_event_loop()
+    ready = threading.Event()
+
+    def serve():
+        asyncio.set_event_loop(loop)
+        loop.run_until_complete(asgi.start())
+        ready.set()
+        loop.run_forever()
+
+    th = threading.Thread(target=serve, daemon=True, name="asgi")
+    th.start()
+    if not ready.wait(120):
+        raise RuntimeError("server did not start")
+    init_s = time.time() - t_init
+
+    def cmd(c):
+        parent_conn.send(c)
+        r = parent_conn.recv()
+        if not r.get("ok"):
+            raise RuntimeError(f"load client failed: {r.get('error')}")
+        return r.get("result")
+
+    cmd("open")
+    if a.warmup > 0:
+        cmd(("run", a.warmup))
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    barrier()
+    t0 = time.perf_counter()
+    res = cmd(("run", a.steps))
+    barrier()
+    elapsed = time.perf_counter() - t0
+    cmd("close")
+    client.join(timeout=30)
+
+    summ = summarize(res)
+    local = {"tokens": res["tokens"], "elapsed": elapsed, "ttft": res["ttft_s"],
+             "cached": res["cached_prompt_tokens"], "prompt": res["prompt_tokens"]}
+    if world > 1:
+        allr = [None] * world
+        dist.all_gather_object(allr, local)
+    else:
+        allr = [local]
+    tokens = sum(r["tokens"] for r in allr)
+    t_max = max(r["elapsed"] for r in allr)
+    ttfts = sorted(x for r in allr for x in r["ttft"])
+    p = lambda q: ttfts[min(len(ttfts) - 1, int(round(q * (len(ttfts) - 1))))] if ttfts else 0.0  # noqa
+    value = tokens / t_max
+    metrics = engine.engine.metrics()
+    if rank == 0:
+        out = {
+            "metric": "output tokens/sec (node) + p50 TTFT over WebSocket, Llama-3-8B at 50 sessions",
+            "value": round(value, 2),
+            "unit": "tokens/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(1e3 * t_max / a.steps, 2),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (random-init Llama-3-8B weights, synthetic English prompts, "
+                    "synthetic Llama-3 tokenizer)",
+            "config": {"model": "Llama-3-8B", "global_batch": a.sessions * world,
+                       "seq_len": engine.engine.max_model_len, "parallelism": f"dp{world}",
+                       "sessions_per_gpu": a.sessions, "tokens_per_turn": a.gen,
+                       "path": "ws/llm -> " + ("direct engine" if a.no_agent else "voice agent") +
+                               " -> in-process engine"},
+            "p50_ttft_ms": round(1e3 * p(0.5), 2),
+            "p99_ttft_ms": round(1e3 * p(0.99), 2),
+            "per_session_tok_s": round(value / (a.sessions * world), 2),
+            "reference_anchor": "8B single stream ~50-80 tok/s, ~200 ms TTFT on RTX 3090 (README.md:567)",
+            "prefix_cache_hit_tokens": sum(r["cached"] for r in allr),
+            "prompt_tokens": sum(r["prompt"] for r in allr),
+            "engine_decode_step_ms": round(metrics.get("decode_step_ms_avg", 0.0), 3),
+            "init_s": round(init_s, 1),
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    loop.call_soon_threadsafe(loop.stop)
+    engine.shutdown()
+
+
+if __name__ == "__main__":
+    main()

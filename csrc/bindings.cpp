@@ -35,6 +35,19 @@ int ft_sample(int* out_tokens, const void* logits, int logits_is_bf16, long logi
               const uint32_t* allow_mask, int mask_words, hipStream_t stream);
 int ft_kv_block_copy(void* k_cache, void* v_cache, const int* src_dst, int num_pairs,
                      long block_elems, hipStream_t stream);
+int ft_skinny_gemm(const void* x, int x_stride, int M, const void* w, int N, int K, float* ws,
+                   void* out, int out_stride, int splits, int nt, int u, hipStream_t stream);
+int ft_row_rmsnorm(const void* x, int x_stride, const float* ws, int splits, void* out,
+                   int out_stride, void* residual, const void* w, int rows, int hidden, float eps,
+                   hipStream_t stream);
+int ft_slab_silu(const float* ws, int splits, int rows, int inter, void* out, int out_stride,
+                 hipStream_t stream);
+int ft_slab_store(const float* ws, int splits, int rows, int cols, void* out, int out_stride,
+                  hipStream_t stream);
+int ft_slab_rope_kv(const float* ws, int splits, int rows, int cols, void* q_out, int q_stride,
+                    const int* positions, const float* cos_sin, const int* slot_mapping,
+                    void* k_cache, void* v_cache, int nq, int nkv, int head_dim, int block_size,
+                    hipStream_t stream);
 }
 
 namespace {
@@ -236,6 +249,117 @@ void kv_block_copy(at::Tensor k_cache, at::Tensor v_cache, at::Tensor src_dst) {
            "kv_block_copy");
 }
 
+void check_ws(const at::Tensor& ws, int64_t need) {
+  check_dev(ws, "workspace");
+  TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.is_contiguous(), "workspace fp32 contiguous");
+  TORCH_CHECK(ws.numel() >= need, "workspace too small: need ", need, " have ", ws.numel());
+}
+
+// y = x W^T for M <= 64 rows; splits > 1 writes fp32 slabs [splits, M, N] into ws
+void skinny_gemm(at::Tensor x, at::Tensor w, c10::optional<at::Tensor> out,
+                 c10::optional<at::Tensor> ws, int64_t splits, int64_t nt, int64_t u) {
+  check_bf16(x, "x");
+  check_bf16(w, "w");
+  check_rows(x, "x");
+  TORCH_CHECK(w.dim() == 2 && w.is_contiguous(), "w must be contiguous [N, K]");
+  const int M = (int)x.size(0), K = (int)x.size(1), N = (int)w.size(0);
+  TORCH_CHECK(w.size(1) == K, "K mismatch");
+  TORCH_CHECK(M <= 64, "skinny_gemm supports M <= 64");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0, "w alignment");
+  float* wsp = nullptr;
+  void* op = nullptr;
+  int ostride = 0;
+  if (splits > 1) {
+    TORCH_CHECK(ws.has_value(), "splits > 1 needs a workspace");
+    check_ws(*ws, (int64_t)splits * M * N);
+    wsp = ws->data_ptr<float>();
+  } else {
+    TORCH_CHECK(out.has_value(), "splits == 1 needs out");
+    check_bf16(*out, "out");
+    TORCH_CHECK(out->dim() == 2 && out->stride(1) == 1 && out->size(0) >= M && out->size(1) >= N,
+                "out shape");
+    op = out->data_ptr();
+    ostride = (int)out->stride(0);
+  }
+  check_rc(ft_skinny_gemm(x.data_ptr(), (int)x.stride(0), M, w.data_ptr(), N, K, wsp, op, ostride,
+                          (int)splits, (int)nt, (int)u, cur_stream()),
+           "skinny_gemm");
+}
+
+// out = rmsnorm([residual +=] src) * w where src = bf16 x or the fp32 slabs in ws
+void row_rmsnorm(at::Tensor out, c10::optional<at::Tensor> x, c10::optional<at::Tensor> ws,
+                 int64_t splits, c10::optional<at::Tensor> residual, at::Tensor w, int64_t rows,
+                 double eps) {
+  check_bf16(out, "out");
+  check_rows(out, "out");
+  check_bf16(w, "weight");
+  const int hidden = (int)w.numel();
+  TORCH_CHECK(out.size(0) >= rows && out.size(1) == hidden, "out shape");
+  void* rp = nullptr;
+  if (residual.has_value()) {
+    check_bf16(*residual, "residual");
+    TORCH_CHECK(residual->is_contiguous() && residual->size(0) >= rows &&
+                    residual->size(1) == hidden, "residual shape");
+    rp = residual->data_ptr();
+  }
+  if (ws.has_value()) {
+    check_ws(*ws, (int64_t)splits * rows * hidden);
+    check_rc(ft_row_rmsnorm(nullptr, 0, ws->data_ptr<float>(), (int)splits, out.data_ptr(),
+                            (int)out.stride(0), rp, w.data_ptr(), (int)rows, hidden, (float)eps,
+                            cur_stream()), "row_rmsnorm");
+  } else {
+    TORCH_CHECK(x.has_value(), "need x or ws");
+    check_bf16(*x, "x");
+    check_rows(*x, "x");
+    TORCH_CHECK(x->size(0) >= rows && x->size(1) == hidden, "x shape");
+    check_rc(ft_row_rmsnorm(x->data_ptr(), (int)x->stride(0), nullptr, 1, out.data_ptr(),
+                            (int)out.stride(0), rp, w.data_ptr(), (int)rows, hidden, (float)eps,
+                            cur_stream()), "row_rmsnorm");
+  }
+}
+
+void slab_silu(at::Tensor ws, int64_t splits, int64_t rows, int64_t inter, at::Tensor out) {
+  check_ws(ws, splits * rows * 2 * inter);
+  check_bf16(out, "out");
+  check_rows(out, "out");
+  TORCH_CHECK(out.size(0) >= rows && out.size(1) >= inter, "out shape");
+  check_rc(ft_slab_silu(ws.data_ptr<float>(), (int)splits, (int)rows, (int)inter, out.data_ptr(),
+                        (int)out.stride(0), cur_stream()), "slab_silu");
+}
+
+void slab_store(at::Tensor ws, int64_t splits, int64_t rows, int64_t cols, at::Tensor out) {
+  check_ws(ws, splits * rows * cols);
+  check_bf16(out, "out");
+  check_rows(out, "out");
+  TORCH_CHECK(out.size(0) >= rows && out.size(1) >= cols, "out shape");
+  check_rc(ft_slab_store(ws.data_ptr<float>(), (int)splits, (int)rows, (int)cols, out.data_ptr(),
+                         (int)out.stride(0), cur_stream()), "slab_store");
+}
+
+void slab_rope_kv(at::Tensor ws, int64_t splits, int64_t rows, int64_t cols, at::Tensor q_out,
+                  at::Tensor positions, at::Tensor cos_sin, at::Tensor slot_mapping,
+                  at::Tensor k_cache, at::Tensor v_cache, int64_t nq, int64_t nkv,
+                  int64_t head_dim) {
+  check_ws(ws, splits * rows * cols);
+  check_bf16(q_out, "q_out");
+  check_rows(q_out, "q_out");
+  check_i32(positions, "positions");
+  check_i32(slot_mapping, "slot_mapping");
+  TORCH_CHECK(cols == (nq + 2 * nkv) * head_dim, "cols");
+  TORCH_CHECK(q_out.size(0) >= rows && q_out.size(1) >= nq * head_dim, "q_out shape");
+  TORCH_CHECK(cos_sin.scalar_type() == at::kFloat && cos_sin.size(1) == head_dim, "cos_sin");
+  check_bf16(k_cache, "k_cache");
+  check_bf16(v_cache, "v_cache");
+  TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(1) == nkv && k_cache.size(3) == head_dim,
+              "k_cache shape");
+  TORCH_CHECK(positions.numel() >= rows && slot_mapping.numel() >= rows, "metadata length");
+  check_rc(ft_slab_rope_kv(ws.data_ptr<float>(), (int)splits, (int)rows, (int)cols,
+                           q_out.data_ptr(), (int)q_out.stride(0), positions.data_ptr<int>(),
+                           cos_sin.data_ptr<float>(), slot_mapping.data_ptr<int>(),
+                           k_cache.data_ptr(), v_cache.data_ptr(), (int)nq, (int)nkv,
+                           (int)head_dim, (int)k_cache.size(2), cur_stream()), "slab_rope_kv");
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_C, m) {
@@ -252,4 +376,12 @@ PYBIND11_MODULE(_C, m) {
         py::arg("top_p"), py::arg("top_k"), py::arg("seeds"), py::arg("steps"),
         py::arg("mask") = py::none());
   m.def("kv_block_copy", &kv_block_copy);
+  m.def("skinny_gemm", &skinny_gemm, py::arg("x"), py::arg("w"), py::arg("out") = py::none(),
+        py::arg("ws") = py::none(), py::arg("splits") = 1, py::arg("nt") = 1, py::arg("u") = 2);
+  m.def("row_rmsnorm", &row_rmsnorm, py::arg("out"), py::arg("x") = py::none(),
+        py::arg("ws") = py::none(), py::arg("splits") = 1, py::arg("residual") = py::none(),
+        py::arg("w"), py::arg("rows"), py::arg("eps"));
+  m.def("slab_silu", &slab_silu);
+  m.def("slab_store", &slab_store);
+  m.def("slab_rope_kv", &slab_rope_kv);
 }

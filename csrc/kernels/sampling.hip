@@ -1,25 +1,42 @@
 // K12: fused sampler -- constrained-decoding mask, temperature, top-k, top-p
-// (nucleus) and the draw, one workgroup per sequence.  SURVEY.md §2.4 K12.
+// (nucleus) and the draw; one 1024-thread workgroup per sequence.
+// SURVEY.md §2.4 K12.
 //
-// No sort: top-k and top-p thresholds are found with a 4-pass MSB radix select
-// over the order-preserving uint32 image of the logits (8 bits per pass,
-// 256-bin LDS histograms; counts for top-k, probability mass for top-p), then
-// the draw is a Gumbel-max over the surviving tokens with a counter-based RNG
-// (splitmix64 of seed, step, token id), so the sampler is deterministic per
-// (seed, step), needs no host round trip and can live inside the captured
-// decode graph.  temperature == 0 is the greedy argmax fast path (one pass).
-// The optional allow-bitmask (1 bit per vocab id) implements the token-mask
-// FSM of JSON-constrained tool calls (E19).
+// Design (measured: the first version, a 4-pass radix select with LDS-atomic
+// histograms, spent 410 us per 50-row step because every logit of a row lands
+// in one or two MSB bins -> fully serialised LDS atomics):
+//   * every pass streams the row (<= 131072 ids, 256 KiB bf16, L2-resident after
+//     the first pass) with 16-B lane loads as ordered 16-bit keys (bf16 bits
+//     made monotonic); a register-cached variant spilled (128-VGPR cap at 1024
+//     threads) and was slower.
+//   * greedy: one pass, argmax (lowest id on ties).
+//   * top-k: 16-step bisection on the 16-bit key (count >= k).
+//   * sampling: inverse CDF in a fixed (thread, slot) order -- one exp pass
+//     gives per-thread masses, a block scan locates the thread holding the
+//     target mass, that thread walks its 16 chunks.
+//   * top-p: exact rejection -- a drawn token s is accepted iff the mass of
+//     strictly more likely kept tokens is < top_p * Z (i.e. s is in the
+//     nucleus); accepted draws are distributed exactly as the renormalised
+//     nucleus.  Acceptance >= top_p per round, 8 rounds max, then argmax
+//     (always in the nucleus).  Each round costs one pass.
+//   * RNG: splitmix64(seed, step, round) -> one uniform per round per row, so
+//     sampling is reproducible per (seed, step) and graph-capturable.
+//   * allow-bitmask (1 bit / vocab id) implements the JSON token FSM (E19).
 #include "ft_common.h"
 
 namespace ft {
 
 constexpr int kSampThreads = 1024;
 constexpr int kSampWaves = kSampThreads / 64;
+constexpr int kSlots = 128;  // keys per lane -> vocab <= 131072
+constexpr uint32_t kNegInfKey = 0x007Fu;  // ordered key of bf16 -inf (0xFF80)
 
-__device__ __forceinline__ uint32_t f2key(float x) {
-  const uint32_t u = __float_as_uint(x);
-  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+__device__ __forceinline__ uint32_t bf16_to_key(uint32_t b) {
+  return (b & 0x8000u) ? (~b & 0xFFFFu) : (b | 0x8000u);
+}
+__device__ __forceinline__ float key_to_f32(uint32_t k) {
+  const uint32_t b = (k & 0x8000u) ? (k & 0x7FFFu) : (~k & 0xFFFFu);
+  return __uint_as_float(b << 16);
 }
 
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
@@ -29,112 +46,95 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
   return x ^ (x >> 31);
 }
 
-template <typename T>
-__device__ __forceinline__ float load_logit(const T* p, long i);
-template <>
-__device__ __forceinline__ float load_logit<float>(const float* p, long i) { return p[i]; }
-template <>
-__device__ __forceinline__ float load_logit<uint16_t>(const uint16_t* p, long i) {
-  return bf16_to_f32(p[i]);
-}
-
 struct SampShared {
-  float hist_f[256];
-  int hist_i[256];
-  float wred[kSampWaves];
-  int wredi[kSampWaves];
-  uint32_t wkey[kSampWaves];
-  int sel_bin;
-  float sel_rem_f;
-  int sel_rem_i;
+  float f[kSampWaves];
+  int i[kSampWaves];
+  uint32_t u[kSampWaves];
+  float scan[kSampWaves];
+  int winner;
+  int found;
 };
 
-// block-wide max of (value, index) preferring the lower index on ties
-__device__ __forceinline__ void block_argmax(float& v, int& idx, SampShared& sh) {
+__device__ __forceinline__ float block_sum_f(float v, SampShared& sh) {
+  v = wave_sum(v);
+  __syncthreads();
+  if (lane_id() == 0) sh.f[wave_id()] = v;
+  __syncthreads();
+  float t = 0.f;
+#pragma unroll
+  for (int w = 0; w < kSampWaves; ++w) t += sh.f[w];
+  return t;
+}
+
+__device__ __forceinline__ int block_sum_i(int v, SampShared& sh) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  __syncthreads();
+  if (lane_id() == 0) sh.i[wave_id()] = v;
+  __syncthreads();
+  int t = 0;
+#pragma unroll
+  for (int w = 0; w < kSampWaves; ++w) t += sh.i[w];
+  return t;
+}
+
+// max key, lowest index on ties
+__device__ __forceinline__ void block_argmax_key(uint32_t& k, int& idx, SampShared& sh) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
-    const float ov = __shfl_xor(v, o, 64);
+    const uint32_t ok = __shfl_xor(k, o, 64);
     const int oi = __shfl_xor(idx, o, 64);
-    if (ov > v || (ov == v && oi < idx)) {
-      v = ov;
+    if (ok > k || (ok == k && oi < idx)) {
+      k = ok;
       idx = oi;
     }
   }
+  __syncthreads();
   if (lane_id() == 0) {
-    sh.wred[wave_id()] = v;
-    sh.wredi[wave_id()] = idx;
+    sh.u[wave_id()] = k;
+    sh.i[wave_id()] = idx;
   }
   __syncthreads();
-  if (threadIdx.x < 64) {
-    v = threadIdx.x < kSampWaves ? sh.wred[threadIdx.x] : -INFINITY;
-    idx = threadIdx.x < kSampWaves ? sh.wredi[threadIdx.x] : 0x7fffffff;
+  k = sh.u[0];
+  idx = sh.i[0];
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const float ov = __shfl_xor(v, o, 64);
-      const int oi = __shfl_xor(idx, o, 64);
-      if (ov > v || (ov == v && oi < idx)) {
-        v = ov;
-        idx = oi;
-      }
-    }
-    if (threadIdx.x == 0) {
-      sh.wred[0] = v;
-      sh.wredi[0] = idx;
+  for (int w = 1; w < kSampWaves; ++w) {
+    if (sh.u[w] > k || (sh.u[w] == k && sh.i[w] < idx)) {
+      k = sh.u[w];
+      idx = sh.i[w];
     }
   }
-  __syncthreads();
-  v = sh.wred[0];
-  idx = sh.wredi[0];
-  __syncthreads();
 }
 
-__device__ __forceinline__ float block_sum(float v, SampShared& sh) {
-  v = wave_sum(v);
-  if (lane_id() == 0) sh.wred[wave_id()] = v;
-  __syncthreads();
-  if (threadIdx.x < 64) {
-    v = threadIdx.x < kSampWaves ? sh.wred[threadIdx.x] : 0.f;
-    v = wave_sum(v);
-    if (threadIdx.x == 0) sh.wred[0] = v;
+
+// 8 consecutive ids starting at `base` (multiple of 8) as ordered keys; masked
+// or out-of-range ids get the key of -inf
+template <typename T>
+__device__ __forceinline__ void load_keys8(const T* x, const uint32_t* mrow, int base, int vocab,
+                                           uint32_t (&key)[8]) {
+  if (base >= vocab) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) key[j] = kNegInfKey;
+    return;
   }
-  __syncthreads();
-  v = sh.wred[0];
-  __syncthreads();
-  return v;
+  uint32_t bits[8];
+  if constexpr (sizeof(T) == 2) {
+    const uint4 v = *reinterpret_cast<const uint4*>(x + base);
+    bits[0] = v.x & 0xFFFFu; bits[1] = v.x >> 16; bits[2] = v.y & 0xFFFFu; bits[3] = v.y >> 16;
+    bits[4] = v.z & 0xFFFFu; bits[5] = v.z >> 16; bits[6] = v.w & 0xFFFFu; bits[7] = v.w >> 16;
+  } else {
+    const float4 a = *reinterpret_cast<const float4*>(x + base);
+    const float4 c = *reinterpret_cast<const float4*>(x + base + 4);
+    bits[0] = f32_to_bf16(a.x); bits[1] = f32_to_bf16(a.y); bits[2] = f32_to_bf16(a.z);
+    bits[3] = f32_to_bf16(a.w); bits[4] = f32_to_bf16(c.x); bits[5] = f32_to_bf16(c.y);
+    bits[6] = f32_to_bf16(c.z); bits[7] = f32_to_bf16(c.w);
+  }
+  const uint32_t mb = mrow ? (mrow[base >> 5] >> (base & 31)) : 0xFFu;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) key[j] = ((mb >> j) & 1u) ? bf16_to_key(bits[j]) : kNegInfKey;
 }
 
-// Given a 256-bin histogram (counts or mass), walk bins from the top (255) and
-// select the bin where the running total first reaches `rem`.  Threads 0..255
-// participate: an inclusive scan over descending bins.
-template <typename V>
-__device__ __forceinline__ void select_bin(V* hist, V rem, SampShared& sh, int* out_bin,
-                                           V* out_rem) {
-  const int t = threadIdx.x;
-  V val = (t < 256) ? hist[255 - t] : V(0);
-  // wave inclusive scan
-  V inc = val;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const V y = __shfl_up(inc, o, 64);
-    if (lane_id() >= o) inc += y;
-  }
-  __shared__ V wtot[4];
-  if (t < 256 && lane_id() == 63) wtot[wave_id()] = inc;
-  __syncthreads();
-  if (t < 256) {
-    V off = V(0);
-    for (int w = 0; w < wave_id(); ++w) off += wtot[w];
-    inc += off;
-    const V exc = inc - val;
-    // the first descending bin whose inclusive total reaches rem
-    const bool hit = (inc >= rem) && (exc < rem);
-    if (hit) {
-      *out_bin = 255 - t;
-      *out_rem = rem - exc;
-    }
-  }
-  __syncthreads();
-}
+constexpr int kChunks = kSlots / 8;  // 16 chunks of 8 ids per lane
 
 template <typename T>
 __global__ __launch_bounds__(kSampThreads) void sample_kernel(
@@ -143,125 +143,189 @@ __global__ __launch_bounds__(kSampThreads) void sample_kernel(
     const int* __restrict__ top_k, const long long* __restrict__ seeds,
     const int* __restrict__ steps, const uint32_t* __restrict__ allow_mask, int mask_words) {
   __shared__ SampShared sh;
+  __shared__ float chunk_mass[kChunks * kSampThreads];  // 64 KiB
   const int row = blockIdx.x;
+  const int tid = threadIdx.x;
   const T* x = logits + (long)row * logit_stride;
   const uint32_t* mrow = allow_mask ? allow_mask + (long)row * mask_words : nullptr;
-  auto masked = [&](int i) -> bool { return mrow && !((mrow[i >> 5] >> (i & 31)) & 1u); };
+  auto chunk_base = [&](int c) { return (tid + c * kSampThreads) * 8; };
 
-  // ---- pass 1: max / argmax --------------------------------------------------------
-  float best = -INFINITY;
+  // ---- pass 1: argmax (exact on fp32 input, bf16 keys otherwise) ----------------------
+  uint32_t bestk = 0u;
   int besti = 0x7fffffff;
-  for (int i = threadIdx.x; i < vocab; i += kSampThreads) {
-    float v = load_logit<T>(x, i);
-    if (masked(i)) v = -INFINITY;
-    if (v > best) {
-      best = v;
-      besti = i;
+  if constexpr (sizeof(T) == 4) {
+    uint32_t best32 = 0u;
+#pragma unroll 4
+    for (int c = 0; c < kChunks; ++c) {
+      const int base = chunk_base(c);
+      if (base >= vocab) continue;
+      const uint32_t mb = mrow ? (mrow[base >> 5] >> (base & 31)) : 0xFFu;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t u = __float_as_uint(x[base + j]);
+        const uint32_t k32 = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+        if (((mb >> j) & 1u) && k32 > best32) {
+          best32 = k32;
+          besti = base + j;
+        }
+      }
     }
+    block_argmax_key(best32, besti, sh);
+    const uint32_t bits = (best32 & 0x80000000u) ? (best32 & 0x7fffffffu) : ~best32;
+    bestk = bf16_to_key(f32_to_bf16(__uint_as_float(bits)));
+  } else {
+#pragma unroll 4
+    for (int c = 0; c < kChunks; ++c) {
+      uint32_t key[8];
+      load_keys8<T>(x, mrow, chunk_base(c), vocab, key);
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (key[j] > bestk) {
+          bestk = key[j];
+          besti = chunk_base(c) + j;
+        }
+    }
+    block_argmax_key(bestk, besti, sh);
   }
-  block_argmax(best, besti, sh);
   const float temp = temperature[row];
-  if (temp <= 0.f || best == -INFINITY) {
-    if (threadIdx.x == 0) out_tokens[row] = (besti == 0x7fffffff) ? 0 : besti;
+  if (temp <= 0.f || besti == 0x7fffffff || bestk <= kNegInfKey) {
+    if (tid == 0) out_tokens[row] = (besti == 0x7fffffff) ? 0 : besti;
     return;
   }
-  const float inv_t = 1.f / temp;
-  const float M = best;
+  const float M = key_to_f32(bestk);
+  const float cexp = 1.4426950408889634f / temp;  // exp(z) = exp2((x - M) * cexp)
 
-  // ---- top-k threshold (radix select on count) ----------------------------------------
-  uint32_t thr = 0u;  // keep keys >= thr
+  // ---- top-k: 16-step bisection on the key ------------------------------------------
+  uint32_t thr = kNegInfKey + 1u;  // keep keys >= thr (drops masked / -inf)
   const int k = top_k[row];
   if (k > 0 && k < vocab) {
-    uint32_t prefix = 0u, pmask = 0u;
-    int rem = k;
-    for (int pass = 0; pass < 4; ++pass) {
-      const int shift = 24 - 8 * pass;
-      if (threadIdx.x < 256) sh.hist_i[threadIdx.x] = 0;
-      __syncthreads();
-      for (int i = threadIdx.x; i < vocab; i += kSampThreads) {
-        if (masked(i)) continue;
-        const uint32_t key = f2key(load_logit<T>(x, i));
-        if ((key & pmask) == prefix) atomicAdd(&sh.hist_i[(key >> shift) & 255u], 1);
+    uint32_t lo = 0u, hi = 0x10000u;
+    while (hi - lo > 1u) {
+      const uint32_t mid = (lo + hi) >> 1;
+      int cnt = 0;
+#pragma unroll 8
+      for (int c = 0; c < kChunks; ++c) {
+        uint32_t key[8];
+        load_keys8<T>(x, mrow, chunk_base(c), vocab, key);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) cnt += key[j] >= mid ? 1 : 0;
       }
-      __syncthreads();
-      select_bin<int>(sh.hist_i, rem, sh, &sh.sel_bin, &sh.sel_rem_i);
-      const int bin = sh.sel_bin;
-      rem = sh.sel_rem_i;
-      prefix |= (uint32_t)bin << shift;
-      pmask |= 255u << shift;
-      __syncthreads();
+      cnt = block_sum_i(cnt, sh);
+      if (cnt >= k) lo = mid; else hi = mid;
     }
-    thr = prefix;
+    if (lo > thr) thr = lo;
   }
 
-  // ---- top-p threshold (radix select on probability mass) ----------------------------
+  // ---- per-chunk masses of kept tokens (LDS), per-thread totals -------------------------
+  float mass = 0.f;
+#pragma unroll 8
+  for (int c = 0; c < kChunks; ++c) {
+    uint32_t key[8];
+    load_keys8<T>(x, mrow, chunk_base(c), vocab, key);
+    float cm = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) cm += key[j] >= thr ? exp2f((key_to_f32(key[j]) - M) * cexp) : 0.f;
+    chunk_mass[c * kSampThreads + tid] = cm;
+    mass += cm;
+  }
+  // block exclusive scan of per-thread masses
+  float incl = mass;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const float y = __shfl_up(incl, o, 64);
+    if (lane_id() >= o) incl += y;
+  }
+  __syncthreads();
+  if (lane_id() == 63) sh.scan[wave_id()] = incl;
+  __syncthreads();
+  float wbase = 0.f, Z = 0.f;
+#pragma unroll
+  for (int w = 0; w < kSampWaves; ++w) {
+    const float t = sh.scan[w];
+    if (w < wave_id()) wbase += t;
+    Z += t;
+  }
+  const float excl = wbase + incl - mass;
+
   const float tp = top_p[row];
-  if (tp < 1.f) {
-    float tot = 0.f;
-    for (int i = threadIdx.x; i < vocab; i += kSampThreads) {
-      if (masked(i)) continue;
-      const float v = load_logit<T>(x, i);
-      if (f2key(v) >= thr) tot += __expf((v - M) * inv_t);
-    }
-    tot = block_sum(tot, sh);
-    float rem = tp * tot;
-    uint32_t prefix = 0u, pmask = 0u;
-    for (int pass = 0; pass < 4; ++pass) {
-      const int shift = 24 - 8 * pass;
-      if (threadIdx.x < 256) sh.hist_f[threadIdx.x] = 0.f;
-      __syncthreads();
-      for (int i = threadIdx.x; i < vocab; i += kSampThreads) {
-        if (masked(i)) continue;
-        const float v = load_logit<T>(x, i);
-        const uint32_t key = f2key(v);
-        if (key >= thr && (key & pmask) == prefix)
-          atomicAdd(&sh.hist_f[(key >> shift) & 255u], __expf((v - M) * inv_t));
-      }
-      __syncthreads();
-      sh.sel_bin = -1;
-      __syncthreads();
-      select_bin<float>(sh.hist_f, rem, sh, &sh.sel_bin, &sh.sel_rem_f);
-      int bin = sh.sel_bin;
-      if (bin < 0) {
-        // rounding: rem slightly above the histogram total -> take the lowest
-        // non-empty bin so the whole remaining mass is kept
-        bin = 0;
-        if (threadIdx.x == 0) {
-          for (int j = 0; j < 256; ++j)
-            if (sh.hist_f[j] > 0.f) { sh.sel_bin = j; break; }
+  const uint64_t s0 =
+      splitmix64((uint64_t)seeds[row] ^ (0x632BE59BD9B4E019ull * (uint64_t)(steps[row] + 1)));
+  int chosen = besti;
+  const int rounds = (tp < 1.f) ? 8 : 1;
+  for (int r = 0; r < rounds; ++r) {
+    const uint64_t h = splitmix64(s0 + (uint64_t)r * 0xD1B54A32D192ED03ull);
+    const float u = ((float)(h >> 40) + 0.5f) * (1.0f / 16777216.0f);
+    const float target = u * Z;
+    __syncthreads();
+    if (tid == 0) sh.found = 0;
+    __syncthreads();
+    // the thread whose [excl, excl + mass) holds the target walks its chunks
+    const bool mine = (target >= excl && target < excl + mass) ||
+                      (tid == kSampThreads - 1 && target >= excl + mass && mass > 0.f);
+    if (mine) {
+      // locate the chunk from the LDS chunk masses, then the id inside it
+      float acc = excl;
+      int cc = -1, lastc = -1;
+      for (int c = 0; c < kChunks; ++c) {
+        const float cm = chunk_mass[c * kSampThreads + tid];
+        if (cm > 0.f) {
+          lastc = c;
+          if (acc + cm > target) {
+            cc = c;
+            break;
+          }
+          acc += cm;
         }
-        __syncthreads();
-        bin = sh.sel_bin < 0 ? 0 : sh.sel_bin;
-        rem = 0.f;
-      } else {
-        rem = sh.sel_rem_f;
       }
-      prefix |= (uint32_t)bin << shift;
-      pmask |= 255u << shift;
-      __syncthreads();
+      if (cc < 0) {
+        cc = lastc;
+        acc = target;  // rounding tail: take the last kept id of the last chunk
+      }
+      int pick = -1;
+      if (cc >= 0) {
+        uint32_t key[8];
+        load_keys8<T>(x, mrow, chunk_base(cc), vocab, key);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          if (key[j] >= thr) {
+            const float pj = exp2f((key_to_f32(key[j]) - M) * cexp);
+            pick = chunk_base(cc) + j;
+            if (acc + pj > target) break;
+            acc += pj;
+          }
+        }
+      }
+      if (pick >= 0 && atomicCAS(&sh.found, 0, 1) == 0) sh.winner = pick;
     }
-    if (prefix > thr) thr = prefix;
-  }
-
-  // ---- Gumbel-max draw over survivors --------------------------------------------------
-  const uint64_t s0 = splitmix64((uint64_t)seeds[row] ^ (0x632BE59BD9B4E019ull * (uint64_t)(steps[row] + 1)));
-  float gbest = -INFINITY;
-  int gi = 0x7fffffff;
-  for (int i = threadIdx.x; i < vocab; i += kSampThreads) {
-    if (masked(i)) continue;
-    const float v = load_logit<T>(x, i);
-    if (f2key(v) < thr) continue;
-    const uint64_t h = splitmix64(s0 + (uint64_t)i);
-    const float u = ((float)(h >> 40) + 0.5f) * (1.0f / 16777216.0f);  // (0,1)
-    const float g = -__logf(-__logf(u));
-    const float sc = (v - M) * inv_t + g;
-    if (sc > gbest) {
-      gbest = sc;
-      gi = i;
+    __syncthreads();
+    const int s = sh.found ? sh.winner : besti;
+    if (tp >= 1.f) {
+      chosen = s;
+      break;
+    }
+    // nucleus membership: mass of strictly more likely kept tokens < top_p * Z
+    uint32_t ks;
+    {
+      uint32_t key[8];
+      load_keys8<T>(x, mrow, s & ~7, vocab, key);
+      ks = key[s & 7];
+    }
+    float above = 0.f;
+#pragma unroll 8
+    for (int c = 0; c < kChunks; ++c) {
+      uint32_t key[8];
+      load_keys8<T>(x, mrow, chunk_base(c), vocab, key);
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        above += (key[j] > ks && key[j] >= thr) ? exp2f((key_to_f32(key[j]) - M) * cexp) : 0.f;
+    }
+    above = block_sum_f(above, sh);
+    if (above < tp * Z) {
+      chosen = s;
+      break;
     }
   }
-  block_argmax(gbest, gi, sh);
-  if (threadIdx.x == 0) out_tokens[row] = (gi == 0x7fffffff) ? besti : gi;
+  if (tid == 0) out_tokens[row] = chosen;
 }
 
 }  // namespace ft
@@ -271,6 +335,8 @@ extern "C" int ft_sample(int* out_tokens, const void* logits, int logits_is_bf16
                          const int* top_k, const long long* seeds, const int* steps,
                          const uint32_t* allow_mask, int mask_words, hipStream_t stream) {
   if (batch <= 0) return 0;
+  if (vocab > ft::kSlots * ft::kSampThreads) return -3;
+  if (vocab % 8 != 0 || logit_stride % 8 != 0) return -4;
   dim3 grid(batch), block(ft::kSampThreads);
   if (logits_is_bf16) {
     hipLaunchKernelGGL(ft::sample_kernel<uint16_t>, grid, block, 0, stream, out_tokens,

@@ -61,7 +61,10 @@ def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, out: Optional[torch.Te
     if x.is_cuda:
         if out is None:
             out = torch.empty_like(x)
-        native().rmsnorm(out, x, w, eps)
+        if x.shape[1] % 2048 == 0:
+            native().row_rmsnorm(out, x, None, 1, None, w, x.shape[0], eps)
+        else:
+            native().rmsnorm(out, x, w, eps)
         return out
     r = ref.rmsnorm(x, w, eps)
     if out is not None:
@@ -73,7 +76,10 @@ def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, out: Optional[torch.Te
 def fused_add_rmsnorm(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, eps: float):
     """residual <- x + residual;  x <- rmsnorm(residual) * w   (both in place)."""
     if x.is_cuda:
-        native().fused_add_rmsnorm(x, x, residual, w, eps)
+        if x.shape[1] % 2048 == 0:
+            native().row_rmsnorm(x, x, None, 1, residual, w, x.shape[0], eps)
+        else:
+            native().fused_add_rmsnorm(x, x, residual, w, eps)
         return x, residual
     y, r = ref.fused_add_rmsnorm(x, residual, w, eps)
     residual.copy_(r)
@@ -177,3 +183,45 @@ def kv_block_copy(k_cache, v_cache, pairs: torch.Tensor):
         p = pairs.view(-1, 2).long()
         k_cache[p[:, 1]] = k_cache[p[:, 0]]
         v_cache[p[:, 1]] = v_cache[p[:, 0]]
+
+
+# ---------------------------------------------------------------------------------
+# decode-shape (M <= 64) weight-streaming GEMM + fused row epilogues
+# ---------------------------------------------------------------------------------
+
+SKINNY_CONFIGS = [(1, 2), (1, 4), (2, 2), (2, 4), (4, 1), (4, 2)]  # (nt, u) instantiated
+
+
+def skinny_gemm_supported(m: int, n: int, k: int) -> bool:
+    return 0 < m <= 64 and n % 16 == 0 and k % 128 == 0
+
+
+def skinny_gemm(x, w, out=None, ws=None, splits: int = 1, nt: int = 1, u: int = 2):
+    """y = x w^T (M <= 64).  splits > 1 leaves fp32 partial slabs in ``ws``
+    ([splits, M, N]) for a fused epilogue; otherwise writes bf16 ``out``."""
+    if splits == 1 and out is None:
+        out = torch.empty(x.shape[0], w.shape[0], dtype=x.dtype, device=x.device)
+    native().skinny_gemm(x, w, out, ws, splits, nt, u)
+    return out if splits == 1 else ws
+
+
+def row_rmsnorm(out, w, eps, rows, x=None, ws=None, splits=1, residual=None):
+    native().row_rmsnorm(out, x, ws, splits, residual, w, rows, eps)
+    return out
+
+
+def slab_silu(ws, splits, rows, inter, out):
+    native().slab_silu(ws, splits, rows, inter, out)
+    return out
+
+
+def slab_store(ws, splits, rows, cols, out):
+    native().slab_store(ws, splits, rows, cols, out)
+    return out
+
+
+def slab_rope_kv(ws, splits, rows, cols, q_out, positions, cos_sin, slot_mapping, k_cache,
+                 v_cache, nq, nkv, head_dim):
+    native().slab_rope_kv(ws, splits, rows, cols, q_out, positions, cos_sin, slot_mapping,
+                          k_cache, v_cache, nq, nkv, head_dim)
+    return q_out
