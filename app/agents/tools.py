@@ -87,8 +87,8 @@ def make_search_tool(rate_limit: float = 1.0, backend: Optional[str] = None) -> 
 
     async def duckduckgo_search(ctx, query: str, max_results: int = 5) -> str:
         max_results = max(1, min(int(max_results or 5), 10))
-        await limiter.wait()
         if backend == "duckduckgo":
+            await limiter.wait()  # only the live endpoint is rate limited
             try:
                 results = await _duckduckgo_html(query, max_results)
             except Exception as e:  # offline or blocked: degrade to the stub

@@ -123,7 +123,9 @@ class Config:
         "ENGINE_MAX_MODEL_LEN", _e("VLLM_MAX_MODEL_LEN", "8192"))))
     engine_gpu_memory_utilization: float = field(default_factory=lambda: float(_e(
         "ENGINE_GPU_MEMORY_UTILIZATION", _e("VLLM_GPU_MEMORY_UTILIZATION", "0.90"))))
-    agent_json_tool_calls: bool = field(default_factory=lambda: _flag("AGENT_GUIDED_TOOL_CALLS"))
+    # opt-in: decode agent tool calls under the JSON-schema token FSM when the user
+    # message asks for search / time / session info (BASELINE config 5)
+    agent_json_tool_calls: bool = field(default_factory=lambda: _flag("AGENT_GUIDED_TOOL_CALLS", "false"))
 
     def __post_init__(self):
         self._validate()

@@ -98,8 +98,7 @@ def main():
     server = WebSocketLLMServer(cfg)
     engine = server.native_handler.engine
     # capture the decode graphs the run will use before serving
-    for ml in (256, 512, 1024, 2048, 4096):
-        engine.engine.runner.warmup(batch_sizes=[a.sessions], max_len=ml)
+    engine.engine.runner.warmup([b for b in engine.engine.runner.graph_sizes if b <= 2 * a.sessions])
     import asyncio
 
     asgi = AiohttpASGIServer(server.app, "127.0.0.1", port)
@@ -183,6 +182,8 @@ def main():
             "prefix_cache_hit_tokens": sum(r["cached"] for r in allr),
             "prompt_tokens": sum(r["prompt"] for r in allr),
             "engine_decode_step_ms": round(metrics.get("decode_step_ms_avg", 0.0), 3),
+            "engine_decode_batch_avg": round(metrics.get("decode_batch_avg", 0.0), 2),
+            "engine_runner": metrics.get("runner", {}),
             "init_s": round(init_s, 1),
         }
         print(json.dumps(out), flush=True)

@@ -3,9 +3,14 @@
 //
 // Decode attention is an HBM stream over the KV cache (4 KiB per token per layer
 // for Llama-3-8B), so the design goal is bytes in flight, not FLOPs:
-//   * grid = (seq * kv_head, split); a workgroup owns PART=256 context tokens of
-//     ONE kv head and computes all G = nq/nkv query heads of that group against
-//     them, so every K/V byte is read once per step (GQA packing).
+//   * grid = (seq * kv_head, split); split s of a sequence of length L owns
+//     the token range [s*P, (s+1)*P) with P = roundup16(ceil(L / splits)) <= 1024,
+//     i.e. every sequence is cut into `splits` near-equal partitions whatever its
+//     length, so the grid depends only on (batch bucket, splits) and ONE hipGraph
+//     per batch bucket covers every context length up to max_model_len (an
+//     earlier power-of-two split bucket forced lazy re-captures mid-serving).
+//     A workgroup computes all G = nq/nkv query heads of its kv head against its
+//     partition, so every K/V byte is read once per step (GQA packing).
 //   * 4 waves; D/8 lanes share a token (16 lanes at D=128 -> 4 tokens per wave
 //     instruction, 1 KiB per wave instruction), each lane owns 8 head dims and
 //     keeps its 8*G query values in registers for the whole partition.
@@ -17,13 +22,16 @@
 //   * partitions write unnormalised fp32 partials + (max, sum); the combine
 //     kernel rescales.  A sequence that fits one partition writes bf16 output
 //     directly and the combine kernel skips it.
-// The grid's split dimension is a fixed bucket (max_splits) so the launch can be
-// captured in a hipGraph; partitions past a sequence's length exit immediately.
 #include "ft_common.h"
 
 namespace ft {
 
-constexpr int kDecodePart = 256;
+constexpr int kMaxPart = 1024;  // LDS score buffer per (head, partition)
+
+__device__ __forceinline__ int decode_part(int L, int splits) {
+  const int p = (L + splits - 1) / splits;
+  return max(16, (p + 15) & ~15);
+}
 
 template <int D, int G>
 __global__ __launch_bounds__(256) void paged_decode_kernel(
@@ -36,9 +44,7 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(
   constexpr int TPW = 64 / LPT;     // tokens per wave instruction
   constexpr int TPB = 4 * TPW;      // tokens per workgroup iteration
   constexpr int U = 4;              // iterations issued together
-  constexpr int PART = kDecodePart;
-
-  __shared__ float s_p[G][PART];
+  __shared__ float s_p[G][kMaxPart];
   __shared__ float s_red[4][G][D];
   __shared__ float s_m[G], s_l[G];
 
@@ -46,9 +52,10 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(
   const int kvh = blockIdx.x - b * nkv;
   const int split = blockIdx.y;
   const int L = seq_lens[b];
+  const int PART = decode_part(L, max_splits);
   const int start = split * PART;
   if (start >= L) return;
-  const int n = min(L - start, PART);
+  const int n = min(min(L - start, PART), kMaxPart);  // host guarantees PART <= kMaxPart
   const int nsplit = (L + PART - 1) / PART;
   const int nq = nkv * G;
 
@@ -203,7 +210,8 @@ __global__ __launch_bounds__(D) void paged_decode_combine_kernel(
     const float* __restrict__ tmp_ml, const int* __restrict__ seq_lens, int nq, int max_splits) {
   const int b = blockIdx.x, h = blockIdx.y, d = threadIdx.x;
   const int L = seq_lens[b];
-  const int ns = (L + kDecodePart - 1) / kDecodePart;
+  const int part = decode_part(L, max_splits);
+  const int ns = (L + part - 1) / part;
   if (ns <= 1) return;
   const size_t base = ((size_t)b * nq + h) * max_splits;
   float M = -INFINITY;
@@ -219,7 +227,8 @@ __global__ __launch_bounds__(D) void paged_decode_combine_kernel(
 
 }  // namespace ft
 
-extern "C" int ft_decode_partition_size() { return ft::kDecodePart; }
+// max tokens one decode partition may hold: splits must be >= ceil(max_len / this)
+extern "C" int ft_decode_partition_size() { return ft::kMaxPart; }
 
 extern "C" int ft_paged_decode_attention(void* out, int out_stride, float* tmp_out, float* tmp_ml,
                                          const void* q, int q_stride, const void* k_cache,
@@ -229,6 +238,7 @@ extern "C" int ft_paged_decode_attention(void* out, int out_stride, float* tmp_o
                                          float scale, hipStream_t stream) {
   if (batch <= 0) return 0;
   if (nq % nkv != 0) return -1;
+  if (max_splits < 1) return -3;
   const int G = nq / nkv;
   dim3 grid(batch * nkv, max_splits), block(256);
 #define FT_DEC_CASE(DD, GG)                                                                   \

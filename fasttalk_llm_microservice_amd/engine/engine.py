@@ -117,13 +117,13 @@ class LLMEngine:
         t0 = time.perf_counter()
         outs: List[RequestOutput] = []
         # sequences the scheduler had to reject (cannot fit in the KV pool)
-        for s, n in zip(batch.seqs, batch.num_tokens):
-            if n == 0 and s.status == SeqStatus.FINISHED and s.finish_reason == "error":
-                self.scheduler.by_id.pop(s.request_id, None)
-                outs.append(self._finalize(s, "error", emit=True,
-                                           error="prompt does not fit in the KV cache"))
-        sampled_seqs = [s for s, n, sm in zip(batch.seqs, batch.num_tokens, batch.sample)
-                        if n > 0 and sm]
+        for s in batch.rejected:
+            self.scheduler.by_id.pop(s.request_id, None)
+            outs.append(self._finalize(s, "error", emit=True,
+                                       error="prompt does not fit in the KV cache"))
+        if not batch.decode_seqs and not batch.prefill_seqs:
+            return outs
+        sampled_seqs = batch.sampled_seqs()
         masks = self._masks_for(sampled_seqs)
         toks = self.runner.execute(batch, masks)
         self.scheduler.post_step(batch)
@@ -132,11 +132,10 @@ class LLMEngine:
             if o is not None:
                 outs.append(o)
         dt = time.perf_counter() - t0
-        self.step_times.append((batch.is_prefill, len(batch.seqs), batch.total_tokens, dt))
-        self.stats["prefill_steps" if batch.is_prefill else "decode_steps"] += 1
+        self.step_times.append((batch.has_prefill, len(batch.decode_seqs), batch.total_tokens, dt))
+        self.stats["mixed_steps" if batch.has_prefill else "decode_steps"] += 1
         self.stats["generated_tokens"] += len(sampled_seqs)
-        if batch.is_prefill:
-            self.stats["prefill_tokens"] += batch.total_tokens
+        self.stats["prefill_tokens"] += sum(batch.prefill_tokens)
         self.last_step_end = time.time()
         return outs
 
@@ -304,6 +303,12 @@ class AsyncEngine:
 
     # ------------------------------------------------------------------ lifecycle
     def start(self):
+        # the engine thread and the asyncio (WebSocket) thread share the GIL: a short
+        # switch interval keeps token frames flowing while the engine runs Python
+        import sys
+
+        if sys.getswitchinterval() > 0.001:
+            sys.setswitchinterval(0.001)
         if self._thread is None:
             self._thread = threading.Thread(target=self._run, name="fasttalk-engine", daemon=True)
             self._thread.start()

@@ -59,8 +59,6 @@ class ModelRunner:
 
         self.num_blocks = self._decide_num_blocks()
         self.kv = self.model.allocate_kv_cache(self.num_blocks, self.bs)
-        self.part = ops.decode_partition_size()
-        self.max_splits_cap = _pow2_ceil(math.ceil(self.max_model_len / self.part))
         nq, d = self.model.nq, self.model.d
 
         # -------- static decode buffers (graph inputs) --------
@@ -94,14 +92,17 @@ class ModelRunner:
         self.d_out = torch.zeros(mb, dtype=i32, device=dv)
         self.h_out = torch.zeros(mb, dtype=i32, pin_memory=pin)
         self.d_logits_idx = torch.arange(mb, dtype=torch.int64, device=dv)
-        self.tmp_out = torch.empty(mb * nq * self.max_splits_cap * d, dtype=torch.float32, device=dv)
-        self.tmp_ml = torch.empty(mb * nq * self.max_splits_cap * 2, dtype=torch.float32, device=dv)
+        # split-K workspace sized for the largest (batch x splits) any bucket uses
+        rows = max(b * self._splits_for_batch(b) for b in self.graph_sizes + [mb])
+        self.tmp_rows = rows
+        self.tmp_out = torch.empty(rows * nq * d, dtype=torch.float32, device=dv)
+        self.tmp_ml = torch.empty(rows * nq * 2, dtype=torch.float32, device=dv)
         self._hs = self.h_small.numpy()
         self._hbt = self.h_bt.numpy()
         self._hf = self.h_f32.numpy()
         self._hseed = self.h_seeds.numpy()
         self._done_event = torch.cuda.Event() if self.is_gpu else None
-        self.graphs: Dict[Tuple[int, int], torch.cuda.CUDAGraph] = {}
+        self.graphs: Dict[int, torch.cuda.CUDAGraph] = {}
         self.graph_pool = None
         self.use_graphs = self.is_gpu and not cfg.enforce_eager
         self.stats = {"graph_replays": 0, "eager_decode": 0, "prefill_steps": 0, "captures": 0}
@@ -126,8 +127,8 @@ class ModelRunner:
         return n
 
     # ------------------------------------------------------------------ helpers
-    def _splits_for(self, max_len: int) -> int:
-        return min(self.max_splits_cap, _pow2_ceil(math.ceil(max_len / self.part)))
+    def _splits_for_batch(self, b: int) -> int:
+        return ops.decode_splits(b, self.model.nkv, self.max_model_len)
 
     def _bucket(self, b: int) -> Optional[int]:
         for s in self.graph_sizes:
@@ -138,10 +139,14 @@ class ModelRunner:
     # ------------------------------------------------------------------ execution
     @torch.inference_mode()
     def execute(self, batch: ScheduledBatch, masks: Optional[np.ndarray] = None) -> List[int]:
-        """Runs one step; returns sampled ids for sequences with ``sample=True``
-        (in batch order)."""
-        if batch.is_prefill:
-            return self._prefill(batch, masks)
+        """Runs one step; returns sampled ids for ``batch.sampled_seqs()`` in order.
+
+        Decode-only steps replay a hipGraph; steps that carry prefill chunks run
+        eagerly as one mixed forward pass (decode rows first)."""
+        if batch.has_prefill:
+            return self._mixed(batch, masks)
+        if not batch.decode_seqs:
+            return []
         return self._decode(batch, masks)
 
     def _sampling_arrays(self, seqs):
@@ -160,20 +165,36 @@ class ModelRunner:
             steps[i] = s.num_output + 131 * s.preemptions
         return temp, topp, topk, seeds, steps
 
-    def _prefill(self, batch: ScheduledBatch, masks) -> List[int]:
+    def _mixed(self, batch: ScheduledBatch, masks) -> List[int]:
         self.stats["prefill_steps"] += 1
-        seqs = [s for s, n in zip(batch.seqs, batch.num_tokens) if n > 0]
-        ntoks = [n for n in batch.num_tokens if n > 0]
-        samp = [sm for sm, n in zip(batch.sample, batch.num_tokens) if n > 0]
-        if not seqs:
-            return []
+        dseqs = batch.decode_seqs
+        pseqs = [s for s, n in zip(batch.prefill_seqs, batch.prefill_tokens) if n > 0]
+        ntoks = [n for n in batch.prefill_tokens if n > 0]
+        psamp = [sm for sm, n in zip(batch.prefill_sample, batch.prefill_tokens) if n > 0]
         bs = self.bs
+        nd = len(dseqs)
         ids, pos, slots = [], [], []
-        seq_lens = np.empty(len(seqs), np.int32)
-        qsl = np.zeros(len(seqs) + 1, np.int32)
-        maxb = max(len(s.block_ids) for s in seqs)
-        bt = np.zeros((len(seqs), maxb), np.int32)
-        for i, (s, n) in enumerate(zip(seqs, ntoks)):
+        # decode rows
+        if nd:
+            d_ids = np.empty(nd, np.int32)
+            d_pos = np.empty(nd, np.int32)
+            d_slot = np.empty(nd, np.int32)
+            d_bt = np.zeros((nd, max(len(s.block_ids) for s in dseqs)), np.int32)
+            for i, s in enumerate(dseqs):
+                p = s.n_tokens - 1
+                d_ids[i] = s.last_token
+                d_pos[i] = p
+                d_slot[i] = s.block_ids[p // bs] * bs + p % bs
+                d_bt[i, : len(s.block_ids)] = s.block_ids
+            ids.append(d_ids)
+            pos.append(d_pos)
+            slots.append(d_slot)
+        # prefill rows
+        seq_lens = np.empty(len(pseqs), np.int32)
+        qsl = np.zeros(len(pseqs) + 1, np.int32)
+        maxb = max([len(s.block_ids) for s in pseqs] or [1])
+        bt = np.zeros((max(1, len(pseqs)), maxb), np.int32)
+        for i, (s, n) in enumerate(zip(pseqs, ntoks)):
             a = s.num_computed
             ids.append(s.tokens[a:a + n])
             p = np.arange(a, a + n, dtype=np.int32)
@@ -184,30 +205,48 @@ class ModelRunner:
             seq_lens[i] = a + n
             qsl[i + 1] = qsl[i] + n
         tiles = ops.build_prefill_tiles(ntoks, ops.prefill_tile_tokens(self.model.nq, self.model.nkv))
+        # logits rows: every decode row + the last row of each prompt that completes
+        lrows = list(range(nd)) + [nd + int(qsl[i + 1]) - 1 for i, sm in enumerate(psamp) if sm]
         dv = self.device
         t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dv, non_blocking=True)  # noqa: E731
         meta = AttnMeta(
-            is_prefill=True,
-            positions=t(np.concatenate(pos)),
+            positions=t(np.concatenate(pos).astype(np.int32)),
             slot_mapping=t(np.concatenate(slots).astype(np.int32)),
-            block_tables=t(bt),
-            seq_lens=t(seq_lens),
-            logits_indices=t((qsl[1:] - 1).astype(np.int64)),
+            logits_indices=t(np.asarray(lrows, np.int64)),
+            num_decode=nd,
+            block_tables=t(bt), seq_lens=t(seq_lens),
             q_start_loc=t(qsl) if self.is_gpu else torch.from_numpy(qsl),
-            tile_info=t(np.asarray(tiles, np.int32).reshape(-1)),
-            num_tiles=len(tiles),
-        )
-        if not self.is_gpu:
-            meta.q_start_loc = torch.from_numpy(qsl)
+            tile_info=t(np.asarray(tiles, np.int32).reshape(-1)), num_tiles=len(tiles))
+        if nd:
+            splits = self._splits_for_batch(nd)
+            meta.dec_block_tables = t(d_bt)
+            meta.dec_seq_lens = t(d_pos + 1)
+            meta.max_splits = splits
+            meta.tmp_out, meta.tmp_ml = self._tmp(nd, splits)
         input_ids = t(np.concatenate(ids).astype(np.int32))
-        h = self.model.forward(input_ids, meta, self.kv)
-        idx = [i for i, sm in enumerate(samp) if sm]
-        if not idx:
+        if not lrows:
+            self.model.forward(input_ids, meta, self.kv)
             return []
-        if len(idx) != len(seqs):
-            h = h[torch.tensor(idx, device=dv)]
-        sseqs = [seqs[i] for i in idx]
+        h = self.model.forward(input_ids, meta, self.kv)
+        sseqs = dseqs + [s for s, sm in zip(pseqs, psamp) if sm]
         return self._sample(h, sseqs, masks)
+
+    def _tmp(self, n: int, splits: int):
+        nq, d = self.model.nq, self.model.d
+        if n * splits > self.tmp_rows:
+            dv = self.device
+            return (torch.empty(n * nq * splits * d, dtype=torch.float32, device=dv),
+                    torch.empty(n * nq * splits * 2, dtype=torch.float32, device=dv))
+        return self.tmp_out, self.tmp_ml
+
+    def _wait(self):
+        """Block until the GPU work queued so far is done WITHOUT holding the GIL:
+        a plain ``.cpu()`` / ``synchronize`` keeps the GIL for the whole step and
+        starves the asyncio thread that streams tokens to the WebSockets."""
+        ev = self._done_event
+        ev.record()
+        while not ev.query():
+            time.sleep(0.0001)
 
     def _sample(self, h, seqs, masks) -> List[int]:
         logits = self.model.compute_logits(h)
@@ -219,16 +258,24 @@ class ModelRunner:
         out = ops.sample(logits, torch.from_numpy(temp).to(dv), torch.from_numpy(topp).to(dv),
                          torch.from_numpy(topk).to(dv), torch.from_numpy(seeds).to(dv),
                          torch.from_numpy(steps).to(dv), mask=m)
-        return out.cpu().tolist()
+        if not self.is_gpu:
+            return out.tolist()
+        n = out.shape[0]
+        if n <= self.h_out.shape[0]:
+            self.h_out[:n].copy_(out, non_blocking=True)
+            self._wait()
+            return self.h_out[:n].tolist()
+        host = torch.empty(n, dtype=out.dtype, pin_memory=True)
+        host.copy_(out, non_blocking=True)
+        self._wait()
+        return host.tolist()
 
     def _decode(self, batch: ScheduledBatch, masks) -> List[int]:
-        seqs = batch.seqs
+        seqs = batch.decode_seqs
         n = len(seqs)
         bucket = self._bucket(n) if (self.use_graphs and masks is None) else None
-        maxlen = max(s.n_tokens for s in seqs)
-        splits = self._splits_for(maxlen)
         if bucket is None:
-            return self._decode_eager(seqs, splits, masks)
+            return self._decode_eager(seqs, self._splits_for_batch(n), masks)
         nb = bucket
         mb = self.max_decode_batch
         hs = self._hs
@@ -265,30 +312,30 @@ class ModelRunner:
         self.d_bt[:nb].copy_(self.h_bt[:nb], non_blocking=True)
         self.d_f32.copy_(self.h_f32, non_blocking=True)
         self.d_seeds.copy_(self.h_seeds, non_blocking=True)
-        g = self.graphs.get((nb, splits))
+        g = self.graphs.get(nb)
         if g is None:
-            g = self._capture(nb, splits)
+            g = self._capture(nb)
         g.replay()
         self.stats["graph_replays"] += 1
         self.h_out[:n].copy_(self.d_out[:n], non_blocking=True)
-        self._done_event.record()
-        self._done_event.synchronize()
+        self._wait()
         return self.h_out[:n].tolist()
 
     def _decode_meta(self, nb: int, splits: int) -> AttnMeta:
-        return AttnMeta(is_prefill=False, positions=self.d_positions[:nb],
-                        slot_mapping=self.d_slots[:nb], block_tables=self.d_bt[:nb],
-                        seq_lens=self.d_seq_lens[:nb], logits_indices=self.d_logits_idx[:nb],
+        assert nb * splits <= self.tmp_rows
+        return AttnMeta(positions=self.d_positions[:nb], slot_mapping=self.d_slots[:nb],
+                        logits_indices=self.d_logits_idx[:nb], num_decode=nb,
+                        dec_block_tables=self.d_bt[:nb], dec_seq_lens=self.d_seq_lens[:nb],
                         max_splits=splits, tmp_out=self.tmp_out, tmp_ml=self.tmp_ml)
 
-    def _graph_body(self, nb: int, splits: int):
-        meta = self._decode_meta(nb, splits)
+    def _graph_body(self, nb: int):
+        meta = self._decode_meta(nb, self._splits_for_batch(nb))
         h = self.model.forward(self.d_input_ids[:nb], meta, self.kv)
         logits = self.model.compute_logits(h)
         ops.sample(logits, self.d_temp[:nb], self.d_top_p[:nb], self.d_top_k[:nb],
                    self.d_seeds[:nb], self.d_steps[:nb], out=self.d_out[:nb])
 
-    def _capture(self, nb: int, splits: int):
+    def _capture(self, nb: int):
         t0 = time.time()
         # inputs must be valid for the warm-up/capture run: no KV writes, 1-token contexts
         saved = (self.d_slots[:nb].clone(), self.d_seq_lens[:nb].clone())
@@ -297,60 +344,34 @@ class ModelRunner:
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):
-            self._graph_body(nb, splits)  # warm-up (allocator, lazy init)
+            self._graph_body(nb)  # warm-up (allocator, lazy init)
         torch.cuda.current_stream(self.device).wait_stream(s)
         if self.graph_pool is None:
             self.graph_pool = torch.cuda.graph_pool_handle()
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, pool=self.graph_pool):
-            self._graph_body(nb, splits)
+            self._graph_body(nb)
         self.d_slots[:nb].copy_(saved[0])
         self.d_seq_lens[:nb].copy_(saved[1])
-        self.graphs[(nb, splits)] = g
+        self.graphs[nb] = g
         self.stats["captures"] += 1
-        log.info("captured decode graph batch=%d splits=%d in %.2fs", nb, splits, time.time() - t0)
+        log.info("captured decode graph batch=%d in %.2fs", nb, time.time() - t0)
         return g
 
     def _decode_eager(self, seqs, splits, masks) -> List[int]:
         self.stats["eager_decode"] += 1
-        n = len(seqs)
-        bs = self.bs
-        maxb = max(len(s.block_ids) for s in seqs)
-        ids = np.empty(n, np.int32)
-        pos = np.empty(n, np.int32)
-        slots = np.empty(n, np.int32)
-        sl = np.empty(n, np.int32)
-        bt = np.zeros((n, maxb), np.int32)
-        for i, s in enumerate(seqs):
-            p = s.n_tokens - 1
-            ids[i] = s.last_token
-            pos[i] = p
-            slots[i] = s.block_ids[p // bs] * bs + p % bs
-            sl[i] = p + 1
-            bt[i, : len(s.block_ids)] = s.block_ids
-        dv = self.device
-        t = lambda a: torch.from_numpy(a).to(dv)  # noqa: E731
-        nq, d = self.model.nq, self.model.d
-        if n > self.max_decode_batch:
-            tmp_out = torch.empty(n * nq * splits * d, dtype=torch.float32, device=dv)
-            tmp_ml = torch.empty(n * nq * splits * 2, dtype=torch.float32, device=dv)
-        else:
-            tmp_out, tmp_ml = self.tmp_out, self.tmp_ml
-        meta = AttnMeta(is_prefill=False, positions=t(pos), slot_mapping=t(slots),
-                        block_tables=t(bt), seq_lens=t(sl),
-                        logits_indices=torch.arange(n, device=dv), max_splits=splits,
-                        tmp_out=tmp_out, tmp_ml=tmp_ml)
-        h = self.model.forward(t(ids), meta, self.kv)
-        return self._sample(h, seqs, masks)
+        from .scheduler import ScheduledBatch as _SB
 
-    def warmup(self, batch_sizes=None, max_len: int = 256):
-        """Pre-capture decode graphs so the first requests do not pay for capture."""
+        return self._mixed(_SB(list(seqs), [], [], []), masks)
+
+    def warmup(self, batch_sizes=None):
+        """Pre-capture decode graphs (one per batch bucket, any context length) so
+        serving never pays for a capture."""
         if not self.use_graphs:
             return
+        t0 = time.time()
         for b in batch_sizes or self.graph_sizes:
             b = self._bucket(b)
-            if b is None:
-                continue
-            sp = self._splits_for(max_len)
-            if (b, sp) not in self.graphs:
-                self._capture(b, sp)
+            if b is not None and b not in self.graphs:
+                self._capture(b)
+        log.info("decode graphs ready (%d) in %.1fs", len(self.graphs), time.time() - t0)

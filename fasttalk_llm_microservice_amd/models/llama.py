@@ -26,21 +26,32 @@ from . import weights as W
 
 @dataclasses.dataclass
 class AttnMeta:
-    """Per-step attention metadata (device tensors, int32)."""
-    is_prefill: bool
+    """Per-step attention metadata (device tensors, int32).
+
+    Rows ``[0, num_decode)`` are decode rows (one new token per sequence, paged
+    split-K decode kernel); rows ``[num_decode, T)`` are prefill chunks (varlen
+    MFMA prefill kernel).  A step may contain either or both (mixed batching).
+    """
     positions: torch.Tensor          # [T]
     slot_mapping: torch.Tensor       # [T]
-    block_tables: torch.Tensor       # [B, max_blocks]
-    seq_lens: torch.Tensor           # [B] total kv length after this step
-    logits_indices: torch.Tensor     # [B] rows of the hidden state that need logits (int64)
-    # prefill
-    q_start_loc: Optional[torch.Tensor] = None   # [B+1]
-    tile_info: Optional[torch.Tensor] = None     # [num_tiles*2]
-    num_tiles: int = 0
-    # decode
+    logits_indices: torch.Tensor     # [B] rows that need logits (int64)
+    num_decode: int = 0
+    # decode rows
+    dec_block_tables: Optional[torch.Tensor] = None   # [num_decode, max_blocks]
+    dec_seq_lens: Optional[torch.Tensor] = None       # [num_decode]
     max_splits: int = 1
     tmp_out: Optional[torch.Tensor] = None
     tmp_ml: Optional[torch.Tensor] = None
+    # prefill rows
+    block_tables: Optional[torch.Tensor] = None       # [P, max_blocks]
+    seq_lens: Optional[torch.Tensor] = None           # [P] kv length after this step
+    q_start_loc: Optional[torch.Tensor] = None        # [P+1], relative to row num_decode
+    tile_info: Optional[torch.Tensor] = None          # [num_tiles*2]
+    num_tiles: int = 0
+
+    @property
+    def is_prefill(self) -> bool:
+        return self.num_decode == 0
 
 
 @dataclasses.dataclass
@@ -163,14 +174,15 @@ class LlamaModel:
             kc, vc = kv_caches[li]
             ops.rope_kv_write(qkv, meta.positions, self.cos_sin, meta.slot_mapping, kc, vc, nq, nkv, d)
             attn = torch.empty(t, nq * d, dtype=x.dtype, device=x.device)
-            if meta.is_prefill:
-                ops.prefill_attention(attn, qkv, kc, vc, meta.block_tables, meta.seq_lens,
+            nd = meta.num_decode
+            if nd > 0:
+                ops.decode_attention(attn[:nd], qkv[:nd], kc, vc, meta.dec_block_tables,
+                                     meta.dec_seq_lens, meta.tmp_out, meta.tmp_ml, nq, nkv, d,
+                                     meta.max_splits, self.scale)
+            if t > nd:
+                ops.prefill_attention(attn[nd:], qkv[nd:], kc, vc, meta.block_tables, meta.seq_lens,
                                       meta.q_start_loc, meta.tile_info, meta.num_tiles, nq, nkv, d,
                                       self.scale)
-            else:
-                ops.decode_attention(attn, qkv, kc, vc, meta.block_tables, meta.seq_lens,
-                                     meta.tmp_out, meta.tmp_ml, nq, nkv, d, meta.max_splits,
-                                     self.scale)
             x = F.linear(attn, L.wo)
             self.comm.all_reduce(x)
             ops.fused_add_rmsnorm(x, residual, L.ln2, eps)

@@ -114,7 +114,19 @@ def rope_kv_write(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, nq, n
 
 
 def decode_partition_size() -> int:
-    return 256
+    """Max tokens per decode partition: callers must pass splits >= ceil(max_len / this)."""
+    return 1024
+
+
+def decode_splits(batch: int, nkv: int, max_model_len: int, target_blocks: int = 2048) -> int:
+    """Split-K factor for the paged decode kernel: enough workgroups to fill the
+    chip at small batch, never a partition longer than the LDS score buffer."""
+    lo = max(1, -(-max_model_len // decode_partition_size()))
+    want = max(1, target_blocks // max(1, batch * nkv))
+    s = 1
+    while s * 2 <= want:
+        s *= 2
+    return int(min(64, max(lo, min(32, s))))
 
 
 def prefill_tile_tokens(nq: int, nkv: int) -> int:

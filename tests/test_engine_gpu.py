@@ -36,7 +36,6 @@ def test_gpu_logits_match_cpu_reference():
         dev = m.device
         ids = torch.arange(100, 100 + T, dtype=torch.int32, device=dev)
         meta = AttnMeta(
-            is_prefill=True,
             positions=torch.arange(T, dtype=torch.int32, device=dev),
             slot_mapping=torch.arange(T, dtype=torch.int32, device=dev),
             block_tables=torch.arange(nblk, dtype=torch.int32, device=dev)[None],

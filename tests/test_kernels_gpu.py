@@ -93,7 +93,8 @@ def _random_tables(lens, bs, nblocks_total):
 
 @pytest.mark.parametrize("nq,nkv,d", [(32, 8, 128), (64, 8, 128), (8, 8, 128), (24, 8, 128),
                                       (32, 8, 64)])
-def test_decode_attention(nq, nkv, d):
+@pytest.mark.parametrize("splits", [None, 32])
+def test_decode_attention(nq, nkv, d, splits):
     bs = 16
     lens = [1, 17, 255, 256, 257, 1000, 2100]
     nblocks = sum((l + bs - 1) // bs for l in lens) + 4
@@ -103,7 +104,7 @@ def test_decode_attention(nq, nkv, d):
     b = len(lens)
     q = torch.randn(b, nq * d, device=DEV).bfloat16()
     part = ops.decode_partition_size()
-    max_splits = math.ceil(max(lens) / part)
+    max_splits = splits or math.ceil(max(lens) / part)
     tmp_out = torch.empty(b * nq * max_splits * d, device=DEV)
     tmp_ml = torch.empty(b * nq * max_splits * 2, device=DEV)
     out = torch.zeros(b, nq * d, device=DEV).bfloat16()
