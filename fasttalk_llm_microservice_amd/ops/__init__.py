@@ -114,19 +114,19 @@ def rope_kv_write(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, nq, n
 
 
 def decode_partition_size() -> int:
-    """Max tokens per decode partition: callers must pass splits >= ceil(max_len / this)."""
-    return 1024
+    """Max tokens per decode partition (the online-softmax kernel has no bound)."""
+    return 1 << 30
 
 
-def decode_splits(batch: int, nkv: int, max_model_len: int, target_blocks: int = 2048) -> int:
-    """Split-K factor for the paged decode kernel: enough workgroups to fill the
-    chip at small batch, never a partition longer than the LDS score buffer."""
-    lo = max(1, -(-max_model_len // decode_partition_size()))
+def decode_splits(batch: int, nkv: int, max_model_len: int = 0, target_blocks: int = 256) -> int:
+    """Split-K factor for the paged decode kernel: the smallest power of two that
+    gives ``target_blocks`` workgroups (4 waves each), so small batches still fill
+    the 256 CUs while large batches skip the combine pass entirely."""
     want = max(1, target_blocks // max(1, batch * nkv))
     s = 1
-    while s * 2 <= want:
+    while s < want:
         s *= 2
-    return int(min(64, max(lo, min(32, s))))
+    return int(min(64, s))
 
 
 def prefill_tile_tokens(nq: int, nkv: int) -> int:

@@ -93,7 +93,7 @@ def _random_tables(lens, bs, nblocks_total):
 
 @pytest.mark.parametrize("nq,nkv,d", [(32, 8, 128), (64, 8, 128), (8, 8, 128), (24, 8, 128),
                                       (32, 8, 64)])
-@pytest.mark.parametrize("splits", [None, 32])
+@pytest.mark.parametrize("splits", [None, 3, 32])
 def test_decode_attention(nq, nkv, d, splits):
     bs = 16
     lens = [1, 17, 255, 256, 257, 1000, 2100]
