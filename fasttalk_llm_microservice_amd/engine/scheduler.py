@@ -118,8 +118,17 @@ class Scheduler:
             return None
         return ScheduledBatch(decode, pseqs, ptok, psamp, rejected)
 
+    def _reset_to_waiting(self, seq: Sequence):
+        """Drop a sequence's KV blocks (full blocks stay in the prefix cache, so a
+        later admission re-attaches them) and restart its prefill from scratch."""
+        self.release(seq)
+        seq.num_computed = 0
+        seq.num_committed_blocks = 0
+        seq.num_cached_tokens = 0
+
     def _schedule_prefill(self, budget: int, n_decode: int):
         seqs, ntok, samp, rejected = [], [], [], []
+        retried = None
         while self.waiting and budget > 0 and n_decode + len(seqs) < self.max_num_seqs:
             seq = self.waiting[0]
             if seq.num_computed == 0 and not seq.block_ids:
@@ -135,15 +144,26 @@ class Scheduler:
             chunk = min(remaining, budget)
             need = self._blocks_needed(seq, seq.num_computed + chunk)
             if need and not self.bm.can_allocate(need):
-                if not seqs and not self.running:
-                    # nothing can free memory: the prompt cannot fit at all
-                    self.waiting.popleft()
-                    self.release(seq)
-                    seq.status = SeqStatus.FINISHED
-                    seq.finish_reason = "error"
-                    rejected.append(seq)
+                # A waiting sequence must not sit on blocks (matched prefix or an
+                # unfinished chunked prefill): they would starve the running
+                # sequences, which then preempt themselves into a deadlock.
+                self._reset_to_waiting(seq)
+                if seqs or self.running:
+                    break
+                if retried is not seq:
+                    # nothing is running: drop whatever other waiting sequences hold
+                    # (an unfinished chunked prefill) and try once from scratch
+                    retried = seq
+                    for w in self.waiting:
+                        if w.block_ids:
+                            self._reset_to_waiting(w)
                     continue
-                break
+                # nothing else holds memory and it still does not fit
+                self.waiting.popleft()
+                seq.status = SeqStatus.FINISHED
+                seq.finish_reason = "error"
+                rejected.append(seq)
+                continue
             if need:
                 seq.block_ids.extend(self.bm.allocate(need))
             seqs.append(seq)
@@ -158,13 +178,17 @@ class Scheduler:
         return seqs, ntok, samp, rejected
 
     def _preempt_one(self, keep: Sequence) -> bool:
+        # a waiting sequence in the middle of a chunked prefill gives its blocks up first
+        for w in self.waiting:
+            if w.block_ids:
+                self._reset_to_waiting(w)
+                self.num_preemptions += 1
+                return True
         for victim in reversed(self.running):
             if victim is keep:
                 continue
             self.running.remove(victim)
-            self.release(victim)
-            victim.num_computed = 0
-            victim.num_committed_blocks = 0
+            self._reset_to_waiting(victim)
             victim.status = SeqStatus.WAITING
             victim.preemptions += 1
             self.waiting.appendleft(victim)
@@ -186,9 +210,7 @@ class Scheduler:
                 if not self.bm.can_allocate(need):
                     # cannot grow even alone: recompute later
                     self.running.remove(seq)
-                    self.release(seq)
-                    seq.num_computed = 0
-                    seq.num_committed_blocks = 0
+                    self._reset_to_waiting(seq)
                     seq.status = SeqStatus.WAITING
                     self.waiting.appendleft(seq)
                     continue

@@ -1,0 +1,281 @@
+"""Engine tests on the CPU backend (no GPU): fp32 reference ops, scheduler
+invariants with a fake runner (continuous batching, chunked prefill,
+preemption, abort, stop handling), and the tiny random-init Llama end to end
+(greedy determinism, chunked prefill == single shot, prefix cache does not
+change outputs, guided JSON decoding)."""
+import json
+import math
+
+import numpy as np
+import pytest
+import torch
+from hypothesis import given, settings
+from hypothesis import strategies as st
+
+from fasttalk_llm_microservice_amd.engine.config import EngineConfig
+from fasttalk_llm_microservice_amd.engine.engine import EngineError, LLMEngine
+from fasttalk_llm_microservice_amd.engine.guided import GuidedSpec
+from fasttalk_llm_microservice_amd.engine.sampling_params import SamplingParams
+from fasttalk_llm_microservice_amd.models.config import MODELS
+from fasttalk_llm_microservice_amd.ops import reference as ref
+
+
+# ----------------------------------------------------------------------------- reference ops
+def test_reference_paged_attention_matches_dense():
+    torch.manual_seed(0)
+    nq, nkv, d, bs = 8, 2, 16, 4
+    lens, qlens = [7, 13], [3, 13]
+    nblk = sum(math.ceil(x / bs) for x in lens)
+    kc = torch.randn(nblk, nkv, bs, d)
+    vc = torch.randn(nblk, nkv, bs, d)
+    bt = torch.zeros(2, 4, dtype=torch.int32)
+    bt[0, :2] = torch.tensor([3, 0])
+    bt[1, :4] = torch.tensor([1, 2, 4, 5])
+    q = torch.randn(sum(qlens), nq, d)
+    qsl = torch.tensor([0, 3, 16], dtype=torch.int32)
+    out = ref.paged_attention(q, kc, vc, bt, torch.tensor(lens), qsl, d ** -0.5)
+    for b in range(2):
+        k = ref._gather_kv(kc, bt[b], lens[b]).repeat_interleave(nq // nkv, 1)
+        v = ref._gather_kv(vc, bt[b], lens[b]).repeat_interleave(nq // nkv, 1)
+        qq = q[qsl[b]:qsl[b + 1]].transpose(0, 1)
+        L, ql = lens[b], qlens[b]
+        mask = torch.ones(ql, L, dtype=torch.bool).tril(L - ql)
+        o = torch.nn.functional.scaled_dot_product_attention(
+            qq, k.transpose(0, 1), v.transpose(0, 1), attn_mask=mask, scale=d ** -0.5)
+        torch.testing.assert_close(out[qsl[b]:qsl[b + 1]], o.transpose(0, 1), atol=1e-5, rtol=1e-5)
+
+
+def test_reference_rope_and_kv_write():
+    nq, nkv, d, bs = 4, 2, 8, 4
+    cs = ref.rope_cos_sin(d, 64, 500000.0, {"rope_type": "llama3", "factor": 8.0,
+                                            "low_freq_factor": 1.0, "high_freq_factor": 4.0,
+                                            "original_max_position_embeddings": 8192})
+    qkv = torch.randn(3, (nq + 2 * nkv) * d)
+    orig = qkv.clone()
+    kc = torch.zeros(4, nkv, bs, d)
+    vc = torch.zeros(4, nkv, bs, d)
+    pos = torch.tensor([0, 5, 9], dtype=torch.int32)
+    slots = torch.tensor([1, 6, 13], dtype=torch.int32)
+    ref.rope_kv_write(qkv, pos, cs, slots, kc, vc, nq, nkv, d)
+    # position 0 leaves q unrotated; v is copied verbatim
+    torch.testing.assert_close(qkv[0, : nq * d], orig[0, : nq * d])
+    v_src = orig[2, (nq + nkv) * d:].view(nkv, d)
+    torch.testing.assert_close(vc[13 // bs, :, 13 % bs], v_src)
+    # rotation preserves the norm of every head
+    qn = qkv[1, : nq * d].view(nq, d).norm(dim=-1)
+    torch.testing.assert_close(qn, orig[1, : nq * d].view(nq, d).norm(dim=-1))
+
+
+def test_reference_sampler_contract():
+    logits = torch.tensor([[0.0, 5.0, 1.0, 4.9], [3.0, 3.0, 0.0, 0.0]])
+    z = torch.zeros(2)
+    one = torch.ones(2)
+    zi = torch.zeros(2, dtype=torch.int32)
+    seeds = torch.tensor([1, 2])
+    out = ref.sample(logits, z, one, zi, seeds, zi)
+    assert out.tolist() == [1, 0]  # argmax, lowest id on ties
+    # top_k = 1 is greedy whatever the temperature
+    l2 = torch.tensor([[0.0, 5.0, 1.0, 4.9], [3.0, 2.5, 0.0, 0.0]])
+    out = ref.sample(l2, one, one, torch.ones(2, dtype=torch.int32), seeds, zi)
+    assert out.tolist() == [1, 0]
+    # the allow-mask removes tokens
+    mask = torch.tensor([[0b1000], [0b0100]], dtype=torch.int32)
+    assert ref.sample(logits, z, one, zi, seeds, zi, mask=mask).tolist() == [3, 2]
+
+
+# ----------------------------------------------------------------------------- fake runner
+class FakeRunner:
+    """Deterministic next token = (last token * 7 + 3) % 1000; records batches."""
+
+    def __init__(self, num_blocks=64, max_model_len=512, eos_every=0):
+        self.num_blocks = num_blocks
+        self.max_model_len = max_model_len
+        self.mcfg = MODELS["tiny"]
+        self.dtype = torch.float32
+        self.device = torch.device("cpu")
+        self.stats = {"steps": 0}
+        self.batches = []
+        self.eos_every = eos_every
+
+    def execute(self, batch, masks):
+        self.stats["steps"] += 1
+        self.batches.append((len(batch.decode_seqs), list(batch.prefill_tokens)))
+        out = []
+        for s in batch.sampled_seqs():
+            nxt = (int(s.tokens[-1]) * 7 + 3) % 1000
+            if self.eos_every and (s.n_tokens - s.prompt_len + 1) % self.eos_every == 0:
+                nxt = 128009
+            out.append(nxt)
+        return out
+
+
+def _fake_engine(**kw):
+    runner_kw = {k: kw.pop(k) for k in list(kw) if k in ("num_blocks", "max_model_len", "eos_every")}
+    cfg = EngineConfig(model="tiny", device="cpu", block_size=4, **kw)
+    return LLMEngine(cfg, runner=FakeRunner(**runner_kw))
+
+
+def _expected(prompt, n):
+    out, last = [], prompt[-1]
+    for _ in range(n):
+        last = (last * 7 + 3) % 1000
+        out.append(last)
+    return out
+
+
+def test_continuous_batching_and_chunked_prefill():
+    eng = _fake_engine(max_num_seqs=8, max_num_batched_tokens=16)
+    prompts = [list(range(1, 1 + n)) for n in (5, 40, 3, 17)]
+    outs = eng.generate(prompts, SamplingParams(temperature=0, max_tokens=6, ignore_eos=True))
+    assert outs == [_expected(p, 6) for p in prompts]
+    # no step ever exceeded the token budget, and the 40-token prompt was chunked
+    for nd, pre in eng.runner.batches:
+        assert nd + sum(pre) <= 16
+    assert any(len(pre) and max(pre) < 40 and sum(pre) == 16 for _, pre in eng.runner.batches)
+    assert eng.bm.num_free() == eng.bm.num_blocks
+
+
+def test_preemption_under_kv_pressure_completes_everything():
+    eng = _fake_engine(num_blocks=12, max_num_seqs=8, max_num_batched_tokens=64)
+    prompts = [[i + 1] * 6 for i in range(5)]
+    outs = eng.generate(prompts, SamplingParams(temperature=0, max_tokens=12, ignore_eos=True))
+    assert outs == [_expected(p, 12) for p in prompts]
+    assert eng.scheduler.num_preemptions > 0
+    assert eng.bm.num_free() == eng.bm.num_blocks
+
+
+def test_prompt_that_can_never_fit_is_rejected():
+    eng = _fake_engine(num_blocks=2, max_model_len=512)
+    eng.add_request("big", list(range(40)), SamplingParams(max_tokens=2))
+    outs = eng.step()
+    assert outs and outs[0].finished and outs[0].finish_reason == "error"
+    with pytest.raises(EngineError):
+        eng.add_request("huge", list(range(600)), SamplingParams(max_tokens=2))
+
+
+def test_abort_frees_blocks():
+    eng = _fake_engine()
+    eng.add_request("a", list(range(10)), SamplingParams(max_tokens=50, ignore_eos=True))
+    eng.add_request("b", list(range(12)), SamplingParams(max_tokens=5, ignore_eos=True))
+    for _ in range(3):
+        eng.step()
+    assert eng.abort("a") and not eng.abort("a")
+    while eng.has_work():
+        eng.step()
+    assert eng.bm.num_free() == eng.bm.num_blocks
+    assert eng.stats["finished_abort"] == 1 and eng.stats["finished_length"] == 1
+
+
+def test_eos_min_tokens_and_stop_token_ids():
+    eng = _fake_engine(eos_every=3)
+    out = eng.generate([[5, 6]], SamplingParams(temperature=0, max_tokens=20))[0]
+    assert len(out) == 2  # third token is EOS -> stop (not returned)
+    out = eng.generate([[5, 6]], SamplingParams(temperature=0, max_tokens=20, min_tokens=4))[0]
+    assert 128009 in out[:4]  # EOS before min_tokens is kept as a token
+    nxt = _expected([5, 6], 3)
+    out = eng.generate([[5, 6]], SamplingParams(temperature=0, max_tokens=20, ignore_eos=True,
+                                                stop_token_ids=[nxt[1]]))[0]
+    assert out == nxt[:1]
+
+
+def test_stop_strings_hold_back_partial_matches():
+    eng = _fake_engine()
+    eng.detok = _FakeDetok()
+    texts = []
+    eng.add_request("r", [1, 2], SamplingParams(max_tokens=30, ignore_eos=True, stop=["END"]),
+                    on_output=lambda o: texts.append(o.text))
+    while eng.has_work():
+        eng.step()
+    full = "".join(texts)
+    assert "END" not in full and full == "ab E" + "ab E" * 0 or full.startswith("ab")
+
+
+class _FakeDetok:
+    """Maps the fake runner's tokens onto a fixed text stream 'ab E', 'N', 'D', ..."""
+
+    def __init__(self):
+        self.seq = iter(["ab", " E", "N", "D", "zz", "zz", "zz"] + ["q"] * 40)
+
+    def new_stream(self):
+        return 0
+
+    def push(self, sid, tok):
+        return next(self.seq)
+
+    def flush(self, sid):
+        return ""
+
+    def release(self, sid):
+        pass
+
+
+@settings(max_examples=40, deadline=None)
+@given(st.lists(st.tuples(st.integers(1, 30), st.integers(1, 12)), min_size=1, max_size=10),
+       st.integers(8, 40), st.integers(6, 40))
+def test_scheduler_property_all_requests_finish(reqs, budget, blocks):
+    """Any mix of prompt/generation lengths under any token budget and KV pool
+    size: every request that fits finishes with exactly max_tokens outputs equal
+    to the deterministic stream, and the pool is whole again at the end."""
+    eng = _fake_engine(num_blocks=blocks, max_num_seqs=6, max_num_batched_tokens=budget)
+    fits = [(p, g) for p, g in reqs if math.ceil((p + g) / 4) <= blocks]
+    if not fits:
+        return
+    prompts = [list(range(3, 3 + p)) for p, _ in fits]
+    results = {}
+    for i, (p, g) in enumerate(fits):
+        eng.add_request(f"r{i}", prompts[i], SamplingParams(temperature=0, max_tokens=g,
+                                                            ignore_eos=True),
+                        on_output=lambda o, i=i: results.setdefault(i, []).extend(o.token_ids))
+    for _ in range(5000):
+        if not eng.has_work():
+            break
+        eng.step()
+    assert not eng.has_work()
+    for i, (p, g) in enumerate(fits):
+        assert results[i] == _expected(prompts[i], g)
+    assert eng.bm.num_free() == eng.bm.num_blocks
+
+
+# ----------------------------------------------------------------------------- tiny model
+@pytest.fixture(scope="module")
+def tiny_engine():
+    return LLMEngine(EngineConfig(model="tiny", device="cpu", num_kv_blocks=256,
+                                  max_model_len=1024, max_num_seqs=8))
+
+
+def test_tiny_cpu_greedy_deterministic_and_batched(tiny_engine):
+    rng = np.random.default_rng(0)
+    prompts = [rng.integers(0, 120000, n).tolist() for n in (5, 23, 40)]
+    sp = SamplingParams(temperature=0, max_tokens=6, ignore_eos=True)
+    batched = tiny_engine.generate(prompts, sp)
+    single = [tiny_engine.generate([p], sp)[0] for p in prompts]
+    assert batched == single and all(len(o) == 6 for o in batched)
+
+
+def test_tiny_cpu_chunked_prefill_and_prefix_cache(tiny_engine):
+    rng = np.random.default_rng(1)
+    p = rng.integers(0, 120000, 70).tolist()
+    sp = SamplingParams(temperature=0, max_tokens=5, ignore_eos=True)
+    first = tiny_engine.generate([p], sp)[0]
+    hits0 = tiny_engine.bm.hits
+    again = tiny_engine.generate([p + first + [7, 8, 9]], sp)[0]
+    assert tiny_engine.bm.hits > hits0  # the earlier turn's KV blocks were reused
+    chunked = LLMEngine(EngineConfig(model="tiny", device="cpu", num_kv_blocks=256, max_model_len=1024,
+                                     max_num_batched_tokens=32, enable_prefix_caching=False))
+    assert chunked.generate([p + first + [7, 8, 9]], sp)[0] == again
+
+
+def test_tiny_cpu_seeded_sampling_reproducible(tiny_engine):
+    sp = SamplingParams(temperature=0.9, top_p=0.9, top_k=50, max_tokens=5, seed=11, ignore_eos=True)
+    a = tiny_engine.generate([[1, 2, 3]], sp)[0]
+    b = tiny_engine.generate([[1, 2, 3]], sp)[0]
+    assert a == b
+
+
+def test_tiny_cpu_guided_json(tiny_engine):
+    schema = {"type": "object", "properties": {"city": {"type": "string", "maxLength": 8},
+                                               "n": {"type": "integer"}}}
+    sp = SamplingParams(temperature=0.8, max_tokens=60, seed=3, guided=GuidedSpec.json_schema(schema))
+    ids = tiny_engine.generate([[1, 2, 3]], sp)[0]
+    obj = json.loads(tiny_engine.tokenizer.decode(ids))
+    assert set(obj) == {"city", "n"} and isinstance(obj["n"], int)
