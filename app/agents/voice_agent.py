@@ -215,8 +215,11 @@ class VoiceAgent:
             held_tokens = 0
             finish = None
             sid = context.session_id
+            # a guided call is a finite JSON language: give it room to finish even
+            # when the spoken-reply budget is small
+            round_mt = max(mt, 256) if guided is not None else mt
             async for out in backend.stream_events(
-                    messages, temperature=temp, max_tokens=mt, top_p=tp, top_k=top_k, stop=stop,
+                    messages, temperature=temp, max_tokens=round_mt, top_p=tp, top_k=top_k, stop=stop,
                     request_id=sid, session_id=sid if (rnd == 0 and guided is None) else None,
                     tools=schemas or None, guided=guided, seed=seed,
                     ignore_eos=ignore_eos and guided is None, min_tokens=min_tokens):

@@ -1,0 +1,215 @@
+"""Agent loop (BASELINE config 5: tool calling + web-search stub with guided JSON
+tool calls on random weights), the OpenAI-compatible facade, the aiohttp ASGI
+transport (real sockets on 127.0.0.1) and the monitoring service, all on the
+CPU backend.  Reference behaviour: app/agents/voice_agent.py:147-344,
+app/monitoring/service_monitor.py:85-137."""
+import asyncio
+import json
+from datetime import datetime
+
+import pytest
+from starlette.testclient import TestClient
+
+from app.agents.tools import make_search_tool, make_session_tool, make_time_tool
+from app.agents.voice_agent import AgentConfig, ConversationContext, VoiceAgent
+from app.core.native_handler import NativeHandler
+from fasttalk_llm_microservice_amd.engine.config import EngineConfig
+from fasttalk_llm_microservice_amd.engine.engine import AsyncEngine, LLMEngine
+
+
+@pytest.fixture(scope="module")
+def engine():
+    eng = AsyncEngine(LLMEngine(EngineConfig(model="tiny", device="cpu", num_kv_blocks=512,
+                                             max_model_len=2048, max_num_seqs=16))).start()
+    yield eng
+    eng.shutdown()
+
+
+def _ctx(sid="s1"):
+    return ConversationContext(user_id="u", session_id=sid, conversation_history=[],
+                               created_at=datetime.now())
+
+
+# ----------------------------------------------------------------------------- tools
+def test_tools_offline():
+    search = make_search_tool(rate_limit=0.0, backend="stub")
+    res = json.loads(asyncio.run(search(None, query="mi355x hbm", max_results=3)))
+    assert len(res) == 3 and {"title", "href", "body"} <= set(res[0])
+    assert "current date" in asyncio.run(make_time_tool()(None))
+    info = asyncio.run(make_session_tool()(_ctx("abcdefghij")))
+    assert info.startswith("Session abcdefgh...")
+    assert search.schema()["function"]["parameters"]["required"] == ["query"]
+
+
+# ----------------------------------------------------------------------------- agent
+def test_agent_guided_tool_call_round_trip(engine):
+    handler = NativeHandler(engine=engine)
+    agent = VoiceAgent(AgentConfig(guided_tool_calls=True, max_tokens=24, temperature=0.7),
+                       backend=handler)
+    assert agent.is_native and set(agent.tools()) == {"duckduckgo_search", "get_current_time",
+                                                       "get_session_info"}
+
+    async def run():
+        return [ev async for ev in agent.generate_events("Search the web for the weather news",
+                                                         _ctx(), seed=5, max_tokens=24)]
+
+    events = asyncio.run(run())
+    calls = [e for e in events if e.tool_call]
+    assert calls, "guided decoding must produce a valid tool call"
+    assert calls[0].tool_call["name"] in agent.tools() and calls[0].tool_result
+    assert events[-1].finish_reason in ("stop", "length")
+
+
+def test_agent_plain_answer_and_custom_tool(engine):
+    handler = NativeHandler(engine=engine)
+    agent = VoiceAgent(AgentConfig(guided_tool_calls=False), backend=handler)
+
+    @agent.tool(description="Adds two numbers", parameters={
+        "type": "object", "properties": {"a": {"type": "integer"}, "b": {"type": "integer"}}})
+    def add(ctx, a, b):
+        return str(a + b)
+
+    assert "add" in agent.tools()
+
+    async def run():
+        evs = [ev async for ev in agent.generate_events("add please", _ctx("s2"), temperature=0.0,
+                                                        max_tokens=8, tool_choice="add", seed=1)]
+        return evs
+
+    evs = asyncio.run(run())
+    call = [e for e in evs if e.tool_call][0]
+    assert call.tool_call["name"] == "add"
+    a, b = call.tool_call["arguments"]["a"], call.tool_call["arguments"]["b"]
+    assert call.tool_result == str(a + b)
+    info = agent.get_model_info()
+    assert info["base_url"] == "in-process" and "add" in info["tools"]
+
+
+def test_ws_agent_path(monkeypatch, engine):
+    from app.core.websocket_server_vllm import WebSocketLLMServer
+    from app.utils.config import Config
+
+    for k, v in {"LLM_PROVIDER": "native", "ENABLE_PYDANTIC_AI": "true",
+                 "COMPUTE_DEVICE": "cpu"}.items():
+        monkeypatch.setenv(k, v)
+    srv = WebSocketLLMServer(Config(), engine=engine)
+    c = TestClient(srv.app)
+    assert c.get("/").json()["pydantic_ai_enabled"] is True
+    with c.websocket_connect("/ws/llm") as ws:
+        assert ws.receive_json()["pydantic_ai_enabled"] is True
+        ws.send_json({"type": "start_session", "config": {"max_tokens": 5, "temperature": 0.0,
+                                                          "ignore_eos": True}})
+        ws.receive_json()
+        ws.send_json({"type": "user_message", "text": "hello"})
+        while True:
+            f = ws.receive_json()
+            if f["type"] == "response_complete":
+                break
+        assert f["stats"]["pydantic_ai_used"] is True and f["stats"]["tokens_generated"] >= 1
+        ws.send_json({"type": "update_config", "config": {"enable_web_search": False}})
+        assert ws.receive_json()["type"] == "config_updated"
+    assert "duckduckgo_search" not in srv.voice_agent.tools()
+
+
+# ----------------------------------------------------------------------------- openai facade
+def test_openai_chat_completions(monkeypatch, engine):
+    from app.core.websocket_server_vllm import WebSocketLLMServer
+    from app.utils.config import Config
+
+    monkeypatch.setenv("LLM_PROVIDER", "native")
+    monkeypatch.setenv("ENABLE_PYDANTIC_AI", "false")
+    c = TestClient(WebSocketLLMServer(Config(), engine=engine).app)
+    assert c.get("/v1/models").json()["data"][0]["id"] == "tiny"
+    body = {"messages": [{"role": "user", "content": "hi"}], "max_tokens": 5, "temperature": 0,
+            "ignore_eos": True}
+    r = c.post("/v1/chat/completions", json=body).json()
+    assert r["object"] == "chat.completion" and r["usage"]["completion_tokens"] == 5
+    assert r["choices"][0]["finish_reason"] == "length"
+    s = c.post("/v1/chat/completions", json=dict(body, stream=True))
+    lines = [x for x in s.text.split("\n\n") if x]
+    assert lines[-1] == "data: [DONE]" and json.loads(lines[0][6:])["object"] == "chat.completion.chunk"
+    tools = [{"type": "function", "function": {"name": "get_weather", "parameters": {
+        "type": "object", "properties": {"city": {"type": "string", "maxLength": 10}}}}}]
+    r = c.post("/v1/chat/completions", json={"messages": [{"role": "user", "content": "w?"}],
+                                             "tools": tools, "tool_choice": "required",
+                                             "max_tokens": 40, "seed": 3}).json()
+    msg = r["choices"][0]["message"]
+    assert r["choices"][0]["finish_reason"] == "tool_calls"
+    assert msg["tool_calls"][0]["function"]["name"] == "get_weather"
+    assert "city" in json.loads(msg["tool_calls"][0]["function"]["arguments"])
+    rf = {"type": "json_schema", "json_schema": {"schema": {
+        "type": "object", "properties": {"ok": {"type": "boolean"}}}}}
+    r = c.post("/v1/chat/completions", json={"messages": [{"role": "user", "content": "j"}],
+                                             "response_format": rf, "max_tokens": 20}).json()
+    assert isinstance(json.loads(r["choices"][0]["message"]["content"])["ok"], bool)
+    assert c.post("/v1/chat/completions", json={"messages": []}).status_code == 400
+
+
+# ----------------------------------------------------------------------------- ASGI over aiohttp
+def test_aiohttp_asgi_transport_serves_ws_and_http(monkeypatch, engine):
+    import aiohttp
+
+    from app.core.websocket_server_vllm import WebSocketLLMServer
+    from app.server.asgi_aiohttp import AiohttpASGIServer
+    from app.utils.config import Config
+
+    monkeypatch.setenv("LLM_PROVIDER", "native")
+    monkeypatch.setenv("ENABLE_PYDANTIC_AI", "false")
+    srv = WebSocketLLMServer(Config(), engine=engine)
+
+    async def main():
+        asgi = AiohttpASGIServer(srv.app, "127.0.0.1", 0)
+        await asgi.start()
+        try:
+            base = f"127.0.0.1:{asgi.port}"
+            async with aiohttp.ClientSession() as s:
+                async with s.get(f"http://{base}/health") as r:
+                    assert r.status == 200 and (await r.json())["status"] == "healthy"
+                async with s.ws_connect(f"ws://{base}/ws/llm") as ws:
+                    hello = json.loads((await ws.receive()).data)
+                    assert hello["type"] == "session_started"
+                    await ws.send_str(json.dumps({"type": "start_session", "config": {
+                        "max_tokens": 4, "temperature": 0, "ignore_eos": True}}))
+                    await ws.receive()
+                    await ws.send_str(json.dumps({"type": "user_message", "text": "yo"}))
+                    n = 0
+                    while True:
+                        f = json.loads((await ws.receive()).data)
+                        n += f["type"] == "token"
+                        if f["type"] == "response_complete":
+                            break
+                    assert f["stats"]["tokens_generated"] == 4 and n >= 1
+        finally:
+            await asgi.stop()
+
+    asyncio.run(main())
+
+
+# ----------------------------------------------------------------------------- monitoring
+def test_service_monitor_metrics_and_prometheus(monkeypatch, engine):
+    from app.core.websocket_server_vllm import WebSocketLLMServer
+    from app.monitoring.service_monitor import MonitoringServer, ServiceMonitor, prometheus_text
+    from app.utils.config import Config
+
+    monkeypatch.setenv("LLM_PROVIDER", "native")
+    monkeypatch.setenv("ENABLE_PYDANTIC_AI", "false")
+    mon = ServiceMonitor()
+    srv = WebSocketLLMServer(Config(), monitor=mon, engine=engine)
+    mon.attach_server(srv)
+    mon.record_request()
+    mon.record_generation(10, 0.5, ttft=0.05)
+    mon.record_error()
+    m = mon.get_metrics()
+    assert m["requests"] == 1 and m["generations"] == 1 and m["errors"] == 1
+    assert m["total_tokens_generated"] == 10 and m["avg_processing_time_seconds"] == pytest.approx(0.5)
+    txt = prometheus_text(m)
+    assert "fasttalk_requests" in txt and "fasttalk_total_tokens_generated 10" in txt
+    ms = MonitoringServer(port=19092, monitor=mon)
+    c = ms.app.test_client()
+    h = c.get("/health").get_json()
+    assert h["status"] == "healthy" and "system" in h
+    assert c.get("/health/ready").get_json() == {"status": "ready"}
+    assert c.get("/health/live").get_json() == {"status": "live"}
+    assert c.get("/metrics").get_json()["requests"] == 1
+    assert c.get("/info").get_json()["service"] == "llm-service"
+    assert b"fasttalk_requests" in c.get("/metrics/prometheus").data
