@@ -62,7 +62,7 @@ def get_shared_engine(engine_cfg) -> "Any":
     with _ENGINE_LOCK:
         eng = _ENGINES.get(key)
         if eng is None:
-            if engine_cfg.dp_size > 1 or engine_cfg.tp_size > 1:
+            if engine_cfg.dp_size > 1:
                 from fasttalk_llm_microservice_amd.parallel.dp_router import MultiGPUEngine
 
                 eng = MultiGPUEngine(engine_cfg).start()

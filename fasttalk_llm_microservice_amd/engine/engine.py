@@ -253,6 +253,13 @@ class LLMEngine:
                         done.add(o.request_id)
         return [results[r] for r in ids]
 
+    def shutdown(self):
+        """Stops tensor-parallel workers (if any)."""
+        g = getattr(self, "tp_group", None)
+        if g is not None:
+            g.shutdown()
+            self.tp_group = None
+
     def kv_usage(self) -> float:
         n = self.bm.num_blocks
         return 1.0 - self.bm.num_free() / n if n else 0.0
@@ -299,6 +306,10 @@ class AsyncEngine:
 
     @classmethod
     def from_config(cls, cfg: EngineConfig) -> "AsyncEngine":
+        if cfg.tp_size > 1:
+            from ..parallel.tp import spawn_tp_engine
+
+            return cls(spawn_tp_engine(cfg))
         return cls(LLMEngine(cfg))
 
     # ------------------------------------------------------------------ lifecycle
@@ -320,6 +331,7 @@ class AsyncEngine:
         if self._thread is not None:
             self._thread.join(timeout=10)
             self._thread = None
+        self.engine.shutdown()
 
     def is_healthy(self, stall_s: float = 120.0) -> bool:
         """Watchdog: the step loop must be alive and, when busy, making progress."""

@@ -106,6 +106,7 @@ class ModelRunner:
         self.graph_pool = None
         self.use_graphs = self.is_gpu and not cfg.enforce_eager
         self.stats = {"graph_replays": 0, "eager_decode": 0, "prefill_steps": 0, "captures": 0}
+        self.bcast = None  # TP rank 0: parallel.shm_broadcast.ShmBroadcast writer
 
     # ------------------------------------------------------------------ memory
     def _decide_num_blocks(self) -> int:
@@ -121,7 +122,7 @@ class ModelRunner:
             n = max(budget // per_block, 64)
         else:
             n = max(1024, (self.max_model_len // self.bs) * 4)
-        n = int(min(n, 4_000_000))
+        n = self.comm.min_int(int(min(n, 4_000_000)))  # every TP rank holds the same pool
         log.info("KV cache: %d blocks x %d tokens = %d tokens (%.1f GiB)", n, self.bs, n * self.bs,
                  n * per_block / 2**30)
         return n
@@ -166,7 +167,14 @@ class ModelRunner:
         return temp, topp, topk, seeds, steps
 
     def _mixed(self, batch: ScheduledBatch, masks) -> List[int]:
-        self.stats["prefill_steps"] += 1
+        host = self._mixed_host(batch)
+        if self.bcast is not None:
+            self.bcast.send(("mixed", host, masks))
+        return self._mixed_run(host, masks)
+
+    def _mixed_host(self, batch: ScheduledBatch) -> Dict[str, object]:
+        """Host-side (numpy) inputs of an eager mixed decode+prefill step; this is
+        also the message tensor-parallel workers receive."""
         dseqs = batch.decode_seqs
         pseqs = [s for s, n in zip(batch.prefill_seqs, batch.prefill_tokens) if n > 0]
         ntoks = [n for n in batch.prefill_tokens if n > 0]
@@ -174,6 +182,7 @@ class ModelRunner:
         bs = self.bs
         nd = len(dseqs)
         ids, pos, slots = [], [], []
+        host: Dict[str, object] = {"nd": nd}
         # decode rows
         if nd:
             d_ids = np.empty(nd, np.int32)
@@ -189,6 +198,8 @@ class ModelRunner:
             ids.append(d_ids)
             pos.append(d_pos)
             slots.append(d_slot)
+            host["d_bt"] = d_bt
+            host["d_sl"] = d_pos + 1
         # prefill rows
         seq_lens = np.empty(len(pseqs), np.int32)
         qsl = np.zeros(len(pseqs) + 1, np.int32)
@@ -207,29 +218,37 @@ class ModelRunner:
         tiles = ops.build_prefill_tiles(ntoks, ops.prefill_tile_tokens(self.model.nq, self.model.nkv))
         # logits rows: every decode row + the last row of each prompt that completes
         lrows = list(range(nd)) + [nd + int(qsl[i + 1]) - 1 for i, sm in enumerate(psamp) if sm]
+        host.update(ids=np.concatenate(ids).astype(np.int32), pos=np.concatenate(pos).astype(np.int32),
+                    slots=np.concatenate(slots).astype(np.int32), lrows=np.asarray(lrows, np.int64),
+                    bt=bt, seq_lens=seq_lens, qsl=qsl, tiles=np.asarray(tiles, np.int32).reshape(-1),
+                    num_tiles=len(tiles))
+        sseqs = dseqs + [s for s, sm in zip(pseqs, psamp) if sm]
+        host["sampling"] = self._sampling_arrays(sseqs)
+        return host
+
+    def _mixed_run(self, host: Dict[str, object], masks) -> List[int]:
+        self.stats["prefill_steps"] += 1
+        nd = host["nd"]
         dv = self.device
         t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dv, non_blocking=True)  # noqa: E731
+        qsl = host["qsl"]
         meta = AttnMeta(
-            positions=t(np.concatenate(pos).astype(np.int32)),
-            slot_mapping=t(np.concatenate(slots).astype(np.int32)),
-            logits_indices=t(np.asarray(lrows, np.int64)),
-            num_decode=nd,
-            block_tables=t(bt), seq_lens=t(seq_lens),
+            positions=t(host["pos"]), slot_mapping=t(host["slots"]),
+            logits_indices=t(host["lrows"]), num_decode=nd,
+            block_tables=t(host["bt"]), seq_lens=t(host["seq_lens"]),
             q_start_loc=t(qsl) if self.is_gpu else torch.from_numpy(qsl),
-            tile_info=t(np.asarray(tiles, np.int32).reshape(-1)), num_tiles=len(tiles))
+            tile_info=t(host["tiles"]), num_tiles=host["num_tiles"])
         if nd:
             splits = self._splits_for_batch(nd)
-            meta.dec_block_tables = t(d_bt)
-            meta.dec_seq_lens = t(d_pos + 1)
+            meta.dec_block_tables = t(host["d_bt"])
+            meta.dec_seq_lens = t(host["d_sl"])
             meta.max_splits = splits
             meta.tmp_out, meta.tmp_ml = self._tmp(nd, splits)
-        input_ids = t(np.concatenate(ids).astype(np.int32))
-        if not lrows:
-            self.model.forward(input_ids, meta, self.kv)
-            return []
+        input_ids = t(host["ids"])
         h = self.model.forward(input_ids, meta, self.kv)
-        sseqs = dseqs + [s for s, sm in zip(pseqs, psamp) if sm]
-        return self._sample(h, sseqs, masks)
+        if len(host["lrows"]) == 0:
+            return []
+        return self._sample(h, host["sampling"], masks)
 
     def _tmp(self, n: int, splits: int):
         nq, d = self.model.nq, self.model.d
@@ -248,9 +267,9 @@ class ModelRunner:
         while not ev.query():
             time.sleep(0.0001)
 
-    def _sample(self, h, seqs, masks) -> List[int]:
+    def _sample(self, h, sampling, masks) -> List[int]:
         logits = self.model.compute_logits(h)
-        temp, topp, topk, seeds, steps = self._sampling_arrays(seqs)
+        temp, topp, topk, seeds, steps = sampling
         dv = self.device
         m = None
         if masks is not None:
@@ -277,6 +296,17 @@ class ModelRunner:
         if bucket is None:
             return self._decode_eager(seqs, self._splits_for_batch(n), masks)
         nb = bucket
+        maxblk = self._decode_fill(seqs, nb)
+        if self.bcast is not None:
+            mb = self.max_decode_batch
+            self.bcast.send(("graph", {"nb": nb, "n": n, "small": self._hs.copy(),
+                                       "bt": self._hbt[:nb, :maxblk].copy(),
+                                       "f32": self._hf.copy(), "seeds": self._hseed.copy()}, None))
+        return self._decode_run(nb, n)
+
+    def _decode_fill(self, seqs, nb: int) -> int:
+        """Writes a decode step's inputs into the pinned staging buffers."""
+        n = len(seqs)
         mb = self.max_decode_batch
         hs = self._hs
         ids = hs[0:mb]
@@ -285,13 +315,16 @@ class ModelRunner:
         sl = hs[3 * mb:4 * mb]
         bt = self._hbt
         bs = self.bs
+        maxblk = 1
         for i, s in enumerate(seqs):
             p = s.n_tokens - 1
             ids[i] = s.last_token
             pos[i] = p
             slots[i] = s.block_ids[p // bs] * bs + p % bs
             sl[i] = p + 1
-            bt[i, :len(s.block_ids)] = s.block_ids
+            nbk = len(s.block_ids)
+            bt[i, :nbk] = s.block_ids
+            maxblk = max(maxblk, nbk)
         temp, topp, topk, seeds, steps = self._sampling_arrays(seqs)
         hs[4 * mb:4 * mb + n] = topk
         hs[5 * mb:5 * mb + n] = steps
@@ -308,6 +341,9 @@ class ModelRunner:
             hs[5 * mb + n:5 * mb + nb] = 0
             self._hf[n:nb] = 0.0
             self._hf[mb + n:mb + nb] = 1.0
+        return maxblk
+
+    def _decode_run(self, nb: int, n: int) -> List[int]:
         self.d_small.copy_(self.h_small, non_blocking=True)
         self.d_bt[:nb].copy_(self.h_bt[:nb], non_blocking=True)
         self.d_f32.copy_(self.h_f32, non_blocking=True)
@@ -320,6 +356,30 @@ class ModelRunner:
         self.h_out[:n].copy_(self.d_out[:n], non_blocking=True)
         self._wait()
         return self.h_out[:n].tolist()
+
+    # ------------------------------------------------------------------ TP workers
+    @torch.inference_mode()
+    def run_remote(self, msg) -> bool:
+        """Executes one message broadcast by TP rank 0 (same kernels, same
+        collectives, same order).  Returns False on ``stop``."""
+        kind, host, masks = msg
+        if kind == "stop":
+            return False
+        if kind == "mixed":
+            self._mixed_run(host, masks)
+        elif kind == "graph":
+            nb, n = host["nb"], host["n"]
+            self._hs[:] = host["small"]
+            bt = host["bt"]
+            self._hbt[:nb, :bt.shape[1]] = bt
+            self._hf[:] = host["f32"]
+            self._hseed[:] = host["seeds"]
+            self._decode_run(nb, n)
+        elif kind == "warmup":
+            self.warmup(host)
+        else:
+            raise ValueError(f"unknown TP message {kind!r}")
+        return True
 
     def _decode_meta(self, nb: int, splits: int) -> AttnMeta:
         assert nb * splits <= self.tmp_rows
@@ -369,6 +429,8 @@ class ModelRunner:
         serving never pays for a capture."""
         if not self.use_graphs:
             return
+        if self.bcast is not None:
+            self.bcast.send(("warmup", list(batch_sizes or self.graph_sizes), None))
         t0 = time.time()
         for b in batch_sizes or self.graph_sizes:
             b = self._bucket(b)

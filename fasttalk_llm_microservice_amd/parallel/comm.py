@@ -47,6 +47,15 @@ class TPComm:
         dist.all_gather(parts, x.contiguous(), group=self.group)
         return torch.cat(parts, dim=-1)
 
+    def min_int(self, v: int) -> int:
+        """Smallest value of ``v`` over the group (e.g. KV blocks every rank can hold)."""
+        if self.world_size == 1:
+            return int(v)
+        dev = "cuda" if dist.get_backend(self.group) == "nccl" else "cpu"
+        t = torch.tensor([int(v)], dtype=torch.int64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.group)
+        return int(t.item())
+
     def broadcast_obj(self, obj, src: int = 0):
         if self.world_size == 1:
             return obj

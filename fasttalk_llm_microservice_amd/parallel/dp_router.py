@@ -1,0 +1,311 @@
+"""Data-parallel serving inside one service (SURVEY.md §2.6 P2 "DP replicas +
+session-affinity router"): ``ENGINE_DP_SIZE=N`` runs N engine replicas, each in
+its own process on its own GPU(s) (replica i owns GPUs [i*tp, (i+1)*tp), and
+``ENGINE_TP_SIZE>1`` makes each replica a TP group of its own).
+
+The router keeps every conversation on the replica that already holds its KV
+blocks (multi-turn prefix reuse only works there) and sends a new conversation
+to the replica with the fewest active requests.  It exposes the AsyncEngine
+surface (``generate`` / ``abort`` / ``is_healthy`` / ``model_info`` and an
+``engine`` facade with tokenizer, chat template and aggregated ``metrics()``)
+so :class:`app.core.native_handler.NativeHandler` cannot tell the difference.
+
+Replica protocol (``multiprocessing`` pipe, both directions pickled):
+  router -> replica: ("add", rid, prompt_ids, params) | ("abort", rid) | ("stop",)
+  replica -> router: ("ready", info) | ("out", [RequestOutput...], metrics) | ("dead", err)
+"""
+from __future__ import annotations
+
+import asyncio
+import collections
+import itertools
+import logging
+import multiprocessing as mp
+import os
+import threading
+import time
+import uuid
+from typing import Any, AsyncIterator, Dict, List, Optional, Sequence as Seq
+
+from ..engine.chat_template import ChatTemplate
+from ..engine.engine import EngineError
+from ..engine.sequence import RequestOutput
+from ..engine.tokenizer import get_tokenizer
+from ..models.config import resolve_model
+
+log = logging.getLogger("fasttalk.dp")
+
+
+def _replica_main(index: int, cfg, conn):
+    """Replica process: one engine (TP group when cfg.tp_size > 1) + step loop."""
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    try:
+        base = index * max(1, cfg.tp_size)
+        if cfg.resolved_device() == "cuda":
+            import torch
+
+            torch.cuda.set_device(base)
+        if cfg.tp_size > 1:
+            from .tp import spawn_tp_engine
+
+            eng = spawn_tp_engine(cfg, device_base=base)
+        else:
+            from ..engine.engine import LLMEngine
+
+            eng = LLMEngine(cfg)
+        if cfg.resolved_device() == "cuda" and not cfg.enforce_eager:
+            eng.runner.warmup()
+    except BaseException as e:  # pragma: no cover - reported to the router
+        conn.send(("dead", repr(e)))
+        return
+    conn.send(("ready", {"num_blocks": eng.bm.num_blocks, "max_model_len": eng.max_model_len}))
+    outs: List[RequestOutput] = []
+    last_metrics = 0.0
+    try:
+        while True:
+            timeout = 0.0 if eng.has_work() else 0.05
+            while conn.poll(timeout):
+                cmd = conn.recv()
+                timeout = 0.0
+                if cmd[0] == "add":
+                    _, rid, prompt, params = cmd
+                    try:
+                        eng.add_request(rid, prompt, params, on_output=outs.append)
+                    except Exception as e:
+                        outs.append(RequestOutput(rid, "", [], finished=True, finish_reason="error",
+                                                  error=str(e)))
+                elif cmd[0] == "abort":
+                    eng.abort(cmd[1])
+                elif cmd[0] == "stop":
+                    return
+            if eng.has_work():
+                eng.step()
+            now = time.time()
+            metrics = None
+            if now - last_metrics > 0.5:
+                metrics = eng.metrics()
+                last_metrics = now
+            if outs or metrics is not None:
+                conn.send(("out", list(outs), metrics))
+                outs.clear()  # the sequences' on_output callbacks append to this list
+    finally:
+        eng.shutdown()
+
+
+class _Replica:
+    def __init__(self, index: int, cfg, ctx):
+        self.index = index
+        self.conn, child = ctx.Pipe()
+        self.proc = ctx.Process(target=_replica_main, args=(index, cfg, child), daemon=True,
+                                name=f"fasttalk-dp{index}")
+        self.proc.start()
+        child.close()
+        self.lock = threading.Lock()
+        self.active = 0
+        self.metrics: Dict[str, Any] = {}
+        self.info: Dict[str, Any] = {}
+        self.error: Optional[str] = None
+
+    def send(self, msg):
+        with self.lock:
+            self.conn.send(msg)
+
+
+class _Facade:
+    """What NativeHandler / the server read from ``engine.engine``."""
+
+    def __init__(self, router: "MultiGPUEngine", cfg):
+        self._router = router
+        self.cfg = cfg
+        self.model_cfg = resolve_model(cfg.weights if cfg.weights not in ("random", None, "")
+                                       else cfg.model)
+        tok_path = cfg.tokenizer or (cfg.weights if cfg.weights not in ("random", None, "") else None)
+        self.tokenizer = get_tokenizer(tok_path)
+        self.template = ChatTemplate(self.tokenizer)
+        self.max_model_len = min(cfg.max_model_len, self.model_cfg.max_position_embeddings)
+
+    def token_trie(self):
+        from ..runtime import rt
+
+        if getattr(self, "_trie", None) is None:
+            self._trie = rt().TokenTrie(self.tokenizer.id_to_bytes)
+        return self._trie
+
+    def metrics(self) -> Dict[str, Any]:
+        reps = [r.metrics for r in self._router.replicas]
+        agg: Dict[str, Any] = {"replicas": len(reps), "per_replica": reps}
+        for key in ("running", "waiting", "kv_blocks_total", "kv_blocks_free", "generated_tokens",
+                    "prefill_tokens", "requests", "preemptions"):
+            agg[key] = sum(int(m.get(key, 0) or 0) for m in reps)
+        tot = agg["kv_blocks_total"]
+        agg["kv_usage"] = 1.0 - agg["kv_blocks_free"] / tot if tot else 0.0
+        return agg
+
+
+class MultiGPUEngine:
+    def __init__(self, cfg):
+        self.cfg = cfg
+        self.dp = max(1, cfg.dp_size)
+        self.ctx = mp.get_context("spawn")
+        self.replicas: List[_Replica] = []
+        self.engine = _Facade(self, cfg)
+        self._streams: Dict[str, asyncio.Queue] = {}
+        self._loops: Dict[str, asyncio.AbstractEventLoop] = {}
+        self._owner: Dict[str, _Replica] = {}
+        self._affinity: "collections.OrderedDict[str, int]" = collections.OrderedDict()
+        self._ids = itertools.count()
+        self._readers: List[threading.Thread] = []
+        self._stop = False
+
+    # ------------------------------------------------------------------ lifecycle
+    def start(self, timeout: float = 1800.0):
+        self.replicas = [_Replica(i, self.cfg, self.ctx) for i in range(self.dp)]
+        t0 = time.time()
+        for r in self.replicas:
+            while not r.conn.poll(1.0):
+                if not r.proc.is_alive() or time.time() - t0 > timeout:
+                    raise EngineError(f"DP replica {r.index} failed to start")
+            kind, payload = r.conn.recv()
+            if kind != "ready":
+                raise EngineError(f"DP replica {r.index} failed: {payload}")
+            r.info = payload
+        for r in self.replicas:
+            th = threading.Thread(target=self._reader, args=(r,), daemon=True,
+                                  name=f"fasttalk-dp-reader{r.index}")
+            th.start()
+            self._readers.append(th)
+        log.info("DP engine: %d replicas ready in %.1fs", self.dp, time.time() - t0)
+        return self
+
+    def shutdown(self):
+        self._stop = True
+        for r in self.replicas:
+            try:
+                r.send(("stop",))
+            except Exception:
+                pass
+        for r in self.replicas:
+            r.proc.join(timeout=30)
+            if r.proc.is_alive():
+                r.proc.terminate()
+
+    def is_healthy(self, stall_s: float = 120.0) -> bool:
+        return bool(self.replicas) and all(r.proc.is_alive() and r.error is None
+                                           for r in self.replicas)
+
+    # ------------------------------------------------------------------ plumbing
+    def _reader(self, r: _Replica):
+        while not self._stop:
+            try:
+                msg = r.conn.recv()
+            except (EOFError, OSError):
+                r.error = "replica exited"
+                self._fail_replica(r)
+                return
+            if msg[0] == "out":
+                _, outs, metrics = msg
+                if metrics is not None:
+                    r.metrics = metrics
+                by_loop: Dict[asyncio.AbstractEventLoop, list] = {}
+                for o in outs:
+                    loop = self._loops.get(o.request_id)
+                    if loop is not None:
+                        by_loop.setdefault(loop, []).append(o)
+                for loop, items in by_loop.items():
+                    try:
+                        loop.call_soon_threadsafe(self._dispatch, items)
+                    except RuntimeError:
+                        pass
+            elif msg[0] == "dead":
+                r.error = msg[1]
+                self._fail_replica(r)
+                return
+
+    def _fail_replica(self, r: _Replica):
+        for rid, owner in list(self._owner.items()):
+            if owner is r:
+                loop = self._loops.get(rid)
+                if loop is not None:
+                    err = RequestOutput(rid, "", [], finished=True, finish_reason="error",
+                                        error=f"DP replica {r.index} failed: {r.error}")
+                    try:
+                        loop.call_soon_threadsafe(self._dispatch, [err])
+                    except RuntimeError:
+                        pass
+
+    def _dispatch(self, items: List[RequestOutput]):
+        for o in items:
+            q = self._streams.get(o.request_id)
+            if q is not None:
+                q.put_nowait(o)
+
+    def _pick(self, rid: str) -> _Replica:
+        key = rid.split("#", 1)[0]
+        idx = self._affinity.get(key)
+        if idx is None or self.replicas[idx].error is not None:
+            live = [r for r in self.replicas if r.error is None] or self.replicas
+            idx = min(live, key=lambda r: r.active).index
+            self._affinity[key] = idx
+            while len(self._affinity) > 100_000:
+                self._affinity.popitem(last=False)
+        else:
+            self._affinity.move_to_end(key)
+        return self.replicas[idx]
+
+    # ------------------------------------------------------------------ public API
+    def new_request_id(self) -> str:
+        return f"dp-{next(self._ids)}-{uuid.uuid4().hex[:6]}"
+
+    async def generate(self, prompt_ids: Seq[int], params, request_id: Optional[str] = None
+                       ) -> AsyncIterator[RequestOutput]:
+        rid = request_id or self.new_request_id()
+        if rid in self._streams:
+            raise EngineError(f"duplicate request id {rid}")
+        rep = self._pick(rid)
+        if rep.error is not None:
+            raise EngineError(f"DP replica {rep.index} failed: {rep.error}")
+        q: asyncio.Queue = asyncio.Queue()
+        self._streams[rid] = q
+        self._loops[rid] = asyncio.get_running_loop()
+        self._owner[rid] = rep
+        rep.active += 1
+        finished = False
+        try:
+            rep.send(("add", rid, list(prompt_ids), params))
+            while True:
+                o = await q.get()
+                finished = o.finished
+                yield o
+                if finished:
+                    break
+        finally:
+            rep.active -= 1
+            self._streams.pop(rid, None)
+            self._loops.pop(rid, None)
+            self._owner.pop(rid, None)
+            if not finished and rep.error is None:
+                try:
+                    rep.send(("abort", rid))
+                except Exception:
+                    pass
+
+    def abort(self, request_id: str) -> bool:
+        rep = self._owner.get(request_id)
+        if rep is None:
+            return False
+        rep.send(("abort", request_id))
+        return True
+
+    def active_requests(self) -> List[str]:
+        return list(self._owner)
+
+    def model_info(self) -> Dict[str, Any]:
+        m = self.engine.model_cfg
+        return {
+            "model": m.name, "num_layers": m.num_layers, "hidden_size": m.hidden_size,
+            "num_heads": m.num_heads, "num_kv_heads": m.num_kv_heads, "vocab_size": m.vocab_size,
+            "max_model_len": self.engine.max_model_len, "weights": self.cfg.weights,
+            "tensor_parallel_size": self.cfg.tp_size, "data_parallel_size": self.dp,
+            "kv_cache_tokens": sum(r.info.get("num_blocks", 0) for r in self.replicas) *
+            self.cfg.block_size,
+        }

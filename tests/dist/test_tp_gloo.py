@@ -1,0 +1,107 @@
+"""Tensor parallelism on the CPU over gloo (SURVEY.md §4 "Distributed": TP logic
+runs with 2 processes, no GPU).  Rank 0 is this test process; rank 1 is a
+spawned worker fed by the shared-memory step broadcast.  Weights of small
+models are drawn unsharded from one seed and sliced, so TP=2 must reproduce
+TP=1 token for token."""
+import multiprocessing as mp
+import time
+
+import numpy as np
+import pytest
+
+from fasttalk_llm_microservice_amd.engine.config import EngineConfig
+from fasttalk_llm_microservice_amd.engine.engine import LLMEngine
+from fasttalk_llm_microservice_amd.engine.sampling_params import SamplingParams
+from fasttalk_llm_microservice_amd.parallel.shm_broadcast import ShmBroadcast
+
+
+def _cfg(**kw):
+    base = dict(model="tiny", device="cpu", num_kv_blocks=256, max_model_len=1024, max_num_seqs=8,
+                max_num_batched_tokens=64)
+    base.update(kw)
+    return EngineConfig(**base)
+
+
+def test_tp2_generation_matches_tp1():
+    from fasttalk_llm_microservice_amd.parallel.tp import spawn_tp_engine
+
+    rng = np.random.default_rng(0)
+    prompts = [rng.integers(0, 120000, n).tolist() for n in (9, 70, 30)]
+    sp = SamplingParams(temperature=0, max_tokens=6, ignore_eos=True)
+    ref = LLMEngine(_cfg()).generate(prompts, sp)
+    eng = spawn_tp_engine(_cfg(tp_size=2))
+    try:
+        assert eng.runner.model.nq == 4 and eng.runner.model.nkv == 1  # half the heads per rank
+        out = eng.generate(prompts, sp)
+        # seeded sampling is identical across ranks too (every rank samples the gathered logits)
+        sp2 = SamplingParams(temperature=0.8, top_p=0.9, max_tokens=4, seed=7, ignore_eos=True)
+        out2 = eng.generate(prompts[:1], sp2)
+    finally:
+        eng.shutdown()
+    assert out == ref
+    assert out2 == LLMEngine(_cfg()).generate(prompts[:1], sp2)
+
+
+def _reader(name, idx, q):
+    b = ShmBroadcast(2, name=name, create=False, reader_index=idx, num_slots=4, slot_bytes=1 << 12)
+    total = 0
+    while True:
+        m = b.recv(timeout=30)
+        if m is None:
+            break
+        total += int(m["x"].sum())
+    q.put(total)
+    b.close()
+
+
+def test_shm_broadcast_ring_and_overflow():
+    w = ShmBroadcast(2, num_slots=4, slot_bytes=1 << 12)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_reader, args=(w.name, i, q)) for i in range(2)]
+    for p in ps:
+        p.start()
+    expect = 0
+    for i in range(200):
+        x = np.arange(i % 7 * 300 + 1)  # every 7th message overflows the 4 KiB slot
+        expect += int(x.sum())
+        w.send({"x": x}, timeout=30)
+    w.send(None, timeout=30)
+    got = sorted([q.get(timeout=60), q.get(timeout=60)])
+    for p in ps:
+        p.join(timeout=30)
+    w.close()
+    assert got == [expect, expect]
+
+
+def test_dp2_router_session_affinity_and_outputs():
+    import asyncio
+
+    from fasttalk_llm_microservice_amd.parallel.dp_router import MultiGPUEngine
+
+    rng = np.random.default_rng(3)
+    prompts = [rng.integers(0, 120000, n).tolist() for n in (12, 40, 25, 7)]
+    sp = SamplingParams(temperature=0, max_tokens=5, ignore_eos=True)
+    ref = LLMEngine(_cfg()).generate(prompts, sp)
+    eng = MultiGPUEngine(_cfg(dp_size=2)).start()
+    try:
+        async def one(i, p, sid):
+            ids = []
+            async for o in eng.generate(p, sp, request_id=f"{sid}#{i}"):
+                ids.extend(o.token_ids)
+            return ids
+
+        async def run():
+            return await asyncio.gather(*[one(i, p, f"sess{i % 2}") for i, p in enumerate(prompts)])
+
+        out = asyncio.run(run())
+        assert out == ref
+        # each conversation stayed on one replica, and both replicas were used
+        assert set(eng._affinity) == {"sess0", "sess1"}
+        assert len(set(eng._affinity.values())) == 2
+        assert eng.is_healthy() and eng.model_info()["data_parallel_size"] == 2
+        time.sleep(0.6)
+        asyncio.run(one(9, prompts[0], "sess0"))
+        assert eng.engine.metrics()["replicas"] == 2
+    finally:
+        eng.shutdown()
