@@ -37,6 +37,10 @@ int ft_kv_block_copy(void* k_cache, void* v_cache, const int* src_dst, int num_p
                      long block_elems, hipStream_t stream);
 int ft_skinny_gemm(const void* x, int x_stride, int M, const void* w, int N, int K, float* ws,
                    void* out, int out_stride, int splits, int nt, int u, hipStream_t stream);
+int ft_skinny_gemm_ks(const void* x, int x_stride, int M, const void* w, int N, int K, float* ws,
+                      void* out, int out_stride, int splits, int nt, hipStream_t stream);
+int ft_skinny_gemm_xs(const void* x, int x_stride, int M, const void* w, int N, int K, float* ws,
+                      void* out, int out_stride, int splits, int nt, hipStream_t stream);
 int ft_row_rmsnorm(const void* x, int x_stride, const float* ws, int splits, void* out,
                    int out_stride, void* residual, const void* w, int rows, int hidden, float eps,
                    hipStream_t stream);
@@ -281,9 +285,18 @@ void skinny_gemm(at::Tensor x, at::Tensor w, c10::optional<at::Tensor> out,
     op = out->data_ptr();
     ostride = (int)out->stride(0);
   }
-  check_rc(ft_skinny_gemm(x.data_ptr(), (int)x.stride(0), M, w.data_ptr(), N, K, wsp, op, ostride,
-                          (int)splits, (int)nt, (int)u, cur_stream()),
-           "skinny_gemm");
+  if (u < 0)  // x-in-LDS variant
+    check_rc(ft_skinny_gemm_xs(x.data_ptr(), (int)x.stride(0), M, w.data_ptr(), N, K, wsp, op,
+                               ostride, (int)splits, (int)nt, cur_stream()),
+             "skinny_gemm_xs");
+  else if (u == 0)  // K-split-wave variant
+    check_rc(ft_skinny_gemm_ks(x.data_ptr(), (int)x.stride(0), M, w.data_ptr(), N, K, wsp, op,
+                               ostride, (int)splits, (int)nt, cur_stream()),
+             "skinny_gemm_ks");
+  else
+    check_rc(ft_skinny_gemm(x.data_ptr(), (int)x.stride(0), M, w.data_ptr(), N, K, wsp, op, ostride,
+                            (int)splits, (int)nt, (int)u, cur_stream()),
+             "skinny_gemm");
 }
 
 // out = rmsnorm([residual +=] src) * w where src = bf16 x or the fp32 slabs in ws

@@ -81,17 +81,15 @@ __device__ __forceinline__ void dec_load_tile(DecTile<D, G>& t, const uint16_t* 
                                               const uint16_t* __restrict__ v_cache, size_t base,
                                               int valid_tokens, int ts, int c) {
   using T = DecTile<D, G>;
+  // unconditional loads (slots past the end re-read the last valid token and
+  // are masked in dec_consume_tile): a uniform load count lets the compiler
+  // wait with exact vmcnt values instead of draining at a branch merge
 #pragma unroll
   for (int u = 0; u < T::U; ++u) {
-    const int tl = u * T::TPW + ts;
-    if (tl < valid_tokens) {
-      const size_t off = base + (size_t)tl * D;
-      t.k[u] = reinterpret_cast<const uint4*>(k_cache + off)[c];
-      t.v[u] = reinterpret_cast<const uint4*>(v_cache + off)[c];
-    } else {
-      t.k[u] = make_uint4(0, 0, 0, 0);
-      t.v[u] = make_uint4(0, 0, 0, 0);
-    }
+    const int tl = min(u * T::TPW + ts, valid_tokens - 1);
+    const size_t off = base + (size_t)tl * D;
+    t.k[u] = reinterpret_cast<const uint4*>(k_cache + off)[c];
+    t.v[u] = reinterpret_cast<const uint4*>(v_cache + off)[c];
   }
 }
 
@@ -209,15 +207,24 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(
     };
     auto tile_valid = [&](int i) { return n - 16 * (wave + 4 * (c0 + i)); };
     // double-buffered: tile i+1's K/V loads are in flight while tile i computes
+    // (a prefetch index past the end re-loads the last tile: L2 hit, never consumed)
+    auto ld = [&](DecTile<D, G>& t, int i) {
+      const int j = min(i, cnt - 1);
+      dec_load_tile<D, G>(t, k_cache, v_cache, tile_base(j), tile_valid(j), ts, c);
+    };
     DecTile<D, G> ta, tb;
-    dec_load_tile<D, G>(ta, k_cache, v_cache, tile_base(0), tile_valid(0), ts, c);
+    ld(ta, 0);
     int i = 0;
+    // sched_barrier(0) keeps each prefetch ahead of the math it overlaps
     for (; i + 1 < cnt; i += 2) {
-      dec_load_tile<D, G>(tb, k_cache, v_cache, tile_base(i + 1), tile_valid(i + 1), ts, c);
+      ld(tb, i + 1);
+      __builtin_amdgcn_sched_barrier(0);
       dec_consume_tile<D, G>(ta, qp, tile_valid(i), ts, scale_log2, m, l, acc);
-      if (i + 2 < cnt)
-        dec_load_tile<D, G>(ta, k_cache, v_cache, tile_base(i + 2), tile_valid(i + 2), ts, c);
+      __builtin_amdgcn_sched_barrier(0);
+      ld(ta, i + 2);
+      __builtin_amdgcn_sched_barrier(0);
       dec_consume_tile<D, G>(tb, qp, tile_valid(i + 1), ts, scale_log2, m, l, acc);
+      __builtin_amdgcn_sched_barrier(0);
     }
     if (i < cnt) dec_consume_tile<D, G>(ta, qp, tile_valid(i), ts, scale_log2, m, l, acc);
   }
