@@ -213,3 +213,29 @@ def test_service_monitor_metrics_and_prometheus(monkeypatch, engine):
     assert c.get("/metrics").get_json()["requests"] == 1
     assert c.get("/info").get_json()["service"] == "llm-service"
     assert b"fasttalk_requests" in c.get("/metrics/prometheus").data
+
+
+def test_manual_client_scripted(monkeypatch, engine, capsys):
+    """The shipped test_llm_client.py drives a real socket session end to end."""
+    import test_llm_client
+
+    from app.core.websocket_server_vllm import WebSocketLLMServer
+    from app.server.asgi_aiohttp import AiohttpASGIServer
+    from app.utils.config import Config
+
+    monkeypatch.setenv("LLM_PROVIDER", "native")
+    monkeypatch.setenv("ENABLE_PYDANTIC_AI", "false")
+    srv = WebSocketLLMServer(Config(), engine=engine)
+
+    async def main():
+        asgi = AiohttpASGIServer(srv.app, "127.0.0.1", 0)
+        await asgi.start()
+        try:
+            return await test_llm_client.run(f"ws://127.0.0.1:{asgi.port}/ws/llm", ["hello", "again"],
+                                             {"max_tokens": 4, "temperature": 0.0, "ignore_eos": True})
+        finally:
+            await asgi.stop()
+
+    assert asyncio.run(main()) == 0
+    out = capsys.readouterr().out
+    assert out.count("[4 tokens") == 2 and "session ended" in out
