@@ -69,7 +69,7 @@ def main():
         out = torch.empty(M, n, device=dev).bfloat16()
         for nt, u in ops.SKINNY_CONFIGS:
             for splits in (1, 2, 4, 8, 16):
-                kstep = 64 * (u if u > 0 else 1) * splits
+                kstep = (512 if u == -2 else 64 * (u if u > 0 else 1)) * splits
                 if n % (16 * nt) or k % kstep or splits * M * n > ws.numel():
                     continue
                 cols = 16 * nt if u == 0 else 64 * nt
@@ -90,7 +90,7 @@ def main():
                 rows.append((t, nt, u, splits, blocks, err))
         rows.sort()
         for t, nt, u, splits, blocks, err in rows[: a.top]:
-            print(f"   {({0: 'ks', -1: 'xs'}).get(u, 'cs')} nt={nt} u={u} splits={splits:2d} blocks={blocks:5d}: "
+            print(f"   {({0: 'ks', -1: 'xs', -2: 'xc'}).get(u, 'cs')} nt={nt} u={u} splits={splits:2d} blocks={blocks:5d}: "
                   f"{t:7.2f} us ({n * k * 2 / t / 1e3:5.0f} GB/s) err={err:.4f}", flush=True)
         bad = [r for r in rows if r[5] > 0.05]
         if bad:

@@ -41,6 +41,8 @@ int ft_skinny_gemm_ks(const void* x, int x_stride, int M, const void* w, int N, 
                       void* out, int out_stride, int splits, int nt, hipStream_t stream);
 int ft_skinny_gemm_xs(const void* x, int x_stride, int M, const void* w, int N, int K, float* ws,
                       void* out, int out_stride, int splits, int nt, hipStream_t stream);
+int ft_skinny_gemm_xc(const void* x, int x_stride, int M, const void* w, int N, int K, float* ws,
+                      void* out, int out_stride, int splits, int nt, hipStream_t stream);
 int ft_row_rmsnorm(const void* x, int x_stride, const float* ws, int splits, void* out,
                    int out_stride, void* residual, const void* w, int rows, int hidden, float eps,
                    hipStream_t stream);
@@ -285,7 +287,11 @@ void skinny_gemm(at::Tensor x, at::Tensor w, c10::optional<at::Tensor> out,
     op = out->data_ptr();
     ostride = (int)out->stride(0);
   }
-  if (u < 0)  // x-in-LDS variant
+  if (u == -2)  // x-chunk variant
+    check_rc(ft_skinny_gemm_xc(x.data_ptr(), (int)x.stride(0), M, w.data_ptr(), N, K, wsp, op,
+                               ostride, (int)splits, (int)nt, cur_stream()),
+             "skinny_gemm_xc");
+  else if (u < 0)  // x-in-LDS variant
     check_rc(ft_skinny_gemm_xs(x.data_ptr(), (int)x.stride(0), M, w.data_ptr(), N, K, wsp, op,
                                ostride, (int)splits, (int)nt, cur_stream()),
              "skinny_gemm_xs");

@@ -386,6 +386,116 @@ __global__ __launch_bounds__(256) void skinny_xs_kernel(
     }
 }
 
+
+// ---------------------------------------------------------------------------
+// Variant "xc" (x chunks in LDS, deep weight streaming): per 512-wide K chunk
+// the workgroup stages x[rows, 512] in LDS once (full-line loads, XOR
+// swizzle) while every wave issues ALL of the chunk's weight loads for its
+// 16*NT columns at once (8 k-steps x NT x 2 x 16 B per lane = 16-32 KiB per
+// wave in flight), then runs the chunk's MFMAs as the weights land.  Two
+// barriers per chunk; x loads are issued before the weight loads so the wait
+// for x is an exact vmcnt that leaves the weight stream in flight.
+template <int MT, int NT>
+__global__ __launch_bounds__(256) void skinny_xc_kernel(
+    const uint16_t* __restrict__ x, int x_stride, int M, const uint16_t* __restrict__ w, int K,
+    float* __restrict__ ws, uint16_t* __restrict__ out, int out_stride, int N, int k_slice) {
+  constexpr int KC = 512;                          // k per chunk (8 MFMA k-steps of 64)
+  constexpr int ROWS = 16 * MT;
+  constexpr int CPR = KC / 8;                      // 16-B chunks per x row per chunk (64)
+  constexpr int XL = ROWS * CPR / 256;             // x loads per thread per chunk
+  __shared__ __attribute__((aligned(16))) uint16_t s_x[ROWS * KC];
+  const int tid = threadIdx.x;
+  const int lane = lane_id(), wave = wave_id();
+  const int l15 = lane & 15, g = lane >> 4;
+  const int n0 = (blockIdx.x * 4 + wave) * (16 * NT);
+  const int s = blockIdx.y;
+  const int kbeg = s * k_slice;
+  const bool active = n0 < N;
+
+  const uint16_t* wp[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j)
+    wp[j] = w + (size_t)min(n0 + 16 * j + l15, N - 1) * K + kbeg + 16 * g;
+
+  sk_floatx4 acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = sk_floatx4{0.f, 0.f, 0.f, 0.f};
+
+  for (int kc = 0; kc < k_slice; kc += KC) {
+    // x chunk: element e = tid + 256*p -> row e / CPR, 16-B chunk e % CPR;
+    // swizzle: chunk c of row r lives at slot c ^ (r & 7) (within its 128-B line group)
+    uint4 xr[XL];
+#pragma unroll
+    for (int p = 0; p < XL; ++p) {
+      const int e = tid + 256 * p;
+      const int row = e / CPR, ch = e % CPR;
+      xr[p] = *reinterpret_cast<const uint4*>(x + (size_t)min(row, M - 1) * x_stride + kbeg + kc +
+                                              ch * 8);
+    }
+    uint4 wr[8][NT][2];
+#pragma unroll
+    for (int st = 0; st < 8; ++st)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        wr[st][j][0] = nt_load16(wp[j] + kc + st * 64);
+        wr[st][j][1] = nt_load16(wp[j] + kc + st * 64 + 8);
+      }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int p = 0; p < XL; ++p) {
+      const int e = tid + 256 * p;
+      const int row = e / CPR, ch = e % CPR;
+      const int slot = (ch & ~7) | ((ch & 7) ^ (row & 7));
+      *reinterpret_cast<uint4*>(&s_x[row * KC + slot * 8]) = xr[p];
+    }
+    __syncthreads();
+    if (active) {
+#pragma unroll
+      for (int st = 0; st < 8; ++st) {
+#pragma unroll
+        for (int i = 0; i < MT; ++i) {
+          const int row = 16 * i + l15;
+          uint4 xf[2];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int ch = st * 8 + 2 * g + h;
+            const int slot = (ch & ~7) | ((ch & 7) ^ (row & 7));
+            xf[h] = *reinterpret_cast<const uint4*>(&s_x[row * KC + slot * 8]);
+          }
+#pragma unroll
+          for (int j = 0; j < NT; ++j) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sk_frag(xf[0]), sk_frag(wr[st][j][0]),
+                                                                acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sk_frag(xf[1]), sk_frag(wr[st][j][1]),
+                                                                acc[i][j], 0, 0, 0);
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (!active) return;
+  float* slab = ws + (size_t)s * M * N;
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = 16 * i + g * 4 + r;
+      if (m < M) {
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          const int n = n0 + 16 * j + l15;
+          if (gridDim.y == 1)
+            out[(size_t)m * out_stride + n] = f32_to_bf16(acc[i][j][r]);
+          else
+            slab[(size_t)m * N + n] = acc[i][j][r];
+        }
+      }
+    }
+}
+
 }  // namespace ft
 
 // Returns 0 on success.  Requirements (checked): M <= 64, N % (16*nt) == 0,
@@ -477,5 +587,34 @@ extern "C" int ft_skinny_gemm_xs(const void* x, int x_stride, int M, const void*
   FT_XS_NT(4)
 #undef FT_XS_NT
 #undef FT_XS
+  return -5;
+}
+
+// x-chunk variant.  Requirements (checked): M <= 64, N % (16*nt) == 0,
+// K % (512*splits) == 0.
+extern "C" int ft_skinny_gemm_xc(const void* x, int x_stride, int M, const void* w, int N, int K,
+                                 float* ws, void* out, int out_stride, int splits, int nt,
+                                 hipStream_t stream) {
+  if (M <= 0) return 0;
+  if (M > 64 || splits < 1) return -1;
+  if (N % (16 * nt) != 0) return -2;
+  if (K % (512 * splits) != 0) return -3;
+  if (splits > 1 && ws == nullptr) return -4;
+  const int mt = (M + 15) / 16;
+  const int cols = 4 * 16 * nt;
+  dim3 grid((N + cols - 1) / cols, splits), block(256);
+  const int k_slice = K / splits;
+#define FT_XC(MT_, NT_)                                                                      \
+  if (mt == MT_ && nt == NT_) {                                                              \
+    hipLaunchKernelGGL((ft::skinny_xc_kernel<MT_, NT_>), grid, block, 0, stream,             \
+                       (const uint16_t*)x, x_stride, M, (const uint16_t*)w, K, ws,           \
+                       (uint16_t*)out, out_stride, N, k_slice);                              \
+    return static_cast<int>(hipGetLastError());                                              \
+  }
+#define FT_XC_NT(NT_) FT_XC(1, NT_) FT_XC(2, NT_) FT_XC(3, NT_) FT_XC(4, NT_)
+  FT_XC_NT(1)
+  FT_XC_NT(2)
+#undef FT_XC_NT
+#undef FT_XC
   return -5;
 }

@@ -202,9 +202,9 @@ def kv_block_copy(k_cache, v_cache, pairs: torch.Tensor):
 # ---------------------------------------------------------------------------------
 
 # (nt, u) instantiated; u == 0 selects the K-split-wave variant (skinny_ks_kernel),
-# u == -1 the x-in-LDS variant (skinny_xs_kernel)
+# u == -1 the x-in-LDS variant (skinny_xs_kernel), u == -2 the x-chunk variant (skinny_xc_kernel)
 SKINNY_CONFIGS = [(1, 2), (1, 4), (2, 2), (2, 4), (4, 1), (4, 2), (1, 0), (2, 0), (4, 0),
-                  (1, -1), (2, -1), (4, -1)]
+                  (1, -1), (2, -1), (4, -1), (1, -2), (2, -2)]
 
 
 def skinny_gemm_supported(m: int, n: int, k: int) -> bool:
