@@ -58,11 +58,12 @@ def engine_config_from_service(config) -> "Any":
 
 def get_shared_engine(engine_cfg) -> "Any":
     """One engine per (model, weights, device) per process."""
-    key = f"{engine_cfg.model}|{engine_cfg.weights}|{engine_cfg.resolved_device()}|{engine_cfg.tp_size}|{engine_cfg.dp_size}"
+    key = (f"{engine_cfg.model}|{engine_cfg.weights}|{engine_cfg.resolved_device()}|"
+           f"{engine_cfg.tp_size}|{engine_cfg.dp_size}|{engine_cfg.separate_process}")
     with _ENGINE_LOCK:
         eng = _ENGINES.get(key)
         if eng is None:
-            if engine_cfg.dp_size > 1:
+            if engine_cfg.dp_size > 1 or engine_cfg.separate_process:
                 from fasttalk_llm_microservice_amd.parallel.dp_router import MultiGPUEngine
 
                 eng = MultiGPUEngine(engine_cfg).start()

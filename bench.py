@@ -97,8 +97,10 @@ def main():
     cfg.port = port
     server = WebSocketLLMServer(cfg)
     engine = server.native_handler.engine
-    # capture the decode graphs the run will use before serving
-    engine.engine.runner.warmup([b for b in engine.engine.runner.graph_sizes if b <= 2 * a.sessions])
+    # capture the decode graphs the run will use before serving (a process-isolated
+    # engine warms itself up before it reports ready)
+    if hasattr(engine.engine, "runner"):
+        engine.engine.runner.warmup([b for b in engine.engine.runner.graph_sizes if b <= 2 * a.sessions])
     import asyncio
 
     asgi = AiohttpASGIServer(server.app, "127.0.0.1", port)
@@ -184,6 +186,7 @@ def main():
             "engine_decode_step_ms": round(metrics.get("decode_step_ms_avg", 0.0), 3),
             "engine_decode_batch_avg": round(metrics.get("decode_batch_avg", 0.0), 2),
             "engine_runner": metrics.get("runner", {}),
+            "engine_decode_host_ms": metrics.get("decode_host_ms", {}),
             "init_s": round(init_s, 1),
         }
         print(json.dumps(out), flush=True)

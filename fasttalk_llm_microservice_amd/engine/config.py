@@ -51,6 +51,7 @@ class EngineConfig:
     enforce_eager: bool = False        # disable hipGraph decode capture
     graph_batch_sizes: Tuple[int, ...] = (1, 2, 4, 8, 16, 24, 32, 48, 64, 80, 96, 128, 160, 192, 224, 256)
     async_output: bool = True          # overlap detokenize/streaming with the next GPU step
+    separate_process: bool = False     # run the step loop in its own process (no GIL sharing)
 
     def resolved_device(self) -> str:
         if self.device != "auto":
@@ -94,6 +95,7 @@ class EngineConfig:
             swap_space_gb=_env(["ENGINE_SWAP_SPACE", "VLLM_SWAP_SPACE"], 4.0, float),
             enable_prefix_caching=_env(["ENGINE_PREFIX_CACHING"], True, _bool),
             enforce_eager=_env(["ENGINE_ENFORCE_EAGER", "VLLM_ENFORCE_EAGER"], False, _bool),
+            separate_process=_env(["ENGINE_SEPARATE_PROCESS"], False, _bool),
         )
         for k, v in overrides.items():
             setattr(c, k, v)

@@ -60,6 +60,9 @@ class LLMEngine:
         self._trie = None
         self.stats = collections.Counter()
         self.step_times = collections.deque(maxlen=512)
+        self.host_prof = collections.Counter()
+        self._inflight = None          # (batch, DecodeHandle) of a queued decode step
+        self._last_complete = 0.0
         self.last_step_end = time.time()
 
     # ------------------------------------------------------------------ requests
@@ -89,7 +92,7 @@ class LLMEngine:
         return True
 
     def has_work(self) -> bool:
-        return self.scheduler.has_work()
+        return self._inflight is not None or self.scheduler.has_work()
 
     # ------------------------------------------------------------------ helpers
     def token_trie(self):
@@ -110,7 +113,76 @@ class LLMEngine:
         return m
 
     # ------------------------------------------------------------------ stepping
+    # ------------------------------------------------------------------ pipelined decode
+    def _pipeline_ok(self, batch: ScheduledBatch) -> bool:
+        """Decode-only steps of graph-replayable batches run pipelined: step n+1 is
+        queued on the GPU (inputs = step n's sampled ids, on the device) before the
+        host processes step n, so detokenizing / streaming / scheduling overlap the
+        GPU instead of idling it between graph replays."""
+        return (self.cfg.async_output and not batch.has_prefill and bool(batch.decode_seqs)
+                and self.runner.__class__.__name__ == "ModelRunner"
+                and self.runner.can_pipeline(len(batch.decode_seqs))
+                and all(s.grammar is None for s in batch.decode_seqs))
+
+    def _speculate(self, batch: ScheduledBatch):
+        """Queue the step after the in-flight one for the same sequences (same rows),
+        assuming none of them stops.  Rows of sequences that do stop are discarded;
+        their extra KV write lands in a block that is not in the prefix cache."""
+        sched = self.scheduler
+        seqs = batch.decode_seqs
+        if sched.waiting or any(s.status == SeqStatus.FINISHED for s in seqs):
+            return None
+        need = 0
+        for s in seqs:
+            if s.n_tokens + 1 >= self.max_model_len:
+                return None
+            need += sched._blocks_needed(s, s.n_tokens + 1)
+        if need and not self.bm.can_allocate(need):
+            return None
+        for s in seqs:
+            k = sched._blocks_needed(s, s.n_tokens + 1)
+            if k:
+                s.block_ids.extend(self.bm.allocate(k))
+        return self.runner.decode_launch(seqs, ahead=1)
+
+    def _step_pipelined(self) -> List[RequestOutput]:
+        batch, handle = self._inflight
+        t0 = time.perf_counter()
+        nxt = self._speculate(batch)
+        tl = time.perf_counter()
+        toks = self.runner.decode_collect(handle)
+        t1 = time.perf_counter()
+        outs = self._complete(batch, batch.decode_seqs, toks)
+        t2 = time.perf_counter()
+        self._inflight = (ScheduledBatch(list(batch.decode_seqs), [], [], []), nxt) if nxt else None
+        dt = t2 - self._last_complete if self._last_complete else t2 - t0
+        self._last_complete = t2
+        self.step_times.append((False, len(batch.decode_seqs), len(batch.decode_seqs), dt))
+        self.stats["decode_steps"] += 1
+        self.stats["pipelined_steps"] += 1
+        hp = self.host_prof
+        hp["launch_next"] += tl - t0
+        hp["collect"] += t1 - tl
+        hp["process"] += t2 - t1
+        hp["steps"] += 1
+        return outs
+
+    def _complete(self, batch: ScheduledBatch, sampled_seqs, toks) -> List[RequestOutput]:
+        outs: List[RequestOutput] = []
+        self.scheduler.post_step(batch)
+        for seq, tok in zip(sampled_seqs, toks):
+            o = self._process_token(seq, int(tok))
+            if o is not None:
+                outs.append(o)
+        self.stats["generated_tokens"] += len(sampled_seqs)
+        self.last_step_end = time.time()
+        return outs
+
     def step(self) -> List[RequestOutput]:
+        if self._inflight is not None:
+            return self._step_pipelined()
+        self._last_complete = 0.0
+        ts = time.perf_counter()
         batch = self.scheduler.schedule()
         if batch is None:
             return []
@@ -123,15 +195,26 @@ class LLMEngine:
                                        error="prompt does not fit in the KV cache"))
         if not batch.decode_seqs and not batch.prefill_seqs:
             return outs
+        if not outs and self._pipeline_ok(batch):
+            self._inflight = (batch, self.runner.decode_launch(batch.decode_seqs))
+            return self._step_pipelined()
         sampled_seqs = batch.sampled_seqs()
         masks = self._masks_for(sampled_seqs)
         toks = self.runner.execute(batch, masks)
+        t1 = time.perf_counter()
         self.scheduler.post_step(batch)
         for seq, tok in zip(sampled_seqs, toks):
             o = self._process_token(seq, int(tok))
             if o is not None:
                 outs.append(o)
-        dt = time.perf_counter() - t0
+        t2 = time.perf_counter()
+        dt = t2 - t0
+        if not batch.has_prefill:  # host-side anatomy of decode steps (ms sums)
+            hp = self.host_prof
+            hp["schedule"] += t0 - ts
+            hp["execute"] += t1 - t0
+            hp["process"] += t2 - t1
+            hp["steps"] += 1
         self.step_times.append((batch.has_prefill, len(batch.decode_seqs), batch.total_tokens, dt))
         self.stats["mixed_steps" if batch.has_prefill else "decode_steps"] += 1
         self.stats["generated_tokens"] += len(sampled_seqs)
@@ -282,6 +365,8 @@ class LLMEngine:
             "prefill_step_ms_avg": 1e3 * sum(x[3] for x in pre) / len(pre) if pre else 0.0,
             **{k: v for k, v in self.stats.items()},
             "runner": dict(getattr(self.runner, "stats", {})),
+            "decode_host_ms": {k: round(1e3 * v / max(1, self.host_prof["steps"]), 3)
+                               for k, v in self.host_prof.items() if k != "steps"},
         }
 
 

@@ -31,6 +31,33 @@ def _pow2_ceil(x: int) -> int:
     return 1 << max(0, (x - 1).bit_length())
 
 
+class _Staging:
+    """Pinned host mirror of the decode graph's device inputs + its output copy.
+    int32 ``small`` fields: ids | pos | slots | seq_lens | top_k | steps."""
+
+    def __init__(self, mb: int, max_blocks: int, pin: bool, gpu: bool):
+        i32 = torch.int32
+        self.h_small = torch.zeros(6 * mb, dtype=i32, pin_memory=pin)
+        self.h_bt = torch.zeros(mb, max_blocks, dtype=i32, pin_memory=pin)
+        self.h_f32 = torch.zeros(2 * mb, dtype=torch.float32, pin_memory=pin)
+        self.h_seeds = torch.zeros(mb, dtype=torch.int64, pin_memory=pin)
+        self.h_out = torch.zeros(mb, dtype=i32, pin_memory=pin)
+        self.hs = self.h_small.numpy()
+        self.hbt = self.h_bt.numpy()
+        self.hf = self.h_f32.numpy()
+        self.hseed = self.h_seeds.numpy()
+        self.event = torch.cuda.Event() if gpu else None
+
+
+class DecodeHandle:
+    __slots__ = ("stage", "n", "nb")
+
+    def __init__(self, stage: "_Staging", n: int, nb: int):
+        self.stage = stage
+        self.n = n
+        self.nb = nb
+
+
 class ModelRunner:
     def __init__(self, cfg: EngineConfig, model_cfg: ModelConfig, comm: TPComm = SINGLE,
                  device: Optional[str] = None):
@@ -73,7 +100,6 @@ class ModelRunner:
         # Static graph inputs live in a few device buffers whose layout mirrors a
         # pinned host staging copy, so a decode step refreshes all inputs with 4
         # async H2D copies.  int32 fields: ids | pos | slots | seq_lens | top_k | steps
-        self.h_small = torch.zeros(6 * mb, dtype=i32, pin_memory=pin)
         self.d_small = torch.zeros(6 * mb, dtype=i32, device=dv)
         self.d_input_ids = self.d_small[0:mb]
         self.d_positions = self.d_small[mb:2 * mb]
@@ -81,26 +107,23 @@ class ModelRunner:
         self.d_seq_lens = self.d_small[3 * mb:4 * mb]
         self.d_top_k = self.d_small[4 * mb:5 * mb]
         self.d_steps = self.d_small[5 * mb:6 * mb]
-        self.h_bt = torch.zeros(mb, self.max_blocks_per_seq, dtype=i32, pin_memory=pin)
         self.d_bt = torch.zeros(mb, self.max_blocks_per_seq, dtype=i32, device=dv)
-        self.h_f32 = torch.zeros(2 * mb, dtype=torch.float32, pin_memory=pin)
         self.d_f32 = torch.zeros(2 * mb, dtype=torch.float32, device=dv)
         self.d_temp = self.d_f32[0:mb]
         self.d_top_p = self.d_f32[mb:2 * mb]
-        self.h_seeds = torch.zeros(mb, dtype=torch.int64, pin_memory=pin)
         self.d_seeds = torch.zeros(mb, dtype=torch.int64, device=dv)
         self.d_out = torch.zeros(mb, dtype=i32, device=dv)
-        self.h_out = torch.zeros(mb, dtype=i32, pin_memory=pin)
+        # two pinned staging sets: while decode step n runs, step n+1 is filled
+        # and queued behind it from the other set (pipelined decode)
+        self.stg = [_Staging(mb, self.max_blocks_per_seq, pin, self.is_gpu) for _ in range(2)]
+        self._stg_next = 0
+        self.h_out = torch.zeros(mb, dtype=i32, pin_memory=pin)  # eager-step sampler output
         self.d_logits_idx = torch.arange(mb, dtype=torch.int64, device=dv)
         # split-K workspace sized for the largest (batch x splits) any bucket uses
         rows = max(b * self._splits_for_batch(b) for b in self.graph_sizes + [mb])
         self.tmp_rows = rows
         self.tmp_out = torch.empty(rows * nq * d, dtype=torch.float32, device=dv)
         self.tmp_ml = torch.empty(rows * nq * 2, dtype=torch.float32, device=dv)
-        self._hs = self.h_small.numpy()
-        self._hbt = self.h_bt.numpy()
-        self._hf = self.h_f32.numpy()
-        self._hseed = self.h_seeds.numpy()
         self._done_event = torch.cuda.Event() if self.is_gpu else None
         self.graphs: Dict[int, torch.cuda.CUDAGraph] = {}
         self.graph_pool = None
@@ -150,7 +173,7 @@ class ModelRunner:
             return []
         return self._decode(batch, masks)
 
-    def _sampling_arrays(self, seqs):
+    def _sampling_arrays(self, seqs, ahead: int = 0):
         n = len(seqs)
         temp = np.empty(n, np.float32)
         topp = np.empty(n, np.float32)
@@ -163,7 +186,7 @@ class ModelRunner:
             topp[i] = p.top_p
             topk[i] = p.top_k
             seeds[i] = p.seed
-            steps[i] = s.num_output + 131 * s.preemptions
+            steps[i] = s.num_output + ahead + 131 * s.preemptions
         return temp, topp, topk, seeds, steps
 
     def _mixed(self, batch: ScheduledBatch, masks) -> List[int]:
@@ -258,14 +281,17 @@ class ModelRunner:
                     torch.empty(n * nq * splits * 2, dtype=torch.float32, device=dv))
         return self.tmp_out, self.tmp_ml
 
-    def _wait(self):
-        """Block until the GPU work queued so far is done WITHOUT holding the GIL:
-        a plain ``.cpu()`` / ``synchronize`` keeps the GIL for the whole step and
-        starves the asyncio thread that streams tokens to the WebSockets."""
-        ev = self._done_event
-        ev.record()
+    def _wait(self, ev=None):
+        """Block until the GPU work queued so far (or up to ``ev``) is done WITHOUT
+        holding the GIL: a plain ``.cpu()`` / ``synchronize`` keeps the GIL for the
+        whole step and starves the asyncio thread that streams to the WebSockets."""
+        if ev is None:
+            ev = self._done_event
+            ev.record()
+        t0 = time.perf_counter()
         while not ev.query():
             time.sleep(0.0001)
+        self.stats["wait_ms"] = self.stats.get("wait_ms", 0.0) + 1e3 * (time.perf_counter() - t0)
 
     def _sample(self, h, sampling, masks) -> List[int]:
         logits = self.model.compute_logits(h)
@@ -295,42 +321,59 @@ class ModelRunner:
         bucket = self._bucket(n) if (self.use_graphs and masks is None) else None
         if bucket is None:
             return self._decode_eager(seqs, self._splits_for_batch(n), masks)
-        nb = bucket
-        maxblk = self._decode_fill(seqs, nb)
-        if self.bcast is not None:
-            mb = self.max_decode_batch
-            self.bcast.send(("graph", {"nb": nb, "n": n, "small": self._hs.copy(),
-                                       "bt": self._hbt[:nb, :maxblk].copy(),
-                                       "f32": self._hf.copy(), "seeds": self._hseed.copy()}, None))
-        return self._decode_run(nb, n)
+        return self.decode_collect(self.decode_launch(seqs))
 
-    def _decode_fill(self, seqs, nb: int) -> int:
-        """Writes a decode step's inputs into the pinned staging buffers."""
+    def can_pipeline(self, n: int) -> bool:
+        return self.use_graphs and self._bucket(n) is not None
+
+    def decode_launch(self, seqs, ahead: int = 0) -> DecodeHandle:
+        """Fills a staging set and queues a graph-replayed decode step (returns at
+        once).  ``ahead=1`` launches the step AFTER the one in flight: positions
+        are one further and the input ids are the in-flight step's sampled ids,
+        copied device-to-device, so the host never waits between steps."""
+        n = len(seqs)
+        nb = self._bucket(n)
+        st = self.stg[self._stg_next]
+        self._stg_next ^= 1
+        maxblk = self._decode_fill(seqs, nb, st, ahead)
+        if self.bcast is not None:
+            self.bcast.send(("graph", {"nb": nb, "n": n, "small": st.hs.copy(),
+                                       "bt": st.hbt[:nb, :maxblk].copy(), "f32": st.hf.copy(),
+                                       "seeds": st.hseed.copy(), "from_device": bool(ahead)}, None))
+        self._decode_enqueue(st, nb, n, from_device=bool(ahead))
+        return DecodeHandle(st, n, nb)
+
+    def decode_collect(self, h: DecodeHandle) -> List[int]:
+        self._wait(h.stage.event)
+        return h.stage.h_out[:h.n].tolist()
+
+    def _decode_fill(self, seqs, nb: int, st: "_Staging", ahead: int = 0) -> int:
+        """Writes a decode step's inputs into a pinned staging set."""
         n = len(seqs)
         mb = self.max_decode_batch
-        hs = self._hs
+        hs = st.hs
         ids = hs[0:mb]
         pos = hs[mb:2 * mb]
         slots = hs[2 * mb:3 * mb]
         sl = hs[3 * mb:4 * mb]
-        bt = self._hbt
+        bt = st.hbt
         bs = self.bs
         maxblk = 1
         for i, s in enumerate(seqs):
-            p = s.n_tokens - 1
-            ids[i] = s.last_token
+            p = s.n_tokens - 1 + ahead
+            ids[i] = s.last_token  # replaced on the device when ahead
             pos[i] = p
             slots[i] = s.block_ids[p // bs] * bs + p % bs
             sl[i] = p + 1
             nbk = len(s.block_ids)
             bt[i, :nbk] = s.block_ids
             maxblk = max(maxblk, nbk)
-        temp, topp, topk, seeds, steps = self._sampling_arrays(seqs)
+        temp, topp, topk, seeds, steps = self._sampling_arrays(seqs, ahead)
         hs[4 * mb:4 * mb + n] = topk
         hs[5 * mb:5 * mb + n] = steps
-        self._hf[:n] = temp
-        self._hf[mb:mb + n] = topp
-        self._hseed[:n] = seeds
+        st.hf[:n] = temp
+        st.hf[mb:mb + n] = topp
+        st.hseed[:n] = seeds
         if nb > n:  # padding rows: no KV write, 1-token context, greedy
             ids[n:nb] = 0
             pos[n:nb] = 0
@@ -339,23 +382,24 @@ class ModelRunner:
             bt[n:nb, 0] = 0
             hs[4 * mb + n:4 * mb + nb] = 0
             hs[5 * mb + n:5 * mb + nb] = 0
-            self._hf[n:nb] = 0.0
-            self._hf[mb + n:mb + nb] = 1.0
+            st.hf[n:nb] = 0.0
+            st.hf[mb + n:mb + nb] = 1.0
         return maxblk
 
-    def _decode_run(self, nb: int, n: int) -> List[int]:
-        self.d_small.copy_(self.h_small, non_blocking=True)
-        self.d_bt[:nb].copy_(self.h_bt[:nb], non_blocking=True)
-        self.d_f32.copy_(self.h_f32, non_blocking=True)
-        self.d_seeds.copy_(self.h_seeds, non_blocking=True)
+    def _decode_enqueue(self, st: "_Staging", nb: int, n: int, from_device: bool = False):
+        self.d_small.copy_(st.h_small, non_blocking=True)
+        self.d_bt[:nb].copy_(st.h_bt[:nb], non_blocking=True)
+        self.d_f32.copy_(st.h_f32, non_blocking=True)
+        self.d_seeds.copy_(st.h_seeds, non_blocking=True)
+        if from_device:  # the previous step's sampled ids feed this step
+            self.d_input_ids[:nb].copy_(self.d_out[:nb])
         g = self.graphs.get(nb)
         if g is None:
             g = self._capture(nb)
         g.replay()
         self.stats["graph_replays"] += 1
-        self.h_out[:n].copy_(self.d_out[:n], non_blocking=True)
-        self._wait()
-        return self.h_out[:n].tolist()
+        st.h_out[:n].copy_(self.d_out[:n], non_blocking=True)
+        st.event.record()
 
     # ------------------------------------------------------------------ TP workers
     @torch.inference_mode()
@@ -369,12 +413,14 @@ class ModelRunner:
             self._mixed_run(host, masks)
         elif kind == "graph":
             nb, n = host["nb"], host["n"]
-            self._hs[:] = host["small"]
+            st = self.stg[0]
+            st.hs[:] = host["small"]
             bt = host["bt"]
-            self._hbt[:nb, :bt.shape[1]] = bt
-            self._hf[:] = host["f32"]
-            self._hseed[:] = host["seeds"]
-            self._decode_run(nb, n)
+            st.hbt[:nb, :bt.shape[1]] = bt
+            st.hf[:] = host["f32"]
+            st.hseed[:] = host["seeds"]
+            self._decode_enqueue(st, nb, n, from_device=host.get("from_device", False))
+            self._wait(st.event)
         elif kind == "warmup":
             self.warmup(host)
         else:

@@ -36,11 +36,11 @@ from ..models.config import resolve_model
 log = logging.getLogger("fasttalk.dp")
 
 
-def _replica_main(index: int, cfg, conn):
+def _replica_main(index: int, cfg, conn, device_base: int = 0):
     """Replica process: one engine (TP group when cfg.tp_size > 1) + step loop."""
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     try:
-        base = index * max(1, cfg.tp_size)
+        base = device_base + index * max(1, cfg.tp_size)
         if cfg.resolved_device() == "cuda":
             import torch
 
@@ -93,11 +93,11 @@ def _replica_main(index: int, cfg, conn):
 
 
 class _Replica:
-    def __init__(self, index: int, cfg, ctx):
+    def __init__(self, index: int, cfg, ctx, device_base: int = 0):
         self.index = index
         self.conn, child = ctx.Pipe()
-        self.proc = ctx.Process(target=_replica_main, args=(index, cfg, child), daemon=True,
-                                name=f"fasttalk-dp{index}")
+        self.proc = ctx.Process(target=_replica_main, args=(index, cfg, child, device_base),
+                                daemon=True, name=f"fasttalk-dp{index}")
         self.proc.start()
         child.close()
         self.lock = threading.Lock()
@@ -133,7 +133,8 @@ class _Facade:
 
     def metrics(self) -> Dict[str, Any]:
         reps = [r.metrics for r in self._router.replicas]
-        agg: Dict[str, Any] = {"replicas": len(reps), "per_replica": reps}
+        agg: Dict[str, Any] = dict(reps[0]) if len(reps) == 1 else {}
+        agg.update({"replicas": len(reps), "per_replica": reps})
         for key in ("running", "waiting", "kv_blocks_total", "kv_blocks_free", "generated_tokens",
                     "prefill_tokens", "requests", "preemptions"):
             agg[key] = sum(int(m.get(key, 0) or 0) for m in reps)
@@ -143,8 +144,16 @@ class _Facade:
 
 
 class MultiGPUEngine:
-    def __init__(self, cfg):
+    """``dp_size`` engine replicas in child processes.  With ``dp_size == 1`` it is
+    the process-isolated single engine (``ENGINE_SEPARATE_PROCESS``): the step loop
+    no longer shares a GIL with the WebSocket event loop."""
+
+    def __init__(self, cfg, device_base: Optional[int] = None):
         self.cfg = cfg
+        if device_base is None:
+            device_base = int(os.environ.get("LOCAL_RANK", "0")) * max(1, cfg.dp_size) * \
+                max(1, cfg.tp_size) if cfg.resolved_device() == "cuda" else 0
+        self.device_base = device_base
         self.dp = max(1, cfg.dp_size)
         self.ctx = mp.get_context("spawn")
         self.replicas: List[_Replica] = []
@@ -159,7 +168,7 @@ class MultiGPUEngine:
 
     # ------------------------------------------------------------------ lifecycle
     def start(self, timeout: float = 1800.0):
-        self.replicas = [_Replica(i, self.cfg, self.ctx) for i in range(self.dp)]
+        self.replicas = [_Replica(i, self.cfg, self.ctx, self.device_base) for i in range(self.dp)]
         t0 = time.time()
         for r in self.replicas:
             while not r.conn.poll(1.0):

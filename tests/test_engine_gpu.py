@@ -98,3 +98,25 @@ def test_many_sequences_continuous_batching():
     out = eng.generate(prompts, SamplingParams(temperature=0.7, max_tokens=20, ignore_eos=True))
     assert all(len(o) == 20 for o in out)
     assert eng.bm.num_free() == eng.bm.num_blocks
+
+
+def test_pipelined_decode_matches_synchronous():
+    """Decode steps queued one ahead on the GPU (ids fed device-to-device) must
+    give exactly the synchronous engine's tokens, including sequences that stop
+    early on a stop token, at max_tokens, or at different lengths."""
+    prompts = _prompts(12, [5 + 7 * i for i in range(12)], seed=3)
+    outs = []
+    for async_output in (True, False):
+        eng = _engine(max_num_seqs=32, num_kv_blocks=1024, async_output=async_output)
+        res = {}
+        for i, p in enumerate(prompts):
+            sp = SamplingParams(temperature=0.8, top_p=0.95, seed=100 + i, max_tokens=8 + 3 * i,
+                                ignore_eos=True, stop_token_ids=[7] if i % 3 == 0 else None)
+            eng.add_request(f"r{i}", p, sp, on_output=lambda o, i=i: res.setdefault(i, []).extend(o.token_ids))
+        while eng.has_work():
+            eng.step()
+        assert eng.bm.num_free() == eng.bm.num_blocks
+        if async_output:
+            assert eng.stats["pipelined_steps"] > 0
+        outs.append([res[i] for i in range(len(prompts))])
+    assert outs[0] == outs[1]
