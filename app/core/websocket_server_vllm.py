@@ -51,6 +51,9 @@ class _Turn:
         self.tokens = 0
         self.text = []
         self.ttft: Optional[float] = None
+        self.last_emit: Optional[float] = None
+        self.itl_sum = 0.0   # inter-token gaps between token frames (s)
+        self.itl_n = 0
         self.finish_reason: Optional[str] = None
         self.prompt_tokens = 0
         self.cached_tokens = 0
@@ -370,6 +373,8 @@ class WebSocketLLMServer:
             }
             if turn.ttft is not None:
                 stats["ttft_ms"] = turn.ttft * 1000.0
+            if turn.itl_n:
+                stats["itl_ms"] = 1000.0 * turn.itl_sum / turn.itl_n
             if turn.finish_reason is not None:
                 stats["finish_reason"] = turn.finish_reason
             if turn.prompt_tokens:
@@ -394,8 +399,13 @@ class WebSocketLLMServer:
             self.connection_manager.update_connection_state(session_id, ConnectionState.ACTIVE)
 
     async def _emit(self, session_id: str, send, turn: _Turn, text: str, ntok: int, t_start: float):
+        now = time.time()
         if turn.ttft is None:
-            turn.ttft = time.time() - t_start
+            turn.ttft = now - t_start
+        elif turn.last_emit is not None:
+            turn.itl_sum += now - turn.last_emit
+            turn.itl_n += 1
+        turn.last_emit = now
         turn.tokens += ntok
         if text:
             turn.text.append(text)

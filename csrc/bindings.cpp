@@ -43,6 +43,8 @@ int ft_skinny_gemm_xs(const void* x, int x_stride, int M, const void* w, int N, 
                       void* out, int out_stride, int splits, int nt, hipStream_t stream);
 int ft_skinny_gemm_xc(const void* x, int x_stride, int M, const void* w, int N, int K, float* ws,
                       void* out, int out_stride, int splits, int nt, hipStream_t stream);
+int ft_embed_rmsnorm(void* out, void* residual, const int* ids, const void* table, const void* w,
+                     int rows, int hidden, int vocab, float eps, hipStream_t stream);
 int ft_row_rmsnorm(const void* x, int x_stride, const float* ws, int splits, void* out,
                    int out_stride, void* residual, const void* w, int rows, int hidden, float eps,
                    hipStream_t stream);
@@ -305,6 +307,25 @@ void skinny_gemm(at::Tensor x, at::Tensor w, c10::optional<at::Tensor> out,
              "skinny_gemm");
 }
 
+// residual = table[ids]; out = rmsnorm(residual) * w  (embedding + first RMSNorm)
+void embed_rmsnorm(at::Tensor out, at::Tensor residual, at::Tensor ids, at::Tensor table,
+                   at::Tensor w, double eps) {
+  check_bf16(out, "out");
+  check_bf16(residual, "residual");
+  check_bf16(table, "table");
+  check_bf16(w, "w");
+  check_i32(ids, "ids");
+  TORCH_CHECK(table.dim() == 2 && table.is_contiguous(), "table must be contiguous [V, H]");
+  const int rows = (int)ids.numel(), hidden = (int)table.size(1);
+  TORCH_CHECK(out.is_contiguous() && residual.is_contiguous() && out.numel() >= (int64_t)rows * hidden &&
+                  residual.numel() >= (int64_t)rows * hidden && w.numel() == hidden,
+              "embed_rmsnorm shapes");
+  check_rc(ft_embed_rmsnorm(out.data_ptr(), residual.data_ptr(), ids.data_ptr<int>(),
+                            table.data_ptr(), w.data_ptr(), rows, hidden, (int)table.size(0),
+                            (float)eps, cur_stream()),
+           "embed_rmsnorm");
+}
+
 // out = rmsnorm([residual +=] src) * w where src = bf16 x or the fp32 slabs in ws
 void row_rmsnorm(at::Tensor out, c10::optional<at::Tensor> x, c10::optional<at::Tensor> ws,
                  int64_t splits, c10::optional<at::Tensor> residual, at::Tensor w, int64_t rows,
@@ -400,6 +421,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("row_rmsnorm", &row_rmsnorm, py::arg("out"), py::arg("x") = py::none(),
         py::arg("ws") = py::none(), py::arg("splits") = 1, py::arg("residual") = py::none(),
         py::arg("w"), py::arg("rows"), py::arg("eps"));
+  m.def("embed_rmsnorm", &embed_rmsnorm);
   m.def("slab_silu", &slab_silu);
   m.def("slab_store", &slab_store);
   m.def("slab_rope_kv", &slab_rope_kv);

@@ -106,6 +106,53 @@ static int launch_rmsnorm(uint16_t* out, const uint16_t* x, uint16_t* residual, 
 }
 
 // ----------------------------------------------------------------------------
+// K1 + first K2: embedding gather fused with the first layer's RMSNorm.
+//   residual[t] = table[ids[t]]   (the residual stream starts as the embedding)
+//   out[t]      = rmsnorm(table[ids[t]]) * w
+// One wave per token row, the gathered row stays in registers between the
+// reduction and both stores (the embedding row is read from HBM once).
+// ----------------------------------------------------------------------------
+template <int NCHUNK>
+__global__ __launch_bounds__(256) void embed_rmsnorm_kernel(uint16_t* __restrict__ out,
+                                                            uint16_t* __restrict__ residual,
+                                                            const int* __restrict__ ids,
+                                                            const uint16_t* __restrict__ table,
+                                                            const uint16_t* __restrict__ weight,
+                                                            int rows, int hidden, int vocab,
+                                                            float eps) {
+  const int row = blockIdx.x * 4 + wave_id();
+  if (row >= rows) return;
+  const int lane = lane_id();
+  const int tok = min(max(ids[row], 0), vocab - 1);
+  const uint4* xr = reinterpret_cast<const uint4*>(table + (size_t)tok * hidden);
+  uint4* rr = reinterpret_cast<uint4*>(residual + (size_t)row * hidden);
+  uint4 v[NCHUNK];
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCHUNK; ++c) {
+    v[c] = xr[c * 64 + lane];
+    rr[c * 64 + lane] = v[c];
+    float a[8];
+    load8(v[c], a);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ss += a[j] * a[j];
+  }
+  ss = wave_sum(ss);
+  const float inv = rsqrtf(ss / (float)hidden + eps);
+  const uint4* wr = reinterpret_cast<const uint4*>(weight);
+  uint4* orow = reinterpret_cast<uint4*>(out + (size_t)row * hidden);
+#pragma unroll
+  for (int c = 0; c < NCHUNK; ++c) {
+    float a[8], w[8];
+    load8(v[c], a);
+    load8(wr[c * 64 + lane], w);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a[j] = bf16_to_f32(f32_to_bf16(a[j] * inv)) * w[j];
+    orow[c * 64 + lane] = store8(a);
+  }
+}
+
+// ----------------------------------------------------------------------------
 // SiLU-and-mul: out[t, i] = silu(gu[t, i]) * gu[t, I + i]
 // ----------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void silu_mul_kernel(uint16_t* __restrict__ out,
@@ -152,5 +199,32 @@ extern "C" int ft_silu_mul(void* out, const void* gu, int rows, int inter, hipSt
   if (grid > 256 * 16) grid = 256 * 16;
   hipLaunchKernelGGL(ft::silu_mul_kernel, dim3(grid), dim3(256), 0, stream, (uint16_t*)out,
                      (const uint16_t*)gu, rows, inter);
+  return static_cast<int>(hipGetLastError());
+}
+
+extern "C" int ft_embed_rmsnorm(void* out, void* residual, const int* ids, const void* table,
+                                const void* w, int rows, int hidden, int vocab, float eps,
+                                hipStream_t stream) {
+  if (rows <= 0) return 0;
+  if (hidden % 512 != 0) return -1;
+  dim3 grid(ft::ceil_div(rows, 4)), block(256);
+#define FT_EMB_CASE(N)                                                                      \
+  case N:                                                                                   \
+    hipLaunchKernelGGL((ft::embed_rmsnorm_kernel<N>), grid, block, 0, stream, (uint16_t*)out, \
+                       (uint16_t*)residual, ids, (const uint16_t*)table, (const uint16_t*)w,  \
+                       rows, hidden, vocab, eps);                                          \
+    break;
+  switch (hidden / 512) {
+    FT_EMB_CASE(1)
+    FT_EMB_CASE(2)
+    FT_EMB_CASE(3)
+    FT_EMB_CASE(4)
+    FT_EMB_CASE(6)
+    FT_EMB_CASE(8)
+    FT_EMB_CASE(16)
+    default:
+      return -2;
+  }
+#undef FT_EMB_CASE
   return static_cast<int>(hipGetLastError());
 }

@@ -63,6 +63,10 @@ class LLMEngine:
         self.host_prof = collections.Counter()
         self._inflight = None          # (batch, DecodeHandle) of a queued decode step
         self._last_complete = 0.0
+        from .debug import FaultInjector, StepProfiler
+
+        self._faults = FaultInjector()
+        self._profiler = StepProfiler()
         self.last_step_end = time.time()
 
     # ------------------------------------------------------------------ requests
@@ -179,6 +183,18 @@ class LLMEngine:
         return outs
 
     def step(self) -> List[RequestOutput]:
+        self._faults.check()
+        self._profiler.before_step()
+        try:
+            return self._step()
+        finally:
+            self._profiler.after_step()
+
+    def reset_inflight(self):
+        """Forget a queued decode step (after a failed step)."""
+        self._inflight = None
+
+    def _step(self) -> List[RequestOutput]:
         if self._inflight is not None:
             return self._step_pipelined()
         self._last_complete = 0.0
@@ -465,9 +481,10 @@ class AsyncEngine:
                 continue
             try:
                 eng.step()
-            except Exception as e:  # pragma: no cover - surfaced through health / streams
+            except Exception as e:  # surfaced through health / streams (FT_FAULT_* tests)
                 log.exception("engine step failed")
                 self.error = e
+                eng.reset_inflight()
                 for seq in list(eng.scheduler.running) + list(eng.scheduler.waiting):
                     eng._finalize(seq, "error", emit=True, error=str(e))
                 self._flush()

@@ -161,13 +161,12 @@ class LlamaModel:
         cfg = self.cfg
         eps = cfg.rms_norm_eps
         nq, nkv, d = self.nq, self.nkv, self.d
-        x = F.embedding(input_ids, self.embed)
-        t = x.shape[0]
+        t = input_ids.shape[0]
         residual = None
+        x = None
         for li, L in enumerate(self.layers):
             if residual is None:
-                residual = x
-                x = ops.rmsnorm(x, L.ln1, eps)
+                x, residual = ops.embed_rmsnorm(input_ids, self.embed, L.ln1, eps)  # K1 + K2
             else:
                 ops.fused_add_rmsnorm(x, residual, L.ln1, eps)
             qkv = F.linear(x, L.wqkv)

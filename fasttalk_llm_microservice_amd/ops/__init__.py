@@ -220,6 +220,19 @@ def skinny_gemm(x, w, out=None, ws=None, splits: int = 1, nt: int = 1, u: int = 
     return out if splits == 1 else ws
 
 
+def embed_rmsnorm(ids: torch.Tensor, table: torch.Tensor, w: torch.Tensor, eps: float):
+    """(rmsnorm(table[ids]) * w, table[ids]): the embedding gather fused with the
+    first layer's input norm; the second tensor starts the residual stream."""
+    if ids.is_cuda:
+        n, h = ids.numel(), table.shape[1]
+        out = torch.empty(n, h, dtype=table.dtype, device=table.device)
+        res = torch.empty(n, h, dtype=table.dtype, device=table.device)
+        native().embed_rmsnorm(out, res, ids, table, w, eps)
+        return out, res
+    res = torch.nn.functional.embedding(ids.long(), table)
+    return ref.rmsnorm(res, w, eps), res
+
+
 def row_rmsnorm(out, w, eps, rows, x=None, ws=None, splits=1, residual=None):
     native().row_rmsnorm(out, x, ws, splits, residual, w, rows, eps)
     return out

@@ -80,7 +80,7 @@ def test_full_session_flow(server):
         assert toks and all(isinstance(f["data"], str) for f in toks)
         stats = frames[-1]["stats"]
         assert stats["tokens_generated"] == 6 and stats["provider"] == "native"
-        assert {"processing_time_ms", "tokens_per_second", "pydantic_ai_used", "ttft_ms"} <= set(stats)
+        assert {"processing_time_ms", "tokens_per_second", "pydantic_ai_used", "ttft_ms", "itl_ms"} <= set(stats)
         # second turn: the first turn's KV blocks are reused (multi-turn prefix cache)
         ws.send_json({"type": "user_message", "text": "And tomorrow?"})
         stats2 = _recv_until(ws, "response_complete")[-1]["stats"]

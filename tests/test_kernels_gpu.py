@@ -327,3 +327,15 @@ def test_slab_rope_kv(nq, nkv, d):
     _close(q_out, qkv[:, : nq * d], atol=3e-2, rtol=2e-2, msg="q")
     _close(k1, k2, atol=3e-2, rtol=2e-2, msg="k")
     _close(v1, v2, atol=3e-2, rtol=2e-2, msg="v")
+
+
+@pytest.mark.parametrize("hidden", [2048, 3072, 4096, 8192])
+def test_embed_rmsnorm(hidden):
+    vocab = 1000
+    table = torch.randn(vocab, hidden, device=DEV).bfloat16()
+    w = (1 + 0.1 * torch.randn(hidden, device=DEV)).bfloat16()
+    ids = torch.randint(0, vocab, (37,), dtype=torch.int32, device=DEV)
+    out, res = ops.embed_rmsnorm(ids, table, w, 1e-5)
+    rows = table[ids.long()]
+    assert torch.equal(res, rows)
+    _close(out, ref.rmsnorm(rows, w, 1e-5), atol=2e-2, rtol=1e-2, msg="embed_rmsnorm")
