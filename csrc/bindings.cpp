@@ -45,6 +45,15 @@ int ft_skinny_gemm_xc(const void* x, int x_stride, int M, const void* w, int N, 
                       void* out, int out_stride, int splits, int nt, hipStream_t stream);
 int ft_embed_rmsnorm(void* out, void* residual, const int* ids, const void* table, const void* w,
                      int rows, int hidden, int vocab, float eps, hipStream_t stream);
+size_t ft_ar_header_bytes();
+int ft_ar_alloc(size_t bytes, void** ptr);
+int ft_ar_free(void* ptr);
+int ft_ar_ipc_handle(void* ptr, char* out64);
+int ft_ar_ipc_open(const char* in64, void** ptr);
+int ft_ar_ipc_close(void* ptr);
+int ft_ar_read_error(void* mine, int* err);
+int ft_ar_allreduce(void* out, const void* x, long n, const uint64_t* peers_dev, int rank, int world,
+                    size_t max_bytes, unsigned spin_budget, hipStream_t stream);
 int ft_row_rmsnorm(const void* x, int x_stride, const float* ws, int splits, void* out,
                    int out_stride, void* residual, const void* w, int rows, int hidden, float eps,
                    hipStream_t stream);
@@ -307,6 +316,43 @@ void skinny_gemm(at::Tensor x, at::Tensor w, c10::optional<at::Tensor> out,
              "skinny_gemm");
 }
 
+// ---- custom one-shot all-reduce (csrc/kernels/custom_ar.hip) ----------------------
+int64_t custom_ar_alloc(int64_t bytes) {
+  void* p = nullptr;
+  check_rc(ft_ar_alloc((size_t)bytes, &p), "custom_ar_alloc");
+  return (int64_t)(uintptr_t)p;
+}
+void custom_ar_free(int64_t p) { check_rc(ft_ar_free((void*)(uintptr_t)p), "custom_ar_free"); }
+py::bytes custom_ar_handle(int64_t p) {
+  char h[64] = {0};
+  check_rc(ft_ar_ipc_handle((void*)(uintptr_t)p, h), "custom_ar_handle");
+  return py::bytes(h, 64);
+}
+int64_t custom_ar_open(py::bytes h) {
+  std::string s = h;
+  TORCH_CHECK(s.size() == 64, "ipc handle must be 64 bytes");
+  void* p = nullptr;
+  check_rc(ft_ar_ipc_open(s.data(), &p), "custom_ar_open");
+  return (int64_t)(uintptr_t)p;
+}
+void custom_ar_close(int64_t p) { check_rc(ft_ar_ipc_close((void*)(uintptr_t)p), "custom_ar_close"); }
+int64_t custom_ar_error(int64_t p) {
+  int e = 0;
+  check_rc(ft_ar_read_error((void*)(uintptr_t)p, &e), "custom_ar_error");
+  return e;
+}
+void custom_ar_allreduce(at::Tensor out, at::Tensor x, at::Tensor peers, int64_t rank, int64_t world,
+                         int64_t max_bytes, int64_t spin_budget) {
+  check_bf16(out, "out");
+  check_bf16(x, "x");
+  TORCH_CHECK(x.is_contiguous() && out.is_contiguous() && out.numel() == x.numel(), "contiguous");
+  TORCH_CHECK(peers.scalar_type() == at::kLong && peers.is_cuda() && peers.numel() == world, "peers");
+  check_rc(ft_ar_allreduce(out.data_ptr(), x.data_ptr(), (long)x.numel(),
+                           reinterpret_cast<const uint64_t*>(peers.data_ptr<int64_t>()), (int)rank,
+                           (int)world, (size_t)max_bytes, (unsigned)spin_budget, cur_stream()),
+           "custom_ar_allreduce");
+}
+
 // residual = table[ids]; out = rmsnorm(residual) * w  (embedding + first RMSNorm)
 void embed_rmsnorm(at::Tensor out, at::Tensor residual, at::Tensor ids, at::Tensor table,
                    at::Tensor w, double eps) {
@@ -422,6 +468,14 @@ PYBIND11_MODULE(_C, m) {
         py::arg("ws") = py::none(), py::arg("splits") = 1, py::arg("residual") = py::none(),
         py::arg("w"), py::arg("rows"), py::arg("eps"));
   m.def("embed_rmsnorm", &embed_rmsnorm);
+  m.def("custom_ar_header_bytes", []() { return (int64_t)ft_ar_header_bytes(); });
+  m.def("custom_ar_alloc", &custom_ar_alloc);
+  m.def("custom_ar_free", &custom_ar_free);
+  m.def("custom_ar_handle", &custom_ar_handle);
+  m.def("custom_ar_open", &custom_ar_open);
+  m.def("custom_ar_close", &custom_ar_close);
+  m.def("custom_ar_error", &custom_ar_error);
+  m.def("custom_ar_allreduce", &custom_ar_allreduce);
   m.def("slab_silu", &slab_silu);
   m.def("slab_store", &slab_store);
   m.def("slab_rope_kv", &slab_rope_kv);

@@ -52,6 +52,7 @@ class EngineConfig:
     graph_batch_sizes: Tuple[int, ...] = (1, 2, 4, 8, 16, 24, 32, 48, 64, 80, 96, 128, 160, 192, 224, 256)
     async_output: bool = True          # overlap detokenize/streaming with the next GPU step
     separate_process: bool = False     # run the step loop in its own process (no GIL sharing)
+    custom_allreduce: bool = False     # TP: one-shot xGMI all-reduce for decode-size messages
 
     def resolved_device(self) -> str:
         if self.device != "auto":
@@ -96,6 +97,7 @@ class EngineConfig:
             enable_prefix_caching=_env(["ENGINE_PREFIX_CACHING"], True, _bool),
             enforce_eager=_env(["ENGINE_ENFORCE_EAGER", "VLLM_ENFORCE_EAGER"], False, _bool),
             separate_process=_env(["ENGINE_SEPARATE_PROCESS"], False, _bool),
+            custom_allreduce=_env(["ENGINE_CUSTOM_ALLREDUCE"], False, _bool),
         )
         for k, v in overrides.items():
             setattr(c, k, v)

@@ -51,6 +51,17 @@ def _set_device(device: str, index: int):
         torch.cuda.set_device(index)
 
 
+def _maybe_custom_ar(cfg, comm: TPComm, device: str):
+    """Every rank of the group calls this at the same point (it is collective)."""
+    if not (getattr(cfg, "custom_allreduce", False) and device == "cuda"):
+        return
+    from .custom_allreduce import CustomAllReduce
+
+    if comm.world_size in CustomAllReduce.SUPPORTED_WORLD:
+        comm.custom = CustomAllReduce(comm.group, comm.rank, comm.world_size,
+                                      torch.device("cuda", torch.cuda.current_device()))
+
+
 def _make_runner(cfg, comm: TPComm):
     from ..engine.runner import ModelRunner
     from ..models.config import resolve_model
@@ -80,6 +91,7 @@ def _spawned_worker(rank: int, world: int, port: int, bcast_name: str, cfg, devi
     dist.init_process_group(_backend(device), init_method=f"tcp://127.0.0.1:{port}", rank=rank,
                             world_size=world, **kw)
     comm = TPComm(dist.group.WORLD, rank, world)
+    _maybe_custom_ar(cfg, comm, device)
     bcast = ShmBroadcast(world - 1, name=bcast_name, create=False, reader_index=rank - 1)
     try:
         worker_loop(cfg, comm, bcast)
@@ -113,6 +125,7 @@ class TPGroup:
         dist.init_process_group(_backend(self.device), init_method=f"tcp://127.0.0.1:{self.port}",
                                 rank=0, world_size=self.world, **kw)
         self.comm = TPComm(dist.group.WORLD, 0, self.world)
+        _maybe_custom_ar(cfg, self.comm, self.device)
 
     def attach(self, runner):
         runner.bcast = self.bcast
@@ -169,6 +182,7 @@ def torchrun_tp(cfg) -> Optional[object]:
         kw = {"device_id": torch.device(f"cuda:{local}")} if device == "cuda" else {}
         dist.init_process_group(_backend(device), **kw)
     comm = TPComm(dist.group.WORLD, rank, world)
+    _maybe_custom_ar(cfg, comm, device)
     name = [None]
     bcast = None
     if rank == 0:
