@@ -55,11 +55,18 @@ def main():
     ap.add_argument("--top-p", type=float, default=0.9)
     ap.add_argument("--no-agent", action="store_true", help="direct engine path instead of the agent")
     ap.add_argument("--port", type=int, default=0)
+    ap.add_argument("--tp", type=int, default=1,
+                    help="tensor parallel: the N ranks form ONE engine (e.g. --model llama3-70b --tp 8); "
+                         "default: data parallel, one engine per rank")
+    ap.add_argument("--custom-allreduce", action="store_true", help="TP: one-shot xGMI all-reduce")
+    ap.add_argument("--device", default="cuda", help="TP mode only: cpu runs the same path over gloo")
     a = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.tp > 1:
+        return bench_tp(a, rank, world, local_rank)
 
     # ---- load generator child first (before this process touches the GPU) ----------
     from ws_load import client_process, summarize
@@ -193,8 +200,124 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    try:
+        asyncio.run_coroutine_threadsafe(asgi.stop(), loop).result(timeout=15)
+    except Exception:
+        pass
     loop.call_soon_threadsafe(loop.stop)
     engine.shutdown()
+
+
+def bench_tp(a, rank: int, world: int, local_rank: int):
+    """BASELINE config 4: one tensor-parallel engine over all ranks (RCCL/xGMI);
+    rank 0 serves the WebSocket stack and drives the load, the other ranks are
+    TP workers replaying rank 0's steps."""
+    if a.tp != world:
+        raise SystemExit(f"--tp {a.tp} needs exactly {a.tp} ranks (got {world})")
+    from ws_load import client_process, summarize
+
+    port = a.port or _free_port(18100)
+    sess_cfg = {"system_prompt": "You are a helpful voice assistant. Keep responses concise and "
+                                 "conversational.",
+                "temperature": a.temperature, "top_p": a.top_p, "max_tokens": a.gen,
+                "ignore_eos": True}
+    client = parent_conn = None
+    if rank == 0:
+        ctx = mp.get_context("spawn")
+        parent_conn, child_conn = ctx.Pipe()
+        client = ctx.Process(target=client_process, daemon=True,
+                             args=(child_conn, f"ws://127.0.0.1:{port}/ws/llm", a.sessions, sess_cfg,
+                                   a.words, 0))
+        client.start()
+    os.environ.setdefault("LOG_LEVEL", "WARNING")
+    os.environ["LLM_PROVIDER"] = "native"
+    os.environ["ENABLE_PYDANTIC_AI"] = "false" if a.no_agent else "true"
+    os.environ.setdefault("LLM_MAX_CONNECTIONS", str(max(64, a.sessions + 8)))
+    if a.device == "cpu":
+        os.environ["COMPUTE_DEVICE"] = "cpu"
+    import torch
+
+    from fasttalk_llm_microservice_amd.engine.config import EngineConfig
+    from fasttalk_llm_microservice_amd.engine.engine import AsyncEngine
+    from fasttalk_llm_microservice_amd.parallel.tp import torchrun_tp
+
+    t_init = time.time()
+    cfg = EngineConfig.from_env(model=a.model, device=a.device, tp_size=world,
+                                custom_allreduce=a.custom_allreduce)
+    if a.device == "cpu":
+        cfg.num_kv_blocks = cfg.num_kv_blocks or 512
+        cfg.max_model_len = min(cfg.max_model_len, 2048)
+    sync = torch.cuda.synchronize if a.device == "cuda" else (lambda: None)
+    eng = torchrun_tp(cfg)
+    if rank != 0:
+        return  # worker: returned after rank 0 sent "stop"
+    eng.runner.warmup([b for b in eng.runner.graph_sizes if b <= 2 * a.sessions])
+    aeng = AsyncEngine(eng).start()
+    from app.core.websocket_server_vllm import WebSocketLLMServer
+    from app.server.asgi_aiohttp import AiohttpASGIServer
+    from app.utils.config import Config
+    import asyncio
+
+    scfg = Config()
+    scfg.port = port
+    server = WebSocketLLMServer(scfg, engine=aeng)
+    asgi = AiohttpASGIServer(server.app, "127.0.0.1", port)
+    loop = asyncio.new_event_loop()
+    ready = threading.Event()
+
+    def serve():
+        asyncio.set_event_loop(loop)
+        loop.run_until_complete(asgi.start())
+        ready.set()
+        loop.run_forever()
+
+    threading.Thread(target=serve, daemon=True, name="asgi").start()
+    if not ready.wait(120):
+        raise RuntimeError("server did not start")
+    init_s = time.time() - t_init
+
+    def cmd(c):
+        parent_conn.send(c)
+        r = parent_conn.recv()
+        if not r.get("ok"):
+            raise RuntimeError(f"load client failed: {r.get('error')}")
+        return r.get("result")
+
+    cmd("open")
+    if a.warmup > 0:
+        cmd(("run", a.warmup))
+    sync()
+    t0 = time.perf_counter()
+    res = cmd(("run", a.steps))
+    sync()
+    elapsed = time.perf_counter() - t0
+    cmd("close")
+    client.join(timeout=30)
+    summ = summarize(res)
+    metrics = eng.metrics()
+    value = res["tokens"] / elapsed
+    out = {
+        "metric": "output tokens/sec (node) + p50 TTFT over WebSocket, "
+                  f"{a.model} TP={world} at {a.sessions} sessions",
+        "value": round(value, 2), "unit": "tokens/s", "n_gpus": world, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": round(1e3 * elapsed / a.steps, 2),
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+        "dtype": "bf16" if a.device == "cuda" else "fp32",
+        "data": "synthetic (random-init weights, synthetic English prompts, synthetic Llama-3 tokenizer)",
+        "config": {"model": a.model, "global_batch": a.sessions, "seq_len": eng.max_model_len,
+                   "parallelism": f"tp{world}", "custom_allreduce": a.custom_allreduce},
+        "p50_ttft_ms": summ.get("p50_ttft_ms"), "p99_ttft_ms": summ.get("p99_ttft_ms"),
+        "engine_decode_step_ms": round(metrics.get("decode_step_ms_avg", 0.0), 3),
+        "engine_decode_batch_avg": round(metrics.get("decode_batch_avg", 0.0), 2),
+        "init_s": round(init_s, 1),
+    }
+    print(json.dumps(out), flush=True)
+    try:
+        asyncio.run_coroutine_threadsafe(asgi.stop(), loop).result(timeout=15)
+    except Exception:
+        pass
+    loop.call_soon_threadsafe(loop.stop)
+    aeng.shutdown()
 
 
 if __name__ == "__main__":
