@@ -69,10 +69,10 @@ def main():
         out = torch.empty(M, n, device=dev).bfloat16()
         for nt, u in ops.SKINNY_CONFIGS:
             for splits in (1, 2, 4, 8, 16):
-                kstep = (512 if u == -2 else 64 * (u if u > 0 else 1)) * splits
+                kstep = (512 if u in (-2, -4) else 64 * (u if u > 0 else 1)) * splits
                 if n % (16 * nt) or k % kstep or splits * M * n > ws.numel():
                     continue
-                cols = 16 * nt if u == 0 else 64 * nt
+                cols = 16 * nt if u in (0, -3) else 64 * nt
                 blocks = (n // cols) * splits
                 if blocks < 128 or blocks > 16384:
                     continue
@@ -81,6 +81,10 @@ def main():
                 else:
                     mk = lambda W, nt=nt, u=u, sp=splits: (
                         lambda: ops.skinny_gemm(x, W, ws=ws, splits=sp, nt=nt, u=u))
+                if u in ops.PACKED_VARIANTS:  # pre-packed weights
+                    packed = [ops.pack_weight(W) for W in Ws]
+                    mk0 = mk
+                    mk = lambda W, mk0=mk0, packed=packed: mk0(packed[[id(x) for x in Ws].index(id(W))])
                 f0 = mk(Ws[0])
                 f0()
                 torch.cuda.synchronize()
@@ -88,9 +92,11 @@ def main():
                 err = (got - ref).abs().max().item()
                 t = graph_time([mk(W) for W in seqW])
                 rows.append((t, nt, u, splits, blocks, err))
+                if u in ops.PACKED_VARIANTS:
+                    del packed
         rows.sort()
         for t, nt, u, splits, blocks, err in rows[: a.top]:
-            print(f"   {({0: 'ks', -1: 'xs', -2: 'xc'}).get(u, 'cs')} nt={nt} u={u} splits={splits:2d} blocks={blocks:5d}: "
+            print(f"   {({0: 'ks', -1: 'xs', -2: 'xc', -3: 'pk', -4: 'xcp'}).get(u, 'cs')} nt={nt} u={u} splits={splits:2d} blocks={blocks:5d}: "
                   f"{t:7.2f} us ({n * k * 2 / t / 1e3:5.0f} GB/s) err={err:.4f}", flush=True)
         bad = [r for r in rows if r[5] > 0.05]
         if bad:

@@ -42,7 +42,7 @@ int ft_skinny_gemm_ks(const void* x, int x_stride, int M, const void* w, int N, 
 int ft_skinny_gemm_xs(const void* x, int x_stride, int M, const void* w, int N, int K, float* ws,
                       void* out, int out_stride, int splits, int nt, hipStream_t stream);
 int ft_skinny_gemm_xc(const void* x, int x_stride, int M, const void* w, int N, int K, float* ws,
-                      void* out, int out_stride, int splits, int nt, hipStream_t stream);
+                      void* out, int out_stride, int splits, int nt, int packed, hipStream_t stream);
 int ft_embed_rmsnorm(void* out, void* residual, const int* ids, const void* table, const void* w,
                      int rows, int hidden, int vocab, float eps, hipStream_t stream);
 size_t ft_ar_header_bytes();
@@ -54,6 +54,8 @@ int ft_ar_ipc_close(void* ptr);
 int ft_ar_read_error(void* mine, int* err);
 int ft_ar_allreduce(void* out, const void* x, long n, const uint64_t* peers_dev, int rank, int world,
                     size_t max_bytes, unsigned spin_budget, hipStream_t stream);
+int ft_skinny_gemm_pk(const void* x, int x_stride, int M, const void* wpk, int N, int K, float* ws,
+                      void* out, int out_stride, int splits, int nt, hipStream_t stream);
 int ft_row_rmsnorm(const void* x, int x_stride, const float* ws, int splits, void* out,
                    int out_stride, void* residual, const void* w, int rows, int hidden, float eps,
                    hipStream_t stream);
@@ -298,9 +300,13 @@ void skinny_gemm(at::Tensor x, at::Tensor w, c10::optional<at::Tensor> out,
     op = out->data_ptr();
     ostride = (int)out->stride(0);
   }
-  if (u == -2)  // x-chunk variant
-    check_rc(ft_skinny_gemm_xc(x.data_ptr(), (int)x.stride(0), M, w.data_ptr(), N, K, wsp, op,
+  if (u == -3)  // pre-packed weights (w is the packed [N/16][K/64][2][64][8] image)
+    check_rc(ft_skinny_gemm_pk(x.data_ptr(), (int)x.stride(0), M, w.data_ptr(), N, K, wsp, op,
                                ostride, (int)splits, (int)nt, cur_stream()),
+             "skinny_gemm_pk");
+  else if (u == -2 || u == -4)  // x-chunk variant (-4: pre-packed weights)
+    check_rc(ft_skinny_gemm_xc(x.data_ptr(), (int)x.stride(0), M, w.data_ptr(), N, K, wsp, op,
+                               ostride, (int)splits, (int)nt, u == -4 ? 1 : 0, cur_stream()),
              "skinny_gemm_xc");
   else if (u < 0)  // x-in-LDS variant
     check_rc(ft_skinny_gemm_xs(x.data_ptr(), (int)x.stride(0), M, w.data_ptr(), N, K, wsp, op,

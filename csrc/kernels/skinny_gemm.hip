@@ -395,7 +395,7 @@ __global__ __launch_bounds__(256) void skinny_xs_kernel(
 // wave in flight), then runs the chunk's MFMAs as the weights land.  Two
 // barriers per chunk; x loads are issued before the weight loads so the wait
 // for x is an exact vmcnt that leaves the weight stream in flight.
-template <int MT, int NT>
+template <int MT, int NT, bool PACKED>
 __global__ __launch_bounds__(256) void skinny_xc_kernel(
     const uint16_t* __restrict__ x, int x_stride, int M, const uint16_t* __restrict__ w, int K,
     float* __restrict__ ws, uint16_t* __restrict__ out, int out_stride, int N, int k_slice) {
@@ -414,8 +414,12 @@ __global__ __launch_bounds__(256) void skinny_xc_kernel(
 
   const uint16_t* wp[NT];
 #pragma unroll
-  for (int j = 0; j < NT; ++j)
-    wp[j] = w + (size_t)min(n0 + 16 * j + l15, N - 1) * K + kbeg + 16 * g;
+  for (int j = 0; j < NT; ++j) {
+    if constexpr (PACKED)  // fragment image: [N/16][K/64][half][lane][8]
+      wp[j] = w + ((size_t)(min(n0 + 16 * j, N - 16) / 16) * (K >> 6) + (kbeg >> 6)) * 1024 + lane * 8;
+    else
+      wp[j] = w + (size_t)min(n0 + 16 * j + l15, N - 1) * K + kbeg + 16 * g;
+  }
 
   sk_floatx4 acc[MT][NT];
 #pragma unroll
@@ -439,8 +443,14 @@ __global__ __launch_bounds__(256) void skinny_xc_kernel(
     for (int st = 0; st < 8; ++st)
 #pragma unroll
       for (int j = 0; j < NT; ++j) {
-        wr[st][j][0] = nt_load16(wp[j] + kc + st * 64);
-        wr[st][j][1] = nt_load16(wp[j] + kc + st * 64 + 8);
+        if constexpr (PACKED) {
+          const uint16_t* p = wp[j] + (size_t)((kc >> 6) + st) * 1024;
+          wr[st][j][0] = nt_load16(p);
+          wr[st][j][1] = nt_load16(p + 512);
+        } else {
+          wr[st][j][0] = nt_load16(wp[j] + kc + st * 64);
+          wr[st][j][1] = nt_load16(wp[j] + kc + st * 64 + 8);
+        }
       }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -494,6 +504,106 @@ __global__ __launch_bounds__(256) void skinny_xc_kernel(
         }
       }
     }
+}
+
+
+// ---------------------------------------------------------------------------
+// Variant "pk" (pre-packed weights): W is re-laid out once at load time so that
+// every (16-column tile, 64-wide k-step) MFMA B-fragment is 2 KiB contiguous
+// in exactly the order the 64 lanes load it ([N/16][K/64][half][lane][8]).  A
+// wave instruction then reads 1 KiB of consecutive bytes (whole lines, one
+// DRAM page stream per wave) instead of 16 rows x 64 B, and a wave streaming
+// its column tile along K walks one contiguous region.  Waves split K as in
+// "ks"; x fragments come straight from L2.
+template <int MT, int NT>
+__global__ __launch_bounds__(256) void skinny_pk_kernel(
+    const uint16_t* __restrict__ x, int x_stride, int M, const uint16_t* __restrict__ wpk, int K,
+    float* __restrict__ ws, uint16_t* __restrict__ out, int out_stride, int N, int k_slice) {
+  __shared__ float s_red[4][MT * NT * 4][64];
+  const int lane = lane_id(), wave = wave_id();
+  const int l15 = lane & 15, g = lane >> 4;
+  const int n0 = blockIdx.x * (16 * NT);
+  const int s = blockIdx.y;
+  const int kbeg = s * k_slice;
+  const int ksteps_total = K >> 6;
+  const int step0 = kbeg >> 6;
+
+  // packed fragment base of column tile (n0/16 + j), k-step 0, this lane
+  const uint16_t* wp[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j)
+    wp[j] = wpk + ((size_t)(n0 / 16 + j) * ksteps_total) * 1024 + lane * 8;
+  const uint16_t* xp[MT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+    const int r = min(16 * i + l15, M - 1);
+    xp[i] = x + (size_t)r * x_stride + kbeg + 16 * g;
+  }
+
+  sk_floatx4 acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = sk_floatx4{0.f, 0.f, 0.f, 0.f};
+
+  const int nsteps = k_slice >> 6;
+  const int my_steps = nsteps > wave ? (nsteps - wave + 3) >> 2 : 0;
+  const int last = my_steps - 1;
+  auto kst = [&](int t) { return wave + 4 * min(t, last); };  // k-step index within the split
+  auto load = [&](SkStage<MT, NT>& st, int t) {
+    const int ks = kst(t);
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const uint16_t* p = wp[j] + (size_t)(step0 + ks) * 1024;
+      st.w[j][0] = nt_load16(p);
+      st.w[j][1] = nt_load16(p + 512);
+    }
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      const uint4* p = reinterpret_cast<const uint4*>(xp[i] + ks * 64);
+      st.x[i][0] = p[0];
+      st.x[i][1] = p[1];
+    }
+  };
+  if (my_steps > 0) {
+    SkStage<MT, NT> a, b;
+    load(a, 0);
+    int t = 0;
+    for (; t + 2 <= my_steps; t += 2) {
+      load(b, t + 1);
+      __builtin_amdgcn_sched_barrier(0);
+      sk_mma_stage<MT, NT>(a, acc);
+      __builtin_amdgcn_sched_barrier(0);
+      load(a, t + 2);
+      __builtin_amdgcn_sched_barrier(0);
+      sk_mma_stage<MT, NT>(b, acc);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (t < my_steps) sk_mma_stage<MT, NT>(a, acc);
+  }
+
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) s_red[wave][(i * NT + j) * 4 + r][lane] = acc[i][j][r];
+  __syncthreads();
+  constexpr int NREG = MT * NT * 4;
+  const int ln = threadIdx.x & 63;
+  float* slab = ws + (size_t)s * M * N;
+  for (int reg = threadIdx.x >> 6; reg < NREG; reg += 4) {
+    const float v = s_red[0][reg][ln] + s_red[1][reg][ln] + s_red[2][reg][ln] + s_red[3][reg][ln];
+    const int i = reg / (NT * 4), j = (reg / 4) % NT, r = reg & 3;
+    const int m = 16 * i + (ln >> 4) * 4 + r;
+    const int n = n0 + 16 * j + (ln & 15);
+    if (m < M) {
+      if (gridDim.y == 1)
+        out[(size_t)m * out_stride + n] = f32_to_bf16(v);
+      else
+        slab[(size_t)m * N + n] = v;
+    }
+  }
 }
 
 }  // namespace ft
@@ -594,7 +704,7 @@ extern "C" int ft_skinny_gemm_xs(const void* x, int x_stride, int M, const void*
 // K % (512*splits) == 0.
 extern "C" int ft_skinny_gemm_xc(const void* x, int x_stride, int M, const void* w, int N, int K,
                                  float* ws, void* out, int out_stride, int splits, int nt,
-                                 hipStream_t stream) {
+                                 int packed, hipStream_t stream) {
   if (M <= 0) return 0;
   if (M > 64 || splits < 1) return -1;
   if (N % (16 * nt) != 0) return -2;
@@ -606,9 +716,14 @@ extern "C" int ft_skinny_gemm_xc(const void* x, int x_stride, int M, const void*
   const int k_slice = K / splits;
 #define FT_XC(MT_, NT_)                                                                      \
   if (mt == MT_ && nt == NT_) {                                                              \
-    hipLaunchKernelGGL((ft::skinny_xc_kernel<MT_, NT_>), grid, block, 0, stream,             \
-                       (const uint16_t*)x, x_stride, M, (const uint16_t*)w, K, ws,           \
-                       (uint16_t*)out, out_stride, N, k_slice);                              \
+    if (packed)                                                                              \
+      hipLaunchKernelGGL((ft::skinny_xc_kernel<MT_, NT_, true>), grid, block, 0, stream,     \
+                         (const uint16_t*)x, x_stride, M, (const uint16_t*)w, K, ws,         \
+                         (uint16_t*)out, out_stride, N, k_slice);                            \
+    else                                                                                     \
+      hipLaunchKernelGGL((ft::skinny_xc_kernel<MT_, NT_, false>), grid, block, 0, stream,    \
+                         (const uint16_t*)x, x_stride, M, (const uint16_t*)w, K, ws,         \
+                         (uint16_t*)out, out_stride, N, k_slice);                            \
     return static_cast<int>(hipGetLastError());                                              \
   }
 #define FT_XC_NT(NT_) FT_XC(1, NT_) FT_XC(2, NT_) FT_XC(3, NT_) FT_XC(4, NT_)
@@ -616,5 +731,34 @@ extern "C" int ft_skinny_gemm_xc(const void* x, int x_stride, int M, const void*
   FT_XC_NT(2)
 #undef FT_XC_NT
 #undef FT_XC
+  return -5;
+}
+
+// Pre-packed-weight variant (wpk from ft_pack_weights layout).  Requirements
+// (checked): M <= 64, N % (16*nt) == 0, K % (64*splits) == 0.
+extern "C" int ft_skinny_gemm_pk(const void* x, int x_stride, int M, const void* wpk, int N, int K,
+                                 float* ws, void* out, int out_stride, int splits, int nt,
+                                 hipStream_t stream) {
+  if (M <= 0) return 0;
+  if (M > 64 || splits < 1) return -1;
+  if (N % (16 * nt) != 0) return -2;
+  if (K % (64 * splits) != 0) return -3;
+  if (splits > 1 && ws == nullptr) return -4;
+  const int mt = (M + 15) / 16;
+  dim3 grid(N / (16 * nt), splits), block(256);
+  const int k_slice = K / splits;
+#define FT_PK(MT_, NT_)                                                                      \
+  if (mt == MT_ && nt == NT_) {                                                              \
+    hipLaunchKernelGGL((ft::skinny_pk_kernel<MT_, NT_>), grid, block, 0, stream,             \
+                       (const uint16_t*)x, x_stride, M, (const uint16_t*)wpk, K, ws,         \
+                       (uint16_t*)out, out_stride, N, k_slice);                              \
+    return static_cast<int>(hipGetLastError());                                              \
+  }
+#define FT_PK_NT(NT_) FT_PK(1, NT_) FT_PK(2, NT_) FT_PK(3, NT_) FT_PK(4, NT_)
+  FT_PK_NT(1)
+  FT_PK_NT(2)
+  FT_PK_NT(4)
+#undef FT_PK_NT
+#undef FT_PK
   return -5;
 }

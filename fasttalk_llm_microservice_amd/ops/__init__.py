@@ -202,9 +202,24 @@ def kv_block_copy(k_cache, v_cache, pairs: torch.Tensor):
 # ---------------------------------------------------------------------------------
 
 # (nt, u) instantiated; u == 0 selects the K-split-wave variant (skinny_ks_kernel),
-# u == -1 the x-in-LDS variant (skinny_xs_kernel), u == -2 the x-chunk variant (skinny_xc_kernel)
+# u == -1 the x-in-LDS variant (skinny_xs_kernel), u == -2 the x-chunk variant (skinny_xc_kernel),
+# u == -3 pre-packed weights (skinny_pk_kernel; pass pack_weight(w) as w), u == -4 the x-chunk
+# variant on pre-packed weights
 SKINNY_CONFIGS = [(1, 2), (1, 4), (2, 2), (2, 4), (4, 1), (4, 2), (1, 0), (2, 0), (4, 0),
-                  (1, -1), (2, -1), (4, -1), (1, -2), (2, -2)]
+                  (1, -1), (2, -1), (4, -1), (1, -2), (2, -2), (1, -3), (2, -3), (4, -3),
+                  (1, -4), (2, -4)]
+PACKED_VARIANTS = (-3, -4)
+
+
+def pack_weight(w: torch.Tensor) -> torch.Tensor:
+    """[N, K] -> the MFMA-fragment image the "pk" kernel streams: every 16-column
+    x 64-k fragment contiguous, lanes in load order ([N/16][K/64][2][64][8]).
+    Returned as an [N, K]-shaped tensor (same bytes, different order)."""
+    n, k = w.shape
+    assert n % 16 == 0 and k % 64 == 0
+    # (t, r, s, g, h, e) -> (t, s, h, g, r, e); lane = g * 16 + r
+    p = w.reshape(n // 16, 16, k // 64, 4, 2, 8).permute(0, 2, 4, 3, 1, 5).contiguous()
+    return p.view(n, k)
 
 
 def skinny_gemm_supported(m: int, n: int, k: int) -> bool:
