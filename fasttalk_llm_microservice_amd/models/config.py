@@ -71,6 +71,8 @@ MODELS = {
     # small shapes for CPU tests (keep kernel constraints: hidden % 512 == 0)
     "tiny": ModelConfig("tiny", 512, 2, 8, 2, 64, 1024, vocab_size=128256),
     "tiny-gqa4": ModelConfig("tiny-gqa4", 512, 2, 8, 2, 64, 1536, vocab_size=128256),
+    # 8B-shaped heads (d=128, GQA 4) at hidden 2048: exercises the packed-weight decode GEMMs
+    "tiny-2k": ModelConfig("tiny-2k", 2048, 2, 16, 4, 128, 4096, vocab_size=128256),
 }
 
 # names used by the reference's configuration / Ollama tags / HF ids

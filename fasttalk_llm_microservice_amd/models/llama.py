@@ -12,6 +12,7 @@ directly.  The same code runs the CPU backend through the fp32 reference ops.
 from __future__ import annotations
 
 import dataclasses
+import os
 from typing import List, Optional, Tuple
 
 import torch
@@ -62,6 +63,15 @@ class LayerWeights:
     wd: torch.Tensor
     ln1: torch.Tensor
     ln2: torch.Tensor
+    wd_pk: Optional[torch.Tensor] = None   # down proj in the MFMA-fragment image (decode GEMM)
+
+
+# decode (<= 64 rows) GEMMs on pre-packed weights, measured from cold caches on
+# MI355X at M = 64 (bench/gemm_sweep.py): down 28 us vs hipBLASLt 40 us, LM head
+# 197 vs 212.  The down projection runs split-K into fp32 slabs that the next
+# residual-add + RMSNorm reduces (no extra kernel); the LM head stores bf16.
+DOWN_SPLITS = 4
+PACKED_ROWS = 64
 
 
 class LlamaModel:
@@ -85,6 +95,10 @@ class LlamaModel:
         self.lm_head: Optional[torch.Tensor] = None
         self.cos_sin = ref.rope_cos_sin(self.d, max(max_model_len, 16) + 1, cfg.rope_theta,
                                         cfg.rope_scaling, device=self.device)
+        self.lm_head_pk: Optional[torch.Tensor] = None
+        self.ws: Optional[torch.Tensor] = None
+        self.use_packed = (self.device.type == "cuda" and dtype == torch.bfloat16
+                           and os.environ.get("FT_PACKED_GEMM", "1") != "0")
 
     # ------------------------------------------------------------------ weights
     def _set_layers(self, shards):
@@ -126,6 +140,7 @@ class LlamaModel:
                 self.lm_head = torch.empty(self.vocab_shard, cfg.hidden_size, dtype=self.dtype,
                                            device=self.device).normal_(0.0, std, generator=g)
         self.norm = torch.ones(cfg.hidden_size, dtype=self.dtype, device=self.device)
+        self._prepare_packed()
         return self
 
     def load_checkpoint(self, ckpt_dir: str):
@@ -143,7 +158,26 @@ class LlamaModel:
         else:
             lm = idx.get("lm_head.weight").to(self.dtype)
         self.lm_head = W._shard_rows(lm, self.rank, self.tp).contiguous().to(self.device)
+        self._prepare_packed()
         return self
+
+    def _prepare_packed(self):
+        """Adds the packed copies the decode GEMMs stream (one extra copy of the
+        down projections and the LM head: ~4 GB for Llama-3-8B, of 288 GB)."""
+        if not self.use_packed:
+            return
+        cfg = self.cfg
+        H = cfg.hidden_size
+        inter = self.layers[0].wd.shape[1] if self.layers else 0
+        down_ok = (self.tp == 1 and H % 2048 == 0 and H % 64 == 0
+                   and inter % (64 * DOWN_SPLITS) == 0)
+        for L in self.layers:
+            L.wd_pk = ops.pack_weight(L.wd) if down_ok else None
+        if self.lm_head is not None and self.lm_head.shape[0] % 32 == 0 and H % 512 == 0:
+            self.lm_head_pk = ops.pack_weight(self.lm_head)
+        if down_ok:
+            self.ws = torch.empty(DOWN_SPLITS * PACKED_ROWS * H, dtype=torch.float32,
+                                  device=self.device)
 
     # ------------------------------------------------------------------ KV cache
     def kv_cache_shape(self, num_blocks: int, block_size: int) -> Tuple[int, ...]:
@@ -162,11 +196,18 @@ class LlamaModel:
         eps = cfg.rms_norm_eps
         nq, nkv, d = self.nq, self.nkv, self.d
         t = input_ids.shape[0]
+        H = cfg.hidden_size
         residual = None
         x = None
+        slab = False  # the previous down projection left fp32 split-K slabs in self.ws
+        packed = t <= PACKED_ROWS and self.ws is not None
         for li, L in enumerate(self.layers):
             if residual is None:
                 x, residual = ops.embed_rmsnorm(input_ids, self.embed, L.ln1, eps)  # K1 + K2
+            elif slab:  # residual += sum(slabs); x = rmsnorm(residual) * ln1
+                x = torch.empty(t, H, dtype=self.dtype, device=self.device)
+                ops.row_rmsnorm(x, L.ln1, eps, t, ws=self.ws, splits=DOWN_SPLITS, residual=residual)
+                slab = False
             else:
                 ops.fused_add_rmsnorm(x, residual, L.ln1, eps)
             qkv = F.linear(x, L.wqkv)
@@ -187,8 +228,15 @@ class LlamaModel:
             ops.fused_add_rmsnorm(x, residual, L.ln2, eps)
             gu = F.linear(x, L.wgu)
             h = ops.silu_mul(gu)
-            x = F.linear(h, L.wd)
-            self.comm.all_reduce(x)
+            if packed and L.wd_pk is not None:
+                ops.skinny_gemm(h, L.wd_pk, ws=self.ws, splits=DOWN_SPLITS, nt=4, u=-3)
+                slab = True
+            else:
+                x = F.linear(h, L.wd)
+                self.comm.all_reduce(x)
+        if slab:
+            x = torch.empty(t, H, dtype=self.dtype, device=self.device)
+            ops.slab_store(self.ws, DOWN_SPLITS, t, H, x)
         idx = meta.logits_indices
         if idx.numel() != t:
             x = x.index_select(0, idx)
@@ -200,5 +248,9 @@ class LlamaModel:
 
     def compute_logits(self, h: torch.Tensor) -> torch.Tensor:
         """[B, H] -> [B, V] logits (bf16 on GPU; vocab-parallel shards gathered)."""
-        logits = F.linear(h, self.lm_head)
+        if self.lm_head_pk is not None and h.shape[0] <= PACKED_ROWS:
+            logits = torch.empty(h.shape[0], self.lm_head.shape[0], dtype=h.dtype, device=h.device)
+            ops.skinny_gemm(h, self.lm_head_pk, out=logits, splits=1, nt=2, u=-4)
+        else:
+            logits = F.linear(h, self.lm_head)
         return self.comm.all_gather_last(logits)

@@ -24,12 +24,16 @@ def _prompts(n, lens, seed=0):
     return [rng.integers(0, 120000, l).tolist() for l in lens[:n]]
 
 
-def test_gpu_logits_match_cpu_reference():
-    """Full prefill forward on GPU (bf16 HIP kernels) vs CPU fp32 reference ops."""
-    cfg = MODELS["tiny-gqa4"]
-    g = LlamaModel(cfg, torch.device("cuda"), torch.bfloat16, max_model_len=512).init_random(3)
+@pytest.mark.parametrize("model", ["tiny-gqa4", "tiny-2k"])
+def test_gpu_logits_match_cpu_reference(model):
+    """Full forward on GPU (bf16 HIP kernels; at hidden 2048 the down projection
+    and LM head run on the packed-weight skinny GEMMs) vs CPU fp32 reference ops."""
+    cfg = MODELS[model]
+    # consistent=True: both draw the same unsharded weights on the host from one seed
+    g = LlamaModel(cfg, torch.device("cuda"), torch.bfloat16, max_model_len=512).init_random(
+        3, consistent=True)
     c = LlamaModel(cfg, torch.device("cpu"), torch.float32, max_model_len=512)
-    c.init_random(3)
+    c.init_random(3, consistent=True)
     T, bs, nblk = 40, 16, 8
     for m in (g, c):
         kv = m.allocate_kv_cache(nblk, bs)
@@ -54,11 +58,12 @@ def test_gpu_logits_match_cpu_reference():
     assert agree > 0.9
 
 
-def test_graph_decode_matches_eager():
+@pytest.mark.parametrize("model", ["tiny", "tiny-2k"])
+def test_graph_decode_matches_eager(model):
     prompts = _prompts(5, [5, 17, 33, 64, 100])
     sp = SamplingParams(temperature=0.0, max_tokens=24, ignore_eos=True)
-    a = _engine(enforce_eager=False).generate(prompts, sp)
-    b = _engine(enforce_eager=True).generate(prompts, sp)
+    a = _engine(model=model, enforce_eager=False).generate(prompts, sp)
+    b = _engine(model=model, enforce_eager=True).generate(prompts, sp)
     assert a == b
 
 

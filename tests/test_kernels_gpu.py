@@ -339,3 +339,22 @@ def test_embed_rmsnorm(hidden):
     rows = table[ids.long()]
     assert torch.equal(res, rows)
     _close(out, ref.rmsnorm(rows, w, 1e-5), atol=2e-2, rtol=1e-2, msg="embed_rmsnorm")
+
+
+@pytest.mark.parametrize("n,k,splits,nt,u", [(4096, 14336, 4, 4, -3), (2048, 4096, 4, 4, -3),
+                                             (128256, 4096, 1, 2, -4), (6144, 4096, 8, 2, -4),
+                                             (4096, 4096, 8, 1, -4)])
+@pytest.mark.parametrize("m", [1, 37, 64])
+def test_skinny_gemm_packed(m, n, k, splits, nt, u):
+    """Packed-weight decode GEMMs vs fp32 torch (split-K slabs summed on the host)."""
+    w = (torch.randn(n, k, device=DEV) * 0.02).bfloat16()
+    x = torch.randn(m, k, device=DEV).bfloat16()
+    ref_y = x.float() @ w.float().t()
+    wp = ops.pack_weight(w)
+    if splits == 1:
+        y = ops.skinny_gemm(x, wp, splits=1, nt=nt, u=u).float()
+    else:
+        ws = torch.empty(splits * m * n, device=DEV)
+        ops.skinny_gemm(x, wp, ws=ws, splits=splits, nt=nt, u=u)
+        y = ws.view(splits, m, n).sum(0)
+    _close(y, ref_y, atol=3e-2, rtol=2e-2, msg="packed skinny gemm")
