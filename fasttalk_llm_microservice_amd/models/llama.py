@@ -64,13 +64,17 @@ class LayerWeights:
     ln1: torch.Tensor
     ln2: torch.Tensor
     wd_pk: Optional[torch.Tensor] = None   # down proj in the MFMA-fragment image (decode GEMM)
+    wgu_pk: Optional[torch.Tensor] = None  # gate_up in the MFMA-fragment image
 
 
 # decode (<= 64 rows) GEMMs on pre-packed weights, measured from cold caches on
-# MI355X at M = 64 (bench/gemm_sweep.py): down 28 us vs hipBLASLt 40 us, LM head
-# 197 vs 212.  The down projection runs split-K into fp32 slabs that the next
-# residual-add + RMSNorm reduces (no extra kernel); the LM head stores bf16.
+# MI355X at M = 64 (bench/gemm_sweep.py): down 28 us vs hipBLASLt 40 us, gate_up
+# 46 vs 55, LM head 197 vs 212.  The down projection runs split-K into fp32 slabs
+# that the next residual-add + RMSNorm reduces (no extra kernel); gate_up's two
+# slabs are reduced by the SiLU-mul kernel (which runs anyway); the LM head
+# stores bf16.
 DOWN_SPLITS = 4
+GU_SPLITS = 2
 PACKED_ROWS = 64
 
 
@@ -171,13 +175,19 @@ class LlamaModel:
         inter = self.layers[0].wd.shape[1] if self.layers else 0
         down_ok = (self.tp == 1 and H % 2048 == 0 and H % 64 == 0
                    and inter % (64 * DOWN_SPLITS) == 0)
+        # gate_up on packed weights measured no faster in the serving loop than
+        # hipBLASLt (the slab reduction eats the GEMM gain) and costs another
+        # copy of the largest weight: opt-in
+        gu_ok = (down_ok and H % (512 * GU_SPLITS) == 0 and (2 * inter) % 32 == 0
+                 and os.environ.get("FT_PACKED_GATE_UP", "0") == "1")
         for L in self.layers:
             L.wd_pk = ops.pack_weight(L.wd) if down_ok else None
+            L.wgu_pk = ops.pack_weight(L.wgu) if gu_ok else None
         if self.lm_head is not None and self.lm_head.shape[0] % 32 == 0 and H % 512 == 0:
             self.lm_head_pk = ops.pack_weight(self.lm_head)
         if down_ok:
-            self.ws = torch.empty(DOWN_SPLITS * PACKED_ROWS * H, dtype=torch.float32,
-                                  device=self.device)
+            n = max(DOWN_SPLITS * H, GU_SPLITS * 2 * inter if gu_ok else 0)
+            self.ws = torch.empty(PACKED_ROWS * n, dtype=torch.float32, device=self.device)
 
     # ------------------------------------------------------------------ KV cache
     def kv_cache_shape(self, num_blocks: int, block_size: int) -> Tuple[int, ...]:
@@ -226,8 +236,14 @@ class LlamaModel:
             x = F.linear(attn, L.wo)
             self.comm.all_reduce(x)
             ops.fused_add_rmsnorm(x, residual, L.ln2, eps)
-            gu = F.linear(x, L.wgu)
-            h = ops.silu_mul(gu)
+            if packed and L.wgu_pk is not None:
+                ops.skinny_gemm(x, L.wgu_pk, ws=self.ws, splits=GU_SPLITS, nt=2, u=-4)
+                inter = L.wgu.shape[0] // 2
+                h = torch.empty(t, inter, dtype=self.dtype, device=self.device)
+                ops.slab_silu(self.ws, GU_SPLITS, t, inter, h)
+            else:
+                gu = F.linear(x, L.wgu)
+                h = ops.silu_mul(gu)
             if packed and L.wd_pk is not None:
                 ops.skinny_gemm(h, L.wd_pk, ws=self.ws, splits=DOWN_SPLITS, nt=4, u=-3)
                 slab = True
