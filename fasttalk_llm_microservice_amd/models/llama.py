@@ -63,19 +63,50 @@ class LayerWeights:
     wd: torch.Tensor
     ln1: torch.Tensor
     ln2: torch.Tensor
-    wd_pk: Optional[torch.Tensor] = None   # down proj in the MFMA-fragment image (decode GEMM)
-    wgu_pk: Optional[torch.Tensor] = None  # gate_up in the MFMA-fragment image
+    # the same weights in the MFMA-fragment image the decode GEMMs stream
+    wqkv_pk: Optional[torch.Tensor] = None
+    wo_pk: Optional[torch.Tensor] = None
+    wgu_pk: Optional[torch.Tensor] = None
+    wd_pk: Optional[torch.Tensor] = None
 
 
-# decode (<= 64 rows) GEMMs on pre-packed weights, measured from cold caches on
-# MI355X at M = 64 (bench/gemm_sweep.py): down 28 us vs hipBLASLt 40 us, gate_up
-# 46 vs 55, LM head 197 vs 212.  The down projection runs split-K into fp32 slabs
-# that the next residual-add + RMSNorm reduces (no extra kernel); gate_up's two
-# slabs are reduced by the SiLU-mul kernel (which runs anyway); the LM head
-# stores bf16.
-DOWN_SPLITS = 4
-GU_SPLITS = 2
+# Decode GEMMs (<= 64 rows) on pre-packed weights (csrc/kernels/skinny_gemm.hip,
+# "pk"/"xcp").  Per projection and row bucket: (nt, u, splits), or None for
+# hipBLASLt.  Chosen from cold-cache sweeps on MI355X (bench/gemm_sweep.py,
+# us at M = 1 / 8 / 16 / 32 / 64 vs hipBLASLt):
+#   qkv     9.8 / 10.3 / 11.1  vs 14-15   (M >= 32: hipBLASLt; its epilogue is RoPE)
+#   o       7.3 / 7.5 / 7.7 / 9.0 / 13.1 vs 14-15   split 2 -> slabs -> add+RMSNorm
+#   gate_up 35 / 38 / 41 / 45            vs 55-66   (M = 64: hipBLASLt)
+#   down    18.6 / 19.3 / 20 / 22 / 28   vs 26-40   split 2-4 -> slabs -> add+RMSNorm
+#   lm_head 148 / 161 / 174 / 184 / 197  vs 188-212
+# Split-K partial sums stay fp32 in one workspace and are reduced inside the
+# residual-add + RMSNorm that follows (row_rmsnorm from slabs): no extra kernel.
 PACKED_ROWS = 64
+_M_BUCKETS = (1, 8, 16, 32, 64)
+PACKED_PLAN = {
+    "qkv": {1: (1, -3, 1), 8: (2, -3, 1), 16: (2, -3, 1)},
+    "o": {1: (1, -3, 2), 8: (2, -3, 2), 16: (2, -3, 2), 32: (2, -3, 2), 64: (2, -3, 2)},
+    "gu": {1: (1, -3, 1), 8: (1, -3, 1), 16: (4, -3, 1), 32: (4, -3, 1)},
+    "down": {1: (1, -3, 2), 8: (2, -3, 4), 16: (4, -3, 4), 32: (4, -3, 4), 64: (4, -3, 4)},
+    "lm": {1: (1, -3, 1), 8: (2, -3, 1), 16: (4, -3, 1), 32: (1, -4, 1), 64: (2, -4, 1)},
+}
+MAX_SPLITS = 4
+
+
+def packed_cfg(proj: str, rows: int):
+    if rows > PACKED_ROWS:
+        return None
+    b = next(m for m in _M_BUCKETS if m >= rows)
+    return PACKED_PLAN[proj].get(b)
+
+
+def _packable(n: int, k: int, proj: str) -> bool:
+    """Every configuration the plan may pick for this projection fits the shape."""
+    for nt, u, sp in PACKED_PLAN[proj].values():
+        kq = 512 if u == -4 else 64
+        if n % (16 * nt) or k % (kq * sp) or n % 64:
+            return False
+    return True
 
 
 class LlamaModel:
@@ -166,28 +197,48 @@ class LlamaModel:
         return self
 
     def _prepare_packed(self):
-        """Adds the packed copies the decode GEMMs stream (one extra copy of the
-        down projections and the LM head: ~4 GB for Llama-3-8B, of 288 GB)."""
-        if not self.use_packed:
+        """Adds the packed copies the decode GEMMs stream (one more copy of the
+        layer weights and the LM head: ~16 GB for Llama-3-8B, of 288 GB)."""
+        if not self.use_packed or not self.layers:
             return
-        cfg = self.cfg
-        H = cfg.hidden_size
-        inter = self.layers[0].wd.shape[1] if self.layers else 0
-        down_ok = (self.tp == 1 and H % 2048 == 0 and H % 64 == 0
-                   and inter % (64 * DOWN_SPLITS) == 0)
-        # gate_up on packed weights measured no faster in the serving loop than
-        # hipBLASLt (the slab reduction eats the GEMM gain) and costs another
-        # copy of the largest weight: opt-in
-        gu_ok = (down_ok and H % (512 * GU_SPLITS) == 0 and (2 * inter) % 32 == 0
-                 and os.environ.get("FT_PACKED_GATE_UP", "0") == "1")
+        H = self.cfg.hidden_size
+        L0 = self.layers[0]
+        # o / down leave split-K slabs for the fused add+RMSNorm: TP=1 only (under
+        # TP the row-parallel outputs are all-reduced first) and hidden % 2048
+        slab_ok = self.tp == 1 and H % 2048 == 0
+        use = {
+            "qkv": _packable(*L0.wqkv.shape, "qkv"),
+            "o": slab_ok and _packable(*L0.wo.shape, "o"),
+            "gu": _packable(*L0.wgu.shape, "gu"),
+            "down": slab_ok and _packable(*L0.wd.shape, "down"),
+        }
         for L in self.layers:
-            L.wd_pk = ops.pack_weight(L.wd) if down_ok else None
-            L.wgu_pk = ops.pack_weight(L.wgu) if gu_ok else None
-        if self.lm_head is not None and self.lm_head.shape[0] % 32 == 0 and H % 512 == 0:
+            L.wqkv_pk = ops.pack_weight(L.wqkv) if use["qkv"] else None
+            L.wo_pk = ops.pack_weight(L.wo) if use["o"] else None
+            L.wgu_pk = ops.pack_weight(L.wgu) if use["gu"] else None
+            L.wd_pk = ops.pack_weight(L.wd) if use["down"] else None
+        if self.lm_head is not None and _packable(*self.lm_head.shape, "lm"):
             self.lm_head_pk = ops.pack_weight(self.lm_head)
-        if down_ok:
-            n = max(DOWN_SPLITS * H, GU_SPLITS * 2 * inter if gu_ok else 0)
-            self.ws = torch.empty(PACKED_ROWS * n, dtype=torch.float32, device=self.device)
+        if use["o"] or use["down"]:
+            self.ws = torch.empty(MAX_SPLITS * PACKED_ROWS * H, dtype=torch.float32,
+                                  device=self.device)
+
+    def _gemm(self, x: torch.Tensor, w: torch.Tensor, w_pk: Optional[torch.Tensor], proj: str):
+        """bf16 y = x w^T: packed decode GEMM when the plan has a split-1 config."""
+        c = packed_cfg(proj, x.shape[0]) if w_pk is not None else None
+        if c is None or c[2] != 1:
+            return F.linear(x, w)
+        nt, u, _ = c
+        return ops.skinny_gemm(x, w_pk, splits=1, nt=nt, u=u)
+
+    def _gemm_slab(self, x: torch.Tensor, w_pk: Optional[torch.Tensor], proj: str) -> int:
+        """Split-K packed GEMM into self.ws; returns the split count (0: not taken)."""
+        c = packed_cfg(proj, x.shape[0]) if (w_pk is not None and self.ws is not None) else None
+        if c is None:
+            return 0
+        nt, u, sp = c
+        ops.skinny_gemm(x, w_pk, ws=self.ws, splits=sp, nt=nt, u=u)
+        return sp
 
     # ------------------------------------------------------------------ KV cache
     def kv_cache_shape(self, num_blocks: int, block_size: int) -> Tuple[int, ...]:
@@ -209,21 +260,19 @@ class LlamaModel:
         H = cfg.hidden_size
         residual = None
         x = None
-        slab = False  # the previous down projection left fp32 split-K slabs in self.ws
-        packed = t <= PACKED_ROWS and self.ws is not None
+        slab = 0  # >0: the previous down projection left that many fp32 slabs in self.ws
         for li, L in enumerate(self.layers):
             if residual is None:
                 x, residual = ops.embed_rmsnorm(input_ids, self.embed, L.ln1, eps)  # K1 + K2
             elif slab:  # residual += sum(slabs); x = rmsnorm(residual) * ln1
                 x = torch.empty(t, H, dtype=self.dtype, device=self.device)
-                ops.row_rmsnorm(x, L.ln1, eps, t, ws=self.ws, splits=DOWN_SPLITS, residual=residual)
-                slab = False
+                ops.row_rmsnorm(x, L.ln1, eps, t, ws=self.ws, splits=slab, residual=residual)
             else:
                 ops.fused_add_rmsnorm(x, residual, L.ln1, eps)
-            qkv = F.linear(x, L.wqkv)
+            qkv = self._gemm(x, L.wqkv, L.wqkv_pk, "qkv")
             kc, vc = kv_caches[li]
             ops.rope_kv_write(qkv, meta.positions, self.cos_sin, meta.slot_mapping, kc, vc, nq, nkv, d)
-            attn = torch.empty(t, nq * d, dtype=x.dtype, device=x.device)
+            attn = torch.empty(t, nq * d, dtype=qkv.dtype, device=qkv.device)
             nd = meta.num_decode
             if nd > 0:
                 ops.decode_attention(attn[:nd], qkv[:nd], kc, vc, meta.dec_block_tables,
@@ -233,26 +282,23 @@ class LlamaModel:
                 ops.prefill_attention(attn[nd:], qkv[nd:], kc, vc, meta.block_tables, meta.seq_lens,
                                       meta.q_start_loc, meta.tile_info, meta.num_tiles, nq, nkv, d,
                                       self.scale)
-            x = F.linear(attn, L.wo)
-            self.comm.all_reduce(x)
-            ops.fused_add_rmsnorm(x, residual, L.ln2, eps)
-            if packed and L.wgu_pk is not None:
-                ops.skinny_gemm(x, L.wgu_pk, ws=self.ws, splits=GU_SPLITS, nt=2, u=-4)
-                inter = L.wgu.shape[0] // 2
-                h = torch.empty(t, inter, dtype=self.dtype, device=self.device)
-                ops.slab_silu(self.ws, GU_SPLITS, t, inter, h)
+            so = self._gemm_slab(attn, L.wo_pk, "o")
+            if so:
+                x = torch.empty(t, H, dtype=self.dtype, device=self.device)
+                ops.row_rmsnorm(x, L.ln2, eps, t, ws=self.ws, splits=so, residual=residual)
             else:
-                gu = F.linear(x, L.wgu)
-                h = ops.silu_mul(gu)
-            if packed and L.wd_pk is not None:
-                ops.skinny_gemm(h, L.wd_pk, ws=self.ws, splits=DOWN_SPLITS, nt=4, u=-3)
-                slab = True
-            else:
+                x = F.linear(attn, L.wo)
+                self.comm.all_reduce(x)
+                ops.fused_add_rmsnorm(x, residual, L.ln2, eps)
+            gu = self._gemm(x, L.wgu, L.wgu_pk, "gu")
+            h = ops.silu_mul(gu)
+            slab = self._gemm_slab(h, L.wd_pk, "down")
+            if not slab:
                 x = F.linear(h, L.wd)
                 self.comm.all_reduce(x)
         if slab:
             x = torch.empty(t, H, dtype=self.dtype, device=self.device)
-            ops.slab_store(self.ws, DOWN_SPLITS, t, H, x)
+            ops.slab_store(self.ws, slab, t, H, x)
         idx = meta.logits_indices
         if idx.numel() != t:
             x = x.index_select(0, idx)
@@ -264,9 +310,5 @@ class LlamaModel:
 
     def compute_logits(self, h: torch.Tensor) -> torch.Tensor:
         """[B, H] -> [B, V] logits (bf16 on GPU; vocab-parallel shards gathered)."""
-        if self.lm_head_pk is not None and h.shape[0] <= PACKED_ROWS:
-            logits = torch.empty(h.shape[0], self.lm_head.shape[0], dtype=h.dtype, device=h.device)
-            ops.skinny_gemm(h, self.lm_head_pk, out=logits, splits=1, nt=2, u=-4)
-        else:
-            logits = F.linear(h, self.lm_head)
+        logits = self._gemm(h, self.lm_head, self.lm_head_pk, "lm")
         return self.comm.all_gather_last(logits)

@@ -343,7 +343,9 @@ def test_embed_rmsnorm(hidden):
 
 @pytest.mark.parametrize("n,k,splits,nt,u", [(4096, 14336, 4, 4, -3), (2048, 4096, 4, 4, -3),
                                              (128256, 4096, 1, 2, -4), (6144, 4096, 8, 2, -4),
-                                             (4096, 4096, 8, 1, -4)])
+                                             (4096, 4096, 8, 1, -4), (6144, 4096, 1, 2, -3),
+                                             (28672, 4096, 1, 1, -3), (4096, 4096, 2, 2, -3),
+                                             (4096, 14336, 2, 1, -3), (128256, 4096, 1, 4, -3)])
 @pytest.mark.parametrize("m", [1, 37, 64])
 def test_skinny_gemm_packed(m, n, k, splits, nt, u):
     """Packed-weight decode GEMMs vs fp32 torch (split-K slabs summed on the host)."""
