@@ -83,6 +83,7 @@ class AgentEvent:
     cached_tokens: int = 0
     tool_call: Optional[Dict[str, Any]] = None
     tool_result: Optional[str] = None
+    engine_ttft_s: Optional[float] = None   # request arrival -> first token inside the engine
 
 
 class VoiceAgent:
@@ -228,7 +229,7 @@ class VoiceAgent:
                 n = len(out.token_ids)
                 if det is None:
                     if out.text or n:
-                        yield AgentEvent(text=out.text, num_tokens=n,
+                        yield AgentEvent(text=out.text, num_tokens=n, engine_ttft_s=out.ttft_s,
                                          prompt_tokens=out.num_prompt_tokens,
                                          cached_tokens=out.num_cached_tokens)
                     continue
@@ -239,6 +240,7 @@ class VoiceAgent:
                         held_tokens = 0
                     if emit or n:
                         yield AgentEvent(text=emit, num_tokens=n, prompt_tokens=out.num_prompt_tokens,
+                                         engine_ttft_s=out.ttft_s,
                                          cached_tokens=out.num_cached_tokens)
                 else:
                     held.append(out.text)

@@ -52,6 +52,7 @@ class _Turn:
         self.text = []
         self.ttft: Optional[float] = None
         self.last_emit: Optional[float] = None
+        self.engine_ttft: Optional[float] = None
         self.itl_sum = 0.0   # inter-token gaps between token frames (s)
         self.itl_n = 0
         self.finish_reason: Optional[str] = None
@@ -375,6 +376,8 @@ class WebSocketLLMServer:
                 stats["ttft_ms"] = turn.ttft * 1000.0
             if turn.itl_n:
                 stats["itl_ms"] = 1000.0 * turn.itl_sum / turn.itl_n
+            if turn.engine_ttft is not None:
+                stats["engine_ttft_ms"] = 1000.0 * turn.engine_ttft
             if turn.finish_reason is not None:
                 stats["finish_reason"] = turn.finish_reason
             if turn.prompt_tokens:
@@ -424,6 +427,8 @@ class WebSocketLLMServer:
                 min_tokens=int(g.get("min_tokens", 0) or 0)):
             if out.token_ids or out.text:
                 await self._emit(session_id, send, turn, out.text, len(out.token_ids), t0)
+            if out.ttft_s is not None and turn.engine_ttft is None:
+                turn.engine_ttft = out.ttft_s
             if out.num_prompt_tokens:
                 turn.prompt_tokens = out.num_prompt_tokens
                 turn.cached_tokens = out.num_cached_tokens
@@ -449,6 +454,8 @@ class WebSocketLLMServer:
                 min_tokens=int(g.get("min_tokens", 0) or 0)):
             if ev.text or ev.num_tokens:
                 await self._emit(session_id, send, turn, ev.text, ev.num_tokens, t0)
+            if ev.engine_ttft_s is not None and turn.engine_ttft is None:
+                turn.engine_ttft = ev.engine_ttft_s
             if ev.prompt_tokens:
                 turn.prompt_tokens = ev.prompt_tokens
                 turn.cached_tokens = ev.cached_tokens

@@ -31,6 +31,11 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "bench"))
 
 
+def _p50(xs):
+    xs = sorted(xs)
+    return round(xs[len(xs) // 2], 2) if xs else None
+
+
 def _free_port(base: int) -> int:
     for p in range(base, base + 200):
         with socket.socket() as s:
@@ -152,6 +157,8 @@ def main():
 
     summ = summarize(res)
     local = {"tokens": res["tokens"], "elapsed": elapsed, "ttft": res["ttft_s"],
+             "server_ttft": res.get("server_ttft_ms", []),
+             "engine_ttft": res.get("engine_ttft_ms", []),
              "cached": res["cached_prompt_tokens"], "prompt": res["prompt_tokens"]}
     if world > 1:
         allr = [None] * world
@@ -186,6 +193,8 @@ def main():
                                " -> in-process engine"},
             "p50_ttft_ms": round(1e3 * p(0.5), 2),
             "p99_ttft_ms": round(1e3 * p(0.99), 2),
+            "p50_server_ttft_ms": _p50([x for r in allr for x in r["server_ttft"]]),
+            "p50_engine_ttft_ms": _p50([x for r in allr for x in r["engine_ttft"]]),
             "per_session_tok_s": round(value / (a.sessions * world), 2),
             "reference_anchor": "8B single stream ~50-80 tok/s, ~200 ms TTFT on RTX 3090 (README.md:567)",
             "prefix_cache_hit_tokens": sum(r["cached"] for r in allr),

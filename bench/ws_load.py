@@ -71,6 +71,7 @@ class Session:
                        "latency_s": time.perf_counter() - t0, "frames": frames,
                        "tokens": int(st.get("tokens_generated", frames)),
                        "server_ttft_ms": st.get("ttft_ms"),
+                       "engine_ttft_ms": st.get("engine_ttft_ms"),
                        "cached_prompt_tokens": st.get("cached_prompt_tokens", 0),
                        "prompt_tokens": st.get("prompt_tokens", 0)}
                 self.turns.append(rec)
@@ -120,6 +121,8 @@ class LoadClient:
         return {"elapsed_s": dt, "tokens": sum(r["tokens"] for r in recs),
                 "frames": sum(r["frames"] for r in recs), "ttft_s": [r["ttft_s"] for r in recs],
                 "latency_s": [r["latency_s"] for r in recs],
+                "server_ttft_ms": [r["server_ttft_ms"] for r in recs if r["server_ttft_ms"] is not None],
+                "engine_ttft_ms": [r["engine_ttft_ms"] for r in recs if r["engine_ttft_ms"] is not None],
                 "cached_prompt_tokens": sum(r["cached_prompt_tokens"] or 0 for r in recs),
                 "prompt_tokens": sum(r["prompt_tokens"] or 0 for r in recs), "turns": len(recs)}
 
