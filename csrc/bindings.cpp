@@ -35,6 +35,8 @@ int ft_sample(int* out_tokens, const void* logits, int logits_is_bf16, long logi
               const uint32_t* allow_mask, int mask_words, hipStream_t stream);
 int ft_kv_block_copy(void* k_cache, void* v_cache, const int* src_dst, int num_pairs,
                      long block_elems, hipStream_t stream);
+int ft_kv_swap(const uint64_t* ptrs_dev, int ncache, const int* ids_dev, int n, void* staging,
+               long block_elems, int to_staging, hipStream_t stream);
 int ft_skinny_gemm(const void* x, int x_stride, int M, const void* w, int N, int K, float* ws,
                    void* out, int out_stride, int splits, int nt, int u, hipStream_t stream);
 int ft_skinny_gemm_ks(const void* x, int x_stride, int M, const void* w, int N, int K, float* ws,
@@ -268,6 +270,24 @@ void kv_block_copy(at::Tensor k_cache, at::Tensor v_cache, at::Tensor src_dst) {
            "kv_block_copy");
 }
 
+// ptrs: int64 device [2L] cache base pointers (every cache [nblk, ...] bf16 with
+// block_elems elements per block); ids: int32 device [n]; staging: bf16 device
+// [n, 2L, block_elems].  The caller bounds-checks ids against the pool size.
+void kv_swap(at::Tensor ptrs, at::Tensor ids, at::Tensor staging, int64_t block_elems,
+             bool to_staging) {
+  check_dev(ptrs, "ptrs");
+  TORCH_CHECK(ptrs.scalar_type() == at::kLong && ptrs.is_contiguous(), "ptrs int64");
+  check_i32(ids, "ids");
+  check_bf16(staging, "staging");
+  TORCH_CHECK(staging.is_contiguous(), "staging contiguous");
+  const int n = (int)ids.numel();
+  TORCH_CHECK(staging.numel() >= (int64_t)n * ptrs.numel() * block_elems, "staging too small");
+  check_rc(ft_kv_swap(reinterpret_cast<const uint64_t*>(ptrs.data_ptr<int64_t>()),
+                      (int)ptrs.numel(), ids.data_ptr<int>(), n, staging.data_ptr(), block_elems,
+                      to_staging ? 1 : 0, cur_stream()),
+           "kv_swap");
+}
+
 void check_ws(const at::Tensor& ws, int64_t need) {
   check_dev(ws, "workspace");
   TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.is_contiguous(), "workspace fp32 contiguous");
@@ -468,6 +488,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("top_p"), py::arg("top_k"), py::arg("seeds"), py::arg("steps"),
         py::arg("mask") = py::none());
   m.def("kv_block_copy", &kv_block_copy);
+  m.def("kv_swap", &kv_swap);
   m.def("skinny_gemm", &skinny_gemm, py::arg("x"), py::arg("w"), py::arg("out") = py::none(),
         py::arg("ws") = py::none(), py::arg("splits") = 1, py::arg("nt") = 1, py::arg("u") = 2);
   m.def("row_rmsnorm", &row_rmsnorm, py::arg("out"), py::arg("x") = py::none(),

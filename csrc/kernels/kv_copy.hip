@@ -30,3 +30,41 @@ extern "C" int ft_kv_block_copy(void* k_cache, void* v_cache, const int* src_dst
                      (uint4*)k_cache, (uint4*)v_cache, src_dst, vec);
   return static_cast<int>(hipGetLastError());
 }
+
+// E6/K13 host swap (vLLM --swap-space): the blocks of a preempted sequence are
+// gathered from all 2L layer caches into a contiguous device staging buffer
+// [n][2L][block] in ONE launch, so the host side is one DMA per block instead
+// of 2L strided copies; swap-in is the reverse scatter.  ptrs: device array of
+// the 2L cache base pointers (k0, v0, k1, v1, ...); ids: device int32 [n].
+namespace ft {
+
+__global__ __launch_bounds__(256) void kv_swap_kernel(const uint64_t* __restrict__ ptrs,
+                                                      const int* __restrict__ ids,
+                                                      uint4* __restrict__ staging,
+                                                      long vec_per_block, int ncache,
+                                                      int to_staging) {
+  const int c = blockIdx.y, p = blockIdx.z;
+  uint4* cache = reinterpret_cast<uint4*>(ptrs[c]) + (long)ids[p] * vec_per_block;
+  uint4* st = staging + ((long)p * ncache + c) * vec_per_block;
+  if (to_staging) {
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < vec_per_block; i += gridDim.x * 256L)
+      st[i] = cache[i];
+  } else {
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < vec_per_block; i += gridDim.x * 256L)
+      cache[i] = st[i];
+  }
+}
+
+}  // namespace ft
+
+extern "C" int ft_kv_swap(const uint64_t* ptrs_dev, int ncache, const int* ids_dev, int n,
+                          void* staging, long block_elems, int to_staging, hipStream_t stream) {
+  if (n <= 0) return 0;
+  if (block_elems % 8 != 0 || ncache <= 0 || ncache > 65535 || n > 65535) return -1;
+  const long vec = block_elems / 8;
+  int gx = (int)((vec + 255) / 256);
+  if (gx > 16) gx = 16;
+  hipLaunchKernelGGL(ft::kv_swap_kernel, dim3(gx, ncache, n), dim3(256), 0, stream, ptrs_dev,
+                     ids_dev, (uint4*)staging, vec, ncache, to_staging);
+  return static_cast<int>(hipGetLastError());
+}

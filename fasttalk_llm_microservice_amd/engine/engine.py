@@ -55,7 +55,8 @@ class LLMEngine:
         self.bm = R.BlockManager(runner.num_blocks, cfg.block_size, cfg.enable_prefix_caching)
         self.detok = R.Detokenizer(self.tokenizer.id_to_bytes)
         self.scheduler = Scheduler(self.bm, cfg.block_size, cfg.max_num_seqs,
-                                   cfg.max_num_batched_tokens, self.max_model_len)
+                                   cfg.max_num_batched_tokens, self.max_model_len,
+                                   host_blocks=getattr(runner, "num_host_blocks", 0))
         self.stop_ids = set(self.tokenizer.stop_ids) | set(self.model_cfg.eos_token_ids)
         self._trie = None
         self.stats = collections.Counter()
@@ -204,6 +205,10 @@ class LLMEngine:
             return []
         t0 = time.perf_counter()
         outs: List[RequestOutput] = []
+        if batch.swap_out or batch.swap_in:  # E6: host swap copies precede the forward
+            self.runner.swap(batch.swap_out, batch.swap_in)
+            self.stats["swapped_out_blocks"] += len(batch.swap_out)
+            self.stats["swapped_in_blocks"] += len(batch.swap_in)
         # sequences the scheduler had to reject (cannot fit in the KV pool)
         for s in batch.rejected:
             self.scheduler.by_id.pop(s.request_id, None)
@@ -376,6 +381,9 @@ class LLMEngine:
             "kv_usage": self.kv_usage(),
             "prefix_cache_hit_rate": (self.bm.hits / self.bm.queries) if self.bm.queries else 0.0,
             "preemptions": self.scheduler.num_preemptions,
+            "swapped": len(self.scheduler.swapped),
+            "swap_outs": self.scheduler.num_swap_out,
+            "swap_ins": self.scheduler.num_swap_in,
             "decode_step_ms_avg": 1e3 * sum(x[3] for x in dec) / len(dec) if dec else 0.0,
             "decode_batch_avg": sum(x[1] for x in dec) / len(dec) if dec else 0.0,
             "prefill_step_ms_avg": 1e3 * sum(x[3] for x in pre) / len(pre) if pre else 0.0,

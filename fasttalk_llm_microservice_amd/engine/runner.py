@@ -86,6 +86,16 @@ class ModelRunner:
 
         self.num_blocks = self._decide_num_blocks()
         self.kv = self.model.allocate_kv_cache(self.num_blocks, self.bs)
+        # E6 host swap pool (--swap-space): capped at 2x the device pool, allocated
+        # (pinned) on the first swap-out so an idle server does not pin host memory
+        k0 = self.kv[0][0]
+        self.kv_block_elems = k0.numel() // k0.shape[0]
+        host_block_bytes = 2 * len(self.kv) * self.kv_block_elems * k0.element_size()
+        self.num_host_blocks = min(int(cfg.swap_space_gb * (1 << 30)) // host_block_bytes,
+                                   2 * self.num_blocks)
+        self.host_kv = None
+        self.swap_staging = None
+        self.kv_ptrs = None
         nq, d = self.model.nq, self.model.d
 
         # -------- static decode buffers (graph inputs) --------
@@ -132,6 +142,51 @@ class ModelRunner:
         self.bcast = None  # TP rank 0: parallel.shm_broadcast.ShmBroadcast writer
 
     # ------------------------------------------------------------------ memory
+    # ------------------------------------------------------------------ host swap (E6)
+    SWAP_CHUNK = 32  # blocks per gather/scatter launch (64 MiB of staging for 8B)
+
+    def swap(self, swap_out, swap_in):
+        """Copies preempted sequences' KV blocks device -> host (``swap_out``:
+        (block, slot) pairs) and resumed ones host -> device (``swap_in``: (slot,
+        block) pairs), in stream order before the step that follows."""
+        if self.bcast is not None:
+            self.bcast.send(("swap", (list(swap_out), list(swap_in)), None))
+        self._swap(swap_out, swap_in)
+
+    def _swap(self, swap_out, swap_in):
+        nl = 2 * len(self.kv)
+        be = self.kv_block_elems
+        if self.host_kv is None:
+            t0 = time.time()
+            self.host_kv = torch.empty(self.num_host_blocks, nl * be, dtype=self.dtype,
+                                       pin_memory=self.is_gpu)
+            self.swap_staging = torch.empty(self.SWAP_CHUNK, nl * be, dtype=self.dtype,
+                                            device=self.device)
+            if self.is_gpu:
+                self.kv_ptrs = torch.tensor([c.data_ptr() for kv in self.kv for c in kv],
+                                            dtype=torch.int64, device=self.device)
+            log.info("host KV swap pool: %d blocks (%.2f GiB) in %.2fs", self.num_host_blocks,
+                     self.host_kv.numel() * self.host_kv.element_size() / (1 << 30),
+                     time.time() - t0)
+        for pairs, out in ((swap_out, True), (swap_in, False)):
+            for c0 in range(0, len(pairs), self.SWAP_CHUNK):
+                chunk = pairs[c0:c0 + self.SWAP_CHUNK]
+                dev_blocks = [p[0] if out else p[1] for p in chunk]
+                slots = [p[1] if out else p[0] for p in chunk]
+                if min(dev_blocks) < 0 or max(dev_blocks) >= self.num_blocks or \
+                        min(slots) < 0 or max(slots) >= self.num_host_blocks:
+                    raise ValueError("swap block id out of range")
+                ids = torch.tensor(dev_blocks, dtype=torch.int32, device=self.device)
+                st = self.swap_staging[:len(chunk)]
+                if not out:
+                    for i, h in enumerate(slots):
+                        st[i].copy_(self.host_kv[h], non_blocking=True)
+                ops.kv_swap(self.kv, self.kv_ptrs, ids, st, to_staging=out)
+                if out:
+                    for i, h in enumerate(slots):
+                        self.host_kv[h].copy_(st[i], non_blocking=True)
+        self.stats["swap_blocks"] = self.stats.get("swap_blocks", 0) + len(swap_out) + len(swap_in)
+
     def _decide_num_blocks(self) -> int:
         cfg = self.cfg
         per_block = self.mcfg.num_layers * 2 * self.model.nkv * self.model.d * self.bs * \
@@ -423,6 +478,8 @@ class ModelRunner:
             self._wait(st.event)
         elif kind == "warmup":
             self.warmup(host)
+        elif kind == "swap":
+            self._swap(*host)
         else:
             raise ValueError(f"unknown TP message {kind!r}")
         return True

@@ -13,15 +13,19 @@ Replaces vLLM's scheduler behind ``--max-num-seqs`` / ``--max-num-batched-tokens
   the same conversation, or a shared system prompt) is attached from the C++
   block manager, so only new tokens are computed.
 * A sequence that needs a new KV block when the pool is empty preempts the
-  most recently admitted sequence (its blocks are released and it is
-  recomputed later -- "recompute" preemption; cached prefix blocks usually make
-  the recompute cheap).
+  most recently admitted sequence.  With host swap space (``--swap-space``,
+  ``docker-compose.vllm.yml:49``) the victim's blocks are copied to pinned host
+  memory and copied back when blocks free up (its generation continues exactly
+  where it stopped, sampling stream included); without it, or when the host
+  pool is full, its blocks are released and it is recomputed later
+  ("recompute" preemption; cached prefix blocks usually make that cheap).
+  Swapped sequences resume before new prompts are admitted.
 """
 from __future__ import annotations
 
 import collections
 import dataclasses
-from typing import Deque, Dict, List, Optional
+from typing import Deque, Dict, List, Optional, Tuple
 
 from .sequence import SeqStatus, Sequence
 
@@ -33,6 +37,10 @@ class ScheduledBatch:
     prefill_tokens: List[int]
     prefill_sample: List[bool]
     rejected: List[Sequence] = dataclasses.field(default_factory=list)
+    # (device block, host slot) copies to run BEFORE this step's forward pass,
+    # swap-outs first: a block freed by a swap-out may be reused by this step
+    swap_out: List[Tuple[int, int]] = dataclasses.field(default_factory=list)
+    swap_in: List[Tuple[int, int]] = dataclasses.field(default_factory=list)
 
     @property
     def is_prefill(self) -> bool:
@@ -54,9 +62,29 @@ class ScheduledBatch:
         return self.decode_seqs + [s for s, sm in zip(self.prefill_seqs, self.prefill_sample) if sm]
 
 
+class HostSwapPool:
+    """Slots of the pinned host KV pool (one slot = one KV block of every layer)."""
+
+    def __init__(self, num_blocks: int):
+        self.num_blocks = num_blocks
+        self._free = list(range(num_blocks - 1, -1, -1))
+
+    def num_free(self) -> int:
+        return len(self._free)
+
+    def can_allocate(self, n: int) -> bool:
+        return len(self._free) >= n
+
+    def allocate(self, n: int) -> List[int]:
+        return [self._free.pop() for _ in range(n)]
+
+    def release(self, slots: List[int]):
+        self._free.extend(reversed(slots))
+
+
 class Scheduler:
     def __init__(self, block_manager, block_size: int, max_num_seqs: int,
-                 max_num_batched_tokens: int, max_model_len: int):
+                 max_num_batched_tokens: int, max_model_len: int, host_blocks: int = 0):
         self.bm = block_manager
         self.bs = block_size
         self.max_num_seqs = max_num_seqs
@@ -67,6 +95,11 @@ class Scheduler:
         self.by_id: Dict[str, Sequence] = {}
         self._admit_counter = 0
         self.num_preemptions = 0
+        self.swapped: Deque[Sequence] = collections.deque()
+        self.host = HostSwapPool(host_blocks) if host_blocks > 0 else None
+        self._swap_out: List[Tuple[int, int]] = []
+        self.num_swap_out = 0
+        self.num_swap_in = 0
 
     # ------------------------------------------------------------------ queue ops
     def add(self, seq: Sequence):
@@ -74,16 +107,20 @@ class Scheduler:
         self.waiting.append(seq)
 
     def has_work(self) -> bool:
-        return bool(self.waiting) or bool(self.running)
+        return bool(self.waiting) or bool(self.running) or bool(self.swapped)
 
     def num_unfinished(self) -> int:
-        return len(self.waiting) + len(self.running)
+        return len(self.waiting) + len(self.running) + len(self.swapped)
 
     def release(self, seq: Sequence):
-        """Free a sequence's KV blocks (full blocks stay cached for reuse)."""
+        """Free a sequence's KV blocks (full blocks stay cached for reuse) and its
+        host swap slots."""
         if seq.block_ids:
             self.bm.free(seq.block_ids)
             seq.block_ids = []
+        if seq.host_slots:
+            self.host.release(seq.host_slots)
+            seq.host_slots = []
 
     def finish(self, seq: Sequence, reason: str):
         seq.status = SeqStatus.FINISHED
@@ -92,10 +129,12 @@ class Scheduler:
         if seq in self.running:
             self.running.remove(seq)
         else:
-            try:
-                self.waiting.remove(seq)
-            except ValueError:
-                pass
+            for q in (self.waiting, self.swapped):
+                try:
+                    q.remove(seq)
+                    break
+                except ValueError:
+                    pass
         self.by_id.pop(seq.request_id, None)
 
     def abort(self, request_id: str) -> Optional[Sequence]:
@@ -111,12 +150,66 @@ class Scheduler:
         return max(0, (upto_tokens + self.bs - 1) // self.bs - len(seq.block_ids))
 
     def schedule(self) -> Optional[ScheduledBatch]:
+        self._swap_out = []
         decode = self._schedule_decode()
+        swap_in: List[Tuple[int, int]] = []
+        if self.swapped and not self._swap_out:
+            resumed, swap_in = self._schedule_swap_in(len(decode))
+            decode += resumed
         budget = self.max_tokens - len(decode)
-        pseqs, ptok, psamp, rejected = self._schedule_prefill(budget, len(decode))
-        if not decode and not pseqs and not rejected:
+        if self.swapped:  # swapped sequences go first; only unfinished chunks continue
+            pseqs, ptok, psamp, rejected = [], [], [], []
+        else:
+            pseqs, ptok, psamp, rejected = self._schedule_prefill(budget, len(decode))
+        swap_out, self._swap_out = self._swap_out, []
+        if not decode and not pseqs and not rejected and not swap_out and not swap_in:
             return None
-        return ScheduledBatch(decode, pseqs, ptok, psamp, rejected)
+        return ScheduledBatch(decode, pseqs, ptok, psamp, rejected, swap_out, swap_in)
+
+    def _swap_out_seq(self, seq: Sequence) -> bool:
+        """Parks a running sequence's KV blocks in host memory (False if there is no
+        host pool or it is full: the caller falls back to recompute)."""
+        n = len(seq.block_ids)
+        if self.host is None or n == 0 or not self.host.can_allocate(n):
+            return False
+        slots = self.host.allocate(n)
+        self._swap_out.extend(zip(seq.block_ids, slots))
+        self.bm.free(seq.block_ids)  # reusable in this step: the copies run first
+        seq.block_ids = []
+        seq.host_slots = slots
+        seq.status = SeqStatus.SWAPPED
+        self.swapped.append(seq)
+        self.num_swap_out += 1
+        return True
+
+    def _schedule_swap_in(self, n_running: int):
+        """Brings swapped sequences back (FIFO) while their blocks, plus the one
+        this step's decode token needs, fit.  Full blocks still in the device
+        prefix cache are re-attached instead of copied."""
+        resumed, pairs = [], []
+        while self.swapped and n_running + len(resumed) < self.max_num_seqs:
+            seq = self.swapped[0]
+            hit = self.bm.match_prefix(seq.tokens, seq.num_committed_blocks) \
+                if seq.num_committed_blocks else []
+            nslots = len(seq.host_slots)
+            total = max((seq.n_tokens + self.bs - 1) // self.bs, nslots)
+            need = total - len(hit)
+            if not self.bm.can_allocate(need):
+                if hit:
+                    self.bm.free(hit)
+                break
+            new = self.bm.allocate(need)
+            # blocks [len(hit), nslots) come back from host; the tail (if any) is new
+            pairs.extend(zip(seq.host_slots[len(hit):], new[:nslots - len(hit)]))
+            self.host.release(seq.host_slots)
+            seq.host_slots = []
+            seq.block_ids = list(hit) + new
+            seq.status = SeqStatus.RUNNING
+            self.swapped.popleft()
+            self.running.append(seq)
+            resumed.append(seq)
+            self.num_swap_in += 1
+        return resumed, pairs
 
     def _reset_to_waiting(self, seq: Sequence):
         """Drop a sequence's KV blocks (full blocks stay in the prefix cache, so a
@@ -188,11 +281,13 @@ class Scheduler:
             if victim is keep:
                 continue
             self.running.remove(victim)
+            self.num_preemptions += 1
+            if self._swap_out_seq(victim):
+                return True
             self._reset_to_waiting(victim)
             victim.status = SeqStatus.WAITING
             victim.preemptions += 1
             self.waiting.appendleft(victim)
-            self.num_preemptions += 1
             return True
         return False
 

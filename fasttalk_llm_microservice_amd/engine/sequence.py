@@ -14,6 +14,7 @@ from .sampling_params import SamplingParams
 class SeqStatus(enum.Enum):
     WAITING = "waiting"
     RUNNING = "running"
+    SWAPPED = "swapped"     # preempted with its KV blocks parked in host memory
     FINISHED = "finished"
 
 
@@ -37,7 +38,7 @@ class Sequence:
                  "num_computed", "num_committed_blocks", "num_cached_tokens", "arrival",
                  "first_token_time", "finish_reason", "detok_stream", "on_output", "grammar",
                  "grammar_state", "stop_buf", "text_len", "aborted", "preemptions", "admit_order",
-                 "meta")
+                 "meta", "host_slots")
 
     def __init__(self, request_id: str, prompt_ids: List[int], params: SamplingParams,
                  on_output: Optional[Callable[[RequestOutput], None]] = None, meta: Any = None):
@@ -66,6 +67,7 @@ class Sequence:
         self.preemptions = 0
         self.admit_order = 0
         self.meta = meta
+        self.host_slots: List[int] = []
 
     # ---------------------------------------------------------------- tokens
     @property

@@ -197,6 +197,29 @@ def kv_block_copy(k_cache, v_cache, pairs: torch.Tensor):
         v_cache[p[:, 1]] = v_cache[p[:, 0]]
 
 
+def kv_swap(caches, ptrs, ids: torch.Tensor, staging: torch.Tensor, to_staging: bool):
+    """Gathers (``to_staging``) or scatters KV blocks ``ids`` of every layer cache
+    to/from ``staging`` [n, 2L, block_elems] (layer-major k0, v0, k1, v1, ...).
+    ``caches``: the model's [(k, v)] list; ``ptrs``: their base pointers as an
+    int64 tensor on the device (GPU path) or None."""
+    n = ids.numel()
+    if n == 0:
+        return
+    flat = [c for kv in caches for c in kv]
+    if staging.is_cuda:
+        nblk = flat[0].shape[0]
+        native().kv_swap(ptrs, ids, staging, flat[0].numel() // nblk, to_staging)
+        return
+    st = staging.view(n, len(flat), -1)
+    idx = ids.long()
+    for c, cache in enumerate(flat):
+        rows = cache.view(cache.shape[0], -1)
+        if to_staging:
+            st[:, c] = rows[idx]
+        else:
+            rows[idx] = st[:, c]
+
+
 # ---------------------------------------------------------------------------------
 # decode-shape (M <= 64) weight-streaming GEMM + fused row epilogues
 # ---------------------------------------------------------------------------------

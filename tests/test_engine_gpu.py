@@ -125,3 +125,19 @@ def test_pipelined_decode_matches_synchronous():
             assert eng.stats["pipelined_steps"] > 0
         outs.append([res[i] for i in range(len(prompts))])
     assert outs[0] == outs[1]
+
+
+def test_host_swap_matches_unconstrained():
+    """E6: a KV pool too small for the batch forces swap-outs to pinned host memory
+    (gather kernel + DMA) and swap-ins (DMA + scatter kernel); the tokens equal a
+    run that never swapped, and every device and host block comes back."""
+    prompts = _prompts(6, [40 + 9 * i for i in range(6)], seed=5)
+    sp = SamplingParams(temperature=0.8, top_p=0.9, seed=21, max_tokens=48, ignore_eos=True)
+    ref = _engine(num_kv_blocks=512).generate(prompts, sp)
+    eng = _engine(num_kv_blocks=20, swap_space_gb=0.5, enable_prefix_caching=False)
+    got = eng.generate(prompts, sp)
+    s = eng.scheduler
+    assert s.num_swap_out > 0 and s.num_swap_in == s.num_swap_out
+    assert s.num_preemptions == s.num_swap_out  # no recompute fallback
+    assert got == ref
+    assert eng.bm.num_free() == eng.bm.num_blocks and s.host.num_free() == s.host.num_blocks

@@ -255,6 +255,29 @@ def test_kv_block_copy():
     assert torch.equal(k[5], k0[1]) and torch.equal(v[7], v0[2]) and torch.equal(k[0], k0[0])
 
 
+def test_kv_swap_gather_scatter():
+    layers = [_alloc_cache(12, 8, 16, 128) for _ in range(3)]
+    ptrs = torch.tensor([c.data_ptr() for kv in layers for c in kv], dtype=torch.int64, device=DEV)
+    be = 8 * 16 * 128
+    ids = torch.tensor([7, 0, 11, 3], dtype=torch.int32, device=DEV)
+    st = torch.empty(4, 6 * be, dtype=torch.bfloat16, device=DEV)
+    ops.kv_swap(layers, ptrs, ids, st, to_staging=True)
+    expect = torch.stack([torch.cat([c[b].flatten() for kv in layers for c in kv])
+                          for b in ids.tolist()])
+    assert torch.equal(st, expect)
+    # scatter a new payload into other blocks; untouched blocks stay as they were
+    before = [c.clone() for kv in layers for c in kv]
+    new = torch.randn(2, 6 * be, device=DEV).bfloat16()
+    ids2 = torch.tensor([5, 9], dtype=torch.int32, device=DEV)
+    ops.kv_swap(layers, ptrs, ids2, new, to_staging=False)
+    flat = [c for kv in layers for c in kv]
+    for ci, c in enumerate(flat):
+        for i, b in enumerate((5, 9)):
+            assert torch.equal(c[b].flatten(), new[i, ci * be:(ci + 1) * be])
+        keep = [b for b in range(12) if b not in (5, 9)]
+        assert torch.equal(c[keep], before[ci][keep])
+
+
 # ----------------------------------------------------------------------------------
 # decode-shape skinny GEMM + fused row epilogues
 # ----------------------------------------------------------------------------------
