@@ -59,7 +59,8 @@ def engine_config_from_service(config) -> "Any":
 def get_shared_engine(engine_cfg) -> "Any":
     """One engine per (model, weights, device) per process."""
     key = (f"{engine_cfg.model}|{engine_cfg.weights}|{engine_cfg.resolved_device()}|"
-           f"{engine_cfg.tp_size}|{engine_cfg.dp_size}|{engine_cfg.separate_process}")
+           f"{engine_cfg.tp_size}|{engine_cfg.dp_size}|{engine_cfg.separate_process}|"
+           f"{engine_cfg.quantization}")
     with _ENGINE_LOCK:
         eng = _ENGINES.get(key)
         if eng is None:

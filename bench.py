@@ -65,7 +65,11 @@ def main():
                          "default: data parallel, one engine per rank")
     ap.add_argument("--custom-allreduce", action="store_true", help="TP: one-shot xGMI all-reduce")
     ap.add_argument("--device", default="cuda", help="TP mode only: cpu runs the same path over gloo")
+    ap.add_argument("--quant", default="", choices=["", "w4", "awq"],
+                    help="W4A16 layer weights (the reference's AWQ-INT4 model); default bf16")
     a = ap.parse_args()
+    if a.quant:
+        os.environ["ENGINE_QUANTIZATION"] = a.quant
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -183,7 +187,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16",
+            "dtype": "w4a16 (bf16 compute)" if a.quant else "bf16",
             "data": "synthetic (random-init Llama-3-8B weights, synthetic English prompts, "
                     "synthetic Llama-3 tokenizer)",
             "config": {"model": "Llama-3-8B", "global_batch": a.sessions * world,
@@ -311,7 +315,7 @@ def bench_tp(a, rank: int, world: int, local_rank: int):
         "value": round(value, 2), "unit": "tokens/s", "n_gpus": world, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": round(1e3 * elapsed / a.steps, 2),
         "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
-        "dtype": "bf16" if a.device == "cuda" else "fp32",
+        "dtype": ("w4a16 (bf16 compute)" if a.quant else "bf16") if a.device == "cuda" else "fp32",
         "data": "synthetic (random-init weights, synthetic English prompts, synthetic Llama-3 tokenizer)",
         "config": {"model": a.model, "global_batch": a.sessions, "seq_len": eng.max_model_len,
                    "parallelism": f"tp{world}", "custom_allreduce": a.custom_allreduce},

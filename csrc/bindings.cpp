@@ -35,6 +35,9 @@ int ft_sample(int* out_tokens, const void* logits, int logits_is_bf16, long logi
               const uint32_t* allow_mask, int mask_words, hipStream_t stream);
 int ft_kv_block_copy(void* k_cache, void* v_cache, const int* src_dst, int num_pairs,
                      long block_elems, hipStream_t stream);
+int ft_w4_gemm(const void* x, int x_stride, int M, const uint32_t* wq, const void* sz, int N, int K,
+               float* ws, void* out, int out_stride, int splits, int nt, hipStream_t stream);
+int ft_w4_dequant(const uint32_t* wq, const void* sz, void* out, int N, int K, hipStream_t stream);
 int ft_kv_swap(const uint64_t* ptrs_dev, int ncache, const int* ids_dev, int n, void* staging,
                long block_elems, int to_staging, hipStream_t stream);
 int ft_skinny_gemm(const void* x, int x_stride, int M, const void* w, int N, int K, float* ws,
@@ -295,6 +298,56 @@ void check_ws(const at::Tensor& ws, int64_t need) {
 }
 
 // y = x W^T for M <= 64 rows; splits > 1 writes fp32 slabs [splits, M, N] into ws
+// W4A16: wq int32 packed image [N/16][K/128][64][4], sz fp32 [N/16][K/128][16][2]
+// (scale, 128 + zero); see w4a16.hip.
+void check_w4(const at::Tensor& wq, const at::Tensor& sz, int64_t N, int64_t K) {
+  check_dev(wq, "wq");
+  check_dev(sz, "sz");
+  TORCH_CHECK(wq.scalar_type() == at::kInt && wq.is_contiguous(), "wq int32 contiguous");
+  TORCH_CHECK(sz.scalar_type() == at::kFloat && sz.is_contiguous(), "sz fp32 contiguous");
+  TORCH_CHECK(N % 16 == 0 && K % 128 == 0, "W4 needs N % 16 == 0 and K % 128 == 0");
+  TORCH_CHECK(wq.numel() == N * K / 8, "wq size");
+  TORCH_CHECK(sz.numel() == N * (K / 128) * 2, "sz size");
+}
+
+void w4_gemm(at::Tensor x, at::Tensor wq, at::Tensor sz, int64_t N, c10::optional<at::Tensor> out,
+             c10::optional<at::Tensor> ws, int64_t splits, int64_t nt) {
+  check_bf16(x, "x");
+  check_rows(x, "x");
+  const int M = (int)x.size(0), K = (int)x.size(1);
+  check_w4(wq, sz, N, K);
+  TORCH_CHECK(M <= 64, "w4_gemm supports M <= 64");
+  float* wsp = nullptr;
+  void* op = nullptr;
+  int ostride = 0;
+  if (ws.has_value()) {  // fp32 slabs (any split count)
+    check_ws(*ws, (int64_t)splits * M * N);
+    wsp = ws->data_ptr<float>();
+  } else {
+    TORCH_CHECK(splits == 1, "splits > 1 needs a workspace");
+    TORCH_CHECK(out.has_value(), "no workspace: needs out");
+    check_bf16(*out, "out");
+    TORCH_CHECK(out->dim() == 2 && out->stride(1) == 1 && out->size(0) >= M && out->size(1) >= N,
+                "out shape");
+    op = out->data_ptr();
+    ostride = (int)out->stride(0);
+  }
+  check_rc(ft_w4_gemm(x.data_ptr(), (int)x.stride(0), M,
+                      reinterpret_cast<const uint32_t*>(wq.data_ptr<int>()), sz.data_ptr(), (int)N,
+                      K, wsp, op, ostride, (int)splits, (int)nt, cur_stream()),
+           "w4_gemm");
+}
+
+void w4_dequant(at::Tensor wq, at::Tensor sz, at::Tensor out) {
+  check_bf16(out, "out");
+  TORCH_CHECK(out.dim() == 2 && out.is_contiguous(), "out [N, K] contiguous");
+  const int64_t N = out.size(0), K = out.size(1);
+  check_w4(wq, sz, N, K);
+  check_rc(ft_w4_dequant(reinterpret_cast<const uint32_t*>(wq.data_ptr<int>()), sz.data_ptr(),
+                         out.data_ptr(), (int)N, (int)K, cur_stream()),
+           "w4_dequant");
+}
+
 void skinny_gemm(at::Tensor x, at::Tensor w, c10::optional<at::Tensor> out,
                  c10::optional<at::Tensor> ws, int64_t splits, int64_t nt, int64_t u) {
   check_bf16(x, "x");
@@ -489,6 +542,10 @@ PYBIND11_MODULE(_C, m) {
         py::arg("mask") = py::none());
   m.def("kv_block_copy", &kv_block_copy);
   m.def("kv_swap", &kv_swap);
+  m.def("w4_gemm", &w4_gemm, py::arg("x"), py::arg("wq"), py::arg("sz"), py::arg("N"),
+        py::arg("out") = py::none(), py::arg("ws") = py::none(), py::arg("splits") = 1,
+        py::arg("nt") = 1);
+  m.def("w4_dequant", &w4_dequant);
   m.def("skinny_gemm", &skinny_gemm, py::arg("x"), py::arg("w"), py::arg("out") = py::none(),
         py::arg("ws") = py::none(), py::arg("splits") = 1, py::arg("nt") = 1, py::arg("u") = 2);
   m.def("row_rmsnorm", &row_rmsnorm, py::arg("out"), py::arg("x") = py::none(),

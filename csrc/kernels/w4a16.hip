@@ -1,0 +1,251 @@
+// E9 / K14: W4A16 (AWQ-style, group 128, asymmetric) weight-only GEMMs.
+//   y[M, N] = x[M, K] . dequant(W)[N, K]^T,  dequant(W)[n, k] = (q[n,k] - z[n,g]) * s[n,g],
+//   g = k / 128, q and z 4-bit.  Reference: --quantization awq
+//   (docker-compose.vllm.yml:45-46, Llama-3.1-8B AWQ in app/utils/config.py:93-96).
+//
+// Decode (M <= 64) is a weight stream, and int4 cuts it 3.6x vs bf16, so the
+// kernel is the packed-fragment skinny GEMM (skinny_gemm.hip, "pk") with the
+// dequantization moved out of the inner loop:
+//   * packed image [N/16][K/128][lane][4 x u32]: one 16-B load per lane = 1 KiB
+//     of consecutive bytes per wave instruction = one 128-wide k-group for a
+//     16-column tile.  Lane (n = l&15, g = l>>4) word w holds the 8 nibbles of
+//     k = 128*grp + 64*(w>>1) + 16*g + 8*(w&1) + {0,2,4,6,1,3,5,7} (bit order),
+//     so ((word >> 4i) & 0x000F000F) | 0x43004300 is the bf16 pair
+//     (128 + q[2i], 128 + q[2i+1]) -- exact in bf16 -- and the four pairs are
+//     the lane's MFMA B fragment: one shift + one and-or per two weights.
+//   * acc_grp = x . (128 + q) over the group (exact bf16 products, fp32 sums),
+//     xsum = x . 1 from two extra MFMAs per row tile (B = ones), then
+//       y += s * (acc_grp - (128 + z) * xsum)       (2 FMAs per acc register)
+//     with (s, 128 + z) as one float2 per (column, group) in a side array
+//     [N/16][K/128][16].
+//   * 4 waves split the groups of a column tile; with a workspace, split-K over
+//     gridDim.y (1 split included) writes fp32 slabs reduced by the row
+//     epilogues (fused_epilogue.hip), exactly as the bf16 packed path; without
+//     one (1 split) it stores bf16.
+// Prefill (M > 64) dequantizes one projection into a bf16 scratch with
+// w4_dequant_kernel and runs the library GEMM.
+#include "ft_common.h"
+
+namespace ft {
+
+typedef __bf16 w4_bf16x8 __attribute__((ext_vector_type(8)));
+typedef float w4_floatx4 __attribute__((ext_vector_type(4)));
+typedef unsigned int w4_u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint4 w4_nt_load16(const uint32_t* p) {
+  const w4_u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const w4_u32x4*>(p));
+  return __builtin_bit_cast(uint4, v);
+}
+
+// one packed u32 (8 nibbles) -> the 8 bf16 values 128 + q of an MFMA B fragment
+__device__ __forceinline__ w4_bf16x8 w4_frag(uint32_t w) {
+  uint4 r;
+  r.x = (w & 0x000F000Fu) | 0x43004300u;
+  r.y = ((w >> 4) & 0x000F000Fu) | 0x43004300u;
+  r.z = ((w >> 8) & 0x000F000Fu) | 0x43004300u;
+  r.w = ((w >> 12) & 0x000F000Fu) | 0x43004300u;
+  return __builtin_bit_cast(w4_bf16x8, r);
+}
+
+__device__ __forceinline__ w4_bf16x8 w4_xfrag(const uint4& v) {
+  return __builtin_bit_cast(w4_bf16x8, v);
+}
+
+template <int MT, int NT>
+struct W4Stage {
+  uint4 w[NT];      // one k-group of NT column tiles
+  float2 sz[NT];    // (scale, 128 + zero) of this lane's column
+  uint4 x[MT][4];   // 2 k-steps x 2 halves
+};
+
+template <int MT, int NT>
+__global__ __launch_bounds__(256) void w4_skinny_kernel(
+    const uint16_t* __restrict__ x, int x_stride, int M, const uint32_t* __restrict__ wq,
+    const float2* __restrict__ sz, int K, float* __restrict__ ws, uint16_t* __restrict__ out,
+    int out_stride, int N, int k_slice) {
+  __shared__ float s_red[4][MT * NT * 4][64];
+  const int lane = lane_id(), wave = wave_id();
+  const int l15 = lane & 15, g = lane >> 4;
+  const int n0 = blockIdx.x * (16 * NT);
+  const int s = blockIdx.y;
+  const int kbeg = s * k_slice;
+  const int groups_total = K >> 7;
+  const int grp0 = kbeg >> 7;
+
+  const uint32_t* wp[NT];
+  const float2* sp[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const size_t tile = (size_t)(n0 / 16 + j) * groups_total;
+    wp[j] = wq + tile * 256 + lane * 4;
+    sp[j] = sz + tile * 16 + l15;
+  }
+  const uint16_t* xp[MT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+    const int r = min(16 * i + l15, M - 1);
+    xp[i] = x + (size_t)r * x_stride + kbeg + 16 * g;
+  }
+
+  w4_floatx4 acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = w4_floatx4{0.f, 0.f, 0.f, 0.f};
+
+  const int ngroups = k_slice >> 7;
+  const int my = ngroups > wave ? (ngroups - wave + 3) >> 2 : 0;
+  const int last = my - 1;
+  auto grp = [&](int t) { return wave + 4 * min(t, last); };
+  auto load = [&](W4Stage<MT, NT>& st, int t) {
+    const int gi = grp(t);
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      st.w[j] = w4_nt_load16(wp[j] + (size_t)(grp0 + gi) * 256);
+      st.sz[j] = sp[j][(size_t)(grp0 + gi) * 16];
+    }
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      const uint4* p = reinterpret_cast<const uint4*>(xp[i] + gi * 128);
+      st.x[i][0] = p[0];
+      st.x[i][1] = p[1];
+      st.x[i][2] = p[8];   // +64 elements: second k-step
+      st.x[i][3] = p[9];
+    }
+  };
+  const uint4 ones4 = make_uint4(0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u);
+  const w4_bf16x8 ones = __builtin_bit_cast(w4_bf16x8, ones4);
+  auto compute = [&](const W4Stage<MT, NT>& st) {
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      w4_floatx4 xs = w4_floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int h = 0; h < 4; ++h)
+        xs = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w4_xfrag(st.x[i][h]), ones, xs, 0, 0, 0);
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const uint32_t wd[4] = {st.w[j].x, st.w[j].y, st.w[j].z, st.w[j].w};
+        w4_floatx4 a = w4_floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int h = 0; h < 4; ++h)
+          a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w4_xfrag(st.x[i][h]), w4_frag(wd[h]), a, 0,
+                                                      0, 0);
+        const float sc = st.sz[j].x, zz = st.sz[j].y;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[i][j][r] = fmaf(sc, fmaf(-zz, xs[r], a[r]), acc[i][j][r]);
+      }
+    }
+  };
+  if (my > 0) {
+    W4Stage<MT, NT> a, b;
+    load(a, 0);
+    int t = 0;
+    for (; t + 2 <= my; t += 2) {
+      load(b, t + 1);
+      __builtin_amdgcn_sched_barrier(0);
+      compute(a);
+      __builtin_amdgcn_sched_barrier(0);
+      load(a, t + 2);
+      __builtin_amdgcn_sched_barrier(0);
+      compute(b);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (t < my) compute(a);
+  }
+
+  // The C fragment of a 16x16 MFMA: column = lane & 15, rows 4*(lane>>4) + r.
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) s_red[wave][(i * NT + j) * 4 + r][lane] = acc[i][j][r];
+  __syncthreads();
+  constexpr int NREG = MT * NT * 4;
+  const int ln = threadIdx.x & 63;
+  float* slab = ws + (size_t)s * M * N;
+  for (int reg = threadIdx.x >> 6; reg < NREG; reg += 4) {
+    const float v = s_red[0][reg][ln] + s_red[1][reg][ln] + s_red[2][reg][ln] + s_red[3][reg][ln];
+    const int i = reg / (NT * 4), j = (reg / 4) % NT, r = reg & 3;
+    const int m = 16 * i + (ln >> 4) * 4 + r;
+    const int n = n0 + 16 * j + (ln & 15);
+    if (m < M) {
+      if (ws == nullptr)
+        out[(size_t)m * out_stride + n] = f32_to_bf16(v);
+      else
+        slab[(size_t)m * N + n] = v;
+    }
+  }
+}
+
+// packed image -> bf16 [N, K] row-major (prefill path and tests).  One thread
+// per (tile, group, lane): 32 weights = 4 runs of 8 consecutive k.
+__global__ __launch_bounds__(256) void w4_dequant_kernel(const uint32_t* __restrict__ wq,
+                                                         const float2* __restrict__ sz,
+                                                         uint16_t* __restrict__ out, int N, int K) {
+  const int groups = K >> 7;
+  const long total = (long)(N / 16) * groups * 64;
+  for (long t = blockIdx.x * 256L + threadIdx.x; t < total; t += (long)gridDim.x * 256L) {
+    const int lane = (int)(t & 63);
+    const long tg = t >> 6;  // tile * groups + group
+    const int grp = (int)(tg % groups);
+    const int tile = (int)(tg / groups);
+    const int n = tile * 16 + (lane & 15), g = lane >> 4;
+    const float2 p = sz[tg * 16 + (lane & 15)];
+    const uint4 w4 = *reinterpret_cast<const uint4*>(wq + t * 4);
+    const uint32_t wd[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      const int k = grp * 128 + 64 * (h >> 1) + 16 * g + 8 * (h & 1);
+      float v[8];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        v[2 * i] = ((float)((wd[h] >> (4 * i)) & 15u) + 128.f - p.y) * p.x;
+        v[2 * i + 1] = ((float)((wd[h] >> (4 * i + 16)) & 15u) + 128.f - p.y) * p.x;
+      }
+      *reinterpret_cast<uint4*>(out + (size_t)n * K + k) = store8(v);
+    }
+  }
+}
+
+}  // namespace ft
+
+// Requirements (checked): M <= 64, N % (16*nt) == 0, K % (128*splits) == 0; ws
+// (fp32 [splits][M][N] slabs) is required for splits > 1 and selects slab output.
+extern "C" int ft_w4_gemm(const void* x, int x_stride, int M, const uint32_t* wq, const void* sz,
+                          int N, int K, float* ws, void* out, int out_stride, int splits, int nt,
+                          hipStream_t stream) {
+  if (M <= 0) return 0;
+  if (M > 64 || splits < 1) return -1;
+  if (N % (16 * nt) != 0) return -2;
+  if (K % (128 * splits) != 0) return -3;
+  if (splits > 1 && ws == nullptr) return -4;
+  if (ws == nullptr && out == nullptr) return -6;
+  const int mt = (M + 15) / 16;
+  dim3 grid(N / (16 * nt), splits), block(256);
+  const int k_slice = K / splits;
+#define FT_W4(MT_, NT_)                                                                      \
+  if (mt == MT_ && nt == NT_) {                                                              \
+    hipLaunchKernelGGL((ft::w4_skinny_kernel<MT_, NT_>), grid, block, 0, stream,             \
+                       (const uint16_t*)x, x_stride, M, wq, (const float2*)sz, K, ws,        \
+                       (uint16_t*)out, out_stride, N, k_slice);                              \
+    return static_cast<int>(hipGetLastError());                                              \
+  }
+#define FT_W4_NT(NT_) FT_W4(1, NT_) FT_W4(2, NT_) FT_W4(3, NT_) FT_W4(4, NT_)
+  FT_W4_NT(1)
+  FT_W4_NT(2)
+  FT_W4_NT(4)
+#undef FT_W4_NT
+#undef FT_W4
+  return -5;
+}
+
+extern "C" int ft_w4_dequant(const uint32_t* wq, const void* sz, void* out, int N, int K,
+                             hipStream_t stream) {
+  if (N % 16 != 0 || K % 128 != 0) return -1;
+  const long total = (long)(N / 16) * (K / 128) * 64;
+  const int blocks = (int)std::min<long>((total + 255) / 256, 4096);
+  hipLaunchKernelGGL(ft::w4_dequant_kernel, dim3(blocks), dim3(256), 0, stream, wq,
+                     (const float2*)sz, (uint16_t*)out, N, K);
+  return static_cast<int>(hipGetLastError());
+}

@@ -53,6 +53,7 @@ class EngineConfig:
     async_output: bool = True          # overlap detokenize/streaming with the next GPU step
     separate_process: bool = False     # run the step loop in its own process (no GIL sharing)
     custom_allreduce: bool = False     # TP: one-shot xGMI all-reduce for decode-size messages
+    quantization: Optional[str] = None  # None | "awq" | "w4" (W4A16, group 128; --quantization awq)
 
     def resolved_device(self) -> str:
         if self.device != "auto":
@@ -98,7 +99,11 @@ class EngineConfig:
             enforce_eager=_env(["ENGINE_ENFORCE_EAGER", "VLLM_ENFORCE_EAGER"], False, _bool),
             separate_process=_env(["ENGINE_SEPARATE_PROCESS"], False, _bool),
             custom_allreduce=_env(["ENGINE_CUSTOM_ALLREDUCE"], False, _bool),
+            quantization=_env(["ENGINE_QUANTIZATION", "VLLM_QUANTIZATION"], None) or None,
         )
         for k, v in overrides.items():
             setattr(c, k, v)
+        if c.quantization is None and "awq" in c.model.lower():
+            # the reference's default model (hugging-quants/...-AWQ-INT4) runs W4A16
+            c.quantization = "awq"
         return c

@@ -75,7 +75,8 @@ class ModelRunner:
         self.max_blocks_per_seq = (self.max_model_len + self.bs - 1) // self.bs
 
         t0 = time.time()
-        self.model = LlamaModel(model_cfg, self.device, self.dtype, comm, self.max_model_len)
+        self.model = LlamaModel(model_cfg, self.device, self.dtype, comm, self.max_model_len,
+                                quantization=cfg.quantization)
         if cfg.weights and cfg.weights != "random":
             self.model.load_checkpoint(cfg.weights)
         else:

@@ -19,6 +19,7 @@ import torch
 import torch.nn.functional as F
 
 from .. import ops
+from ..ops import quant as Q
 from ..ops import reference as ref
 from ..parallel.comm import SINGLE, TPComm
 from .config import ModelConfig
@@ -57,10 +58,10 @@ class AttnMeta:
 
 @dataclasses.dataclass
 class LayerWeights:
-    wqkv: torch.Tensor
-    wo: torch.Tensor
-    wgu: torch.Tensor
-    wd: torch.Tensor
+    wqkv: Optional[torch.Tensor]   # None when the projection is held as W4 only
+    wo: Optional[torch.Tensor]
+    wgu: Optional[torch.Tensor]
+    wd: Optional[torch.Tensor]
     ln1: torch.Tensor
     ln2: torch.Tensor
     # the same weights in the MFMA-fragment image the decode GEMMs stream
@@ -68,6 +69,11 @@ class LayerWeights:
     wo_pk: Optional[torch.Tensor] = None
     wgu_pk: Optional[torch.Tensor] = None
     wd_pk: Optional[torch.Tensor] = None
+    # W4A16 (AWQ) projections by name ("qkv", "o", "gu", "down"), GPU only
+    q4: Optional[dict] = None
+
+
+_ATTR = {"qkv": "wqkv", "o": "wo", "gu": "wgu", "down": "wd"}
 
 
 # Decode GEMMs (<= 64 rows) on pre-packed weights (csrc/kernels/skinny_gemm.hip,
@@ -92,6 +98,28 @@ PACKED_PLAN = {
 }
 MAX_SPLITS = 4
 
+# W4A16 decode GEMMs (csrc/kernels/w4a16.hip): (nt, splits) per projection and
+# row bucket, from cold-cache sweeps on MI355X (bench/w4_sweep.py, us at M = 1 /
+# 8 / 16 / 32 / 64; bf16 packed plan in brackets):
+#   qkv   5.7 / 6.0 / 6.5 / 9.2 / 16.3   [9.8 / 10.3 / 11.1 / hipBLASLt]
+#   o     4.4 / 4.7 / 5.1 / 7.2 / 12.1   [7.3 / 7.5 / 7.7 / 9.0 / 13.1]
+#   gu    15.2 / 14.9 / 16.7 / 26.8 / 47.5  [35 / 38 / 41 / 45 / hipBLASLt 55-66]
+#   down  9.2 / 8.5 / 9.1 / 12.9 / 22.7  [18.6 / 19.3 / 20 / 22 / 28]
+# qkv, o and down leave split-K slabs: qkv's are reduced by the RoPE + KV-write
+# kernel (slab_rope_kv), o's and down's by the fused add+RMSNorm.
+W4_ROWS = 64
+W4_PLAN = {
+    "qkv": {1: (2, 8), 8: (4, 2), 16: (4, 2), 32: (4, 2), 64: (4, 2)},
+    "o": {1: (2, 8), 8: (2, 8), 16: (4, 8), 32: (4, 4), 64: (4, 4)},
+    "gu": {1: (4, 1), 8: (4, 1), 16: (4, 1), 32: (4, 1), 64: (4, 1)},
+    "down": {1: (4, 4), 8: (4, 4), 16: (4, 4), 32: (4, 4), 64: (4, 4)},
+}
+
+
+def w4_cfg(proj: str, rows: int):
+    b = next(m for m in _M_BUCKETS if m >= rows)
+    return W4_PLAN[proj][b]
+
 
 def packed_cfg(proj: str, rows: int):
     if rows > PACKED_ROWS:
@@ -111,7 +139,7 @@ def _packable(n: int, k: int, proj: str) -> bool:
 
 class LlamaModel:
     def __init__(self, cfg: ModelConfig, device: torch.device, dtype: torch.dtype = torch.bfloat16,
-                 comm: TPComm = SINGLE, max_model_len: int = 8192):
+                 comm: TPComm = SINGLE, max_model_len: int = 8192, quantization: Optional[str] = None):
         self.cfg = cfg
         self.device = torch.device(device)
         self.dtype = dtype
@@ -134,6 +162,12 @@ class LlamaModel:
         self.ws: Optional[torch.Tensor] = None
         self.use_packed = (self.device.type == "cuda" and dtype == torch.bfloat16
                            and os.environ.get("FT_PACKED_GEMM", "1") != "0")
+        # "awq" / "w4": layer projections as W4A16 (group 128).  On the GPU only the
+        # packed int4 image is kept; the CPU backend holds the dequantized weights.
+        self.quant = (quantization or "").lower() or None
+        if self.quant not in (None, "awq", "w4"):
+            raise ValueError(f"unsupported quantization {quantization!r} (awq | w4)")
+        self._w4_scratch: Optional[torch.Tensor] = None
 
     # ------------------------------------------------------------------ weights
     def _set_layers(self, shards):
@@ -175,17 +209,27 @@ class LlamaModel:
                 self.lm_head = torch.empty(self.vocab_shard, cfg.hidden_size, dtype=self.dtype,
                                            device=self.device).normal_(0.0, std, generator=g)
         self.norm = torch.ones(cfg.hidden_size, dtype=self.dtype, device=self.device)
+        self._quantize_layers()
         self._prepare_packed()
         return self
 
     def load_checkpoint(self, ckpt_dir: str):
         cfg = self.cfg
         idx = W.SafetensorsIndex(ckpt_dir)
+        awq = W.is_awq_checkpoint(idx)
+        if awq and self.quant is None:
+            self.quant = "awq"
         shards = []
         for li in range(cfg.num_layers):
-            full = W.load_full_layer(idx, li, self.dtype)
-            shards.append(W.shard_full_layer(cfg, full, self.rank, self.tp))
-        self._set_layers(shards)
+            if awq:
+                shards.append(W.load_awq_layer_shard(cfg, idx, li, self.rank, self.tp))
+            else:
+                full = W.load_full_layer(idx, li, self.dtype)
+                shards.append(W.shard_full_layer(cfg, full, self.rank, self.tp))
+        if awq:
+            self._set_w4_layers(shards)
+        else:
+            self._set_layers(shards)
         self.embed = idx.get("model.embed_tokens.weight").to(self.device, self.dtype)
         self.norm = idx.get("model.norm.weight").to(self.device, self.dtype)
         if cfg.tie_word_embeddings or not idx.has("lm_head.weight"):
@@ -193,8 +237,79 @@ class LlamaModel:
         else:
             lm = idx.get("lm_head.weight").to(self.dtype)
         self.lm_head = W._shard_rows(lm, self.rank, self.tp).contiguous().to(self.device)
+        if not awq:  # AWQ layers arrive quantized
+            self._quantize_layers()
         self._prepare_packed()
         return self
+
+    # ------------------------------------------------------------------ W4A16
+    def _install_w4(self, L: LayerWeights, proj: str, q, z, s):
+        if self.device.type == "cuda":
+            if L.q4 is None:
+                L.q4 = {}
+            L.q4[proj] = Q.pack_w4(q.to(self.device), z.to(self.device), s.to(self.device))
+            setattr(L, _ATTR[proj], None)
+        else:  # CPU reference backend: the dequantized weight
+            setattr(L, _ATTR[proj], Q.dequantize_w4(q, z, s).to(self.dtype))
+
+    def _quantize_layers(self):
+        """Round-to-nearest W4 of bf16 layer weights (random init or a bf16 checkpoint
+        with ``quantization='w4'``); AWQ checkpoints arrive quantized."""
+        if self.quant is None:
+            return
+        for L in self.layers:
+            for proj, attr in _ATTR.items():
+                w = getattr(L, attr)
+                if w is None:
+                    continue
+                # from the bf16 values on every backend, so the CPU reference and the
+                # GPU hold the same quantized weights
+                q, z, sc = Q.quantize_w4(w.to(torch.bfloat16))
+                self._install_w4(L, proj, q, z, sc)
+            if self.device.type == "cuda":
+                torch.cuda.synchronize(self.device)  # free the bf16 copies as we go
+
+    def _set_w4_layers(self, shards):
+        self.layers = []
+        for sh in shards:
+            L = LayerWeights(wqkv=None, wo=None, wgu=None, wd=None,
+                             ln1=sh["ln1"].to(self.device, self.dtype),
+                             ln2=sh["ln2"].to(self.device, self.dtype))
+            for proj, attr in _ATTR.items():
+                self._install_w4(L, proj, *sh[attr])
+            self.layers.append(L)
+
+    def _w4_dense(self, w: "Q.W4Weight") -> torch.Tensor:
+        """bf16 copy of a W4 projection in a shared scratch (prefill-size GEMMs)."""
+        need = w.n * w.k
+        if self._w4_scratch is None or self._w4_scratch.numel() < need:
+            big = max(q.n * q.k for L in self.layers for q in (L.q4 or {}).values())
+            self._w4_scratch = torch.empty(max(need, big), dtype=self.dtype, device=self.device)
+        return Q.w4_dequant(w, out=self._w4_scratch[:need].view(w.n, w.k))
+
+    def _proj(self, x: torch.Tensor, L: LayerWeights, proj: str) -> torch.Tensor:
+        """bf16 y = x W^T for one layer projection (W4, packed bf16 or hipBLASLt)."""
+        q = L.q4.get(proj) if L.q4 else None
+        if q is None:
+            attr = _ATTR[proj]
+            return self._gemm(x, getattr(L, attr), getattr(L, attr + "_pk"), proj)
+        if x.shape[0] <= W4_ROWS:
+            nt, _ = w4_cfg(proj, x.shape[0])
+            return Q.w4_gemm(x, q, nt=nt)
+        return F.linear(x, self._w4_dense(q))
+
+    def _proj_slab(self, x: torch.Tensor, L: LayerWeights, proj: str) -> int:
+        """Split-K projection into self.ws fp32 slabs; returns the split count (0: not taken)."""
+        q = L.q4.get(proj) if L.q4 else None
+        if q is None:
+            if proj == "qkv":  # bf16 qkv stores bf16 (its plan has no split-K)
+                return 0
+            return self._gemm_slab(x, getattr(L, _ATTR[proj] + "_pk"), proj)
+        if self.ws is None or x.shape[0] > W4_ROWS:
+            return 0
+        nt, sp = w4_cfg(proj, x.shape[0])
+        Q.w4_gemm(x, q, ws=self.ws, splits=sp, nt=nt)
+        return sp
 
     def _prepare_packed(self):
         """Adds the packed copies the decode GEMMs stream (one more copy of the
@@ -206,22 +321,28 @@ class LlamaModel:
         # o / down leave split-K slabs for the fused add+RMSNorm: TP=1 only (under
         # TP the row-parallel outputs are all-reduced first) and hidden % 2048
         slab_ok = self.tp == 1 and H % 2048 == 0
-        use = {
-            "qkv": _packable(*L0.wqkv.shape, "qkv"),
-            "o": slab_ok and _packable(*L0.wo.shape, "o"),
-            "gu": _packable(*L0.wgu.shape, "gu"),
-            "down": slab_ok and _packable(*L0.wd.shape, "down"),
-        }
+        use = {}
+        need_ws = MAX_SPLITS * PACKED_ROWS * H
+        for proj, attr in _ATTR.items():
+            w = getattr(L0, attr)
+            if w is None:  # W4: the slab path depends on the shape rules only
+                q = L0.q4[proj]
+                sp_max = max(sp for _, sp in W4_PLAN[proj].values())
+                use[proj] = proj in ("qkv", "o", "down") and slab_ok \
+                    and q.k % (128 * sp_max) == 0 \
+                    and all(q.n % (16 * nt) == 0 for nt, _ in W4_PLAN[proj].values())
+                if use[proj]:
+                    need_ws = max(need_ws, max(sp * b * q.n for b, (_, sp) in W4_PLAN[proj].items()))
+                continue
+            use[proj] = _packable(*w.shape, proj) and (proj in ("qkv", "gu") or slab_ok)
         for L in self.layers:
-            L.wqkv_pk = ops.pack_weight(L.wqkv) if use["qkv"] else None
-            L.wo_pk = ops.pack_weight(L.wo) if use["o"] else None
-            L.wgu_pk = ops.pack_weight(L.wgu) if use["gu"] else None
-            L.wd_pk = ops.pack_weight(L.wd) if use["down"] else None
+            for proj, attr in _ATTR.items():
+                w = getattr(L, attr)
+                setattr(L, attr + "_pk", ops.pack_weight(w) if use[proj] and w is not None else None)
         if self.lm_head is not None and _packable(*self.lm_head.shape, "lm"):
             self.lm_head_pk = ops.pack_weight(self.lm_head)
-        if use["o"] or use["down"]:
-            self.ws = torch.empty(MAX_SPLITS * PACKED_ROWS * H, dtype=torch.float32,
-                                  device=self.device)
+        if use["o"] or use["down"] or use["qkv"] and L0.q4:
+            self.ws = torch.empty(need_ws, dtype=torch.float32, device=self.device)
 
     def _gemm(self, x: torch.Tensor, w: torch.Tensor, w_pk: Optional[torch.Tensor], proj: str):
         """bf16 y = x w^T: packed decode GEMM when the plan has a split-1 config."""
@@ -269,9 +390,16 @@ class LlamaModel:
                 ops.row_rmsnorm(x, L.ln1, eps, t, ws=self.ws, splits=slab, residual=residual)
             else:
                 ops.fused_add_rmsnorm(x, residual, L.ln1, eps)
-            qkv = self._gemm(x, L.wqkv, L.wqkv_pk, "qkv")
             kc, vc = kv_caches[li]
-            ops.rope_kv_write(qkv, meta.positions, self.cos_sin, meta.slot_mapping, kc, vc, nq, nkv, d)
+            sq = self._proj_slab(x, L, "qkv")
+            if sq:  # split-K slabs -> RoPE'd q and the paged K/V write in one kernel
+                qkv = torch.empty(t, (nq + 2 * nkv) * d, dtype=self.dtype, device=self.device)
+                ops.slab_rope_kv(self.ws, sq, t, qkv.shape[1], qkv, meta.positions, self.cos_sin,
+                                 meta.slot_mapping, kc, vc, nq, nkv, d)
+            else:
+                qkv = self._proj(x, L, "qkv")
+                ops.rope_kv_write(qkv, meta.positions, self.cos_sin, meta.slot_mapping, kc, vc,
+                                  nq, nkv, d)
             attn = torch.empty(t, nq * d, dtype=qkv.dtype, device=qkv.device)
             nd = meta.num_decode
             if nd > 0:
@@ -282,19 +410,19 @@ class LlamaModel:
                 ops.prefill_attention(attn[nd:], qkv[nd:], kc, vc, meta.block_tables, meta.seq_lens,
                                       meta.q_start_loc, meta.tile_info, meta.num_tiles, nq, nkv, d,
                                       self.scale)
-            so = self._gemm_slab(attn, L.wo_pk, "o")
+            so = self._proj_slab(attn, L, "o")
             if so:
                 x = torch.empty(t, H, dtype=self.dtype, device=self.device)
                 ops.row_rmsnorm(x, L.ln2, eps, t, ws=self.ws, splits=so, residual=residual)
             else:
-                x = F.linear(attn, L.wo)
+                x = self._proj(attn, L, "o")
                 self.comm.all_reduce(x)
                 ops.fused_add_rmsnorm(x, residual, L.ln2, eps)
-            gu = self._gemm(x, L.wgu, L.wgu_pk, "gu")
+            gu = self._proj(x, L, "gu")
             h = ops.silu_mul(gu)
-            slab = self._gemm_slab(h, L.wd_pk, "down")
+            slab = self._proj_slab(h, L, "down")
             if not slab:
-                x = F.linear(h, L.wd)
+                x = self._proj(h, L, "down")
                 self.comm.all_reduce(x)
         if slab:
             x = torch.empty(t, H, dtype=self.dtype, device=self.device)

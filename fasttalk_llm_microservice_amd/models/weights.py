@@ -62,9 +62,9 @@ def shard_full_layer(cfg: ModelConfig, full: Dict[str, torch.Tensor], rank: int,
     v = full["v"].view(cfg.num_kv_heads, d, -1)
     nq, _ = tp_heads(cfg, tp)
     k0, k1 = kv_head_range(cfg, tp, rank)
-    qs = q[rank * nq:(rank + 1) * nq].reshape(-1, cfg.hidden_size)
-    ks = k[k0:k1].reshape(-1, cfg.hidden_size)
-    vs = v[k0:k1].reshape(-1, cfg.hidden_size)
+    qs = q[rank * nq:(rank + 1) * nq].reshape(-1, q.shape[-1])
+    ks = k[k0:k1].reshape(-1, k.shape[-1])
+    vs = v[k0:k1].reshape(-1, v.shape[-1])
     gate = _shard_rows(full["gate"], rank, tp)
     up = _shard_rows(full["up"], rank, tp)
     return {
@@ -161,6 +161,76 @@ def load_full_layer(idx: SafetensorsIndex, layer: int, dtype) -> Dict[str, torch
         "ln1": "input_layernorm.weight", "ln2": "post_attention_layernorm.weight",
     }
     return {k: idx.get(p + v).to(dtype) for k, v in names.items()}
+
+
+# --------------------------------------------------------------------------------------
+# AWQ (W4A16) checkpoints: AutoAWQ "GEMM" tensors per projection
+# --------------------------------------------------------------------------------------
+_HF_PROJ = {"q": "self_attn.q_proj", "k": "self_attn.k_proj", "v": "self_attn.v_proj",
+            "o": "self_attn.o_proj", "gate": "mlp.gate_proj", "up": "mlp.up_proj",
+            "down": "mlp.down_proj"}
+
+
+def is_awq_checkpoint(idx: SafetensorsIndex) -> bool:
+    cfg_path = os.path.join(idx.dir, "config.json")
+    if os.path.exists(cfg_path):
+        with open(cfg_path) as f:
+            qc = json.load(f).get("quantization_config") or {}
+        if str(qc.get("quant_method", "")).lower() == "awq":
+            if int(qc.get("bits", 4)) != 4 or int(qc.get("group_size", 128)) != 128:
+                raise ValueError("only 4-bit AWQ with group size 128 is supported")
+            return True
+    return idx.has("model.layers.0.self_attn.q_proj.qweight")
+
+
+def load_awq_layer_shard(cfg: ModelConfig, idx: SafetensorsIndex, layer: int, rank: int, tp: int):
+    """One layer of an AWQ checkpoint -> this rank's fused shards as (q, z, s)
+    triples ([N, K] uint8, [N, K/128] uint8, [N, K/128] fp32).  The head / row /
+    column slicing is the bf16 path's (:func:`shard_full_layer`) applied to q, z
+    and s alike: groups run along K, so a row-parallel shard of K/tp columns
+    (a multiple of 128) keeps whole groups."""
+    from ..ops.quant import awq_unpack
+
+    p = f"model.layers.{layer}."
+    parts = {"q": {}, "z": {}, "s": {}}
+    for name, hf in _HF_PROJ.items():
+        q, z, s = awq_unpack(idx.get(p + hf + ".qweight"), idx.get(p + hf + ".qzeros"),
+                             idx.get(p + hf + ".scales"))
+        parts["q"][name], parts["z"][name], parts["s"][name] = q, z, s
+    ln = {"ln1": idx.get(p + "input_layernorm.weight"),
+          "ln2": idx.get(p + "post_attention_layernorm.weight")}
+    sh = {k: shard_full_layer(cfg, dict(v, **ln), rank, tp) for k, v in parts.items()}
+    out = {a: (sh["q"][a], sh["z"][a], sh["s"][a]) for a in ("wqkv", "wo", "wgu", "wd")}
+    out.update(ln1=ln["ln1"], ln2=ln["ln2"])
+    return out
+
+
+def save_awq_checkpoint(cfg: ModelConfig, full_layers, embed, norm, lm_head, out_dir: str):
+    """Quantize full-precision layers (RTN, group 128) and write them in the
+    AutoAWQ GEMM layout with an HF ``quantization_config`` (tests and tooling)."""
+    from safetensors.torch import save_file
+
+    from ..ops.quant import awq_pack, quantize_w4
+
+    save_hf_checkpoint(cfg, [], embed, norm, lm_head, out_dir)
+    path = os.path.join(out_dir, "model.safetensors")
+    from safetensors.torch import load_file
+
+    t = load_file(path)
+    for li, L in enumerate(full_layers):
+        p = f"model.layers.{li}."
+        for name, hf in _HF_PROJ.items():
+            qw, qz, sc = awq_pack(*quantize_w4(L[name]))
+            t[p + hf + ".qweight"], t[p + hf + ".qzeros"], t[p + hf + ".scales"] = qw, qz, sc
+        t[p + "input_layernorm.weight"] = L["ln1"].contiguous()
+        t[p + "post_attention_layernorm.weight"] = L["ln2"].contiguous()
+    save_file(t, path)
+    with open(os.path.join(out_dir, "config.json")) as f:
+        hf_cfg = json.load(f)
+    hf_cfg["quantization_config"] = {"quant_method": "awq", "bits": 4, "group_size": 128,
+                                     "zero_point": True, "version": "gemm"}
+    with open(os.path.join(out_dir, "config.json"), "w") as f:
+        json.dump(hf_cfg, f, indent=1)
 
 
 def save_hf_checkpoint(cfg: ModelConfig, full_layers, embed, norm, lm_head: Optional[torch.Tensor],

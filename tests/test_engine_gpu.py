@@ -24,17 +24,23 @@ def _prompts(n, lens, seed=0):
     return [rng.integers(0, 120000, l).tolist() for l in lens[:n]]
 
 
-@pytest.mark.parametrize("model", ["tiny-gqa4", "tiny-2k"])
-def test_gpu_logits_match_cpu_reference(model):
+@pytest.mark.parametrize("model,quant,T", [("tiny-gqa4", None, 40), ("tiny-2k", None, 40),
+                                            ("tiny-2k", "w4", 40), ("tiny-2k", "w4", 100),
+                                            ("tiny", "w4", 40)])
+def test_gpu_logits_match_cpu_reference(model, quant, T):
     """Full forward on GPU (bf16 HIP kernels; at hidden 2048 the down projection
-    and LM head run on the packed-weight skinny GEMMs) vs CPU fp32 reference ops."""
+    and LM head run on the packed-weight skinny GEMMs) vs CPU fp32 reference ops.
+    W4: <= 64 rows run the W4A16 kernels (o / down into split-K slabs), 100 rows
+    the dequantize + hipBLASLt path; the CPU side holds the dequantized weights."""
     cfg = MODELS[model]
     # consistent=True: both draw the same unsharded weights on the host from one seed
-    g = LlamaModel(cfg, torch.device("cuda"), torch.bfloat16, max_model_len=512).init_random(
-        3, consistent=True)
-    c = LlamaModel(cfg, torch.device("cpu"), torch.float32, max_model_len=512)
+    g = LlamaModel(cfg, torch.device("cuda"), torch.bfloat16, max_model_len=512,
+                   quantization=quant).init_random(3, consistent=True)
+    c = LlamaModel(cfg, torch.device("cpu"), torch.float32, max_model_len=512, quantization=quant)
     c.init_random(3, consistent=True)
-    T, bs, nblk = 40, 16, 8
+    if quant:
+        assert g.layers[0].q4 and g.layers[0].wgu is None and c.layers[0].q4 is None
+    bs, nblk = 16, 8
     for m in (g, c):
         kv = m.allocate_kv_cache(nblk, bs)
         dev = m.device
@@ -141,3 +147,12 @@ def test_host_swap_matches_unconstrained():
     assert s.num_preemptions == s.num_swap_out  # no recompute fallback
     assert got == ref
     assert eng.bm.num_free() == eng.bm.num_blocks and s.host.num_free() == s.host.num_blocks
+
+
+def test_w4_engine_graph_matches_eager():
+    """W4A16 decode through hipGraphs equals eager W4A16 decode token for token."""
+    prompts = _prompts(6, [9, 30, 65, 17, 80, 3], seed=9)
+    sp = SamplingParams(temperature=0, max_tokens=24, ignore_eos=True)
+    outs = [_engine(model="tiny-2k", quantization="w4", enforce_eager=e).generate(prompts, sp)
+            for e in (False, True)]
+    assert outs[0] == outs[1]

@@ -279,6 +279,45 @@ def test_kv_swap_gather_scatter():
 
 
 # ----------------------------------------------------------------------------------
+# W4A16 (AWQ-style int4, group 128)
+# ----------------------------------------------------------------------------------
+
+def _w4(n, k, seed=0):
+    from fasttalk_llm_microservice_amd.ops import quant as Q
+
+    g = torch.Generator().manual_seed(seed)
+    w = torch.randn(n, k, generator=g) * 0.05
+    q, z, s = Q.quantize_w4(w)
+    return Q, Q.pack_w4(q.to(DEV), z.to(DEV), s.to(DEV)), Q.dequantize_w4(q, z, s)
+
+
+@pytest.mark.parametrize("n,k", [(1024, 4096), (512, 1024), (4096, 14336), (6144, 4096)])
+def test_w4_dequant_exact(n, k):
+    Q, W, ref_w = _w4(n, k)
+    out = Q.w4_dequant(W)
+    assert torch.equal(out.float().cpu(), ref_w.bfloat16().float())
+
+
+@pytest.mark.parametrize("m", [1, 5, 16, 29, 48, 64])
+@pytest.mark.parametrize("n,k,nt,splits", [(1024, 4096, 1, 1), (1024, 4096, 2, 1),
+                                           (2048, 4096, 4, 1), (512, 1024, 1, 2),
+                                           (4096, 14336, 1, 4), (1024, 4096, 2, 2)])
+def test_w4_gemm_matches_fp32(m, n, k, nt, splits):
+    Q, W, ref_w = _w4(n, k, seed=m)
+    x = torch.randn(m, k, generator=torch.Generator().manual_seed(7)).bfloat16()
+    ref_y = x.float() @ ref_w.t()
+    xd = x.to(DEV)
+    if splits == 1:
+        y = Q.w4_gemm(xd, W, nt=nt).float().cpu()
+        tol = 2e-2 * ref_y.abs().max().item() + 1e-2
+        assert (y - ref_y).abs().max().item() < tol
+    ws = torch.full((splits * m * n,), float("nan"), device=DEV)
+    Q.w4_gemm(xd, W, ws=ws, splits=splits, nt=nt)
+    y = ws.view(splits, m, n).sum(0).cpu()
+    assert (y - ref_y).abs().max().item() < 1e-3 * ref_y.abs().max().item() + 1e-3
+
+
+# ----------------------------------------------------------------------------------
 # decode-shape skinny GEMM + fused row epilogues
 # ----------------------------------------------------------------------------------
 
