@@ -220,7 +220,7 @@ def save_awq_checkpoint(cfg: ModelConfig, full_layers, embed, norm, lm_head, out
     for li, L in enumerate(full_layers):
         p = f"model.layers.{li}."
         for name, hf in _HF_PROJ.items():
-            qw, qz, sc = awq_pack(*quantize_w4(L[name]))
+            qw, qz, sc = awq_pack(*quantize_w4(L[name].to(torch.bfloat16)))
             t[p + hf + ".qweight"], t[p + hf + ".qzeros"], t[p + hf + ".scales"] = qw, qz, sc
         t[p + "input_layernorm.weight"] = L["ln1"].contiguous()
         t[p + "post_attention_layernorm.weight"] = L["ln2"].contiguous()

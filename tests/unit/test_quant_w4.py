@@ -93,7 +93,8 @@ def test_awq_checkpoint_loads_and_matches_rtn_engine(tmp_path):
     assert awq.runner.model.quant == "awq"
     m = awq.runner.model
     L0 = layers[0]
-    deq = {k: Q.dequantize_w4(*Q.quantize_w4(L0[k])) for k in ("q", "k", "v", "gate", "up")}
+    deq = {k: Q.dequantize_w4(*Q.quantize_w4(L0[k].bfloat16()))
+           for k in ("q", "k", "v", "gate", "up")}
     torch.testing.assert_close(m.layers[0].wqkv, torch.cat([deq["q"], deq["k"], deq["v"]], 0),
                                rtol=1e-3, atol=1e-5)  # scales go through fp16 in the AWQ file
     torch.testing.assert_close(m.layers[0].wgu, torch.cat([deq["gate"], deq["up"]], 0),
