@@ -26,10 +26,44 @@ def summarize(db: str, top: int = 40, per_step: int = 0) -> str:
     return "\n".join(out)
 
 
+def busy(db: str, last_ms: float = 0.0) -> str:
+    """GPU busy time (union of kernel intervals) vs wall span, over the whole
+    trace or its last ``last_ms`` milliseconds: how much of a step is gaps."""
+    c = sqlite3.connect(db)
+    iv = sorted(c.execute("select start, end from kernels").fetchall())
+    if not iv:
+        return "no kernels"
+    t1 = max(e for _, e in iv)
+    t0 = t1 - last_ms * 1e6 if last_ms else iv[0][0]
+    tot, cur_s, cur_e, gaps = 0, None, None, []
+    for s, e in iv:
+        if e <= t0:
+            continue
+        s = max(s, t0)
+        if cur_e is None or s > cur_e:
+            if cur_e is not None:
+                tot += cur_e - cur_s
+                gaps.append(s - cur_e)
+            cur_s, cur_e = s, e
+        else:
+            cur_e = max(cur_e, e)
+    tot += cur_e - cur_s
+    span = t1 - t0
+    gaps.sort()
+    med = gaps[len(gaps) // 2] / 1e3 if gaps else 0.0
+    return (f"window {span / 1e6:.2f} ms: GPU busy {tot / 1e6:.2f} ms ({100 * tot / span:.1f}%), "
+            f"{len(gaps)} gaps, median gap {med:.2f} us, gaps > 50 us: "
+            f"{sum(g for g in gaps if g > 50e3) / 1e6:.2f} ms")
+
+
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("db")
     ap.add_argument("--top", type=int, default=40)
     ap.add_argument("--per-step", type=int, default=0)
+    ap.add_argument("--busy-last-ms", type=float, default=-1,
+                    help="also report GPU busy vs wall over the last N ms (0: whole trace)")
     a = ap.parse_args()
     print(summarize(a.db, a.top, a.per_step))
+    if a.busy_last_ms >= 0:
+        print(busy(a.db, a.busy_last_ms))

@@ -275,6 +275,11 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(
   }
 }
 
+// One workgroup per (sequence, q head): wave 0 turns the partitions' (m, l) into
+// merge weights (lane s = partition s, wave-wide max / sum), then every thread
+// sums its head dim over the partitions with 16 loads in flight (clamped
+// indices, zero weights past the end) -- the merge is a handful of dependent
+// round trips, not one per partition.
 template <int D>
 __global__ __launch_bounds__(D) void paged_decode_combine_kernel(
     uint16_t* __restrict__ out, int out_stride, const float* __restrict__ tmp_out,
@@ -284,16 +289,31 @@ __global__ __launch_bounds__(D) void paged_decode_combine_kernel(
   const int part = decode_part(L, max_splits);
   const int ns = (L + part - 1) / part;
   if (ns <= 1) return;
+  __shared__ float s_w[64];
   const size_t base = ((size_t)b * nq + h) * max_splits;
-  float M = -INFINITY;
-  for (int s = 0; s < ns; ++s) M = fmaxf(M, tmp_ml[(base + s) * 2]);
-  float den = 0.f, acc = 0.f;
-  for (int s = 0; s < ns; ++s) {
-    const float w = exp2f(tmp_ml[(base + s) * 2] - M);
-    den += w * tmp_ml[(base + s) * 2 + 1];
-    acc += w * tmp_out[(base + s) * D + d];
+  if (d < 64) {  // max_splits <= 64 (checked by the launcher)
+    const float ms = d < ns ? tmp_ml[(base + d) * 2] : -INFINITY;
+    const float ls = d < ns ? tmp_ml[(base + d) * 2 + 1] : 0.f;
+    float M = ms;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) M = fmaxf(M, __shfl_xor(M, o, 64));
+    const float w = d < ns ? exp2f(ms - M) : 0.f;
+    float den = w * ls;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) den += __shfl_xor(den, o, 64);
+    s_w[d] = w / den;
   }
-  out[(size_t)b * out_stride + h * D + d] = f32_to_bf16(acc / den);
+  __syncthreads();
+  const float* src = tmp_out + base * D + d;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int s0 = 0; s0 < ns; s0 += 16) {
+    float v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) v[u] = src[(size_t)min(s0 + u, ns - 1) * D];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) acc[u & 3] += (s0 + u < ns ? s_w[s0 + u] : 0.f) * v[u];
+  }
+  out[(size_t)b * out_stride + h * D + d] = f32_to_bf16((acc[0] + acc[1]) + (acc[2] + acc[3]));
 }
 
 }  // namespace ft
@@ -309,7 +329,7 @@ extern "C" int ft_paged_decode_attention(void* out, int out_stride, float* tmp_o
                                          float scale, hipStream_t stream) {
   if (batch <= 0) return 0;
   if (nq % nkv != 0) return -1;
-  if (max_splits < 1) return -3;
+  if (max_splits < 1 || max_splits > 64) return -3;
   if (block_size < 16 || (block_size & (block_size - 1))) return -4;
   const int bs_shift = __builtin_ctz(block_size);
   const int G = nq / nkv;

@@ -27,16 +27,27 @@ struct SrcBf16 {
 struct SrcSlab {
   const float* ws;
   int splits, rows, cols;
+  // Slabs are read 4 at a time with clamped (always valid) addresses, so up to 4
+  // loads per half are in flight instead of one dependent round trip per split.
   __device__ __forceinline__ void load8(int row, int col, float (&f)[8]) const {
     const float* p = ws + (size_t)row * cols + col;
+    const size_t slab = (size_t)rows * cols;
     float4 a = reinterpret_cast<const float4*>(p)[0];
     float4 b = reinterpret_cast<const float4*>(p)[1];
-    for (int s = 1; s < splits; ++s) {
-      const float* q = p + (size_t)s * rows * cols;
-      const float4 c = reinterpret_cast<const float4*>(q)[0];
-      const float4 d = reinterpret_cast<const float4*>(q)[1];
-      a.x += c.x; a.y += c.y; a.z += c.z; a.w += c.w;
-      b.x += d.x; b.y += d.y; b.z += d.z; b.w += d.w;
+    for (int s0 = 1; s0 < splits; s0 += 4) {
+      float4 c[4], d[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float* q = p + (size_t)min(s0 + u, splits - 1) * slab;
+        c[u] = reinterpret_cast<const float4*>(q)[0];
+        d[u] = reinterpret_cast<const float4*>(q)[1];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float k = s0 + u < splits ? 1.f : 0.f;
+        a.x += k * c[u].x; a.y += k * c[u].y; a.z += k * c[u].z; a.w += k * c[u].w;
+        b.x += k * d[u].x; b.y += k * d[u].y; b.z += k * d[u].z; b.w += k * d[u].w;
+      }
     }
     f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w;
     f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
@@ -144,7 +155,8 @@ __global__ __launch_bounds__(256) void slab_rope_kv_kernel(
   const int blk = slot >= 0 ? slot / block_size : 0;
   const int off = slot >= 0 ? slot - blk * block_size : 0;
   const int n_rot = (nq + nkv) * CPH;
-  for (int item = threadIdx.x; item < n_rot; item += blockDim.x) {
+  const int tid = blockIdx.y * blockDim.x + threadIdx.x, nthr = gridDim.y * blockDim.x;
+  for (int item = tid; item < n_rot; item += nthr) {
     const int head = item / CPH, c = item - (item / CPH) * CPH;
     float x1[8], x2[8];
     src.load8(t, head * D + c * 8, x1);
@@ -168,7 +180,7 @@ __global__ __launch_bounds__(256) void slab_rope_kv_kernel(
   }
   if (slot >= 0) {
     const int nv = nkv * (D / 8);
-    for (int item = threadIdx.x; item < nv; item += blockDim.x) {
+    for (int item = tid; item < nv; item += nthr) {
       const int kh = item / (D / 8), c = item - kh * (D / 8);
       float f[8];
       src.load8(t, (nq + nkv) * D + kh * D + c * 8, f);
@@ -256,11 +268,11 @@ extern "C" int ft_slab_rope_kv(const float* ws, int splits, int rows, int cols, 
   if (rows <= 0) return 0;
   ft::SrcSlab src{ws, splits, rows, cols};
   if (head_dim == 128) {
-    hipLaunchKernelGGL(ft::slab_rope_kv_kernel<128>, dim3(rows), dim3(256), 0, stream, src,
+    hipLaunchKernelGGL(ft::slab_rope_kv_kernel<128>, dim3(rows, 2), dim3(256), 0, stream, src,
                        (uint16_t*)q_out, q_stride, positions, cos_sin, slot_mapping,
                        (uint16_t*)k_cache, (uint16_t*)v_cache, nq, nkv, block_size);
   } else if (head_dim == 64) {
-    hipLaunchKernelGGL(ft::slab_rope_kv_kernel<64>, dim3(rows), dim3(256), 0, stream, src,
+    hipLaunchKernelGGL(ft::slab_rope_kv_kernel<64>, dim3(rows, 2), dim3(256), 0, stream, src,
                        (uint16_t*)q_out, q_stride, positions, cos_sin, slot_mapping,
                        (uint16_t*)k_cache, (uint16_t*)v_cache, nq, nkv, block_size);
   } else {
