@@ -61,6 +61,9 @@ int ft_ar_allreduce(void* out, const void* x, long n, const uint64_t* peers_dev,
                     size_t max_bytes, unsigned spin_budget, hipStream_t stream);
 int ft_skinny_gemm_pk(const void* x, int x_stride, int M, const void* wpk, int N, int K, float* ws,
                       void* out, int out_stride, int splits, int nt, hipStream_t stream);
+int ft_pkr_gemm(const void* x, int x_stride, int M, const void* wpk, int N, int K, float* ws,
+                void* out, int out_stride, void* residual, int res_stride, int* tickets,
+                int splits, int nt, int depth, int epi, int norm, float eps, hipStream_t stream);
 int ft_row_rmsnorm(const void* x, int x_stride, const float* ws, int splits, void* out,
                    int out_stride, void* residual, const void* w, int rows, int hidden, float eps,
                    hipStream_t stream);
@@ -71,7 +74,7 @@ int ft_slab_store(const float* ws, int splits, int rows, int cols, void* out, in
 int ft_slab_rope_kv(const float* ws, int splits, int rows, int cols, void* q_out, int q_stride,
                     const int* positions, const float* cos_sin, const int* slot_mapping,
                     void* k_cache, void* v_cache, int nq, int nkv, int head_dim, int block_size,
-                    hipStream_t stream);
+                    const void* residual, int hidden, float eps, hipStream_t stream);
 }
 
 namespace {
@@ -395,6 +398,55 @@ void skinny_gemm(at::Tensor x, at::Tensor w, c10::optional<at::Tensor> out,
              "skinny_gemm");
 }
 
+// Ring-pipelined packed decode GEMM with fused epilogues (csrc/kernels/skinny_pkr.hip).
+// epi: 0 store (out or slabs), 1 silu (gate/up interleaved, out [M, N/2]), 2 resid.
+void pkr_gemm(at::Tensor x, at::Tensor w, c10::optional<at::Tensor> out,
+              c10::optional<at::Tensor> ws, c10::optional<at::Tensor> residual,
+              c10::optional<at::Tensor> tickets, int64_t splits, int64_t nt, int64_t depth,
+              int64_t epi, bool norm, double eps) {
+  check_bf16(x, "x");
+  check_bf16(w, "w");
+  check_rows(x, "x");
+  TORCH_CHECK(w.dim() == 2 && w.is_contiguous(), "w must be contiguous [N, K]");
+  const int M = (int)x.size(0), K = (int)x.size(1), N = (int)w.size(0);
+  TORCH_CHECK(w.size(1) == K, "K mismatch");
+  TORCH_CHECK(M <= 64, "pkr_gemm supports M <= 64");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0, "w alignment");
+  float* wsp = nullptr;
+  void* op = nullptr;
+  void* rp = nullptr;
+  int* tp = nullptr;
+  int ostride = 0, rstride = 0;
+  if (ws.has_value()) {
+    check_ws(*ws, splits * M * N);
+    wsp = ws->data_ptr<float>();
+  }
+  if (out.has_value()) {
+    check_bf16(*out, "out");
+    TORCH_CHECK(out->dim() == 2 && out->stride(1) == 1 && out->size(0) >= M &&
+                    out->size(1) >= (epi == 1 ? N / 2 : N),
+                "out shape");
+    op = out->data_ptr();
+    ostride = (int)out->stride(0);
+  }
+  if (residual.has_value()) {
+    check_bf16(*residual, "residual");
+    check_rows(*residual, "residual");
+    TORCH_CHECK(residual->size(0) >= M && residual->size(1) == N, "residual shape");
+    rp = residual->data_ptr();
+    rstride = (int)residual->stride(0);
+  }
+  if (tickets.has_value()) {
+    check_i32(*tickets, "tickets");
+    TORCH_CHECK(tickets->numel() >= N / (16 * nt), "tickets too small");
+    tp = tickets->data_ptr<int>();
+  }
+  check_rc(ft_pkr_gemm(x.data_ptr(), (int)x.stride(0), M, w.data_ptr(), N, K, wsp, op, ostride, rp,
+                       rstride, tp, (int)splits, (int)nt, (int)depth, (int)epi, norm ? 1 : 0,
+                       (float)eps, cur_stream()),
+           "pkr_gemm");
+}
+
 // ---- custom one-shot all-reduce (csrc/kernels/custom_ar.hip) ----------------------
 int64_t custom_ar_alloc(int64_t bytes) {
   void* p = nullptr;
@@ -504,8 +556,16 @@ void slab_store(at::Tensor ws, int64_t splits, int64_t rows, int64_t cols, at::T
 void slab_rope_kv(at::Tensor ws, int64_t splits, int64_t rows, int64_t cols, at::Tensor q_out,
                   at::Tensor positions, at::Tensor cos_sin, at::Tensor slot_mapping,
                   at::Tensor k_cache, at::Tensor v_cache, int64_t nq, int64_t nkv,
-                  int64_t head_dim) {
+                  int64_t head_dim, c10::optional<at::Tensor> residual, double eps) {
   check_ws(ws, splits * rows * cols);
+  const void* rp = nullptr;
+  int hidden = 0;
+  if (residual.has_value()) {
+    check_bf16(*residual, "residual");
+    TORCH_CHECK(residual->is_contiguous() && residual->size(0) >= rows, "residual shape");
+    rp = residual->data_ptr();
+    hidden = (int)residual->size(1);
+  }
   check_bf16(q_out, "q_out");
   check_rows(q_out, "q_out");
   check_i32(positions, "positions");
@@ -522,7 +582,8 @@ void slab_rope_kv(at::Tensor ws, int64_t splits, int64_t rows, int64_t cols, at:
                            q_out.data_ptr(), (int)q_out.stride(0), positions.data_ptr<int>(),
                            cos_sin.data_ptr<float>(), slot_mapping.data_ptr<int>(),
                            k_cache.data_ptr(), v_cache.data_ptr(), (int)nq, (int)nkv,
-                           (int)head_dim, (int)k_cache.size(2), cur_stream()), "slab_rope_kv");
+                           (int)head_dim, (int)k_cache.size(2), rp, hidden, (float)eps,
+                           cur_stream()), "slab_rope_kv");
 }
 
 }  // namespace
@@ -548,6 +609,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("w4_dequant", &w4_dequant);
   m.def("skinny_gemm", &skinny_gemm, py::arg("x"), py::arg("w"), py::arg("out") = py::none(),
         py::arg("ws") = py::none(), py::arg("splits") = 1, py::arg("nt") = 1, py::arg("u") = 2);
+  m.def("pkr_gemm", &pkr_gemm, py::arg("x"), py::arg("w"), py::arg("out") = py::none(),
+        py::arg("ws") = py::none(), py::arg("residual") = py::none(),
+        py::arg("tickets") = py::none(), py::arg("splits") = 1, py::arg("nt") = 2,
+        py::arg("depth") = 3, py::arg("epi") = 0, py::arg("norm") = false, py::arg("eps") = 0.0);
   m.def("row_rmsnorm", &row_rmsnorm, py::arg("out"), py::arg("x") = py::none(),
         py::arg("ws") = py::none(), py::arg("splits") = 1, py::arg("residual") = py::none(),
         py::arg("w"), py::arg("rows"), py::arg("eps"));
@@ -562,5 +627,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("custom_ar_allreduce", &custom_ar_allreduce);
   m.def("slab_silu", &slab_silu);
   m.def("slab_store", &slab_store);
-  m.def("slab_rope_kv", &slab_rope_kv);
+  m.def("slab_rope_kv", &slab_rope_kv, py::arg("ws"), py::arg("splits"), py::arg("rows"),
+        py::arg("cols"), py::arg("q_out"), py::arg("positions"), py::arg("cos_sin"),
+        py::arg("slot_mapping"), py::arg("k_cache"), py::arg("v_cache"), py::arg("nq"),
+        py::arg("nkv"), py::arg("head_dim"), py::arg("residual") = py::none(),
+        py::arg("eps") = 0.0);
 }

@@ -145,7 +145,7 @@ __global__ __launch_bounds__(256) void slab_rope_kv_kernel(
     SrcSlab src, uint16_t* __restrict__ q_out, int q_stride, const int* __restrict__ positions,
     const float* __restrict__ cos_sin, const int* __restrict__ slot_mapping,
     uint16_t* __restrict__ k_cache, uint16_t* __restrict__ v_cache, int nq, int nkv,
-    int block_size) {
+    int block_size, const uint16_t* __restrict__ residual, int hidden, float eps) {
   constexpr int HALF = D / 2;
   constexpr int CPH = HALF / 8;
   const int t = blockIdx.x;
@@ -154,6 +154,25 @@ __global__ __launch_bounds__(256) void slab_rope_kv_kernel(
   const float* cs = cos_sin + (size_t)pos * D;
   const int blk = slot >= 0 ? slot / block_size : 0;
   const int off = slot >= 0 ? slot - blk * block_size : 0;
+  // fused decode layer: the QKV GEMM ran on the raw residual stream with the
+  // input-norm weight folded into W, so the RMS scale of the row applies here
+  // (RoPE is linear): qkv = rsqrt(mean(res^2) + eps) * sum(slabs)
+  float rs = 1.f;
+  if (residual != nullptr) {
+    __shared__ float red[4];
+    const uint4* rr = reinterpret_cast<const uint4*>(residual + (size_t)t * hidden);
+    float ss = 0.f;
+    for (int c = threadIdx.x; c < hidden / 8; c += blockDim.x) {
+      float f[8];
+      load8(rr[c], f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ss += f[j] * f[j];
+    }
+    ss = wave_sum(ss);
+    if (lane_id() == 0) red[wave_id()] = ss;
+    __syncthreads();
+    rs = rsqrtf((red[0] + red[1] + red[2] + red[3]) / (float)hidden + eps);
+  }
   const int n_rot = (nq + nkv) * CPH;
   const int tid = blockIdx.y * blockDim.x + threadIdx.x, nthr = gridDim.y * blockDim.x;
   for (int item = tid; item < n_rot; item += nthr) {
@@ -165,6 +184,8 @@ __global__ __launch_bounds__(256) void slab_rope_kv_kernel(
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const float co = cs[c * 8 + j], si = cs[HALF + c * 8 + j];
+      x1[j] *= rs;
+      x2[j] *= rs;
       y1[j] = x1[j] * co - x2[j] * si;
       y2[j] = x2[j] * co + x1[j] * si;
     }
@@ -184,6 +205,8 @@ __global__ __launch_bounds__(256) void slab_rope_kv_kernel(
       const int kh = item / (D / 8), c = item - kh * (D / 8);
       float f[8];
       src.load8(t, (nq + nkv) * D + kh * D + c * 8, f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] *= rs;
       uint16_t* vp = v_cache + (((size_t)blk * nkv + kh) * block_size + off) * D;
       *reinterpret_cast<uint4*>(vp + c * 8) = store8(f);
     }
@@ -264,17 +287,21 @@ extern "C" int ft_slab_store(const float* ws, int splits, int rows, int cols, vo
 extern "C" int ft_slab_rope_kv(const float* ws, int splits, int rows, int cols, void* q_out,
                                int q_stride, const int* positions, const float* cos_sin,
                                const int* slot_mapping, void* k_cache, void* v_cache, int nq,
-                               int nkv, int head_dim, int block_size, hipStream_t stream) {
+                               int nkv, int head_dim, int block_size, const void* residual,
+                               int hidden, float eps, hipStream_t stream) {
   if (rows <= 0) return 0;
+  if (residual != nullptr && hidden % 8 != 0) return -2;
   ft::SrcSlab src{ws, splits, rows, cols};
   if (head_dim == 128) {
     hipLaunchKernelGGL(ft::slab_rope_kv_kernel<128>, dim3(rows, 2), dim3(256), 0, stream, src,
                        (uint16_t*)q_out, q_stride, positions, cos_sin, slot_mapping,
-                       (uint16_t*)k_cache, (uint16_t*)v_cache, nq, nkv, block_size);
+                       (uint16_t*)k_cache, (uint16_t*)v_cache, nq, nkv, block_size,
+                       (const uint16_t*)residual, hidden, eps);
   } else if (head_dim == 64) {
     hipLaunchKernelGGL(ft::slab_rope_kv_kernel<64>, dim3(rows, 2), dim3(256), 0, stream, src,
                        (uint16_t*)q_out, q_stride, positions, cos_sin, slot_mapping,
-                       (uint16_t*)k_cache, (uint16_t*)v_cache, nq, nkv, block_size);
+                       (uint16_t*)k_cache, (uint16_t*)v_cache, nq, nkv, block_size,
+                       (const uint16_t*)residual, hidden, eps);
   } else {
     return -1;
   }

@@ -287,7 +287,48 @@ def slab_store(ws, splits, rows, cols, out):
 
 
 def slab_rope_kv(ws, splits, rows, cols, q_out, positions, cos_sin, slot_mapping, k_cache,
-                 v_cache, nq, nkv, head_dim):
+                 v_cache, nq, nkv, head_dim, residual=None, eps: float = 0.0):
+    """Reduces the QKV split-K slabs, applies RoPE, writes q and the paged K/V.  With
+    ``residual`` (fused decode layer) the slabs are scaled by the RMS of the residual
+    row first (the input-norm weight is folded into the packed QKV weight)."""
     native().slab_rope_kv(ws, splits, rows, cols, q_out, positions, cos_sin, slot_mapping,
-                          k_cache, v_cache, nq, nkv, head_dim)
+                          k_cache, v_cache, nq, nkv, head_dim, residual, eps)
     return q_out
+
+
+# ---------------------------------------------------------------------------------
+# fused decode layer GEMMs (csrc/kernels/skinny_pkr.hip)
+# ---------------------------------------------------------------------------------
+
+_PKR_EPI = {"store": 0, "silu": 1, "resid": 2}
+# (nt, depth) instantiated for every epilogue; "silu" needs an even nt
+PKR_CONFIGS = [(1, 2), (1, 4), (2, 2), (2, 3), (2, 4), (4, 2), (4, 3)]
+
+
+def interleave_gate_up(w: torch.Tensor, nh: int) -> torch.Tensor:
+    """[2I, K] gate rows then up rows -> the row order of the fused gate_up + SiLU
+    kernel with nt = 2 * nh column tiles per workgroup: for each block of 16 * nh
+    outputs, its gate rows then its up rows."""
+    two_i, k = w.shape
+    inter = two_i // 2
+    r = 16 * nh
+    assert inter % r == 0
+    g = w[:inter].reshape(inter // r, r, k)
+    u = w[inter:].reshape(inter // r, r, k)
+    return torch.stack([g, u], dim=1).reshape(two_i, k)
+
+
+def pkr_gemm(x, w_pk, epi: str = "store", out=None, ws=None, residual=None, tickets=None,
+             splits: int = 1, nt: int = 2, depth: int = 3, norm: bool = False, eps: float = 0.0):
+    """Ring-pipelined decode GEMM (M <= 64) on pack_weight() images.
+
+    * ``store``: bf16 ``out`` (one split) or fp32 slabs [splits, M, N] in ``ws``.
+    * ``silu``: w_pk packs interleave_gate_up(W_gu, nt // 2); returns h = silu(g) * u
+      [M, N/2]; ``norm``: x rows RMS-normalised on the fly (norm weight folded into W).
+    * ``resid``: ``residual`` += x w^T, split-K reduced inside the launch (``tickets``:
+      zeroed int32, >= N / (16 nt), left zeroed)."""
+    if epi == "silu" and out is None:
+        out = torch.empty(x.shape[0], w_pk.shape[0] // 2, dtype=x.dtype, device=x.device)
+    native().pkr_gemm(x, w_pk, out, ws, residual, tickets, splits, nt, depth, _PKR_EPI[epi],
+                      norm, eps)
+    return out

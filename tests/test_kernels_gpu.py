@@ -422,3 +422,90 @@ def test_skinny_gemm_packed(m, n, k, splits, nt, u):
         ops.skinny_gemm(x, wp, ws=ws, splits=splits, nt=nt, u=u)
         y = ws.view(splits, m, n).sum(0)
     _close(y, ref_y, atol=3e-2, rtol=2e-2, msg="packed skinny gemm")
+
+
+# ---- fused decode layer GEMMs (csrc/kernels/skinny_pkr.hip) ------------------------
+
+@pytest.mark.parametrize("nt,depth", [(1, 4), (2, 3), (4, 3), (4, 2)])
+@pytest.mark.parametrize("m", [1, 13, 37, 64])
+@pytest.mark.parametrize("splits", [1, 4])
+def test_pkr_store(m, nt, depth, splits):
+    n, k = 1024, 4096
+    w = (torch.randn(n, k, device=DEV) * 0.02).bfloat16()
+    x = torch.randn(m, k, device=DEV).bfloat16()
+    wp = ops.pack_weight(w)
+    ref_y = x.float() @ w.float().t()
+    if splits == 1:
+        out = torch.empty(m, n, device=DEV).bfloat16()
+        y = ops.pkr_gemm(x, wp, out=out, nt=nt, depth=depth).float()
+    else:
+        ws = torch.empty(splits * m * n, device=DEV)
+        ops.pkr_gemm(x, wp, ws=ws, splits=splits, nt=nt, depth=depth)
+        y = ws.view(splits, m, n).sum(0)
+    _close(y, ref_y, atol=3e-2, rtol=2e-2, msg="pkr store")
+
+
+@pytest.mark.parametrize("m", [1, 29, 64])
+@pytest.mark.parametrize("splits,nt", [(1, 2), (2, 4), (7, 2), (8, 1)])
+def test_pkr_residual_in_launch_reduce(m, splits, nt):
+    """residual += x W^T with the split-K slabs reduced by the last-arriving split:
+    correct, bit-identical across launches (split-order sum whoever arrives last),
+    and the tickets are left re-armed."""
+    n, k = 2048, 14336
+    w = (torch.randn(n, k, device=DEV) * 0.02).bfloat16()
+    x = torch.randn(m, k, device=DEV).bfloat16()
+    wp = ops.pack_weight(w)
+    res0 = torch.randn(m, n, device=DEV).bfloat16()
+    ws = torch.empty(splits * m * n, device=DEV)
+    tickets = torch.zeros(256, dtype=torch.int32, device=DEV)
+    outs = []
+    for _ in range(3):
+        res = res0.clone()
+        ops.pkr_gemm(x, wp, "resid", residual=res, ws=ws, tickets=tickets, splits=splits, nt=nt,
+                     depth=3 if nt == 2 else (4 if nt == 1 else 2))
+        outs.append(res)
+    torch.cuda.synchronize()
+    assert int(tickets.abs().sum().item()) == 0
+    _close(outs[0], res0.float() + x.float() @ w.float().t(), atol=5e-2, rtol=1e-2, msg="resid")
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+
+
+@pytest.mark.parametrize("m", [1, 20, 64])
+@pytest.mark.parametrize("nt,depth", [(2, 4), (4, 3)])
+def test_pkr_gate_up_silu_norm(m, nt, depth):
+    """RMSNorm (weight folded into W) + gate_up + SiLU-mul in one launch vs fp32."""
+    hidden, inter, eps = 4096, 1024, 1e-5
+    wg = (torch.randn(inter, hidden, device=DEV) * 0.02).bfloat16()
+    wu = (torch.randn(inter, hidden, device=DEV) * 0.02).bfloat16()
+    gamma = (1 + 0.1 * torch.randn(hidden, device=DEV)).bfloat16()
+    res = torch.randn(m, hidden, device=DEV).bfloat16()
+    xn = ref.rmsnorm(res.float(), gamma.float(), eps)
+    h_ref = torch.nn.functional.silu(xn @ wg.float().t()) * (xn @ wu.float().t())
+    wgu = (torch.cat([wg, wu]).float() * gamma.float()[None, :]).bfloat16()
+    wp = ops.pack_weight(ops.interleave_gate_up(wgu, nt // 2))
+    h = ops.pkr_gemm(res, wp, "silu", nt=nt, depth=depth, norm=True, eps=eps)
+    assert h.shape == (m, inter)
+    _close(h, h_ref, atol=3e-2, rtol=3e-2, msg="gate_up silu norm")
+
+
+def test_slab_rope_kv_residual_norm():
+    """slab_rope_kv with the residual row's RMS scale (fused decode layer)."""
+    nq, nkv, d = 8, 2, 128
+    t, bs, nblocks, splits, hidden, eps = 11, 16, 8, 2, 2048, 1e-5
+    cols = (nq + 2 * nkv) * d
+    parts = torch.randn(splits, t, cols, device=DEV)
+    res = torch.randn(t, hidden, device=DEV).bfloat16()
+    pos = torch.randint(0, 4000, (t,), device=DEV, dtype=torch.int32)
+    cs = ref.rope_cos_sin(d, 8192, 500000.0, None, DEV)
+    slots = torch.randperm(nblocks * bs, device=DEV)[:t].int()
+    k1, v1 = _alloc_cache(nblocks, nkv, bs, d)
+    k2, v2 = k1.clone(), v1.clone()
+    q_out = torch.zeros(t, nq * d, device=DEV).bfloat16()
+    ops.slab_rope_kv(parts.flatten(), splits, t, cols, q_out, pos, cs, slots, k1, v1, nq, nkv, d,
+                     residual=res, eps=eps)
+    r = torch.rsqrt(res.float().pow(2).mean(-1, keepdim=True) + eps)
+    qkv = (parts.sum(0) * r).bfloat16()
+    ref.rope_kv_write(qkv, pos, cs, slots, k2, v2, nq, nkv, d)
+    _close(q_out, qkv[:, : nq * d], atol=3e-2, rtol=2e-2, msg="q")
+    _close(k1, k2, atol=3e-2, rtol=2e-2, msg="k")
+    _close(v1, v2, atol=3e-2, rtol=2e-2, msg="v")
