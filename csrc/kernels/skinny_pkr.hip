@@ -251,6 +251,17 @@ __global__ __launch_bounds__(256) void skinny_pkr_kernel(PrArgs a) {
   }
 
   // ---- EPI_RESID ----------------------------------------------------------------
+  // the residual tile is read before the slab handshake so its latency overlaps it
+  float res_pre[MT][NT][4];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = min(16 * i + 4 * g + r, M - 1);
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+        res_pre[i][j][r] = bf16_to_f32(a.residual[(size_t)m * a.res_stride + n0 + 16 * j + l15]);
+    }
   if (gridDim.y > 1) {
     float* slab = a.ws + (size_t)s * M * N;
 #pragma unroll
@@ -301,8 +312,8 @@ __global__ __launch_bounds__(256) void skinny_pkr_kernel(PrArgs a) {
       if (m < M) {
 #pragma unroll
         for (int j = 0; j < NT; ++j) {
-          uint16_t* p = a.residual + (size_t)m * a.res_stride + n0 + 16 * j + l15;
-          *p = f32_to_bf16(bf16_to_f32(*p) + acc[i][j][r]);
+          a.residual[(size_t)m * a.res_stride + n0 + 16 * j + l15] =
+              f32_to_bf16(res_pre[i][j][r] + acc[i][j][r]);
         }
       }
     }

@@ -12,6 +12,7 @@ directly.  The same code runs the CPU backend through the fp32 reference ops.
 from __future__ import annotations
 
 import dataclasses
+import json
 import os
 from typing import List, Optional, Tuple
 
@@ -69,6 +70,13 @@ class LayerWeights:
     wo_pk: Optional[torch.Tensor] = None
     wgu_pk: Optional[torch.Tensor] = None
     wd_pk: Optional[torch.Tensor] = None
+    # fused decode layer (skinny_pkr.hip): QKV / gate_up packed with the input norms
+    # folded in (W diag(ln)), gate_up rows interleaved for the SiLU epilogue; o / down
+    # share the packed images above when present
+    fqkv: Optional[torch.Tensor] = None
+    fo: Optional[torch.Tensor] = None
+    fgu: Optional[torch.Tensor] = None
+    fd: Optional[torch.Tensor] = None
     # W4A16 (AWQ) projections by name ("qkv", "o", "gu", "down"), GPU only
     q4: Optional[dict] = None
 
@@ -97,6 +105,65 @@ PACKED_PLAN = {
     "lm": {1: (1, -3, 1), 8: (2, -3, 1), 16: (4, -3, 1), 32: (1, -4, 1), 64: (2, -4, 1)},
 }
 MAX_SPLITS = 4
+
+# Fused decode layer (csrc/kernels/skinny_pkr.hip), <= FUSED_ROWS rows, bf16, TP=1:
+# per layer four ring-pipelined packed GEMMs + RoPE/KV + attention, and no separate
+# norm / SiLU / residual-add launches:
+#   qkv   store -> split-K slabs; slab_rope_kv scales each row by its residual RMS
+#   o     resid -> residual += attn Wo^T (split-K reduced inside the launch)
+#   gu    silu + norm -> h = silu(g) * u of rmsnorm(residual) (ln2 folded into W)
+#   down  resid -> residual += h Wd^T
+# Per projection and row bucket: (nt, depth, splits).  fused_plan.json (written by
+# bench/pkr_sweep.py --plan-out from cold-cache sweeps on MI355X) overrides these.
+# Row limit of the fused layer: at 32-64 rows the ring kernels lose to the unfused
+# packed / hipBLASLt plan (50 sessions: 8.1 ms vs 5.7 ms per decode step)
+FUSED_ROWS = int(os.environ.get("FT_FUSED_ROWS", "16"))
+MAX_FUSED_SPLITS = 8
+FUSED_PLAN = {
+    "qkv": {1: (2, 3, 8), 8: (2, 3, 8), 16: (2, 3, 4), 32: (2, 3, 2), 64: (2, 3, 2)},
+    "o": {1: (1, 4, 1), 8: (1, 4, 1), 16: (1, 4, 1), 32: (1, 4, 2), 64: (1, 4, 2)},
+    "gu": {1: (4, 2, 1), 8: (4, 2, 1), 16: (4, 2, 1), 32: (4, 3, 1), 64: (4, 3, 1)},
+    "down": {1: (1, 4, 1), 8: (1, 4, 1), 16: (1, 4, 1), 32: (1, 4, 2), 64: (1, 4, 2)},
+}
+_SILU_CONFIGS = ((2, 2), (2, 3), (2, 4), (4, 2), (4, 3))
+_FUSED_PLAN_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "fused_plan.json")
+
+
+def load_fused_plan(path: str = _FUSED_PLAN_FILE):
+    """Overlays a measured plan {proj: {bucket: [nt, depth, splits]}} on FUSED_PLAN."""
+    if not os.path.exists(path):
+        return
+    with open(path) as f:
+        plan = json.load(f)
+    for proj, per in plan.items():
+        ok = _SILU_CONFIGS if proj == "gu" else [tuple(c) for c in ops.PKR_CONFIGS]
+        for b, c in per.items():
+            c = tuple(int(v) for v in c[:3])
+            if proj in FUSED_PLAN and int(b) in _M_BUCKETS and c[:2] in ok \
+                    and 1 <= c[2] <= MAX_FUSED_SPLITS:
+                FUSED_PLAN[proj][int(b)] = c
+
+
+load_fused_plan()
+
+
+def fused_cfg(proj: str, rows: int, n: int, k: int, nt_fixed: Optional[int] = None):
+    """(nt, depth, splits) for one fused-layer GEMM: the plan entry, unless the shape
+    rules it out (then one split, and nt 1 if the columns do not tile)."""
+    b = next(m for m in _M_BUCKETS if m >= rows)
+    nt, depth, sp = FUSED_PLAN[proj][b]
+    if nt_fixed is not None and nt != nt_fixed:  # gate_up: the packing fixes nt
+        nt, depth = nt_fixed, 2
+    if k % (64 * sp):
+        sp = 1
+    if n % (16 * nt):
+        nt, depth = 1, 2
+    return nt, depth, sp
+
+
+def _fold_norm(w: torch.Tensor, ln: torch.Tensor) -> torch.Tensor:
+    """W diag(ln): the RMSNorm weight moved onto the GEMM's K axis."""
+    return (w.float() * ln.float()[None, :]).to(w.dtype)
 
 # W4A16 decode GEMMs (csrc/kernels/w4a16.hip): (nt, splits) per projection and
 # row bucket, from cold-cache sweeps on MI355X (bench/w4_sweep.py, us at M = 1 /
@@ -168,6 +235,9 @@ class LlamaModel:
         if self.quant not in (None, "awq", "w4"):
             raise ValueError(f"unsupported quantization {quantization!r} (awq | w4)")
         self._w4_scratch: Optional[torch.Tensor] = None
+        self.fused = False
+        self.gu_nt = 2
+        self.tickets: Optional[torch.Tensor] = None
 
     # ------------------------------------------------------------------ weights
     def _set_layers(self, shards):
@@ -343,6 +413,37 @@ class LlamaModel:
             self.lm_head_pk = ops.pack_weight(self.lm_head)
         if use["o"] or use["down"] or use["qkv"] and L0.q4:
             self.ws = torch.empty(need_ws, dtype=torch.float32, device=self.device)
+        self._prepare_fused()
+
+    def _prepare_fused(self):
+        """Weights of the fused decode layer: QKV and gate_up packed with ln1 / ln2
+        folded in (the kernels scale by the row RMS only), gate_up interleaved for
+        the SiLU epilogue.  Above FUSED_ROWS rows the unfused layer runs; it keeps
+        its unfolded QKV / gate_up packs only where PACKED_PLAN uses them there."""
+        self.fused = False
+        cfg = self.cfg
+        H, I = cfg.hidden_size, cfg.intermediate_size
+        nqkv = (self.nq + 2 * self.nkv) * self.d
+        self.gu_nt = FUSED_PLAN["gu"][next(m for m in _M_BUCKETS if m >= FUSED_ROWS)][0]
+        if (self.quant or self.tp != 1 or os.environ.get("FT_FUSED_DECODE", "1") == "0"
+                or self.layers[0].wqkv is None or H % 64 or I % 64 or nqkv % 16
+                or I % (8 * self.gu_nt)):
+            return
+        for L in self.layers:
+            L.fqkv = ops.pack_weight(_fold_norm(L.wqkv, L.ln1))
+            L.fgu = ops.pack_weight(ops.interleave_gate_up(_fold_norm(L.wgu, L.ln2),
+                                                           self.gu_nt // 2))
+            L.fo = L.wo_pk if L.wo_pk is not None else ops.pack_weight(L.wo)
+            L.fd = L.wd_pk if L.wd_pk is not None else ops.pack_weight(L.wd)
+            if not any(b > FUSED_ROWS for b in PACKED_PLAN["qkv"]):
+                L.wqkv_pk = None
+            if not any(b > FUSED_ROWS for b in PACKED_PLAN["gu"]):
+                L.wgu_pk = None
+        need = MAX_FUSED_SPLITS * FUSED_ROWS * max(nqkv, H)
+        if self.ws is None or self.ws.numel() < need:
+            self.ws = torch.empty(need, dtype=torch.float32, device=self.device)
+        self.tickets = torch.zeros(max(4096, H // 16), dtype=torch.int32, device=self.device)
+        self.fused = True
 
     def _gemm(self, x: torch.Tensor, w: torch.Tensor, w_pk: Optional[torch.Tensor], proj: str):
         """bf16 y = x w^T: packed decode GEMM when the plan has a split-1 config."""
@@ -372,8 +473,64 @@ class LlamaModel:
                 for _ in range(self.cfg.num_layers)]
 
     # ------------------------------------------------------------------ forward
+    def _attention(self, qkv: torch.Tensor, meta: AttnMeta, kc, vc) -> torch.Tensor:
+        """Decode rows through the paged split-K kernel, prefill rows through the
+        varlen MFMA kernel; q is read from the RoPE'd qkv rows."""
+        t = qkv.shape[0]
+        nq, nkv, d = self.nq, self.nkv, self.d
+        attn = torch.empty(t, nq * d, dtype=qkv.dtype, device=qkv.device)
+        nd = meta.num_decode
+        if nd > 0:
+            ops.decode_attention(attn[:nd], qkv[:nd], kc, vc, meta.dec_block_tables,
+                                 meta.dec_seq_lens, meta.tmp_out, meta.tmp_ml, nq, nkv, d,
+                                 meta.max_splits, self.scale)
+        if t > nd:
+            ops.prefill_attention(attn[nd:], qkv[nd:], kc, vc, meta.block_tables, meta.seq_lens,
+                                  meta.q_start_loc, meta.tile_info, meta.num_tiles, nq, nkv, d,
+                                  self.scale)
+        return attn
+
+    def _forward_fused(self, input_ids: torch.Tensor, meta: AttnMeta, kv_caches) -> torch.Tensor:
+        """The fused decode layer (FUSED_PLAN): the residual stream is the GEMM input
+        and the in-place output; every norm rides in a GEMM or the RoPE kernel."""
+        cfg = self.cfg
+        eps = cfg.rms_norm_eps
+        nq, nkv, d = self.nq, self.nkv, self.d
+        t = input_ids.shape[0]
+        H, I = cfg.hidden_size, cfg.intermediate_size
+        nqkv = (nq + 2 * nkv) * d
+        residual = self.embed.index_select(0, input_ids)
+        cq = fused_cfg("qkv", t, nqkv, H)
+        co = fused_cfg("o", t, H, nq * d)
+        cg = fused_cfg("gu", t, 2 * I, H, nt_fixed=self.gu_nt)
+        cd = fused_cfg("down", t, H, I)
+        ws, tk = self.ws, self.tickets
+        for li, L in enumerate(self.layers):
+            kc, vc = kv_caches[li]
+            nt, dp, sp = cq
+            ops.pkr_gemm(residual, L.fqkv, "store", ws=ws, splits=sp, nt=nt, depth=dp)
+            qkv = torch.empty(t, nqkv, dtype=self.dtype, device=self.device)
+            ops.slab_rope_kv(ws, sp, t, nqkv, qkv, meta.positions, self.cos_sin,
+                             meta.slot_mapping, kc, vc, nq, nkv, d, residual=residual, eps=eps)
+            attn = self._attention(qkv, meta, kc, vc)
+            nt, dp, sp = co
+            ops.pkr_gemm(attn, L.fo, "resid", residual=residual, ws=ws, tickets=tk, splits=sp,
+                         nt=nt, depth=dp)
+            nt, dp, _ = cg
+            h = ops.pkr_gemm(residual, L.fgu, "silu", nt=nt, depth=dp, norm=True, eps=eps)
+            nt, dp, sp = cd
+            ops.pkr_gemm(h, L.fd, "resid", residual=residual, ws=ws, tickets=tk, splits=sp,
+                         nt=nt, depth=dp)
+        idx = meta.logits_indices
+        rows = residual.index_select(0, idx) if idx.numel() != t else residual
+        if rows.shape[0] == 0:
+            return rows
+        return ops.rmsnorm(rows, self.norm, eps)
+
     def forward(self, input_ids: torch.Tensor, meta: AttnMeta, kv_caches) -> torch.Tensor:
         """Returns the final-normed hidden rows at ``meta.logits_indices``."""
+        if self.fused and input_ids.shape[0] <= FUSED_ROWS:
+            return self._forward_fused(input_ids, meta, kv_caches)
         cfg = self.cfg
         eps = cfg.rms_norm_eps
         nq, nkv, d = self.nq, self.nkv, self.d
@@ -400,16 +557,7 @@ class LlamaModel:
                 qkv = self._proj(x, L, "qkv")
                 ops.rope_kv_write(qkv, meta.positions, self.cos_sin, meta.slot_mapping, kc, vc,
                                   nq, nkv, d)
-            attn = torch.empty(t, nq * d, dtype=qkv.dtype, device=qkv.device)
-            nd = meta.num_decode
-            if nd > 0:
-                ops.decode_attention(attn[:nd], qkv[:nd], kc, vc, meta.dec_block_tables,
-                                     meta.dec_seq_lens, meta.tmp_out, meta.tmp_ml, nq, nkv, d,
-                                     meta.max_splits, self.scale)
-            if t > nd:
-                ops.prefill_attention(attn[nd:], qkv[nd:], kc, vc, meta.block_tables, meta.seq_lens,
-                                      meta.q_start_loc, meta.tile_info, meta.num_tiles, nq, nkv, d,
-                                      self.scale)
+            attn = self._attention(qkv, meta, kc, vc)
             so = self._proj_slab(attn, L, "o")
             if so:
                 x = torch.empty(t, H, dtype=self.dtype, device=self.device)

@@ -24,7 +24,7 @@ def _prompts(n, lens, seed=0):
     return [rng.integers(0, 120000, l).tolist() for l in lens[:n]]
 
 
-@pytest.mark.parametrize("model,quant,T", [("tiny-gqa4", None, 40), ("tiny-2k", None, 40),
+@pytest.mark.parametrize("model,quant,T", [("tiny-gqa4", None, 40), ("tiny-2k", None, 40), ("tiny-2k", None, 7),
                                             ("tiny-2k", "w4", 40), ("tiny-2k", "w4", 100),
                                             ("tiny", "w4", 40)])
 def test_gpu_logits_match_cpu_reference(model, quant, T):
