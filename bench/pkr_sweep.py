@@ -57,23 +57,26 @@ def sweep_shape(n, k, epi, Ms, ws, tickets):
         for M in Ms:
             x, res = xs[M], ress[M]
             for sp in ((1,) if epi == "silu" else (1, 2, 4, 8)):
+              for wn in ((False, True) if M > 32 and n % (64 * nt) == 0 else (False,)):
                 if k % (64 * sp) or sp * M * n > ws.numel():
                     continue
 
-                def f(W, nt=nt, sp=sp, d=depth, x=x, res=res):
+                def f(W, nt=nt, sp=sp, d=depth, x=x, res=res, wn=wn):
                     if epi == "store":
-                        return lambda: ops.pkr_gemm(x, W, "store", ws=ws, splits=sp, nt=nt, depth=d)
+                        return lambda: ops.pkr_gemm(x, W, "store", ws=ws, splits=sp, nt=nt, depth=d,
+                                                    wn=wn)
                     if epi == "resid":
                         return lambda: ops.pkr_gemm(x, W, "resid", residual=res, ws=ws, tickets=tickets,
-                                                    splits=sp, nt=nt, depth=d)
-                    return lambda: ops.pkr_gemm(x, W, "silu", nt=nt, depth=d, norm=True, eps=1e-5)
+                                                    splits=sp, nt=nt, depth=d, wn=wn)
+                    return lambda: ops.pkr_gemm(x, W, "silu", nt=nt, depth=d, norm=True, eps=1e-5,
+                                                wn=wn)
                 err = 0.0
                 if epi != "silu":  # numerics of the GEMM part (slabs)
-                    ops.pkr_gemm(x, Wp[0], "store", ws=ws, splits=sp, nt=nt, depth=depth)
+                    ops.pkr_gemm(x, Wp[0], "store", ws=ws, splits=sp, nt=nt, depth=depth, wn=wn)
                     got = ws[: sp * M * n].view(sp, M, n).sum(0)
                     err = (got - F.linear(x, Ws[0]).float()).abs().max().item()
                 t = graph_time([f(Wp[i % ncopy]) for i in range(CALLS)])
-                rows[M].append((t, nt, depth, sp, err))
+                rows[M].append((t, nt, depth, sp, int(wn), err))
     del Ws, Wp
     torch.cuda.empty_cache()
     return bl, rows
@@ -89,7 +92,7 @@ def make_plan(results):
                 return sum(min((r[0] for r in rs if r[1] == nt), default=1e9) for rs in per.values())
             nt_best = min(nts, key=total)
             per = {M: [r for r in rs if r[1] == nt_best] for M, rs in per.items()}
-        plan[name] = {str(M): list(min(rs)[1:4]) for M, rs in per.items() if rs}
+        plan[name] = {str(M): list(min(rs)[1:5]) for M, rs in per.items() if rs}
     return plan
 
 
@@ -114,14 +117,14 @@ def main():
             rs = sorted(rows[M])
             print(f"{name} M={M} N={n} K={k} epi={epi}: hipblaslt {bl[M]:.2f} us "
                   f"({n * k * 2 / bl[M] / 1e3:.0f} GB/s)", flush=True)
-            for t, nt, depth, sp, err in rs[: a.top]:
-                print(f"   nt={nt} depth={depth} splits={sp}: {t:7.2f} us "
+            for t, nt, depth, sp, wn, err in rs[: a.top]:
+                print(f"   nt={nt} depth={depth} splits={sp} wn={wn}: {t:7.2f} us "
                       f"({n * k * 2 / t / 1e3:5.0f} GB/s) err={err:.4f}", flush=True)
-            bad = [r for r in rs if r[4] > 0.06]
+            bad = [r for r in rs if r[5] > 0.06]
             if bad:
                 print("   !!! numerics failures:", bad[:3], flush=True)
             summary.setdefault(name, {})[M] = {"hipblaslt_us": round(bl[M], 2),
-                                               "best": [round(rs[0][0], 2)] + list(rs[0][1:4])}
+                                               "best": [round(rs[0][0], 2)] + list(rs[0][1:5])}
     assert int(tickets.abs().sum().item()) == 0, "tickets not re-armed"
     print(json.dumps(summary))
     if a.plan_out:

@@ -63,7 +63,8 @@ int ft_skinny_gemm_pk(const void* x, int x_stride, int M, const void* wpk, int N
                       void* out, int out_stride, int splits, int nt, hipStream_t stream);
 int ft_pkr_gemm(const void* x, int x_stride, int M, const void* wpk, int N, int K, float* ws,
                 void* out, int out_stride, void* residual, int res_stride, int* tickets,
-                int splits, int nt, int depth, int epi, int norm, float eps, hipStream_t stream);
+                int splits, int nt, int depth, int epi, int norm, int wn, float eps,
+                hipStream_t stream);
 int ft_row_rmsnorm(const void* x, int x_stride, const float* ws, int splits, void* out,
                    int out_stride, void* residual, const void* w, int rows, int hidden, float eps,
                    hipStream_t stream);
@@ -403,7 +404,7 @@ void skinny_gemm(at::Tensor x, at::Tensor w, c10::optional<at::Tensor> out,
 void pkr_gemm(at::Tensor x, at::Tensor w, c10::optional<at::Tensor> out,
               c10::optional<at::Tensor> ws, c10::optional<at::Tensor> residual,
               c10::optional<at::Tensor> tickets, int64_t splits, int64_t nt, int64_t depth,
-              int64_t epi, bool norm, double eps) {
+              int64_t epi, bool norm, double eps, bool wn) {
   check_bf16(x, "x");
   check_bf16(w, "w");
   check_rows(x, "x");
@@ -443,7 +444,7 @@ void pkr_gemm(at::Tensor x, at::Tensor w, c10::optional<at::Tensor> out,
   }
   check_rc(ft_pkr_gemm(x.data_ptr(), (int)x.stride(0), M, w.data_ptr(), N, K, wsp, op, ostride, rp,
                        rstride, tp, (int)splits, (int)nt, (int)depth, (int)epi, norm ? 1 : 0,
-                       (float)eps, cur_stream()),
+                       wn ? 1 : 0, (float)eps, cur_stream()),
            "pkr_gemm");
 }
 
@@ -612,7 +613,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("pkr_gemm", &pkr_gemm, py::arg("x"), py::arg("w"), py::arg("out") = py::none(),
         py::arg("ws") = py::none(), py::arg("residual") = py::none(),
         py::arg("tickets") = py::none(), py::arg("splits") = 1, py::arg("nt") = 2,
-        py::arg("depth") = 3, py::arg("epi") = 0, py::arg("norm") = false, py::arg("eps") = 0.0);
+        py::arg("depth") = 3, py::arg("epi") = 0, py::arg("norm") = false, py::arg("eps") = 0.0,
+        py::arg("wn") = false);
   m.def("row_rmsnorm", &row_rmsnorm, py::arg("out"), py::arg("x") = py::none(),
         py::arg("ws") = py::none(), py::arg("splits") = 1, py::arg("residual") = py::none(),
         py::arg("w"), py::arg("rows"), py::arg("eps"));

@@ -29,6 +29,13 @@
 //              does not depend on arrival order), updates the residual and
 //              re-arms the ticket (cdna_hip_programming.md, "In-launch split-K
 //              reduction").  O and down projections need no separate add launch.
+//
+// WN (wave-split-N, for 33-64 rows): the K-split layout above makes every wave read
+// its own x fragments, so x leaves L2 (N / 16NT) * M * K * 2 bytes per launch --
+// at M = 64 four times the weight bytes of the O projection, and the kernel fell to
+// half of hipBLASLt.  With WN the 4 waves own 4 * NT adjacent column tiles and walk
+// the same k-steps, so one x fragment load serves the workgroup through L1 and no
+// LDS reduction is needed; every wave runs the epilogue of its own tile.
 #include "ft_common.h"
 
 namespace ft {
@@ -73,7 +80,7 @@ struct PrStage {
   uint4 x[MT][2];
 };
 
-template <int MT, int NT, int S, int EPI, bool NORM>
+template <int MT, int NT, int S, int EPI, bool NORM, bool WN>
 __global__ __launch_bounds__(256) void skinny_pkr_kernel(PrArgs a) {
   // waves 1..3 hand their partial tiles to wave 0 through LDS
   __shared__ float s_red[3][MT * NT * 4][64];
@@ -81,7 +88,8 @@ __global__ __launch_bounds__(256) void skinny_pkr_kernel(PrArgs a) {
   const int lane = lane_id(), wave = wave_id();
   const int l15 = lane & 15, g = lane >> 4;
   const int M = a.M, N = a.N;
-  const int n0 = blockIdx.x * (16 * NT);
+  const int tile = WN ? blockIdx.x * 4 + wave : blockIdx.x;  // 16*NT-column tile
+  const int n0 = tile * (16 * NT);
   const int s = blockIdx.y;
   const int kbeg = s * a.k_slice;
   const int ksteps_total = a.K >> 6;
@@ -108,10 +116,10 @@ __global__ __launch_bounds__(256) void skinny_pkr_kernel(PrArgs a) {
   }
 
   const int nsteps = a.k_slice >> 6;
-  const int my_steps = nsteps > wave ? (nsteps - wave + 3) >> 2 : 0;
+  const int my_steps = WN ? nsteps : nsteps > wave ? (nsteps - wave + 3) >> 2 : 0;
 
   auto load = [&](PrStage<MT, NT>& st, int t) {
-    const int ks = wave + 4 * t;  // k-step within this split
+    const int ks = WN ? t : wave + 4 * t;  // k-step within this split
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
       const uint16_t* p = wp[j] + (size_t)ks * 1024;
@@ -182,6 +190,10 @@ __global__ __launch_bounds__(256) void skinny_pkr_kernel(PrArgs a) {
       if (g == 0) s_ss[wave][i * 16 + l15] = v;
     }
   }
+  // WN: the wave's own sums of squares cover all of K; s_ss[wave] is written and
+  // read by this wave only (LDS ops of a wave complete in order)
+  if constexpr (WN) {
+  } else {
   if (wave > 0) {
 #pragma unroll
     for (int i = 0; i < MT; ++i)
@@ -201,11 +213,12 @@ __global__ __launch_bounds__(256) void skinny_pkr_kernel(PrArgs a) {
         const int reg = (i * NT + j) * 4 + r;
         acc[i][j][r] += s_red[0][reg][lane] + s_red[1][reg][lane] + s_red[2][reg][lane];
       }
+  }
 
   // C layout: col = lane & 15 (n), row = (lane >> 4) * 4 + r (m)
   if constexpr (EPI == kEpiSilu) {
     constexpr int NH = NT / 2;
-    const int c0 = blockIdx.x * (16 * NH);
+    const int c0 = tile * (16 * NH);
 #pragma unroll
     for (int i = 0; i < MT; ++i)
 #pragma unroll
@@ -214,7 +227,8 @@ __global__ __launch_bounds__(256) void skinny_pkr_kernel(PrArgs a) {
         float rs = 1.f;
         if constexpr (NORM) {
           const int q = i * 16 + 4 * g + r;
-          rs = rsqrtf((s_ss[0][q] + s_ss[1][q] + s_ss[2][q] + s_ss[3][q]) / (float)a.K + a.eps);
+          const float sq = WN ? s_ss[wave][q] : s_ss[0][q] + s_ss[1][q] + s_ss[2][q] + s_ss[3][q];
+          rs = rsqrtf(sq / (float)a.K + a.eps);
         }
         if (m < M) {
 #pragma unroll
@@ -280,7 +294,7 @@ __global__ __launch_bounds__(256) void skinny_pkr_kernel(PrArgs a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     int prev = 0;
     if (lane == 0)
-      prev = __hip_atomic_fetch_add(a.tickets + blockIdx.x, 1, __ATOMIC_RELAXED,
+      prev = __hip_atomic_fetch_add(a.tickets + tile, 1, __ATOMIC_RELAXED,
                                     __HIP_MEMORY_SCOPE_AGENT);
     prev = __shfl(prev, 0, 64);
     if (prev != (int)gridDim.y - 1) return;
@@ -302,7 +316,7 @@ __global__ __launch_bounds__(256) void skinny_pkr_kernel(PrArgs a) {
           for (int j = 0; j < NT; ++j) acc[i][j][r] += sl[(size_t)m * N + n0 + 16 * j + l15];
         }
     }
-    if (lane == 0) a.tickets[blockIdx.x] = 0;  // re-arm for the next launch
+    if (lane == 0) a.tickets[tile] = 0;  // re-arm for the next launch
   }
 #pragma unroll
   for (int i = 0; i < MT; ++i)
@@ -329,7 +343,7 @@ __global__ __launch_bounds__(256) void skinny_pkr_kernel(PrArgs a) {
 extern "C" int ft_pkr_gemm(const void* x, int x_stride, int M, const void* wpk, int N, int K,
                            float* ws, void* out, int out_stride, void* residual, int res_stride,
                            int* tickets, int splits, int nt, int depth, int epi, int norm,
-                           float eps, hipStream_t stream) {
+                           int wn, float eps, hipStream_t stream) {
   if (M <= 0) return 0;
   if (M > 64 || splits < 1 || splits > 64) return -1;
   if (N % (16 * nt) != 0) return -2;
@@ -341,16 +355,21 @@ extern "C" int ft_pkr_gemm(const void* x, int x_stride, int M, const void* wpk, 
     return -7;
   if (norm && epi != ft::kEpiSilu) return -8;
   const int mt = (M + 15) / 16;
+  if (wn && (N % (64 * nt) != 0 || mt < 3)) return -9;
   ft::PrArgs a{(const uint16_t*)x, (const uint16_t*)wpk, ws, (uint16_t*)out, (uint16_t*)residual,
                tickets, x_stride, M, K, N, K / splits, out_stride, res_stride, eps};
-  dim3 grid(N / (16 * nt), splits), block(256);
-#define FT_PR(MT_, NT_, S_, E_, N_)                                                          \
-  if (mt == MT_ && nt == NT_ && depth == S_ && epi == E_ && (norm != 0) == N_) {             \
-    hipLaunchKernelGGL((ft::skinny_pkr_kernel<MT_, NT_, S_, E_, N_>), grid, block, 0, stream, a); \
+  dim3 grid(N / (16 * nt) / (wn ? 4 : 1), splits), block(256);
+#define FT_PRW(MT_, NT_, S_, E_, N_, W_)                                                     \
+  if (mt == MT_ && nt == NT_ && depth == S_ && epi == E_ && (norm != 0) == N_ &&             \
+      (wn != 0) == W_) {                                                                     \
+    hipLaunchKernelGGL((ft::skinny_pkr_kernel<MT_, NT_, S_, E_, N_, W_>), grid, block, 0,     \
+                       stream, a);                                                           \
     return static_cast<int>(hipGetLastError());                                              \
   }
-#define FT_PR_MT(NT_, S_, E_, N_) \
-  FT_PR(1, NT_, S_, E_, N_) FT_PR(2, NT_, S_, E_, N_) FT_PR(3, NT_, S_, E_, N_) FT_PR(4, NT_, S_, E_, N_)
+#define FT_PR(MT_, NT_, S_, E_, N_) FT_PRW(MT_, NT_, S_, E_, N_, false)
+#define FT_PR_MT(NT_, S_, E_, N_)                                                   \
+  FT_PR(1, NT_, S_, E_, N_) FT_PR(2, NT_, S_, E_, N_) FT_PR(3, NT_, S_, E_, N_)     \
+  FT_PR(4, NT_, S_, E_, N_) FT_PRW(3, NT_, S_, E_, N_, true) FT_PRW(4, NT_, S_, E_, N_, true)
   // ring stages stay within ~192 VGPRs: S * (MT + NT) * 8 <= 192 at MT = 4
 #define FT_PR_PLAIN(NT_, S_) FT_PR_MT(NT_, S_, 0, false) FT_PR_MT(NT_, S_, 2, false)
 #define FT_PR_SILU(NT_, S_) FT_PR_MT(NT_, S_, 1, true)
@@ -370,5 +389,6 @@ extern "C" int ft_pkr_gemm(const void* x, int x_stride, int M, const void* wpk, 
 #undef FT_PR_PLAIN
 #undef FT_PR_MT
 #undef FT_PR
+#undef FT_PRW
   return -5;
 }

@@ -113,17 +113,24 @@ MAX_SPLITS = 4
 #   o     resid -> residual += attn Wo^T (split-K reduced inside the launch)
 #   gu    silu + norm -> h = silu(g) * u of rmsnorm(residual) (ln2 folded into W)
 #   down  resid -> residual += h Wd^T
-# Per projection and row bucket: (nt, depth, splits).  fused_plan.json (written by
-# bench/pkr_sweep.py --plan-out from cold-cache sweeps on MI355X) overrides these.
-# Row limit of the fused layer: at 32-64 rows the ring kernels lose to the unfused
-# packed / hipBLASLt plan (50 sessions: 8.1 ms vs 5.7 ms per decode step)
-FUSED_ROWS = int(os.environ.get("FT_FUSED_ROWS", "16"))
+# Per projection and row bucket: (nt, depth, splits, wn) -- wn: wave-split-N layout
+# (33-64 rows).  fused_plan.json (written by bench/pkr_sweep.py --plan-out from
+# cold-cache sweeps on MI355X) overrides these.
+# Row limit of the fused layer (decode step, Llama-3-8B, MI355X): 8 sessions 2.3k vs
+# 2.06k tok/s unfused, 32 sessions 4.52 vs 4.53 ms, 48 sessions 5.47 vs 5.54 ms; at
+# 49-64 rows (four 16-row m-tiles) the ring kernels lose (50 sessions 6.2 vs 5.7 ms)
+FUSED_ROWS = int(os.environ.get("FT_FUSED_ROWS", "48"))
 MAX_FUSED_SPLITS = 8
+_FUSED_BUCKETS = (1, 8, 16, 32, 48, 64)
 FUSED_PLAN = {
-    "qkv": {1: (2, 3, 8), 8: (2, 3, 8), 16: (2, 3, 4), 32: (2, 3, 2), 64: (2, 3, 2)},
-    "o": {1: (1, 4, 1), 8: (1, 4, 1), 16: (1, 4, 1), 32: (1, 4, 2), 64: (1, 4, 2)},
-    "gu": {1: (4, 2, 1), 8: (4, 2, 1), 16: (4, 2, 1), 32: (4, 3, 1), 64: (4, 3, 1)},
-    "down": {1: (1, 4, 1), 8: (1, 4, 1), 16: (1, 4, 1), 32: (1, 4, 2), 64: (1, 4, 2)},
+    "qkv": {1: (2, 3, 8, 0), 8: (2, 3, 8, 0), 16: (2, 3, 4, 0), 32: (2, 3, 2, 0),
+            48: (4, 2, 8, 1), 64: (4, 2, 8, 1)},
+    "o": {1: (1, 4, 1, 0), 8: (1, 4, 1, 0), 16: (1, 4, 1, 0), 32: (1, 4, 2, 0),
+          48: (1, 2, 1, 0), 64: (1, 2, 1, 0)},
+    "gu": {1: (2, 2, 1, 0), 8: (2, 4, 1, 0), 16: (2, 4, 1, 0), 32: (2, 4, 1, 0),
+           48: (2, 2, 1, 1), 64: (2, 2, 1, 1)},
+    "down": {1: (1, 4, 1, 0), 8: (1, 4, 1, 0), 16: (1, 4, 1, 0), 32: (1, 4, 2, 0),
+             48: (4, 2, 4, 0), 64: (4, 2, 4, 0)},
 }
 _SILU_CONFIGS = ((2, 2), (2, 3), (2, 4), (4, 2), (4, 3))
 _FUSED_PLAN_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "fused_plan.json")
@@ -138,27 +145,31 @@ def load_fused_plan(path: str = _FUSED_PLAN_FILE):
     for proj, per in plan.items():
         ok = _SILU_CONFIGS if proj == "gu" else [tuple(c) for c in ops.PKR_CONFIGS]
         for b, c in per.items():
-            c = tuple(int(v) for v in c[:3])
-            if proj in FUSED_PLAN and int(b) in _M_BUCKETS and c[:2] in ok \
-                    and 1 <= c[2] <= MAX_FUSED_SPLITS:
+            c = tuple(int(v) for v in c[:4]) + (0,) * (4 - len(c[:4]))
+            if proj in FUSED_PLAN and int(b) in _FUSED_BUCKETS and c[:2] in ok \
+                    and 1 <= c[2] <= MAX_FUSED_SPLITS and c[3] in (0, 1):
                 FUSED_PLAN[proj][int(b)] = c
 
 
 load_fused_plan()
 
 
+def fused_bucket(rows: int) -> int:
+    return next(m for m in _FUSED_BUCKETS if m >= rows)
+
+
 def fused_cfg(proj: str, rows: int, n: int, k: int, nt_fixed: Optional[int] = None):
-    """(nt, depth, splits) for one fused-layer GEMM: the plan entry, unless the shape
-    rules it out (then one split, and nt 1 if the columns do not tile)."""
-    b = next(m for m in _M_BUCKETS if m >= rows)
-    nt, depth, sp = FUSED_PLAN[proj][b]
+    """(nt, depth, splits, wn) for one fused-layer GEMM: the plan entry, unless the
+    shape rules it out (then one split, nt 1 if the columns do not tile, no wn)."""
+    nt, depth, sp, wn = FUSED_PLAN[proj][fused_bucket(rows)]
     if nt_fixed is not None and nt != nt_fixed:  # gate_up: the packing fixes nt
         nt, depth = nt_fixed, 2
     if k % (64 * sp):
         sp = 1
     if n % (16 * nt):
         nt, depth = 1, 2
-    return nt, depth, sp
+    wn = bool(wn) and rows > 32 and n % (64 * nt) == 0
+    return nt, depth, sp, wn
 
 
 def _fold_norm(w: torch.Tensor, ln: torch.Tensor) -> torch.Tensor:
@@ -424,7 +435,7 @@ class LlamaModel:
         cfg = self.cfg
         H, I = cfg.hidden_size, cfg.intermediate_size
         nqkv = (self.nq + 2 * self.nkv) * self.d
-        self.gu_nt = FUSED_PLAN["gu"][next(m for m in _M_BUCKETS if m >= FUSED_ROWS)][0]
+        self.gu_nt = FUSED_PLAN["gu"][fused_bucket(FUSED_ROWS)][0]
         if (self.quant or self.tp != 1 or os.environ.get("FT_FUSED_DECODE", "1") == "0"
                 or self.layers[0].wqkv is None or H % 64 or I % 64 or nqkv % 16
                 or I % (8 * self.gu_nt)):
@@ -507,20 +518,20 @@ class LlamaModel:
         ws, tk = self.ws, self.tickets
         for li, L in enumerate(self.layers):
             kc, vc = kv_caches[li]
-            nt, dp, sp = cq
-            ops.pkr_gemm(residual, L.fqkv, "store", ws=ws, splits=sp, nt=nt, depth=dp)
+            nt, dp, sp, wn = cq
+            ops.pkr_gemm(residual, L.fqkv, "store", ws=ws, splits=sp, nt=nt, depth=dp, wn=wn)
             qkv = torch.empty(t, nqkv, dtype=self.dtype, device=self.device)
             ops.slab_rope_kv(ws, sp, t, nqkv, qkv, meta.positions, self.cos_sin,
                              meta.slot_mapping, kc, vc, nq, nkv, d, residual=residual, eps=eps)
             attn = self._attention(qkv, meta, kc, vc)
-            nt, dp, sp = co
+            nt, dp, sp, wn = co
             ops.pkr_gemm(attn, L.fo, "resid", residual=residual, ws=ws, tickets=tk, splits=sp,
-                         nt=nt, depth=dp)
-            nt, dp, _ = cg
-            h = ops.pkr_gemm(residual, L.fgu, "silu", nt=nt, depth=dp, norm=True, eps=eps)
-            nt, dp, sp = cd
+                         nt=nt, depth=dp, wn=wn)
+            nt, dp, _, wn = cg
+            h = ops.pkr_gemm(residual, L.fgu, "silu", nt=nt, depth=dp, norm=True, eps=eps, wn=wn)
+            nt, dp, sp, wn = cd
             ops.pkr_gemm(h, L.fd, "resid", residual=residual, ws=ws, tickets=tk, splits=sp,
-                         nt=nt, depth=dp)
+                         nt=nt, depth=dp, wn=wn)
         idx = meta.logits_indices
         rows = residual.index_select(0, idx) if idx.numel() != t else residual
         if rows.shape[0] == 0:

@@ -319,16 +319,19 @@ def interleave_gate_up(w: torch.Tensor, nh: int) -> torch.Tensor:
 
 
 def pkr_gemm(x, w_pk, epi: str = "store", out=None, ws=None, residual=None, tickets=None,
-             splits: int = 1, nt: int = 2, depth: int = 3, norm: bool = False, eps: float = 0.0):
+             splits: int = 1, nt: int = 2, depth: int = 3, norm: bool = False, eps: float = 0.0,
+             wn: bool = False):
     """Ring-pipelined decode GEMM (M <= 64) on pack_weight() images.
 
     * ``store``: bf16 ``out`` (one split) or fp32 slabs [splits, M, N] in ``ws``.
     * ``silu``: w_pk packs interleave_gate_up(W_gu, nt // 2); returns h = silu(g) * u
       [M, N/2]; ``norm``: x rows RMS-normalised on the fly (norm weight folded into W).
     * ``resid``: ``residual`` += x w^T, split-K reduced inside the launch (``tickets``:
-      zeroed int32, >= N / (16 nt), left zeroed)."""
+      zeroed int32, >= N / (16 nt), left zeroed).
+    * ``wn``: wave-split-N layout for 33-64 rows (N % (64 nt) == 0): x fragments
+      shared by the workgroup's 4 waves through L1."""
     if epi == "silu" and out is None:
         out = torch.empty(x.shape[0], w_pk.shape[0] // 2, dtype=x.dtype, device=x.device)
     native().pkr_gemm(x, w_pk, out, ws, residual, tickets, splits, nt, depth, _PKR_EPI[epi],
-                      norm, eps)
+                      norm, eps, wn)
     return out

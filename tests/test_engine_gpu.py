@@ -24,14 +24,20 @@ def _prompts(n, lens, seed=0):
     return [rng.integers(0, 120000, l).tolist() for l in lens[:n]]
 
 
-@pytest.mark.parametrize("model,quant,T", [("tiny-gqa4", None, 40), ("tiny-2k", None, 40), ("tiny-2k", None, 7),
-                                            ("tiny-2k", "w4", 40), ("tiny-2k", "w4", 100),
-                                            ("tiny", "w4", 40)])
-def test_gpu_logits_match_cpu_reference(model, quant, T):
+@pytest.mark.parametrize("model,quant,T,fused_rows", [
+    ("tiny-gqa4", None, 40, None), ("tiny-2k", None, 40, None), ("tiny-2k", None, 7, None),
+    ("tiny-2k", None, 40, 64), ("tiny-2k", "w4", 40, None), ("tiny-2k", "w4", 100, None),
+    ("tiny", "w4", 40, None)])
+def test_gpu_logits_match_cpu_reference(model, quant, T, fused_rows, monkeypatch):
     """Full forward on GPU (bf16 HIP kernels; at hidden 2048 the down projection
     and LM head run on the packed-weight skinny GEMMs) vs CPU fp32 reference ops.
-    W4: <= 64 rows run the W4A16 kernels (o / down into split-K slabs), 100 rows
-    the dequantize + hipBLASLt path; the CPU side holds the dequantized weights."""
+    bf16 <= FUSED_ROWS rows: the fused decode layer (fused_rows=64 at 40 rows runs
+    the 48-row bucket, wave-split-N GEMMs).  W4: <= 64 rows run the W4A16 kernels
+    (o / down into split-K slabs), 100 rows the dequantize + hipBLASLt path; the CPU
+    side holds the dequantized weights."""
+    if fused_rows is not None:
+        from fasttalk_llm_microservice_amd.models import llama
+        monkeypatch.setattr(llama, "FUSED_ROWS", fused_rows)
     cfg = MODELS[model]
     # consistent=True: both draw the same unsharded weights on the host from one seed
     g = LlamaModel(cfg, torch.device("cuda"), torch.bfloat16, max_model_len=512,

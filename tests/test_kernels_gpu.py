@@ -429,7 +429,10 @@ def test_skinny_gemm_packed(m, n, k, splits, nt, u):
 @pytest.mark.parametrize("nt,depth", [(1, 4), (2, 3), (4, 3), (4, 2)])
 @pytest.mark.parametrize("m", [1, 13, 37, 64])
 @pytest.mark.parametrize("splits", [1, 4])
-def test_pkr_store(m, nt, depth, splits):
+@pytest.mark.parametrize("wn", [False, True])
+def test_pkr_store(m, nt, depth, splits, wn):
+    if wn and m <= 32:
+        pytest.skip("wave-split-N layout is for 33-64 rows")
     n, k = 1024, 4096
     w = (torch.randn(n, k, device=DEV) * 0.02).bfloat16()
     x = torch.randn(m, k, device=DEV).bfloat16()
@@ -437,20 +440,23 @@ def test_pkr_store(m, nt, depth, splits):
     ref_y = x.float() @ w.float().t()
     if splits == 1:
         out = torch.empty(m, n, device=DEV).bfloat16()
-        y = ops.pkr_gemm(x, wp, out=out, nt=nt, depth=depth).float()
+        y = ops.pkr_gemm(x, wp, out=out, nt=nt, depth=depth, wn=wn).float()
     else:
         ws = torch.empty(splits * m * n, device=DEV)
-        ops.pkr_gemm(x, wp, ws=ws, splits=splits, nt=nt, depth=depth)
+        ops.pkr_gemm(x, wp, ws=ws, splits=splits, nt=nt, depth=depth, wn=wn)
         y = ws.view(splits, m, n).sum(0)
     _close(y, ref_y, atol=3e-2, rtol=2e-2, msg="pkr store")
 
 
 @pytest.mark.parametrize("m", [1, 29, 64])
 @pytest.mark.parametrize("splits,nt", [(1, 2), (2, 4), (7, 2), (8, 1)])
-def test_pkr_residual_in_launch_reduce(m, splits, nt):
+@pytest.mark.parametrize("wn", [False, True])
+def test_pkr_residual_in_launch_reduce(m, splits, nt, wn):
     """residual += x W^T with the split-K slabs reduced by the last-arriving split:
     correct, bit-identical across launches (split-order sum whoever arrives last),
     and the tickets are left re-armed."""
+    if wn and m <= 32:
+        pytest.skip("wave-split-N layout is for 33-64 rows")
     n, k = 2048, 14336
     w = (torch.randn(n, k, device=DEV) * 0.02).bfloat16()
     x = torch.randn(m, k, device=DEV).bfloat16()
@@ -462,7 +468,7 @@ def test_pkr_residual_in_launch_reduce(m, splits, nt):
     for _ in range(3):
         res = res0.clone()
         ops.pkr_gemm(x, wp, "resid", residual=res, ws=ws, tickets=tickets, splits=splits, nt=nt,
-                     depth=3 if nt == 2 else (4 if nt == 1 else 2))
+                     depth=3 if nt == 2 else (4 if nt == 1 else 2), wn=wn)
         outs.append(res)
     torch.cuda.synchronize()
     assert int(tickets.abs().sum().item()) == 0
@@ -471,9 +477,12 @@ def test_pkr_residual_in_launch_reduce(m, splits, nt):
 
 
 @pytest.mark.parametrize("m", [1, 20, 64])
-@pytest.mark.parametrize("nt,depth", [(2, 4), (4, 3)])
-def test_pkr_gate_up_silu_norm(m, nt, depth):
+@pytest.mark.parametrize("nt,depth,wn", [(2, 4, False), (4, 3, False), (2, 3, True),
+                                         (4, 2, True)])
+def test_pkr_gate_up_silu_norm(m, nt, depth, wn):
     """RMSNorm (weight folded into W) + gate_up + SiLU-mul in one launch vs fp32."""
+    if wn and m <= 32:
+        pytest.skip("wave-split-N layout is for 33-64 rows")
     hidden, inter, eps = 4096, 1024, 1e-5
     wg = (torch.randn(inter, hidden, device=DEV) * 0.02).bfloat16()
     wu = (torch.randn(inter, hidden, device=DEV) * 0.02).bfloat16()
@@ -483,7 +492,7 @@ def test_pkr_gate_up_silu_norm(m, nt, depth):
     h_ref = torch.nn.functional.silu(xn @ wg.float().t()) * (xn @ wu.float().t())
     wgu = (torch.cat([wg, wu]).float() * gamma.float()[None, :]).bfloat16()
     wp = ops.pack_weight(ops.interleave_gate_up(wgu, nt // 2))
-    h = ops.pkr_gemm(res, wp, "silu", nt=nt, depth=depth, norm=True, eps=eps)
+    h = ops.pkr_gemm(res, wp, "silu", nt=nt, depth=depth, norm=True, eps=eps, wn=wn)
     assert h.shape == (m, inter)
     _close(h, h_ref, atol=3e-2, rtol=3e-2, msg="gate_up silu norm")
 
