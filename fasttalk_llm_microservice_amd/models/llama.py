@@ -106,6 +106,22 @@ PACKED_PLAN = {
 }
 MAX_SPLITS = 4
 
+
+def _overlay_packed_plan(spec: str):
+    """FT_PACKED_PLAN='{"qkv": {"64": [4, -3, 2]}}' overlays PACKED_PLAN entries
+    (A/B tuning on the GPU box without code edits); [] removes a bucket."""
+    for proj, per in json.loads(spec).items():
+        for b, c in per.items():
+            if proj in PACKED_PLAN and int(b) in (1, 8, 16, 32, 64):
+                if c:
+                    PACKED_PLAN[proj][int(b)] = tuple(int(v) for v in c[:3])
+                else:
+                    PACKED_PLAN[proj].pop(int(b), None)
+
+
+if os.environ.get("FT_PACKED_PLAN"):
+    _overlay_packed_plan(os.environ["FT_PACKED_PLAN"])
+
 # Fused decode layer (csrc/kernels/skinny_pkr.hip), <= FUSED_ROWS rows, bf16, TP=1:
 # per layer four ring-pipelined packed GEMMs + RoPE/KV + attention, and no separate
 # norm / SiLU / residual-add launches:
@@ -383,8 +399,10 @@ class LlamaModel:
         """Split-K projection into self.ws fp32 slabs; returns the split count (0: not taken)."""
         q = L.q4.get(proj) if L.q4 else None
         if q is None:
-            if proj == "qkv":  # bf16 qkv stores bf16 (its plan has no split-K)
-                return 0
+            if proj == "qkv":  # bf16 qkv: split-K slabs only where its plan splits K
+                c = packed_cfg(proj, x.shape[0])
+                if c is None or c[2] == 1:
+                    return 0
             return self._gemm_slab(x, getattr(L, _ATTR[proj] + "_pk"), proj)
         if self.ws is None or x.shape[0] > W4_ROWS:
             return 0
@@ -404,6 +422,11 @@ class LlamaModel:
         slab_ok = self.tp == 1 and H % 2048 == 0
         use = {}
         need_ws = MAX_SPLITS * PACKED_ROWS * H
+        for proj, attr in _ATTR.items():  # split-K slabs of every planned config
+            w = getattr(L0, attr)
+            if w is not None:
+                need_ws = max(need_ws, max((sp * b * w.shape[0] for b, (_, _, sp)
+                                            in PACKED_PLAN[proj].items()), default=0))
         for proj, attr in _ATTR.items():
             w = getattr(L0, attr)
             if w is None:  # W4: the slab path depends on the shape rules only
