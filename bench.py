@@ -101,9 +101,18 @@ def main():
     import torch
     import torch.distributed as dist
 
-    torch.cuda.set_device(local_rank)
+    # FT_BENCH_SHARED_GPU=1: rehearse the N-rank DP path with every rank on one
+    # GPU (ranks map round-robin onto the visible devices, gloo instead of RCCL,
+    # which refuses two ranks on one device); size ENGINE_GPU_MEMORY_UTILIZATION
+    # to 1/N then.  The driver's multi-GPU runs leave it unset.
+    shared = os.environ.get("FT_BENCH_SHARED_GPU", "0") == "1"
+    dev_idx = local_rank % max(1, torch.cuda.device_count()) if shared else local_rank
+    torch.cuda.set_device(dev_idx)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
+        if shared:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{dev_idx}"))
     from app.core.websocket_server_vllm import WebSocketLLMServer
     from app.server.asgi_aiohttp import AiohttpASGIServer
     from app.utils.config import Config
