@@ -10,7 +10,8 @@
 //     made monotonic); a register-cached variant spilled (128-VGPR cap at 1024
 //     threads) and was slower.
 //   * greedy: one pass, argmax (lowest id on ties).
-//   * top-k: 16-step bisection on the 16-bit key (count >= k).
+//   * top-k: 4-ary search on the 16-bit key (count >= k), 8 passes (was a
+//     16-pass bisection).
 //   * sampling: inverse CDF in a fixed (thread, slot) order -- one exp pass
 //     gives per-thread masses, a block scan locates the thread holding the
 //     target mass, that thread walks its 16 chunks.
@@ -51,6 +52,7 @@ struct SampShared {
   int i[kSampWaves];
   uint32_t u[kSampWaves];
   float scan[kSampWaves];
+  int i3[3][kSampWaves];
   int winner;
   int found;
 };
@@ -76,6 +78,30 @@ __device__ __forceinline__ int block_sum_i(int v, SampShared& sh) {
 #pragma unroll
   for (int w = 0; w < kSampWaves; ++w) t += sh.i[w];
   return t;
+}
+
+// three block sums behind one pair of barriers
+__device__ __forceinline__ void block_sum_i3(int& a, int& b, int& c, SampShared& sh) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    a += __shfl_xor(a, o, 64);
+    b += __shfl_xor(b, o, 64);
+    c += __shfl_xor(c, o, 64);
+  }
+  __syncthreads();
+  if (lane_id() == 0) {
+    sh.i3[0][wave_id()] = a;
+    sh.i3[1][wave_id()] = b;
+    sh.i3[2][wave_id()] = c;
+  }
+  __syncthreads();
+  a = b = c = 0;
+#pragma unroll
+  for (int w = 0; w < kSampWaves; ++w) {
+    a += sh.i3[0][w];
+    b += sh.i3[1][w];
+    c += sh.i3[2][w];
+  }
 }
 
 // max key, lowest index on ties
@@ -195,23 +221,29 @@ __global__ __launch_bounds__(kSampThreads) void sample_kernel(
   const float M = key_to_f32(bestk);
   const float cexp = 1.4426950408889634f / temp;  // exp(z) = exp2((x - M) * cexp)
 
-  // ---- top-k: 16-step bisection on the key ------------------------------------------
+  // ---- top-k: 4-ary search on the 16-bit key (2 bits per pass, 8 passes) -------------
+  // invariant: count(key >= lo) >= k and the answer -- the largest t with
+  // count(key >= t) >= k -- lies in [lo, lo + 4 << shift)
   uint32_t thr = kNegInfKey + 1u;  // keep keys >= thr (drops masked / -inf)
   const int k = top_k[row];
   if (k > 0 && k < vocab) {
-    uint32_t lo = 0u, hi = 0x10000u;
-    while (hi - lo > 1u) {
-      const uint32_t mid = (lo + hi) >> 1;
-      int cnt = 0;
+    uint32_t lo = 0u;
+    for (int shift = 14; shift >= 0; shift -= 2) {
+      const uint32_t t1 = lo + (1u << shift), t2 = lo + (2u << shift), t3 = lo + (3u << shift);
+      int c1 = 0, c2 = 0, c3 = 0;
 #pragma unroll 8
       for (int c = 0; c < kChunks; ++c) {
         uint32_t key[8];
         load_keys8<T>(x, mrow, chunk_base(c), vocab, key);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) cnt += key[j] >= mid ? 1 : 0;
+        for (int j = 0; j < 8; ++j) {
+          c1 += key[j] >= t1 ? 1 : 0;
+          c2 += key[j] >= t2 ? 1 : 0;
+          c3 += key[j] >= t3 ? 1 : 0;
+        }
       }
-      cnt = block_sum_i(cnt, sh);
-      if (cnt >= k) lo = mid; else hi = mid;
+      block_sum_i3(c1, c2, c3, sh);
+      lo = (c3 >= k) ? t3 : (c2 >= k) ? t2 : (c1 >= k) ? t1 : lo;
     }
     if (lo > thr) thr = lo;
   }

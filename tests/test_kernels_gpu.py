@@ -192,6 +192,21 @@ def test_sample_topk_membership():
     assert all(lf[i, out[i]].item() >= kth[i].item() for i in range(64))
 
 
+@pytest.mark.parametrize("kk", [3, 40])
+def test_sample_topk_exact_set(kk):
+    """At a huge temperature the kept set is drawn ~uniformly: over many seeds
+    every one of the k largest logits (distinct values) must show up and no other
+    id, so the top-k threshold search is exact, not just conservative."""
+    b, v = 512, 128256
+    base = torch.randn(v) * 0.5
+    top = torch.randperm(v)[:kk]
+    base[top] = 4.0 + 0.0625 * torch.arange(kk, dtype=torch.float32)  # exact in bf16
+    logits = base.to(DEV).bfloat16().unsqueeze(0).repeat(b, 1)
+    t, p, k, s, st = _sp(b, 1e4, 1.0, kk)
+    out = set(ops.sample(logits, t, p, k, s, st).long().cpu().tolist())
+    assert out == set(top.tolist())
+
+
 def test_sample_topp_membership():
     logits = torch.randn(64, 32000, device=DEV) * 4
     t, p, k, s, st = _sp(64, 0.7, 0.5, 0)
