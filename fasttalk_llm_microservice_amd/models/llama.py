@@ -135,8 +135,10 @@ if os.environ.get("FT_PACKED_PLAN"):
 # cold-cache sweeps on MI355X) overrides these.
 # Row limit of the fused layer (decode step, Llama-3-8B, MI355X): 8 sessions 2.3k vs
 # 2.06k tok/s unfused, 32 sessions 4.52 vs 4.53 ms, 48 sessions 5.47 vs 5.54 ms; at
-# 49-64 rows (four 16-row m-tiles) the ring kernels lose (50 sessions 6.2 vs 5.7 ms)
-FUSED_ROWS = int(os.environ.get("FT_FUSED_ROWS", "48"))
+# 49-64 rows (four 16-row m-tiles) the ring kernels lose (50 sessions 6.2 vs 5.7 ms).
+# Since gate_up at 33-64 rows runs as split-K slabs + slab_silu, the unfused layer
+# also wins at 33-48 rows (40 sequences: 5.15 vs 5.45 ms/step), so the limit is 32.
+FUSED_ROWS = int(os.environ.get("FT_FUSED_ROWS", "32"))
 MAX_FUSED_SPLITS = 8
 _FUSED_BUCKETS = (1, 8, 16, 32, 48, 64)
 FUSED_PLAN = {
