@@ -15,12 +15,24 @@ Extras the WS server uses:
   assistant text was detokenized (re-tokenizing it would not round-trip);
 * token-aware history truncation to ``max_model_len - max_tokens``
   (Appendix D Q17): the oldest non-system messages are dropped first.
+* history window with hysteresis: once ``ConversationManager`` starts trimming
+  to ``max_history_length`` (reference ``conversation_manager.py:34-53``) the
+  API history slides by one message per message added, which would change the
+  token prefix right after the system block on EVERY turn and defeat the
+  prefix cache.  The engine therefore renders a window that is always a suffix
+  of the API history (the model never sees more than the reference would) and,
+  when the API drops a message the window still holds, cuts the window back to
+  ``ENGINE_HISTORY_KEEP`` (fraction of the cap, default 0.5) in one go, so the
+  prefix stays stable for the next ~cap/4 turns.  The kept size is jittered per
+  session (down by up to ``ENGINE_HISTORY_JITTER`` of the cap, default 0.3), so
+  sessions that reach the cap on the same turn cut again on different turns.
 """
 from __future__ import annotations
 
 import asyncio
 import hashlib
 import logging
+import os
 import threading
 import time
 from typing import Any, AsyncIterator, Dict, Iterator, List, Optional
@@ -88,10 +100,11 @@ def _fingerprint(messages: List[Dict[str, Any]]) -> List[str]:
 
 
 class _SessionTokens:
-    __slots__ = ("fps", "prompt_ids", "gen_ids", "reply_fp", "tools_fp")
+    __slots__ = ("fps", "head", "prompt_ids", "gen_ids", "reply_fp", "tools_fp")
 
     def __init__(self):
-        self.fps: List[str] = []
+        self.fps: List[str] = []          # messages of the engine window (rendered)
+        self.head = 0                     # 1 when fps[0] is the system message
         self.prompt_ids: List[int] = []
         self.gen_ids: List[int] = []
         self.reply_fp: Optional[str] = None
@@ -124,6 +137,9 @@ class NativeHandler:
         self._sessions: Dict[str, _SessionTokens] = {}
         self._lock = threading.Lock()
         self._seq = 0
+        self.history_cap = int(getattr(config, "max_history_length", 0) or 0)
+        self.keep_frac = float(os.environ.get("ENGINE_HISTORY_KEEP", "0.5"))
+        self.jitter_frac = float(os.environ.get("ENGINE_HISTORY_JITTER", "0.3"))
 
     # ------------------------------------------------------------------ health / info
     def check_connection(self) -> bool:
@@ -146,36 +162,93 @@ class NativeHandler:
             self._sessions.pop(session_id, None)
 
     # ------------------------------------------------------------------ prompt building
+    def _window_limit(self, session_id: Optional[str]) -> int:
+        """Most non-system messages the engine window may hold (0: no count cap):
+        what ConversationManager keeps (cap - 1 besides the system prompt)."""
+        cap = self.history_cap
+        return cap - 1 if cap > 2 else 0
+
+    def _keep(self, limit: int, session_id: Optional[str]) -> int:
+        """Messages a cut window keeps: ENGINE_HISTORY_KEEP of the limit, minus a
+        per-session jitter of up to ENGINE_HISTORY_JITTER of it, so sessions that
+        hit the cap on the same turn cut again on different turns afterwards."""
+        keep = self.keep_frac * limit
+        span = int(self.jitter_frac * limit)
+        if span > 0 and session_id:
+            h = int(hashlib.blake2b(str(session_id).encode(), digest_size=4).hexdigest(), 16)
+            keep -= h % (span + 1)
+        return max(1, min(limit - 1, int(round(keep))))
+
+    def _cut_window(self, msgs: List[Dict[str, Any]], head: int, session_id: Optional[str],
+                    at_cap: bool = False):
+        """Drops the oldest non-system messages down to the keep size when the
+        body exceeds the window limit (or reaches it, ``at_cap``: the API history is
+        trimming and no longer continues the previous window); the window starts
+        at a user turn."""
+        limit = self._window_limit(session_id)
+        body = len(msgs) - head
+        if not limit or body < limit or (body == limit and not at_cap):
+            return msgs
+        keep = self._keep(limit, session_id)
+        start = len(msgs) - keep
+        while start < len(msgs) - 1 and msgs[start].get("role") != "user":
+            start += 1
+        return msgs[:head] + msgs[start:]
+
+    @staticmethod
+    def _find_window(fps: List[str], head: int, prev: List[str], prev_head: int) -> int:
+        """Index j such that the previous engine window (system + body) continues
+        inside the new history at body offset j with new messages after it; -1 if
+        it does not (history edited, or the API dropped part of the window)."""
+        if head != prev_head or (head and fps[0] != prev[0]):
+            return -1
+        body, pbody = fps[head:], prev[prev_head:]
+        n = len(pbody)
+        for j in range(0, len(body) - n):
+            if body[j:j + n] == pbody:
+                return j
+        return -1
+
     def build_prompt(self, messages: List[Dict[str, Any]], max_tokens: int,
                      session_id: Optional[str] = None, tools=None) -> List[int]:
         budget = max(16, self.max_model_len - max(1, max_tokens) - 1)
         msgs = list(messages)
+        head = 1 if msgs and msgs[0].get("role") == "system" else 0
         fps = _fingerprint(msgs)
         tfp = _tools_fp(tools)
         st = self._sessions.get(session_id) if session_id else None
         ids: Optional[List[int]] = None
         if st is not None and st.reply_fp is not None and st.tools_fp == tfp:
             prev = st.fps + [st.reply_fp]
-            if len(fps) > len(prev) and fps[: len(prev)] == prev:
+            j = self._find_window(fps, head, prev, st.head)
+            n_new = len(msgs) - head - j - (len(prev) - st.head)
+            limit = self._window_limit(session_id)
+            if j >= 0 and (not limit or len(prev) - st.head + n_new <= limit):
                 ids = st.prompt_ids + st.gen_ids + [self.tokenizer.eot_id]
-                for m in msgs[len(prev):]:
+                for m in msgs[len(msgs) - n_new:]:
                     ids += self.template.message_ids(m)
                 ids += self.template.generation_prompt()
-        if ids is None or len(ids) > budget:
+                msgs = msgs[:head] + msgs[head + j:]
+                fps = fps[:head] + fps[head + j:]
+                if len(ids) > budget:
+                    ids = None
+        if ids is None:
+            msgs = self._cut_window(msgs, head, session_id, at_cap=st is not None)
             ids = self.template.render(msgs, tools=tools)
-            # token-aware truncation: drop the oldest non-system messages
-            while len(ids) > budget and len(msgs) > 1:
-                drop = 1 if msgs[0].get("role") == "system" else 0
-                if drop >= len(msgs) - 1:
-                    break
-                msgs.pop(drop)
-                ids = self.template.render(msgs, tools=tools)
+            if len(ids) > budget:
+                # token-aware truncation: drop the oldest non-system messages, down to
+                # 3/4 of the budget so the next turns extend the prefix again
+                target = max(16, (3 * budget) // 4)
+                while len(ids) > target and len(msgs) > head + 1:
+                    msgs.pop(head)
+                    ids = self.template.render(msgs, tools=tools)
             fps = _fingerprint(msgs)
             if len(ids) > budget:
                 ids = ids[-budget:]
         if session_id is not None:
             st = self._sessions.setdefault(session_id, _SessionTokens())
-            st.fps, st.prompt_ids, st.gen_ids, st.reply_fp, st.tools_fp = fps, ids, [], None, tfp
+            st.fps, st.head, st.prompt_ids, st.gen_ids, st.reply_fp, st.tools_fp = \
+                fps, head, ids, [], None, tfp
         return ids
 
     def _remember_reply(self, session_id: Optional[str], gen_ids: List[int], text: str):

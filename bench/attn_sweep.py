@@ -1,7 +1,11 @@
-"""Decode-attention split sweep: us/call and effective KV bandwidth of the paged
-decode kernel at Llama-3-8B head shapes over (batch, context, splits).
+"""Decode-attention sweep: us/call and effective KV bandwidth of the paged MFMA
+decode kernel (csrc/kernels/attn_decode.hip) at Llama-3-8B head shapes over
+(batch, context).  Lengths are ragged (uniform in [ctx/2, ctx], first = ctx)
+unless --uniform; KV blocks are scattered (random permutation), like a pool
+that has served many sessions.
 
-python bench/attn_sweep.py [--nq 32 --nkv 8]
+python bench/attn_sweep.py [--nq 32 --nkv 8] [--uniform]
+FT_DECODE_RING=2|3|4 selects the kernel's register-ring depth (default 3).
 """
 from __future__ import annotations
 
@@ -18,40 +22,41 @@ import torch  # noqa: E402
 from fasttalk_llm_microservice_amd import ops  # noqa: E402
 from kernel_bench import timeit  # noqa: E402
 
+SHAPES = [(1, 512), (1, 8192), (8, 2048), (50, 640), (50, 3000), (50, 4500), (64, 1024),
+          (64, 4096), (256, 1024)]
+
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--nq", type=int, default=32)
     ap.add_argument("--nkv", type=int, default=8)
     ap.add_argument("--d", type=int, default=128)
+    ap.add_argument("--uniform", action="store_true")
     a = ap.parse_args()
     nq, nkv, d, bs = a.nq, a.nkv, a.d, 16
     dev = "cuda"
-    res = []
-    for B, ctx in [(1, 512), (1, 8192), (8, 2048), (50, 640), (64, 1024), (64, 4096), (256, 1024)]:
+    for B, ctx in SHAPES:
         nblk = math.ceil(ctx / bs)
         nblocks = B * nblk + 8
         kc = torch.randn(nblocks, nkv, bs, d, device=dev).bfloat16()
-        vc = torch.randn(nblocks, nkv, bs, d, device=dev).bfloat16()
+        vc = torch.randn(nblocks, nkv, d, bs, device=dev).bfloat16()
         bt = torch.randperm(nblocks, device=dev)[: B * nblk].int().view(B, nblk)
-        sl = torch.randint(max(1, ctx // 2), ctx + 1, (B,), dtype=torch.int32, device=dev)
-        sl[0] = ctx
+        if a.uniform:
+            sl = torch.full((B,), ctx, dtype=torch.int32, device=dev)
+        else:
+            sl = torch.randint(max(1, ctx // 2), ctx + 1, (B,), dtype=torch.int32, device=dev)
+            sl[0] = ctx
         q = torch.randn(B, (nq + 2 * nkv) * d, device=dev).bfloat16()
         out = torch.empty(B, nq * d, device=dev).bfloat16()
-        tmp_o = torch.empty(B * nq * 64 * d, device=dev)
-        tmp_ml = torch.empty(B * nq * 64 * 2, device=dev)
+        n_out, n_ml = ops.decode_workspace(B, nq, nkv, d)
+        tmp_o = torch.empty(n_out, device=dev)
+        tmp_ml = torch.empty(n_ml, device=dev)
         nbytes = int(sl.sum().item()) * nkv * d * 2 * 2
-        row = {"B": B, "ctx": ctx, "policy": ops.decode_splits(B, nkv)}
-        for s in (1, 2, 4, 8, 16, 32, 64):
-            us = timeit(lambda: ops.decode_attention(out, q, kc, vc, bt, sl, tmp_o, tmp_ml, nq, nkv, d,
-                                                     s, d ** -0.5), iters=100, warmup=10)
-            row[f"s{s}"] = round(us, 2)
-        best = min((row[f"s{s}"], s) for s in (1, 2, 4, 8, 16, 32, 64))
-        row["best"] = best[1]
-        row["best_GBps"] = round(nbytes / best[0] / 1e3, 1)
-        row["policy_GBps"] = round(nbytes / row[f"s{row['policy']}"] / 1e3, 1)
-        print(json.dumps(row), flush=True)
-        res.append(row)
+        us = timeit(lambda: ops.decode_attention(out, q, kc, vc, bt, sl, tmp_o, tmp_ml, nq, nkv, d,
+                                                 d ** -0.5), iters=100, warmup=10)
+        print(json.dumps({"B": B, "ctx": ctx, "uniform": a.uniform,
+                          "ring": int(os.environ.get("FT_DECODE_RING", "3")),
+                          "us": round(us, 2), "GBps": round(nbytes / us / 1e3, 1)}), flush=True)
         del kc, vc
 
 

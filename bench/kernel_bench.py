@@ -78,18 +78,17 @@ def main():
     nblk_per = math.ceil(ctx / bs)
     nblocks = B * nblk_per + 8
     kc = torch.randn(nblocks, nkv, bs, d, device=dev).bfloat16()
-    vc = torch.randn(nblocks, nkv, bs, d, device=dev).bfloat16()
+    vc = torch.randn(nblocks, nkv, d, bs, device=dev).bfloat16()   # transposed V blocks
     bt = torch.randperm(nblocks, device=dev)[: B * nblk_per].int().view(B, nblk_per)
     sl = torch.full((B,), ctx, dtype=torch.int32, device=dev)
     q = torch.randn(B, (nq + 2 * nkv) * d, device=dev).bfloat16()
     out = torch.empty(B, nq * d, device=dev).bfloat16()
-    part = ops.decode_partition_size()
-    ms = 1 << max(0, (math.ceil(ctx / part) - 1).bit_length())
-    tmp_o = torch.empty(B * nq * 64 * d, device=dev)
-    tmp_ml = torch.empty(B * nq * 64 * 2, device=dev)
+    n_out, n_ml = ops.decode_workspace(B, nq, nkv, d)
+    tmp_o = torch.empty(n_out, device=dev)
+    tmp_ml = torch.empty(n_ml, device=dev)
     if not a.only or "attn" in a.only:
         rep(f"decode_attn B={B} ctx={ctx}",
-            timeit(lambda: ops.decode_attention(out, q, kc, vc, bt, sl, tmp_o, tmp_ml, nq, nkv, d, ms,
+            timeit(lambda: ops.decode_attention(out, q, kc, vc, bt, sl, tmp_o, tmp_ml, nq, nkv, d,
                                                 d ** -0.5)), B * ctx * nkv * d * 2 * 2)
     slots = torch.arange(B, dtype=torch.int32, device=dev)
     pos = torch.full((B,), ctx - 1, dtype=torch.int32, device=dev)

@@ -17,12 +17,13 @@ int ft_silu_mul(void* out, const void* gu, int rows, int inter, hipStream_t stre
 int ft_rope_kv_write(void* qkv, int qkv_stride, const int* positions, const float* cos_sin,
                      const int* slot_mapping, void* k_cache, void* v_cache, int tokens, int nq,
                      int nkv, int head_dim, int block_size, hipStream_t stream);
-int ft_decode_partition_size();
+int ft_decode_waves();
+int ft_decode_max_batch();
 int ft_paged_decode_attention(void* out, int out_stride, float* tmp_out, float* tmp_ml,
                               const void* q, int q_stride, const void* k_cache,
                               const void* v_cache, const int* block_tables, int bt_stride,
                               const int* seq_lens, int batch, int nq, int nkv, int head_dim,
-                              int block_size, int max_splits, float scale, hipStream_t stream);
+                              int block_size, float scale, hipStream_t stream);
 int ft_prefill_tile_tokens(int nq, int nkv);
 int ft_prefill_attention(void* out, int out_stride, const void* q, int q_stride,
                          const void* k_cache, const void* v_cache, const int* block_tables,
@@ -102,6 +103,21 @@ void check_rows(const at::Tensor& t, const char* name) {
   TORCH_CHECK(t.stride(0) % 8 == 0, name, " row stride must be a multiple of 8 elements");
 }
 
+// KV caches: K [blocks, nkv, block_size, D] (token rows), V [blocks, nkv, D,
+// block_size] (transposed, rope_kv.hip); a mismatched V layout would be read as
+// garbage by the attention kernels, so every op touching the caches checks both
+void check_kv_caches(const at::Tensor& k_cache, const at::Tensor& v_cache, int64_t nkv,
+                     int64_t head_dim) {
+  check_bf16(k_cache, "k_cache");
+  check_bf16(v_cache, "v_cache");
+  TORCH_CHECK(k_cache.is_contiguous() && v_cache.is_contiguous(), "KV caches must be contiguous");
+  TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(1) == nkv && k_cache.size(3) == head_dim,
+              "k_cache must be [blocks, nkv, block_size, head_dim]");
+  TORCH_CHECK(v_cache.dim() == 4 && v_cache.size(0) == k_cache.size(0) && v_cache.size(1) == nkv &&
+                  v_cache.size(2) == head_dim && v_cache.size(3) == k_cache.size(2),
+              "v_cache must be [blocks, nkv, head_dim, block_size] (transposed V blocks)");
+}
+
 void rmsnorm(at::Tensor out, at::Tensor x, at::Tensor w, double eps) {
   check_bf16(out, "out");
   check_bf16(x, "x");
@@ -155,11 +171,7 @@ void rope_kv_write(at::Tensor qkv, at::Tensor positions, at::Tensor cos_sin,
   TORCH_CHECK(cos_sin.scalar_type() == at::kFloat && cos_sin.is_contiguous() &&
                   cos_sin.size(1) == head_dim,
               "cos_sin must be fp32 [max_pos, head_dim]");
-  check_bf16(k_cache, "k_cache");
-  check_bf16(v_cache, "v_cache");
-  TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(1) == nkv && k_cache.size(3) == head_dim,
-              "k_cache must be [blocks, nkv, block_size, head_dim]");
-  TORCH_CHECK(v_cache.sizes() == k_cache.sizes(), "v_cache shape");
+  check_kv_caches(k_cache, v_cache, nkv, head_dim);
   TORCH_CHECK(qkv.size(1) >= (nq + 2 * nkv) * head_dim, "qkv width");
   const int tokens = (int)qkv.size(0);
   TORCH_CHECK(positions.numel() >= tokens && slot_mapping.numel() >= tokens, "metadata length");
@@ -173,36 +185,33 @@ void rope_kv_write(at::Tensor qkv, at::Tensor positions, at::Tensor cos_sin,
 void paged_decode_attention(at::Tensor out, at::Tensor q, at::Tensor k_cache, at::Tensor v_cache,
                             at::Tensor block_tables, at::Tensor seq_lens, at::Tensor tmp_out,
                             at::Tensor tmp_ml, int64_t nq, int64_t nkv, int64_t head_dim,
-                            int64_t max_splits, double scale) {
+                            double scale) {
   check_bf16(out, "out");
   check_bf16(q, "q");
   check_rows(out, "out");
   check_rows(q, "q");
-  check_bf16(k_cache, "k_cache");
-  check_bf16(v_cache, "v_cache");
+  check_kv_caches(k_cache, v_cache, nkv, head_dim);
   check_i32(block_tables, "block_tables");
   check_i32(seq_lens, "seq_lens");
-  TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(1) == nkv && k_cache.size(3) == head_dim,
-              "k_cache shape");
   const int batch = (int)q.size(0);
   TORCH_CHECK(out.size(0) >= batch && seq_lens.numel() >= batch && block_tables.size(0) >= batch,
               "batch sizes");
-  TORCH_CHECK(max_splits >= 1, "max_splits");
-  if (max_splits > 1) {
-    TORCH_CHECK(tmp_out.scalar_type() == at::kFloat && tmp_ml.scalar_type() == at::kFloat,
-                "tmp buffers fp32");
-    TORCH_CHECK(tmp_out.numel() >= (int64_t)batch * nq * max_splits * head_dim &&
-                    tmp_ml.numel() >= (int64_t)batch * nq * max_splits * 2,
-                "tmp buffers too small");
-  }
-  check_rc(ft_paged_decode_attention(out.data_ptr(), (int)out.stride(0),
-                                     max_splits > 1 ? tmp_out.data_ptr<float>() : nullptr,
-                                     max_splits > 1 ? tmp_ml.data_ptr<float>() : nullptr,
-                                     q.data_ptr(), (int)q.stride(0), k_cache.data_ptr(),
-                                     v_cache.data_ptr(), block_tables.data_ptr<int>(),
-                                     (int)block_tables.stride(0), seq_lens.data_ptr<int>(), batch,
-                                     (int)nq, (int)nkv, (int)head_dim, (int)k_cache.size(2),
-                                     (int)max_splits, (float)scale, cur_stream()),
+  TORCH_CHECK(batch <= ft_decode_max_batch(), "decode batch above ", ft_decode_max_batch());
+  TORCH_CHECK(nq % nkv == 0 && nq / nkv <= 16, "GQA group must be <= 16");
+  // partial slots: one per (sequence, kv head) + one per wave of the grid
+  const int64_t slots = (int64_t)batch * nkv + ft_decode_waves();
+  TORCH_CHECK(tmp_out.scalar_type() == at::kFloat && tmp_ml.scalar_type() == at::kFloat,
+              "tmp buffers fp32");
+  TORCH_CHECK(tmp_out.numel() >= slots * (nq / nkv) * head_dim &&
+                  tmp_ml.numel() >= slots * (nq / nkv) * 2,
+              "decode workspace too small (ops.decode_workspace)");
+  check_rc(ft_paged_decode_attention(out.data_ptr(), (int)out.stride(0), tmp_out.data_ptr<float>(),
+                                     tmp_ml.data_ptr<float>(), q.data_ptr(), (int)q.stride(0),
+                                     k_cache.data_ptr(), v_cache.data_ptr(),
+                                     block_tables.data_ptr<int>(), (int)block_tables.stride(0),
+                                     seq_lens.data_ptr<int>(), batch, (int)nq, (int)nkv,
+                                     (int)head_dim, (int)k_cache.size(2), (float)scale,
+                                     cur_stream()),
            "paged_decode_attention");
 }
 
@@ -214,14 +223,11 @@ void prefill_attention(at::Tensor out, at::Tensor q, at::Tensor k_cache, at::Ten
   check_bf16(q, "q");
   check_rows(out, "out");
   check_rows(q, "q");
-  check_bf16(k_cache, "k_cache");
-  check_bf16(v_cache, "v_cache");
+  check_kv_caches(k_cache, v_cache, nkv, head_dim);
   check_i32(block_tables, "block_tables");
   check_i32(seq_lens, "seq_lens");
   check_i32(q_start_loc, "q_start_loc");
   check_i32(tile_info, "tile_info");
-  TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(1) == nkv && k_cache.size(3) == head_dim,
-              "k_cache shape");
   TORCH_CHECK(tile_info.numel() >= 2 * num_tiles, "tile_info too small");
   check_rc(ft_prefill_attention(out.data_ptr(), (int)out.stride(0), q.data_ptr(),
                                 (int)q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
@@ -574,10 +580,7 @@ void slab_rope_kv(at::Tensor ws, int64_t splits, int64_t rows, int64_t cols, at:
   TORCH_CHECK(cols == (nq + 2 * nkv) * head_dim, "cols");
   TORCH_CHECK(q_out.size(0) >= rows && q_out.size(1) >= nq * head_dim, "q_out shape");
   TORCH_CHECK(cos_sin.scalar_type() == at::kFloat && cos_sin.size(1) == head_dim, "cos_sin");
-  check_bf16(k_cache, "k_cache");
-  check_bf16(v_cache, "v_cache");
-  TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(1) == nkv && k_cache.size(3) == head_dim,
-              "k_cache shape");
+  check_kv_caches(k_cache, v_cache, nkv, head_dim);
   TORCH_CHECK(positions.numel() >= rows && slot_mapping.numel() >= rows, "metadata length");
   check_rc(ft_slab_rope_kv(ws.data_ptr<float>(), (int)splits, (int)rows, (int)cols,
                            q_out.data_ptr(), (int)q_out.stride(0), positions.data_ptr<int>(),
@@ -596,7 +599,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("silu_mul", &silu_mul);
   m.def("rope_kv_write", &rope_kv_write);
   m.def("paged_decode_attention", &paged_decode_attention);
-  m.def("decode_partition_size", []() { return ft_decode_partition_size(); });
+  m.def("decode_waves", []() { return ft_decode_waves(); });
+  m.def("decode_max_batch", []() { return ft_decode_max_batch(); });
   m.def("prefill_attention", &prefill_attention);
   m.def("prefill_tile_tokens", [](int64_t nq, int64_t nkv) { return ft_prefill_tile_tokens((int)nq, (int)nkv); });
   m.def("sample", &sample, py::arg("out_tokens"), py::arg("logits"), py::arg("temperature"),

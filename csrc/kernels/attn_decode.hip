@@ -1,361 +1,387 @@
-// K6: paged decode attention (one query token per sequence), split-K
-// ("flash-decoding") with an optional combine kernel.  SURVEY.md §2.4 K6.
+// K6: paged decode attention (one query token per sequence) on MFMA, with a
+// load-balanced flattened work partition.  SURVEY.md §2.4 K6.
 //
 // Decode attention is an HBM stream over the KV cache (4 KiB per token per layer
-// for Llama-3-8B); the kernel is designed around bytes in flight and a short
-// dependent-latency chain per workgroup, not FLOPs:
-//   * grid = (seq * kv_head, split).  Split s of a sequence of length L owns the
-//     token range [s*P, (s+1)*P), P = roundup16(ceil(L / splits)): every sequence
-//     is cut into `splits` near-equal partitions whatever its length, so the grid
-//     depends only on (batch bucket, splits) and ONE hipGraph per batch bucket
-//     covers every context length.  There is no upper bound on P (no LDS score
-//     buffer): the host picks `splits` only to fill the chip.
-//   * a workgroup computes all G = nq/nkv query heads of its kv head (GQA
-//     packing: every K/V byte is read once per step).
-//   * the 4 waves take interleaved 16-token tiles (one aligned piece of one KV
-//     block each) and run an independent online softmax (exp2 domain).  The KV
-//     offsets of a wave's next 64 tiles come from ONE block-table load (lane i
-//     holds tile i's, read back with v_readlane), and the tiles are double
-//     buffered in registers, so after the prologue every K/V round trip overlaps
-//     the previous tile's math instead of following a block-table read.
-//   * QK^T: 16 lanes share a token (8 head dims each); q stays packed bf16 and
-//     the dot is v_dot2_f32_bf16 on the raw K words (no K unpacking); the
-//     16-lane sum is 4 DPP adds (quad_perm, row_half_mirror, row_mirror), no
-//     LDS traffic.  P.V accumulates fp32 in registers.
-//   * the waves' (m, l, acc) merge through LDS; a partition that is the whole
-//     sequence writes bf16 output directly, otherwise fp32 partials + (m, l) for
-//     the combine kernel (launched only when splits > 1).
+// for Llama-3-8B).  What bounds it on MI355X is bytes in flight per CU and how
+// evenly the CUs are loaded, so the kernel is built around those two things:
+//
+// * Layout.  K blocks are [block_size tok][D] (row-major); V blocks are stored
+//   TRANSPOSED, [D][block_size tok] (csrc/kernels/rope_kv.hip writes them so).
+//   With that, every MFMA operand of a 16-token tile loads straight from HBM
+//   into registers with no LDS round trip and no transposing read:
+//     S[16 tok x 16 heads] = K[16 x D] . Qpad^T      v_mfma_f32_16x16x32_bf16
+//        A = K rows (16 B per lane), B = the G query heads of the kv head (GQA
+//        packed, padded to 16 columns), C lane (g, n) = tokens 4g..4g+3, head n
+//     O[16 heads x D]     += P[16 x 16 tok] . V       v_mfma_f32_16x16x16_bf16
+//        A = P: exactly the S C-layout (lane (g, n) = head n, tokens 4g..4g+3)
+//        converted to bf16 in place; B = V^T rows: tokens 4g..4g+3 of dim n =
+//        8 contiguous bytes of the transposed V block.
+//   VALU work per tile is the online softmax of 4 values per lane (v3, the VALU
+//   dot2 kernel this replaces, needed ~440 instructions and 247 VGPRs per wave
+//   for the same tile; at 2 waves/SIMD the CUs were latency-starved).
+// * Partition.  Every (sequence, kv head, 16-token tile) is flattened into one
+//   index space of `total` tiles and the grid's waves (all resident) each take
+//   an equal contiguous range, so every CU streams the same number of bytes
+//   whatever the mix of context lengths (v3 gave each (sequence, kv head) a
+//   workgroup: 400 workgroups on 256 CUs at the 50-session batch).  A wave walks
+//   its range segment by segment ((b, h) pieces) with an R-deep register ring
+//   (R-1 tiles in flight while one computes).  A segment that one wave covers
+//   whole is written as bf16 at once; pieces of shared segments leave fp32
+//   (acc, m, l) partials at slot = segment + wave (collision-free: consecutive
+//   segments share at most one wave) for paged_decode_combine.
 #include "ft_common.h"
+
+#include <stdlib.h>
 
 namespace ft {
 
-typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef short short4_t __attribute__((ext_vector_type(4)));
+typedef float floatx4_t __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ int decode_part(int L, int splits) {
-  const int p = (L + splits - 1) / splits;
-  return max(16, (p + 15) & ~15);
-}
+constexpr int kDecMaxBatch = 1024;
+constexpr int kDecMinTiles = 4;   // >= 64 tokens per wave: short contexts use fewer waves
 
-__device__ __forceinline__ float dot2_bf16(uint32_t a, uint32_t b, float c) {
-  return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, a),
-                                         __builtin_bit_cast(bf16x2_t, b), c, false);
-}
-
-// sum over aligned groups of LPT (8 or 16) lanes; every lane gets the group sum
-template <int LPT>
-__device__ __forceinline__ float lane_group_sum(float v) {
-  v += __builtin_amdgcn_update_dpp(0.f, v, 0xB1, 0xf, 0xf, false);   // quad_perm [1,0,3,2]
-  v += __builtin_amdgcn_update_dpp(0.f, v, 0x4E, 0xf, 0xf, false);   // quad_perm [2,3,0,1]
-  v += __builtin_amdgcn_update_dpp(0.f, v, 0x141, 0xf, 0xf, false);  // row_half_mirror
-  if constexpr (LPT == 16) v += __builtin_amdgcn_update_dpp(0.f, v, 0x140, 0xf, 0xf, false);
-  return v;
-}
-
-// reduce across the token groups of a wave (lanes differing above log2(LPT))
-template <int LPT>
-__device__ __forceinline__ float token_group_max(float v) {
+// s_pre[b] = sum_{b' < b} ceil(L_b' / 16) (tiles per kv head), b = 0..batch; wave-wide scan
+__device__ __forceinline__ void dec_prefix(int* s_pre, const int* __restrict__ seq_lens, int batch) {
+  const int lane = lane_id();
+  int run = 0;
+  for (int b0 = 0; b0 < batch; b0 += 64) {
+    const int b = b0 + lane;
+    int x = b < batch ? (max(seq_lens[b], 0) + 15) >> 4 : 0;
 #pragma unroll
-  for (int o = LPT; o < 64; o <<= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
-}
-template <int LPT>
-__device__ __forceinline__ float token_group_sum(float v) {
-#pragma unroll
-  for (int o = LPT; o < 64; o <<= 1) v += __shfl_xor(v, o, 64);
-  return v;
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(x, o, 64);
+      if (lane >= o) x += y;
+    }
+    if (b < batch) s_pre[b + 1] = run + x;
+    run += __shfl(x, 63, 64);
+  }
+  if (lane == 0) s_pre[0] = 0;
 }
 
-// one wave tile = 16 consecutive tokens = one aligned 16-token piece of one KV
-// block (block_size is a power of two >= 16 and partitions start at multiples
-// of 16), so a tile needs exactly one block-table entry.
-template <int D, int G>
-struct DecTile {
-  static constexpr int LPT = D / 8;      // lanes per token
-  static constexpr int TPW = 64 / LPT;   // tokens per wave instruction
-  static constexpr int U = 16 / TPW;     // loads of K (and of V) per lane per tile
-  uint4 k[U], v[U];
+__device__ __forceinline__ int dec_num_waves(int total, int nw_grid) {
+  return max(1, min(nw_grid, (total + kDecMinTiles - 1) / kDecMinTiles));
+}
+
+// one 16-token tile of one kv head in registers: K rows (A operand of QK^T, one
+// uint4 per 32-deep k-step) and V^T rows (B operand of PV, 4 tokens per 16 dims)
+template <int D>
+struct MTile {
+  uint4 k[D / 32];
+  uint2 v[D / 16];
 };
 
-template <int D, int G>
-__device__ __forceinline__ void dec_load_tile(DecTile<D, G>& t, const uint16_t* __restrict__ k_cache,
-                                              const uint16_t* __restrict__ v_cache, size_t base,
-                                              int valid_tokens, int ts, int c) {
-  using T = DecTile<D, G>;
-  // unconditional loads (slots past the end re-read the last valid token and
-  // are masked in dec_consume_tile): a uniform load count lets the compiler
-  // wait with exact vmcnt values instead of draining at a branch merge
+template <int D>
+__device__ __forceinline__ void mt_load(MTile<D>& t, const uint16_t* __restrict__ k_cache,
+                                        const uint16_t* __restrict__ v_cache, size_t kbase,
+                                        size_t vbase, int koff, int voff, int bsz) {
+  // wave-uniform tile bases (SGPR pairs) + 32-bit lane offsets
+  const uint16_t* kb = k_cache + kbase;
+  const uint16_t* vb = v_cache + vbase;
 #pragma unroll
-  for (int u = 0; u < T::U; ++u) {
-    const int tl = min(u * T::TPW + ts, valid_tokens - 1);
-    const size_t off = base + (size_t)tl * D;
-    t.k[u] = reinterpret_cast<const uint4*>(k_cache + off)[c];
-    t.v[u] = reinterpret_cast<const uint4*>(v_cache + off)[c];
-  }
+  for (int kc = 0; kc < D / 32; ++kc)
+    t.k[kc] = *reinterpret_cast<const uint4*>(kb + koff + kc * 32);
+#pragma unroll
+  for (int nd = 0; nd < D / 16; ++nd)
+    t.v[nd] = *reinterpret_cast<const uint2*>(vb + voff + nd * 16 * bsz);
 }
 
-template <int D, int G>
-__device__ __forceinline__ void dec_consume_tile(const DecTile<D, G>& t, const uint4 (&qp)[G],
-                                                 int valid_tokens, int ts, float scale_log2,
-                                                 float (&m)[G], float (&l)[G], float (&acc)[G][8]) {
-  using T = DecTile<D, G>;
-  constexpr int U = T::U, LPT = T::LPT;
-  float s[U][G];
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const bool valid = u * T::TPW + ts < valid_tokens;
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-      float d = dot2_bf16(t.k[u].x, qp[g].x, 0.f);
-      d = dot2_bf16(t.k[u].y, qp[g].y, d);
-      d = dot2_bf16(t.k[u].z, qp[g].z, d);
-      d = dot2_bf16(t.k[u].w, qp[g].w, d);
-      d = lane_group_sum<LPT>(d);
-      s[u][g] = valid ? d * scale_log2 : -INFINITY;
-    }
-  }
-#pragma unroll
-  for (int g = 0; g < G; ++g) {
-    float tm = s[0][g];
-#pragma unroll
-    for (int u = 1; u < U; ++u) tm = fmaxf(tm, s[u][g]);
-    tm = token_group_max<LPT>(tm);
-    const float mn = fmaxf(m[g], tm);
-    const float alpha = exp2f(m[g] - mn);
-    m[g] = mn;
-    l[g] *= alpha;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[g][j] *= alpha;
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      s[u][g] = exp2f(s[u][g] - mn);
-      l[g] += s[u][g];
-    }
-  }
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    float vf[8];
-    load8(t.v[u], vf);
-#pragma unroll
-    for (int g = 0; g < G; ++g)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc[g][j] += s[u][g] * vf[j];
-  }
-}
-
-template <int D, int G>
-__global__ __launch_bounds__(256) void paged_decode_kernel(
+template <int D, int G, int R>
+__global__ __launch_bounds__(256, R == 2 ? 3 : 2) void paged_decode_kernel(
     uint16_t* __restrict__ out, int out_stride, float* __restrict__ tmp_out,
     float* __restrict__ tmp_ml, const uint16_t* __restrict__ q, int q_stride,
     const uint16_t* __restrict__ k_cache, const uint16_t* __restrict__ v_cache,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ seq_lens,
-    int nkv, int bs_shift, int max_splits, float scale_log2) {
-  using T = DecTile<D, G>;
-  constexpr int LPT = T::LPT;
-  __shared__ float s_acc[4][G][D];
-  __shared__ float s_m[4][G], s_l[4][G];
-
-  const int b = blockIdx.x / nkv;
-  const int kvh = blockIdx.x - b * nkv;
-  const int split = blockIdx.y;
-  const int L = seq_lens[b];
-  const int PART = decode_part(L, max_splits);
-  const int start = split * PART;
-  if (start >= L) return;
-  const int n = min(L - start, PART);
-  const int nsplit = (L + PART - 1) / PART;
-  const int nq = nkv * G;
-  const int bmask = (1 << bs_shift) - 1;
-
-  const int lane = lane_id(), wave = wave_id();
-  const int c = lane % LPT;       // 8-dim chunk owned by this lane
-  const int ts = lane / LPT;      // token slot within a wave instruction
-
-  uint4 qp[G];
-#pragma unroll
-  for (int g = 0; g < G; ++g)
-    qp[g] = reinterpret_cast<const uint4*>(q + (size_t)b * q_stride + (kvh * G + g) * D)[c];
-
-  const int* bt = block_tables + (size_t)b * bt_stride;
-  const size_t head_off = (size_t)kvh * (bmask + 1) * D;
-  const size_t blk_stride = (size_t)nkv * (bmask + 1) * D;
-
-  float m[G], l[G], acc[G][8];
-#pragma unroll
-  for (int g = 0; g < G; ++g) {
-    m[g] = -INFINITY;
-    l[g] = 0.f;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[g][j] = 0.f;
-  }
-
-  // this wave's tiles: i = 0.. with first token start + 16*(wave + 4 i).  The
-  // KV-cache base offset of 64 consecutive tiles is fetched in ONE load (lane i
-  // holds tile i's), so the K/V loads never wait on a block-table read.
-  const int ntiles = (n + 15) >> 4;
-  const int my_tiles = ntiles > wave ? (ntiles - wave + 3) >> 2 : 0;
-  for (int c0 = 0; c0 < my_tiles; c0 += 64) {
-    const int cnt = min(64, my_tiles - c0);
-    size_t my_base = 0;
-    if (lane < cnt) {
-      const int tok = start + 16 * (wave + 4 * (c0 + lane));
-      my_base = (size_t)bt[tok >> bs_shift] * blk_stride + head_off + (size_t)(tok & bmask) * D;
-    }
-    auto tile_base = [&](int i) -> size_t {
-      const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)my_base, i);
-      const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(my_base >> 32), i);
-      return ((size_t)hi << 32) | lo;
-    };
-    auto tile_valid = [&](int i) { return n - 16 * (wave + 4 * (c0 + i)); };
-    // double-buffered: tile i+1's K/V loads are in flight while tile i computes
-    // (a prefetch index past the end re-loads the last tile: L2 hit, never consumed)
-    auto ld = [&](DecTile<D, G>& t, int i) {
-      const int j = min(i, cnt - 1);
-      dec_load_tile<D, G>(t, k_cache, v_cache, tile_base(j), tile_valid(j), ts, c);
-    };
-    DecTile<D, G> ta, tb;
-    ld(ta, 0);
-    int i = 0;
-    // sched_barrier(0) keeps each prefetch ahead of the math it overlaps
-    for (; i + 1 < cnt; i += 2) {
-      ld(tb, i + 1);
-      __builtin_amdgcn_sched_barrier(0);
-      dec_consume_tile<D, G>(ta, qp, tile_valid(i), ts, scale_log2, m, l, acc);
-      __builtin_amdgcn_sched_barrier(0);
-      ld(ta, i + 2);
-      __builtin_amdgcn_sched_barrier(0);
-      dec_consume_tile<D, G>(tb, qp, tile_valid(i + 1), ts, scale_log2, m, l, acc);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    if (i < cnt) dec_consume_tile<D, G>(ta, qp, tile_valid(i), ts, scale_log2, m, l, acc);
-  }
-
-  // ---- merge token slots of the wave, then the 4 waves ---------------------------
-#pragma unroll
-  for (int g = 0; g < G; ++g) {
-    l[g] = token_group_sum<LPT>(l[g]);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[g][j] = token_group_sum<LPT>(acc[g][j]);
-  }
-  if (lane < LPT) {
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) s_acc[wave][g][c * 8 + j] = acc[g][j];
-      if (lane == 0) {
-        s_m[wave][g] = m[g];
-        s_l[wave][g] = l[g];
-      }
-    }
-  }
+    int batch, int nkv, int bs_shift, float scale_log2) {
+  static_assert(G >= 1 && G <= 16, "GQA group must fit the 16 MFMA columns");
+  constexpr int KC = D / 32, ND = D / 16;
+  __shared__ int s_pre[kDecMaxBatch + 1];
+  if (wave_id() == 0) dec_prefix(s_pre, seq_lens, batch);
   __syncthreads();
+  const int total = nkv * s_pre[batch];
+  const int nw = dec_num_waves(total, gridDim.x * 4);
+  const int w = wave_id() * gridDim.x + blockIdx.x;  // spreads low wave ids over CUs
+  if (total == 0 || w >= nw) return;
+  int f = (int)(((long long)w * total) / nw);
+  const int f1 = (int)(((long long)(w + 1) * total) / nw);
 
-  for (int i = threadIdx.x; i < G * D; i += blockDim.x) {
-    const int g = i / D, d = i - g * D;
-    float M = s_m[0][g];
-#pragma unroll
-    for (int w = 1; w < 4; ++w) M = fmaxf(M, s_m[w][g]);
-    float num = 0.f, den = 0.f;
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-      const float e = (s_l[w][g] > 0.f) ? exp2f(s_m[w][g] - M) : 0.f;
-      num += e * s_acc[w][g][d];
-      den += e * s_l[w][g];
+  const int lane = lane_id();
+  const int n = lane & 15;   // MFMA column (head) / row (token) / dim within a tile
+  const int g = lane >> 4;   // k group
+  const int bsz = 1 << bs_shift;
+  const int bmask = bsz - 1;
+  const size_t blk_stride = (size_t)nkv * bsz * D;
+  // per-lane offsets inside a 16-token tile
+  const int koff = n * D + 8 * g;          // K row n, dims 8g.. (+32 kc)
+  const int voff = n * bsz + 4 * g;        // V^T row n (+16 nd), tokens 4g..4g+3
+
+  while (f < f1) {
+    // segment (b, h) holding flattened tile f: b = last sequence with nkv * pre[b] <= f
+    int lo = 0, hi = batch - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (nkv * s_pre[mid] <= f) lo = mid; else hi = mid - 1;
     }
-    const int h = kvh * G + g;
-    if (nsplit == 1) {
-      out[(size_t)b * out_stride + h * D + d] = f32_to_bf16(num / den);
-    } else {
-      const size_t o = ((size_t)b * nq + h) * max_splits + split;
-      tmp_out[o * D + d] = num;
-      if (d == 0) {
-        tmp_ml[o * 2] = M;
-        tmp_ml[o * 2 + 1] = den;
+    const int b = lo;
+    const int nb = s_pre[b + 1] - s_pre[b];
+    const int rel = f - nkv * s_pre[b];
+    const int h = rel / nb;
+    const int t0 = rel - h * nb;
+    const int cnt = min(f1 - f, nb - t0);
+    const int L = seq_lens[b];
+
+    // Q^T fragments (B operand): lane (g, n) = head n of this kv head, dims 8g.. (+32 kc)
+    uint4 qb[KC];
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc)
+      qb[kc] = n < G ? *reinterpret_cast<const uint4*>(q + (size_t)b * q_stride +
+                                                       (h * G + n) * D + kc * 32 + 8 * g)
+                     : make_uint4(0, 0, 0, 0);
+    floatx4_t o[ND];
+#pragma unroll
+    for (int nd = 0; nd < ND; ++nd) o[nd] = floatx4_t{0.f, 0.f, 0.f, 0.f};
+    float m_run = -INFINITY;   // running max of head n (uniform over g)
+    float l_run = 0.f;         // this lane's share of the running sum of head n
+
+    const int* bt = block_tables + (size_t)b * bt_stride;
+    for (int c0 = 0; c0 < cnt; c0 += 64) {
+      const int cc = min(64, cnt - c0);
+      // lane i holds tile (t0 + c0 + i)'s block index and in-block token offset
+      int my_blk = 0, my_off = 0;
+      if (lane < cc) {
+        const int tok = (t0 + c0 + lane) << 4;
+        my_blk = bt[tok >> bs_shift];
+        my_off = tok & bmask;
+      }
+      auto ld = [&](MTile<D>& t, int i) {
+        const int j = min(i, cc - 1);  // past the end: re-load the last tile (never consumed)
+        const size_t blk = (size_t)(uint32_t)__builtin_amdgcn_readlane(my_blk, j);
+        const int off = __builtin_amdgcn_readlane(my_off, j);
+        const size_t hb = blk * blk_stride + (size_t)h * bsz * D;
+        mt_load<D>(t, k_cache, v_cache, hb + (size_t)off * D, hb + off, koff, voff, bsz);
+      };
+      auto consume = [&](const MTile<D>& t, int i) {
+        const int valid = L - ((t0 + c0 + i) << 4);   // tokens of this tile inside the sequence
+        floatx4_t s = floatx4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kc = 0; kc < KC; ++kc)
+          s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, t.k[kc]),
+                                                      __builtin_bit_cast(bf16x8_t, qb[kc]), s, 0, 0, 0);
+        float tm = -INFINITY;
+#pragma unroll
+        for (int i4 = 0; i4 < 4; ++i4) {
+          float v = s[i4] * scale_log2;
+          if (valid < 16 && 4 * g + i4 >= valid) v = -INFINITY;
+          s[i4] = v;
+          tm = fmaxf(tm, v);
+        }
+        tm = fmaxf(tm, __shfl_xor(tm, 16, 64));
+        tm = fmaxf(tm, __shfl_xor(tm, 32, 64));
+        const float mn = fmaxf(m_run, tm);
+        const float alpha = exp2f(m_run - mn);
+        m_run = mn;
+        float p[4];
+#pragma unroll
+        for (int i4 = 0; i4 < 4; ++i4) p[i4] = exp2f(s[i4] - mn);
+        l_run = l_run * alpha + ((p[0] + p[1]) + (p[2] + p[3]));
+        // rescale O rows (heads 4g'+i of the C layout) only when some max moved
+        if (__builtin_amdgcn_ballot_w64(alpha != 1.f)) {
+          float a[4];
+#pragma unroll
+          for (int i4 = 0; i4 < 4; ++i4) a[i4] = __shfl(alpha, (4 * g + i4) & 15, 64);
+#pragma unroll
+          for (int nd = 0; nd < ND; ++nd)
+#pragma unroll
+            for (int i4 = 0; i4 < 4; ++i4) o[nd][i4] *= a[i4];
+        }
+        short4_t pa;
+#pragma unroll
+        for (int i4 = 0; i4 < 4; ++i4) pa[i4] = (short)f32_to_bf16(p[i4]);
+#pragma unroll
+        for (int nd = 0; nd < ND; ++nd)
+          o[nd] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(pa, __builtin_bit_cast(short4_t, t.v[nd]),
+                                                           o[nd], 0, 0, 0);
+      };
+      MTile<D> ring[R];
+#pragma unroll
+      for (int r = 0; r + 1 < R; ++r) ld(ring[r], r);
+      for (int i = 0; i < cc; i += R) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          ld(ring[(r + R - 1) % R], i + r + R - 1);
+          __builtin_amdgcn_sched_barrier(0);
+          if (i + r < cc) consume(ring[r], i + r);
+          __builtin_amdgcn_sched_barrier(0);
+        }
       }
     }
+
+    // head n's sum over the 4 token groups
+    float l_tot = l_run + __shfl_xor(l_run, 16, 64);
+    l_tot += __shfl_xor(l_tot, 32, 64);
+    // C-layout rows of O: lane (g, n) holds heads 4g+i, dim n (+16 nd)
+    const int seg = b * nkv + h;
+    if (t0 == 0 && cnt == nb) {   // the whole segment: final bf16 output
+#pragma unroll
+      for (int i4 = 0; i4 < 4; ++i4) {
+        const int r = 4 * g + i4;
+        const float lr = __shfl(l_tot, r & 15, 64);
+        if (r < G) {
+          const float inv = 1.f / lr;
+          uint16_t* op = out + (size_t)b * out_stride + (h * G + r) * D + n;
+#pragma unroll
+          for (int nd = 0; nd < ND; ++nd) op[nd * 16] = f32_to_bf16(o[nd][i4] * inv);
+        }
+      }
+    } else {
+      const size_t slot = (size_t)(seg + w);
+#pragma unroll
+      for (int i4 = 0; i4 < 4; ++i4) {
+        const int r = 4 * g + i4;
+        const float lr = __shfl(l_tot, r & 15, 64);
+        const float mr = __shfl(m_run, r & 15, 64);
+        if (r < G) {
+          float* dst = tmp_out + (slot * G + r) * D + n;
+#pragma unroll
+          for (int nd = 0; nd < ND; ++nd) dst[nd * 16] = o[nd][i4];
+          if (n == 0) {
+            tmp_ml[(slot * G + r) * 2] = mr;
+            tmp_ml[(slot * G + r) * 2 + 1] = lr;
+          }
+        }
+      }
+    }
+    f += cnt;
   }
 }
 
-// One workgroup per (sequence, q head): wave 0 turns the partitions' (m, l) into
-// merge weights (lane s = partition s, wave-wide max / sum), then every thread
-// sums its head dim over the partitions with 16 loads in flight (clamped
-// indices, zero weights past the end) -- the merge is a handful of dependent
-// round trips, not one per partition.
-template <int D>
-__global__ __launch_bounds__(D) void paged_decode_combine_kernel(
+// One workgroup per (sequence, kv head): merges the partials of a segment that
+// several waves shared (slots segment + w, w = first..last wave of the segment).
+template <int D, int G>
+__global__ __launch_bounds__(256) void paged_decode_combine_kernel(
     uint16_t* __restrict__ out, int out_stride, const float* __restrict__ tmp_out,
-    const float* __restrict__ tmp_ml, const int* __restrict__ seq_lens, int nq, int max_splits) {
-  const int b = blockIdx.x, h = blockIdx.y, d = threadIdx.x;
-  const int L = seq_lens[b];
-  const int part = decode_part(L, max_splits);
-  const int ns = (L + part - 1) / part;
-  if (ns <= 1) return;
-  __shared__ float s_w[64];
-  const size_t base = ((size_t)b * nq + h) * max_splits;
-  if (d < 64) {  // max_splits <= 64 (checked by the launcher)
-    const float ms = d < ns ? tmp_ml[(base + d) * 2] : -INFINITY;
-    const float ls = d < ns ? tmp_ml[(base + d) * 2 + 1] : 0.f;
-    float M = ms;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) M = fmaxf(M, __shfl_xor(M, o, 64));
-    const float w = d < ns ? exp2f(ms - M) : 0.f;
-    float den = w * ls;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) den += __shfl_xor(den, o, 64);
-    s_w[d] = w / den;
+    const float* __restrict__ tmp_ml, const int* __restrict__ seq_lens, int batch, int nkv,
+    int nw_grid) {
+  __shared__ int s_pre[kDecMaxBatch + 1];
+  __shared__ float s_M[G], s_den[G];
+  if (wave_id() == 0) dec_prefix(s_pre, seq_lens, batch);
+  __syncthreads();
+  const int total = nkv * s_pre[batch];
+  const int nw = dec_num_waves(total, nw_grid);
+  const int seg = blockIdx.x;
+  const int b = seg / nkv, h = seg - b * nkv;
+  const int nb = s_pre[b + 1] - s_pre[b];
+  uint16_t* o = out + (size_t)b * out_stride + h * G * D;
+  if (nb == 0) {  // empty sequence: define the output
+    for (int i = threadIdx.x; i < G * D; i += blockDim.x) o[i] = 0;
+    return;
+  }
+  const int S = nkv * s_pre[b] + h * nb, E = S + nb;
+  const int wf = (int)(((long long)(S + 1) * nw - 1) / total);
+  const int wl = (int)(((long long)E * nw - 1) / total);
+  const int np = wl - wf + 1;
+  if (np <= 1) return;  // one wave covered it and wrote bf16 directly
+  const size_t base = (size_t)(seg + wf);
+  const int lane = lane_id();
+  for (int g = wave_id(); g < G; g += blockDim.x / 64) {
+    float M = -INFINITY;
+    for (int k = lane; k < np; k += 64) M = fmaxf(M, tmp_ml[((base + k) * G + g) * 2]);
+    M = wave_max(M);
+    float den = 0.f;
+    for (int k = lane; k < np; k += 64)
+      den += exp2f(tmp_ml[((base + k) * G + g) * 2] - M) * tmp_ml[((base + k) * G + g) * 2 + 1];
+    den = wave_sum(den);
+    if (lane == 0) {
+      s_M[g] = M;
+      s_den[g] = den;
+    }
   }
   __syncthreads();
-  const float* src = tmp_out + base * D + d;
-  float acc[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int s0 = 0; s0 < ns; s0 += 16) {
-    float v[16];
-#pragma unroll
-    for (int u = 0; u < 16; ++u) v[u] = src[(size_t)min(s0 + u, ns - 1) * D];
-#pragma unroll
-    for (int u = 0; u < 16; ++u) acc[u & 3] += (s0 + u < ns ? s_w[s0 + u] : 0.f) * v[u];
+  for (int i = threadIdx.x; i < G * D; i += blockDim.x) {
+    const int g = i / D, d = i - g * D;
+    const float M = s_M[g];
+    float a0 = 0.f, a1 = 0.f;
+    int k = 0;
+    for (; k + 1 < np; k += 2) {
+      const size_t s0 = (base + k) * G + g, s1 = (base + k + 1) * G + g;
+      a0 += exp2f(tmp_ml[s0 * 2] - M) * tmp_out[s0 * D + d];
+      a1 += exp2f(tmp_ml[s1 * 2] - M) * tmp_out[s1 * D + d];
+    }
+    if (k < np) {
+      const size_t s0 = (base + k) * G + g;
+      a0 += exp2f(tmp_ml[s0 * 2] - M) * tmp_out[s0 * D + d];
+    }
+    o[i] = f32_to_bf16((a0 + a1) / s_den[g]);
   }
-  out[(size_t)b * out_stride + h * D + d] = f32_to_bf16((acc[0] + acc[1]) + (acc[2] + acc[3]));
 }
 
 }  // namespace ft
 
-// partitions are unbounded (online softmax): any splits >= 1 covers any length
-extern "C" int ft_decode_partition_size() { return 1 << 30; }
+static int ft_num_cus() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+  }
+  return n;
+}
+
+// workgroups per CU (all resident): ring depth 2 fits 3 waves/SIMD (168 VGPRs),
+// deeper rings 2 waves/SIMD
+static int dec_wg_per_cu(int ring) { return ring == 2 ? 3 : 2; }
+
+// upper bound on the waves of the decode grid: the workspace holds batch * nkv +
+// waves partial slots
+extern "C" int ft_decode_waves() { return ft_num_cus() * 3 * 4; }
+extern "C" int ft_decode_max_batch() { return ft::kDecMaxBatch; }
 
 extern "C" int ft_paged_decode_attention(void* out, int out_stride, float* tmp_out, float* tmp_ml,
                                          const void* q, int q_stride, const void* k_cache,
                                          const void* v_cache, const int* block_tables,
                                          int bt_stride, const int* seq_lens, int batch, int nq,
-                                         int nkv, int head_dim, int block_size, int max_splits,
-                                         float scale, hipStream_t stream) {
+                                         int nkv, int head_dim, int block_size, float scale,
+                                         hipStream_t stream) {
   if (batch <= 0) return 0;
   if (nq % nkv != 0) return -1;
-  if (max_splits < 1 || max_splits > 64) return -3;
+  if (batch > ft::kDecMaxBatch) return -5;
   if (block_size < 16 || (block_size & (block_size - 1))) return -4;
   const int bs_shift = __builtin_ctz(block_size);
   const int G = nq / nkv;
   const float scale_log2 = scale * 1.4426950408889634f;
-  dim3 grid(batch * nkv, max_splits), block(256);
-#define FT_DEC_CASE(DD, GG)                                                                  \
-  if (head_dim == DD && G == GG) {                                                               \
-    hipLaunchKernelGGL((ft::paged_decode_kernel<DD, GG>), grid, block, 0, stream,            \
+  // register-ring depth (tiles per wave: R - 1 in flight); FT_DECODE_RING overrides
+  // the default for the A/B sweeps (bench/attn_sweep.py)
+  static const int ring = [] {
+    const char* e = getenv("FT_DECODE_RING");
+    const int r = e ? atoi(e) : 3;
+    return (r >= 2 && r <= 4) ? r : 3;
+  }();
+  int nwg = 0;
+#define FT_DEC_CASE(DD, GG, RR)                                                                \
+  if (head_dim == DD && G == GG) {                                                             \
+    nwg = ft_num_cus() * dec_wg_per_cu(RR);                                                    \
+    hipLaunchKernelGGL((ft::paged_decode_kernel<DD, GG, RR>), dim3(nwg), dim3(256), 0, stream, \
                        (uint16_t*)out, out_stride, tmp_out, tmp_ml, (const uint16_t*)q,          \
                        q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache,             \
-                       block_tables, bt_stride, seq_lens, nkv, bs_shift, max_splits, scale_log2); \
-    if (max_splits > 1)                                                                          \
-      hipLaunchKernelGGL((ft::paged_decode_combine_kernel<DD>), dim3(batch, nq), dim3(DD), 0,    \
-                         stream, (uint16_t*)out, out_stride, tmp_out, tmp_ml, seq_lens, nq,      \
-                         max_splits);                                                            \
+                       block_tables, bt_stride, seq_lens, batch, nkv, bs_shift, scale_log2);     \
+    hipLaunchKernelGGL((ft::paged_decode_combine_kernel<DD, GG>), dim3(batch * nkv), dim3(256),  \
+                       0, stream, (uint16_t*)out, out_stride, tmp_out, tmp_ml, seq_lens, batch,  \
+                       nkv, nwg * 4);                                                            \
     return static_cast<int>(hipGetLastError());                                                  \
   }
-  FT_DEC_CASE(128, 1)
-  FT_DEC_CASE(128, 2)
-  FT_DEC_CASE(128, 3)
-  FT_DEC_CASE(128, 4)
-  FT_DEC_CASE(128, 8)
-  FT_DEC_CASE(64, 1)
-  FT_DEC_CASE(64, 2)
-  FT_DEC_CASE(64, 4)
-  FT_DEC_CASE(64, 8)
+  if (ring == 2) { FT_DEC_CASE(128, 4, 2) }
+  if (ring == 4) { FT_DEC_CASE(128, 4, 4) }
+  FT_DEC_CASE(128, 1, 3)
+  FT_DEC_CASE(128, 2, 3)
+  FT_DEC_CASE(128, 3, 3)
+  FT_DEC_CASE(128, 4, 3)
+  FT_DEC_CASE(128, 8, 3)
+  FT_DEC_CASE(64, 1, 3)
+  FT_DEC_CASE(64, 2, 3)
+  FT_DEC_CASE(64, 4, 3)
+  FT_DEC_CASE(64, 8, 3)
 #undef FT_DEC_CASE
   return -2;
 }

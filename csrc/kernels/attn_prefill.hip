@@ -11,10 +11,11 @@
 //   * K is staged row-major into LDS with a 16-B-chunk XOR swizzle
 //     (chunk ^ (row & 15)) so the B-operand reads (16 different rows, same
 //     column) are bank-conflict free (guide T2).
-//   * V is staged row-major too (coalesced 16-B loads, no transposing writes)
-//     with the dual-use XOR image of guide T10 (b); the PV B-operand (k = token,
-//     n = head dim) is fetched with two ds_read_b64_tr_b16 hardware-transpose
-//     reads per MFMA.
+//   * V blocks are stored transposed in the cache ([D][block_size], see
+//     rope_kv.hip), so the tile is staged as a [D][64 tok] image (rows padded to
+//     72 elements against bank conflicts) with whole-row 16-B copies, and the
+//     PV B operand (k = 8 consecutive tokens, n = one head dim) is one plain
+//     ds_read_b128 per MFMA.
 //   * S = Q K^T with v_mfma_f32_16x16x32_bf16 (Q fragments live in registers for
 //     the whole kernel), causal + length mask, online softmax in the log2
 //     domain, P goes through a per-wave LDS tile to become the A operand of
@@ -27,29 +28,13 @@ namespace ft {
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef float floatx4_t __attribute__((ext_vector_type(4)));
 
-typedef short v4s_t __attribute__((ext_vector_type(4)));
-
 __device__ __forceinline__ bf16x8_t as_frag(const uint4& v) {
   return __builtin_bit_cast(bf16x8_t, v);
 }
 
-// gfx950 ds_read_b64_tr_b16: per 16-lane group, lane 4q+p supplies row q /
-// columns 4p..4p+3 of a 4x16 block; lane i receives column i of the 4 rows.
-__device__ __forceinline__ uint2 lds_tr16(const uint16_t* p) {
-  const v4s_t r = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-      (__attribute__((address_space(3))) v4s_t*)(p));
-  return __builtin_bit_cast(uint2, r);
-}
-
-// 16-B chunk swizzle of the V image (rows of D bf16)
-template <int NCH>
-__device__ __forceinline__ int v_swz(int t) {
-  if constexpr (NCH >= 16) return ((t & 3) << 2) | ((t >> 2) & 3);
-  else return ((t & 3) << 1) | ((t >> 2) & 1);
-}
-
 constexpr int kPrefillBK = 64;   // kv tokens per tile
 constexpr int kPStride = 72;     // per-wave P tile row stride
+constexpr int kVtStride = 72;    // V^T image row stride (64 tokens + 8 pad)
 
 template <int D, int G>
 __global__ __launch_bounds__(256) void prefill_attn_kernel(
@@ -65,7 +50,7 @@ __global__ __launch_bounds__(256) void prefill_attn_kernel(
   constexpr int SWZ = (NCH >= 16) ? 15 : (NCH - 1);
 
   __shared__ __attribute__((aligned(16))) uint16_t Ks[kPrefillBK * D];
-  __shared__ __attribute__((aligned(16))) uint16_t Vs[kPrefillBK * D];
+  __shared__ __attribute__((aligned(16))) uint16_t Vs[D * kVtStride];   // V^T [D][64 tok]
   __shared__ __attribute__((aligned(16))) uint16_t Ps[4][16 * kPStride];
 
   const int tile = blockIdx.x;
@@ -116,23 +101,39 @@ __global__ __launch_bounds__(256) void prefill_attn_kernel(
   const int* bt = block_tables + (size_t)b * bt_stride;
   const size_t head_off = (size_t)kvh * block_size * D;
   const size_t blk_stride = (size_t)nkv * block_size * D;
+  const int vt_tb = min(block_size, kPrefillBK);   // tokens of one block inside a tile
+  const int vt_cpr = vt_tb / 8;                     // 16-B chunks per V^T row and block
 
   for (int kt = 0; kt < ntiles; ++kt) {
     const int kbase = kt * kPrefillBK;
-    // ---- stage K and V (swizzled rows) --------------------------------------------
+    // ---- stage K (swizzled rows) and V^T (padded dim rows) ---------------------------
     for (int idx = threadIdx.x; idx < kPrefillBK * NCH; idx += 256) {
       const int t = idx / NCH, ch = idx - (idx / NCH) * NCH;
       const int p = kbase + t;
-      uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
+      uint4 kv = make_uint4(0, 0, 0, 0);
       if (p < kv_end) {
         const int blk = bt[p / block_size];
         const int off = p - (p / block_size) * block_size;
-        const size_t a = blk * blk_stride + head_off + (size_t)off * D + ch * 8;
-        kv = *reinterpret_cast<const uint4*>(k_cache + a);
-        vv = *reinterpret_cast<const uint4*>(v_cache + a);
+        kv = *reinterpret_cast<const uint4*>(k_cache + blk * blk_stride + head_off +
+                                             (size_t)off * D + ch * 8);
       }
       reinterpret_cast<uint4*>(Ks + t * D)[ch ^ (t & SWZ)] = kv;
-      reinterpret_cast<uint4*>(Vs + t * D)[ch ^ v_swz<NCH>(t)] = vv;
+    }
+    // V^T: item = (block j of the tile, dim d, 8-token chunk cc); consecutive lanes
+    // read consecutive 16 B of a transposed block
+    for (int idx = threadIdx.x; idx < kPrefillBK * NCH; idx += 256) {
+      const int cc = idx % vt_cpr, rest = idx / vt_cpr;
+      const int d = rest % D, j = rest / D;
+      const int t = j * vt_tb + cc * 8;  // first token of the chunk within the tile
+      const int p = kbase + t;
+      uint4 vv = make_uint4(0, 0, 0, 0);
+      if (p < kv_end) {
+        const int blk = bt[p / block_size];
+        const int off = p - (p / block_size) * block_size;
+        vv = *reinterpret_cast<const uint4*>(v_cache + blk * blk_stride + head_off +
+                                             (size_t)d * block_size + off);
+      }
+      *reinterpret_cast<uint4*>(Vs + d * kVtStride + t) = vv;
     }
     __syncthreads();
 
@@ -194,14 +195,11 @@ __global__ __launch_bounds__(256) void prefill_attn_kernel(
 #pragma unroll
     for (int kc = 0; kc < 2; ++kc) {
       const uint4 pa = *reinterpret_cast<const uint4*>(pw + l15 * kPStride + kc * 32 + 8 * lg);
-      const int qq = l15 >> 2, pp = l15 & 3;
-      const int ra = kc * 32 + 8 * lg + qq, rb = ra + 4;
 #pragma unroll
       for (int nd = 0; nd < ND; ++nd) {
-        const int ch = 2 * nd + (pp >> 1);
-        const uint2 va = lds_tr16(Vs + ra * D + (ch ^ v_swz<NCH>(ra)) * 8 + 4 * (pp & 1));
-        const uint2 vb2 = lds_tr16(Vs + rb * D + (ch ^ v_swz<NCH>(rb)) * 8 + 4 * (pp & 1));
-        const uint4 vb = make_uint4(va.x, va.y, vb2.x, vb2.y);
+        // B operand: tokens kc*32 + 8 lg .. +8 of head dim nd*16 + l15
+        const uint4 vb = *reinterpret_cast<const uint4*>(Vs + (nd * 16 + l15) * kVtStride +
+                                                         kc * 32 + 8 * lg);
         o[nd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(pa), as_frag(vb), o[nd], 0, 0, 0);
       }
     }

@@ -207,8 +207,10 @@ __global__ __launch_bounds__(256) void slab_rope_kv_kernel(
       src.load8(t, (nq + nkv) * D + kh * D + c * 8, f);
 #pragma unroll
       for (int j = 0; j < 8; ++j) f[j] *= rs;
-      uint16_t* vp = v_cache + (((size_t)blk * nkv + kh) * block_size + off) * D;
-      *reinterpret_cast<uint4*>(vp + c * 8) = store8(f);
+      // V blocks are transposed ([D][block_size], rope_kv.hip)
+      uint16_t* vp = v_cache + (((size_t)blk * nkv + kh) * D + c * 8) * block_size + off;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) vp[j * block_size] = f32_to_bf16(f[j]);
     }
   }
 }

@@ -9,9 +9,11 @@
 // scaling included) as fp32 [max_pos, D] = [cos(D/2) | sin(D/2)], so the kernel
 // does no transcendental math (Appendix B "Element-wise": trig tables on host).
 //
-// Cache layout: [num_blocks, n_kv_heads, block_size, D] so that one (block,
-// head) tile is a contiguous block_size*D*2-byte run (decode/prefill attention
-// stream it with 16-B lane loads).
+// Cache layouts: K [num_blocks, n_kv_heads, block_size, D] (token rows) and V
+// [num_blocks, n_kv_heads, D, block_size] (TRANSPOSED: dim rows), so one (block,
+// head) tile of either is a contiguous block_size*D*2-byte run and both MFMA
+// operands of the attention kernels load straight from it: K rows are the A
+// operand of QK^T, V^T rows (consecutive tokens of one dim) the B operand of PV.
 #include "ft_common.h"
 
 namespace ft {
@@ -73,8 +75,15 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(uint16_t* __restrict__ qkv
     const uint4* vsrc = reinterpret_cast<const uint4*>(row + (nq + nkv) * D);
     for (int item = threadIdx.x; item < nv; item += blockDim.x) {
       const int kh = item / (D / 8), c = item - kh * (D / 8);
-      uint16_t* vp = v_cache + (((size_t)blk * nkv + kh) * block_size + off) * D;
-      reinterpret_cast<uint4*>(vp)[c] = vsrc[item];
+      // V blocks are transposed ([D][block_size]): dims c*8.. of this token
+      uint16_t* vp = v_cache + (((size_t)blk * nkv + kh) * D + c * 8) * block_size + off;
+      const uint4 v = vsrc[item];
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        vp[(2 * j) * block_size] = (uint16_t)(w[j] & 0xffffu);
+        vp[(2 * j + 1) * block_size] = (uint16_t)(w[j] >> 16);
+      }
     }
   }
 }

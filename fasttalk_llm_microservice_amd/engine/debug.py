@@ -6,9 +6,11 @@ env hooks (FT_FAULT_*) for tests").
   wraps that many engine steps (after skipping some) in ``torch.profiler`` with
   CPU + GPU activities and writes a Chrome trace (viewable in Perfetto); for
   kernel-level counters use ``rocprofv3 --kernel-trace --stats`` instead.
-* ``FT_FAULT_STEP=<n>`` raises inside the n-th engine step (once);
-  ``FT_FAULT_KIND=runtime|oom`` picks a recoverable RuntimeError or a fatal
-  MemoryError, which exercises the AsyncEngine error path and ``/health``.
+* ``FT_FAULT_STEP=<n>`` raises inside the n-th engine step (and the
+  ``FT_FAULT_REPEAT - 1`` steps after it); ``FT_FAULT_KIND=runtime|oom|device``
+  picks a recoverable RuntimeError, a fatal MemoryError, or a RuntimeError with
+  the text of a sticky HIP fault (fatal), which exercises the AsyncEngine error
+  path and ``/health``.
 """
 from __future__ import annotations
 
@@ -60,14 +62,18 @@ class FaultInjector:
     def __init__(self):
         self.at: Optional[int] = int(os.environ["FT_FAULT_STEP"]) if os.environ.get("FT_FAULT_STEP") else None
         self.kind = os.environ.get("FT_FAULT_KIND", "runtime")
+        self.repeat = max(1, int(os.environ.get("FT_FAULT_REPEAT", "1")))
         self._n = 0
 
     def check(self):
         if self.at is None:
             return
         self._n += 1
-        if self._n == self.at:
-            self.at = None
+        if self.at <= self._n < self.at + self.repeat:
+            if self._n == self.at + self.repeat - 1:
+                self.at = None
             if self.kind == "oom":
                 raise MemoryError("FT_FAULT: injected out-of-memory in engine step")
+            if self.kind == "device":
+                raise RuntimeError("FT_FAULT: HIP error: an illegal memory access was encountered")
             raise RuntimeError("FT_FAULT: injected failure in engine step")

@@ -195,6 +195,15 @@ class LLMEngine:
         """Forget a queued decode step (after a failed step)."""
         self._inflight = None
 
+    def fail_unfinished(self, error: str):
+        """After a failed step: every unfinished sequence ends with an error and
+        gives back its KV blocks and host swap slots -- swapped-out ones too (if
+        the failing step was the swap itself their host copies may be garbage)."""
+        self.reset_inflight()
+        sched = self.scheduler
+        for seq in list(sched.running) + list(sched.waiting) + list(sched.swapped):
+            self._finalize(seq, "error", emit=True, error=error)
+
     def _step(self) -> List[RequestOutput]:
         if self._inflight is not None:
             return self._step_pipelined()
@@ -412,6 +421,12 @@ class AsyncEngine:
         self._ids = itertools.count()
         self.error: Optional[BaseException] = None
         self.heartbeat = time.time()
+        self._fail_streak = 0
+        # consecutive failed steps after which the engine is declared broken even
+        # when each failure looked recoverable (ENGINE_MAX_FAIL_STREAK)
+        import os as _os
+
+        self.max_fail_streak = int(_os.environ.get("ENGINE_MAX_FAIL_STREAK", "3"))
 
     @classmethod
     def from_config(cls, cfg: EngineConfig) -> "AsyncEngine":
@@ -492,17 +507,38 @@ class AsyncEngine:
             except Exception as e:  # surfaced through health / streams (FT_FAULT_* tests)
                 log.exception("engine step failed")
                 self.error = e
-                eng.reset_inflight()
-                for seq in list(eng.scheduler.running) + list(eng.scheduler.waiting):
-                    eng._finalize(seq, "error", emit=True, error=str(e))
+                eng.fail_unfinished(str(e))
                 self._flush()
-                self.error = None if self._recoverable(e) else e
+                self._fail_streak += 1
+                fatal = not self._recoverable(e) or self._fail_streak >= self.max_fail_streak
+                self.error = e if fatal else None
                 continue
+            self._fail_streak = 0
             self._flush()
 
-    @staticmethod
-    def _recoverable(e: BaseException) -> bool:
-        return not isinstance(e, (MemoryError,))
+    # RuntimeError texts of device faults that leave the HIP context unusable
+    _FATAL_DEVICE_ERRORS = ("illegal memory access", "illegal instruction", "hipErrorLaunchFailure",
+                            "unspecified launch failure", "device-side assert", "HIP error: an illegal",
+                            "hipErrorIllegalAddress", "memory access fault", "out of memory",
+                            "hipErrorOutOfMemory", "GPU hang", "hipErrorECCNotCorrectable")
+
+    @classmethod
+    def _recoverable(cls, e: BaseException) -> bool:
+        """A step failure that only failed its own requests (bad input, a transient
+        host error) vs one after which the device cannot be trusted: host OOM,
+        device OOM (torch.cuda.OutOfMemoryError) and sticky HIP faults are fatal,
+        so /health turns unhealthy instead of every later step failing silently."""
+        if isinstance(e, MemoryError):
+            return False
+        try:
+            import torch
+
+            if isinstance(e, torch.cuda.OutOfMemoryError):
+                return False
+        except Exception:  # pragma: no cover
+            pass
+        msg = str(e)
+        return not any(pat in msg for pat in cls._FATAL_DEVICE_ERRORS)
 
     def _handle(self, cmd):
         kind = cmd[0]

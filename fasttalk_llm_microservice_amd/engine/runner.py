@@ -130,11 +130,13 @@ class ModelRunner:
         self._stg_next = 0
         self.h_out = torch.zeros(mb, dtype=i32, pin_memory=pin)  # eager-step sampler output
         self.d_logits_idx = torch.arange(mb, dtype=torch.int64, device=dv)
-        # split-K workspace sized for the largest (batch x splits) any bucket uses
-        rows = max(b * self._splits_for_batch(b) for b in self.graph_sizes + [mb])
-        self.tmp_rows = rows
-        self.tmp_out = torch.empty(rows * nq * d, dtype=torch.float32, device=dv)
-        self.tmp_ml = torch.empty(rows * nq * 2, dtype=torch.float32, device=dv)
+        # decode-attention partials: one slot per (sequence, kv head) + one per wave
+        # of the kernel's grid (any step has at most max_num_seqs decode rows)
+        self.max_decode_rows = max(mb, cfg.max_num_seqs)
+        n_out, n_ml = ops.decode_workspace(self.max_decode_rows, nq, self.model.nkv, d,
+                                           waves=None if self.is_gpu else 0)
+        self.tmp_out = torch.empty(max(1, n_out), dtype=torch.float32, device=dv)
+        self.tmp_ml = torch.empty(max(1, n_ml), dtype=torch.float32, device=dv)
         self._done_event = torch.cuda.Event() if self.is_gpu else None
         self.graphs: Dict[int, torch.cuda.CUDAGraph] = {}
         self.graph_pool = None
@@ -207,9 +209,6 @@ class ModelRunner:
         return n
 
     # ------------------------------------------------------------------ helpers
-    def _splits_for_batch(self, b: int) -> int:
-        return ops.decode_splits(b, self.model.nkv, self.max_model_len)
-
     def _bucket(self, b: int) -> Optional[int]:
         for s in self.graph_sizes:
             if s >= b:
@@ -318,24 +317,16 @@ class ModelRunner:
             q_start_loc=t(qsl) if self.is_gpu else torch.from_numpy(qsl),
             tile_info=t(host["tiles"]), num_tiles=host["num_tiles"])
         if nd:
-            splits = self._splits_for_batch(nd)
+            if nd > self.max_decode_rows:
+                raise ValueError(f"{nd} decode rows exceed max_num_seqs {self.max_decode_rows}")
             meta.dec_block_tables = t(host["d_bt"])
             meta.dec_seq_lens = t(host["d_sl"])
-            meta.max_splits = splits
-            meta.tmp_out, meta.tmp_ml = self._tmp(nd, splits)
+            meta.tmp_out, meta.tmp_ml = self.tmp_out, self.tmp_ml
         input_ids = t(host["ids"])
         h = self.model.forward(input_ids, meta, self.kv)
         if len(host["lrows"]) == 0:
             return []
         return self._sample(h, host["sampling"], masks)
-
-    def _tmp(self, n: int, splits: int):
-        nq, d = self.model.nq, self.model.d
-        if n * splits > self.tmp_rows:
-            dv = self.device
-            return (torch.empty(n * nq * splits * d, dtype=torch.float32, device=dv),
-                    torch.empty(n * nq * splits * 2, dtype=torch.float32, device=dv))
-        return self.tmp_out, self.tmp_ml
 
     def _wait(self, ev=None):
         """Block until the GPU work queued so far (or up to ``ev``) is done WITHOUT
@@ -376,7 +367,7 @@ class ModelRunner:
         n = len(seqs)
         bucket = self._bucket(n) if (self.use_graphs and masks is None) else None
         if bucket is None:
-            return self._decode_eager(seqs, self._splits_for_batch(n), masks)
+            return self._decode_eager(seqs, masks)
         return self.decode_collect(self.decode_launch(seqs))
 
     def can_pipeline(self, n: int) -> bool:
@@ -430,11 +421,11 @@ class ModelRunner:
         st.hf[:n] = temp
         st.hf[mb:mb + n] = topp
         st.hseed[:n] = seeds
-        if nb > n:  # padding rows: no KV write, 1-token context, greedy
+        if nb > n:  # padding rows: no KV write, empty context (no attention work), greedy
             ids[n:nb] = 0
             pos[n:nb] = 0
             slots[n:nb] = -1
-            sl[n:nb] = 1
+            sl[n:nb] = 0
             bt[n:nb, 0] = 0
             hs[4 * mb + n:4 * mb + nb] = 0
             hs[5 * mb + n:5 * mb + nb] = 0
@@ -485,15 +476,15 @@ class ModelRunner:
             raise ValueError(f"unknown TP message {kind!r}")
         return True
 
-    def _decode_meta(self, nb: int, splits: int) -> AttnMeta:
-        assert nb * splits <= self.tmp_rows
+    def _decode_meta(self, nb: int) -> AttnMeta:
+        assert nb <= self.max_decode_rows
         return AttnMeta(positions=self.d_positions[:nb], slot_mapping=self.d_slots[:nb],
                         logits_indices=self.d_logits_idx[:nb], num_decode=nb,
                         dec_block_tables=self.d_bt[:nb], dec_seq_lens=self.d_seq_lens[:nb],
-                        max_splits=splits, tmp_out=self.tmp_out, tmp_ml=self.tmp_ml)
+                        tmp_out=self.tmp_out, tmp_ml=self.tmp_ml)
 
     def _graph_body(self, nb: int):
-        meta = self._decode_meta(nb, self._splits_for_batch(nb))
+        meta = self._decode_meta(nb)
         h = self.model.forward(self.d_input_ids[:nb], meta, self.kv)
         logits = self.model.compute_logits(h)
         ops.sample(logits, self.d_temp[:nb], self.d_top_p[:nb], self.d_top_k[:nb],
@@ -501,10 +492,10 @@ class ModelRunner:
 
     def _capture(self, nb: int):
         t0 = time.time()
-        # inputs must be valid for the warm-up/capture run: no KV writes, 1-token contexts
+        # inputs must be valid for the warm-up/capture run: no KV writes, empty contexts
         saved = (self.d_slots[:nb].clone(), self.d_seq_lens[:nb].clone())
         self.d_slots[:nb].fill_(-1)
-        self.d_seq_lens[:nb].fill_(1)
+        self.d_seq_lens[:nb].fill_(0)
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):
@@ -522,7 +513,7 @@ class ModelRunner:
         log.info("captured decode graph batch=%d in %.2fs", nb, time.time() - t0)
         return g
 
-    def _decode_eager(self, seqs, splits, masks) -> List[int]:
+    def _decode_eager(self, seqs, masks) -> List[int]:
         self.stats["eager_decode"] += 1
         from .scheduler import ScheduledBatch as _SB
 

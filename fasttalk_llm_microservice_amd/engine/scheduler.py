@@ -204,6 +204,9 @@ class Scheduler:
             self.host.release(seq.host_slots)
             seq.host_slots = []
             seq.block_ids = list(hit) + new
+            # the restored blocks are fresh (unhashed) device blocks: let the next
+            # post_step commit them to the prefix cache again
+            seq.num_committed_blocks = len(hit)
             seq.status = SeqStatus.RUNNING
             self.swapped.popleft()
             self.running.append(seq)

@@ -3,7 +3,7 @@ reference talks to over HTTP: ``app/core/vllm_handler.py:53-62``).
 
 Per layer:  fused add+RMSNorm (K2, HIP) -> QKV GEMM (K3,
 hipBLASLt) -> RoPE + paged KV write (K4, HIP) -> prefill flash attention (K5,
-HIP/MFMA) or paged split-K decode attention (K6, HIP) -> O GEMM (K7) [+ RCCL
+HIP/MFMA) or paged MFMA decode attention (K6, HIP) -> O GEMM (K7) [+ RCCL
 all-reduce under TP] -> fused add+RMSNorm -> gate_up GEMM (K8) -> SiLU-mul
 (K9, HIP) -> down GEMM (K10) [+ all-reduce].  Only the last-token rows reach the
 final norm and the LM head (K11), and the sampler (K12) consumes bf16 logits
@@ -42,8 +42,7 @@ class AttnMeta:
     # decode rows
     dec_block_tables: Optional[torch.Tensor] = None   # [num_decode, max_blocks]
     dec_seq_lens: Optional[torch.Tensor] = None       # [num_decode]
-    max_splits: int = 1
-    tmp_out: Optional[torch.Tensor] = None
+    tmp_out: Optional[torch.Tensor] = None            # decode partials (ops.decode_workspace)
     tmp_ml: Optional[torch.Tensor] = None
     # prefill rows
     block_tables: Optional[torch.Tensor] = None       # [P, max_blocks]
@@ -513,12 +512,19 @@ class LlamaModel:
 
     # ------------------------------------------------------------------ KV cache
     def kv_cache_shape(self, num_blocks: int, block_size: int) -> Tuple[int, ...]:
+        """K cache shape; the V cache holds the same blocks transposed
+        ([num_blocks, nkv, D, block_size]) so both MFMA operands of the attention
+        kernels load straight from HBM (csrc/kernels/attn_decode.hip)."""
         return (num_blocks, self.nkv, block_size, self.d)
 
+    def v_cache_shape(self, num_blocks: int, block_size: int) -> Tuple[int, ...]:
+        return (num_blocks, self.nkv, self.d, block_size)
+
     def allocate_kv_cache(self, num_blocks: int, block_size: int):
-        shp = self.kv_cache_shape(num_blocks, block_size)
-        return [(torch.zeros(shp, dtype=self.dtype, device=self.device),
-                 torch.zeros(shp, dtype=self.dtype, device=self.device))
+        ks = self.kv_cache_shape(num_blocks, block_size)
+        vs = self.v_cache_shape(num_blocks, block_size)
+        return [(torch.zeros(ks, dtype=self.dtype, device=self.device),
+                 torch.zeros(vs, dtype=self.dtype, device=self.device))
                 for _ in range(self.cfg.num_layers)]
 
     # ------------------------------------------------------------------ forward
@@ -532,7 +538,7 @@ class LlamaModel:
         if nd > 0:
             ops.decode_attention(attn[:nd], qkv[:nd], kc, vc, meta.dec_block_tables,
                                  meta.dec_seq_lens, meta.tmp_out, meta.tmp_ml, nq, nkv, d,
-                                 meta.max_splits, self.scale)
+                                 self.scale)
         if t > nd:
             ops.prefill_attention(attn[nd:], qkv[nd:], kc, vc, meta.block_tables, meta.seq_lens,
                                   meta.q_start_loc, meta.tile_info, meta.num_tiles, nq, nkv, d,

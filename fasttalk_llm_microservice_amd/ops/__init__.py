@@ -113,20 +113,15 @@ def rope_kv_write(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, nq, n
                           head_dim)
 
 
-def decode_partition_size() -> int:
-    """Max tokens per decode partition (the online-softmax kernel has no bound)."""
-    return 1 << 30
-
-
-def decode_splits(batch: int, nkv: int, max_model_len: int = 0, target_blocks: int = 256) -> int:
-    """Split-K factor for the paged decode kernel: the smallest power of two that
-    gives ``target_blocks`` workgroups (4 waves each), so small batches still fill
-    the 256 CUs while large batches skip the combine pass entirely."""
-    want = max(1, target_blocks // max(1, batch * nkv))
-    s = 1
-    while s < want:
-        s *= 2
-    return int(min(64, s))
+def decode_workspace(batch: int, nq: int, nkv: int, head_dim: int, waves: Optional[int] = None):
+    """(tmp_out, tmp_ml) element counts of the decode kernel's partial workspace:
+    one fp32 slot per (sequence, kv head) plus one per wave of the grid
+    (csrc/kernels/attn_decode.hip), each holding the G = nq / nkv heads."""
+    if waves is None:
+        waves = native().decode_waves() if native_available() else 0
+    slots = batch * nkv + waves
+    g = nq // nkv
+    return slots * g * head_dim, slots * g * 2
 
 
 def prefill_tile_tokens(nq: int, nkv: int) -> int:
@@ -134,11 +129,12 @@ def prefill_tile_tokens(nq: int, nkv: int) -> int:
 
 
 def decode_attention(out, q, k_cache, v_cache, block_tables, seq_lens, tmp_out, tmp_ml, nq, nkv,
-                     head_dim, max_splits, scale):
-    """out[b] = attention of the single new query of sequence b (q: [B, >=nq*D] rows)."""
+                     head_dim, scale):
+    """out[b] = attention of the single new query of sequence b (q: [B, >=nq*D] rows).
+    k_cache [blocks, nkv, bs, D]; v_cache [blocks, nkv, D, bs] (transposed blocks)."""
     if q.is_cuda:
         native().paged_decode_attention(out, q, k_cache, v_cache, block_tables, seq_lens, tmp_out,
-                                        tmp_ml, nq, nkv, head_dim, max_splits, scale)
+                                        tmp_ml, nq, nkv, head_dim, scale)
         return out
     b = q.shape[0]
     qq = q[:, : nq * head_dim].reshape(b, nq, head_dim)

@@ -88,10 +88,13 @@ def rope_kv_write(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, nq, n
         s = slots[keep]
         blk, off = s // bs, s % bs
         k_cache[blk, :, off, :] = kr[keep]
-        v_cache[blk, :, off, :] = v[keep]
+        v_cache[blk, :, :, off] = v[keep]   # V blocks are transposed: [blocks, nkv, D, bs]
 
 
-def _gather_kv(cache, table_row, length):
+def _gather_kv(cache, table_row, length, transposed: bool = False):
+    """[length, H, D] rows of one sequence; ``transposed``: V blocks [H, D, bs]."""
+    if transposed:
+        cache = cache.transpose(2, 3)
     bs = cache.shape[2]
     nblk = (length + bs - 1) // bs
     blocks = table_row[:nblk].long()
@@ -102,7 +105,8 @@ def _gather_kv(cache, table_row, length):
 
 def paged_attention(q: torch.Tensor, k_cache, v_cache, block_tables, seq_lens, q_start_loc,
                     scale: float) -> torch.Tensor:
-    """Causal varlen attention over the paged cache.
+    """Causal varlen attention over the paged cache (K blocks [nkv, bs, D], V
+    blocks transposed [nkv, D, bs]).
 
     q: [T, nq, D] (new tokens of every sequence, packed by q_start_loc)
     Each sequence b attends to kv positions [0, seq_lens[b]); its new tokens
@@ -120,7 +124,7 @@ def paged_attention(q: torch.Tensor, k_cache, v_cache, block_tables, seq_lens, q
             continue
         L = sl[b]
         k = _gather_kv(k_cache, block_tables[b], L).float()  # [L, nkv, D]
-        v = _gather_kv(v_cache, block_tables[b], L).float()
+        v = _gather_kv(v_cache, block_tables[b], L, transposed=True).float()
         qq = q[q0:q1].float()  # [ql, nq, D]
         ql = q1 - q0
         k = k.repeat_interleave(g, dim=1)

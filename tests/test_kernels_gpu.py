@@ -53,8 +53,9 @@ def test_silu_mul():
 
 
 def _alloc_cache(nblocks, nkv, bs, d):
+    """K blocks [nkv, bs, d]; V blocks transposed [nkv, d, bs] (the engine's layout)."""
     k = torch.randn(nblocks, nkv, bs, d, device=DEV).bfloat16()
-    v = torch.randn(nblocks, nkv, bs, d, device=DEV).bfloat16()
+    v = torch.randn(nblocks, nkv, d, bs, device=DEV).bfloat16()
     return k, v
 
 
@@ -91,28 +92,48 @@ def _random_tables(lens, bs, nblocks_total):
     return bt
 
 
-@pytest.mark.parametrize("nq,nkv,d", [(32, 8, 128), (64, 8, 128), (8, 8, 128), (24, 8, 128),
-                                      (32, 8, 64)])
-@pytest.mark.parametrize("splits", [None, 3, 32])
-def test_decode_attention(nq, nkv, d, splits):
-    bs = 16
-    lens = [1, 17, 255, 256, 257, 1000, 2100]
+def _decode_case(lens, nq, nkv, d, bs=16, seed=0):
+    torch.manual_seed(seed)
     nblocks = sum((l + bs - 1) // bs for l in lens) + 4
     k, v = _alloc_cache(nblocks, nkv, bs, d)
     bt = _random_tables(lens, bs, nblocks).to(DEV)
     sl = torch.tensor(lens, dtype=torch.int32, device=DEV)
     b = len(lens)
     q = torch.randn(b, nq * d, device=DEV).bfloat16()
-    part = ops.decode_partition_size()
-    max_splits = splits or math.ceil(max(lens) / part)
-    tmp_out = torch.empty(b * nq * max_splits * d, device=DEV)
-    tmp_ml = torch.empty(b * nq * max_splits * 2, device=DEV)
-    out = torch.zeros(b, nq * d, device=DEV).bfloat16()
+    n_out, n_ml = ops.decode_workspace(b, nq, nkv, d)
+    tmp_out = torch.full((n_out,), float("nan"), device=DEV)
+    tmp_ml = torch.full((n_ml,), float("nan"), device=DEV)
+    out = torch.full((b, nq * d), float("nan"), device=DEV).bfloat16()
     scale = d ** -0.5
-    ops.decode_attention(out, q, k, v, bt, sl, tmp_out, tmp_ml, nq, nkv, d, max_splits, scale)
+    ops.decode_attention(out, q, k, v, bt, sl, tmp_out, tmp_ml, nq, nkv, d, scale)
     expect = ref.paged_attention(q.view(b, nq, d), k, v, bt, sl,
                                  torch.arange(b + 1, dtype=torch.int32), scale).view(b, nq * d)
+    return out, expect
+
+
+@pytest.mark.parametrize("nq,nkv,d", [(32, 8, 128), (64, 8, 128), (8, 8, 128), (24, 8, 128),
+                                      (32, 8, 64), (8, 1, 128), (16, 8, 128)])
+def test_decode_attention(nq, nkv, d):
+    # lengths around tile / block edges; one long sequence spreads over many waves
+    out, expect = _decode_case([1, 17, 255, 256, 257, 1000, 2100], nq, nkv, d)
     _close(out, expect, atol=2e-2, rtol=2e-2, msg="decode attention")
+
+
+@pytest.mark.parametrize("b,max_len", [(1, 8192), (50, 6000), (64, 8192), (256, 700)])
+def test_decode_attention_serving_shapes(b, max_len):
+    """Headline shapes: ragged contexts up to max_model_len at the 50/64-row buckets."""
+    g = torch.Generator().manual_seed(b)
+    lens = torch.randint(max(1, max_len // 4), max_len + 1, (b,), generator=g).tolist()
+    lens[0] = max_len
+    out, expect = _decode_case(lens, 32, 8, 128, seed=b)
+    assert torch.isfinite(out.float()).all()
+    _close(out, expect, atol=2e-2, rtol=2e-2, msg=f"decode attention b={b}")
+
+
+@pytest.mark.parametrize("bs", [32, 64])
+def test_decode_attention_block_sizes(bs):
+    out, expect = _decode_case([5, 64, 300, 1025], 32, 8, 128, bs=bs)
+    _close(out, expect, atol=2e-2, rtol=2e-2, msg=f"decode attention bs={bs}")
 
 
 @pytest.mark.parametrize("nq,nkv,d", [(32, 8, 128), (24, 8, 128), (64, 8, 128), (32, 8, 64),

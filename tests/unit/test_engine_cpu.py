@@ -27,7 +27,7 @@ def test_reference_paged_attention_matches_dense():
     lens, qlens = [7, 13], [3, 13]
     nblk = sum(math.ceil(x / bs) for x in lens)
     kc = torch.randn(nblk, nkv, bs, d)
-    vc = torch.randn(nblk, nkv, bs, d)
+    vc = torch.randn(nblk, nkv, d, bs)   # V blocks transposed
     bt = torch.zeros(2, 4, dtype=torch.int32)
     bt[0, :2] = torch.tensor([3, 0])
     bt[1, :4] = torch.tensor([1, 2, 4, 5])
@@ -36,7 +36,7 @@ def test_reference_paged_attention_matches_dense():
     out = ref.paged_attention(q, kc, vc, bt, torch.tensor(lens), qsl, d ** -0.5)
     for b in range(2):
         k = ref._gather_kv(kc, bt[b], lens[b]).repeat_interleave(nq // nkv, 1)
-        v = ref._gather_kv(vc, bt[b], lens[b]).repeat_interleave(nq // nkv, 1)
+        v = ref._gather_kv(vc, bt[b], lens[b], transposed=True).repeat_interleave(nq // nkv, 1)
         qq = q[qsl[b]:qsl[b + 1]].transpose(0, 1)
         L, ql = lens[b], qlens[b]
         mask = torch.ones(ql, L, dtype=torch.bool).tril(L - ql)
@@ -53,14 +53,14 @@ def test_reference_rope_and_kv_write():
     qkv = torch.randn(3, (nq + 2 * nkv) * d)
     orig = qkv.clone()
     kc = torch.zeros(4, nkv, bs, d)
-    vc = torch.zeros(4, nkv, bs, d)
+    vc = torch.zeros(4, nkv, d, bs)
     pos = torch.tensor([0, 5, 9], dtype=torch.int32)
     slots = torch.tensor([1, 6, 13], dtype=torch.int32)
     ref.rope_kv_write(qkv, pos, cs, slots, kc, vc, nq, nkv, d)
     # position 0 leaves q unrotated; v is copied verbatim
     torch.testing.assert_close(qkv[0, : nq * d], orig[0, : nq * d])
     v_src = orig[2, (nq + nkv) * d:].view(nkv, d)
-    torch.testing.assert_close(vc[13 // bs, :, 13 % bs], v_src)
+    torch.testing.assert_close(vc[13 // bs, :, :, 13 % bs], v_src)  # V blocks transposed
     # rotation preserves the norm of every head
     qn = qkv[1, : nq * d].view(nq, d).norm(dim=-1)
     torch.testing.assert_close(qn, orig[1, : nq * d].view(nq, d).norm(dim=-1))

@@ -1,6 +1,7 @@
 """Failure detection and tracing hooks: an injected step failure
 fails only the in-flight requests and the engine keeps serving; a fatal one
-(MemoryError) turns /health unhealthy; FT_PROFILE writes a torch.profiler trace."""
+(MemoryError, a sticky HIP fault, or a streak of failing steps) turns /health
+unhealthy; FT_PROFILE writes a torch.profiler trace."""
 import asyncio
 import glob
 import os
@@ -62,3 +63,41 @@ def test_profiler_trace(monkeypatch, tmp_path):
     eng.generate([[1, 2, 3]], SamplingParams(temperature=0, max_tokens=5, ignore_eos=True))
     traces = glob.glob(os.path.join(tmp_path, "engine_steps_*.json"))
     assert traces and os.path.getsize(traces[0]) > 0
+
+
+@pytest.mark.parametrize("kind,repeat", [("device", 1), ("runtime", 3)])
+def test_device_fault_or_failure_streak_marks_unhealthy(monkeypatch, kind, repeat):
+    monkeypatch.setenv("FT_FAULT_STEP", "2")
+    monkeypatch.setenv("FT_FAULT_KIND", kind)
+    monkeypatch.setenv("FT_FAULT_REPEAT", str(repeat))
+    eng = _async_engine()
+    try:
+        for _ in range(repeat):
+            out = asyncio.run(_collect(eng, [1, 2, 3], 10))
+            assert out[-1].finish_reason == "error"
+        assert not eng.is_healthy()
+        assert eng.engine.bm.num_free() == eng.engine.bm.num_blocks
+    finally:
+        eng.shutdown()
+
+
+def test_failure_streak_resets_after_a_good_step(monkeypatch):
+    monkeypatch.setenv("FT_FAULT_STEP", "2")
+    monkeypatch.setenv("FT_FAULT_REPEAT", "2")
+    eng = _async_engine()
+    try:
+        for _ in range(2):
+            assert asyncio.run(_collect(eng, [1, 2, 3], 10))[-1].finish_reason == "error"
+        assert eng.is_healthy()
+        assert asyncio.run(_collect(eng, [4, 5], 4))[-1].finish_reason == "length"
+        assert eng._fail_streak == 0 and eng.is_healthy()
+    finally:
+        eng.shutdown()
+
+
+def test_classifies_device_oom_as_fatal():
+    import torch
+
+    assert not AsyncEngine._recoverable(torch.cuda.OutOfMemoryError("HIP out of memory"))
+    assert not AsyncEngine._recoverable(RuntimeError("HIP error: an illegal memory access"))
+    assert AsyncEngine._recoverable(ValueError("prompt too long"))

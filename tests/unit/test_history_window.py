@@ -1,0 +1,108 @@
+"""Engine history window with hysteresis.
+
+``ConversationManager`` trims to ``max_history_length`` messages exactly like the
+reference (``/root/reference/app/core/conversation_manager.py:34-53``); past the
+cap the API history slides by one message per message, which would change the
+token prefix right after the system block every turn.  ``NativeHandler`` keeps
+an engine window that is a suffix of the API history and cuts it in chunks, so
+the engine's prefix cache keeps matching across turns."""
+import random
+
+from app.core.conversation_manager import ConversationManager
+from app.core.native_handler import NativeHandler
+from fasttalk_llm_microservice_amd.engine.chat_template import ChatTemplate
+from fasttalk_llm_microservice_amd.engine.tokenizer import get_tokenizer
+
+BS = 16
+
+
+class _Cfg:
+    max_history_length = 50
+
+
+class _FakeEngine:
+    def __init__(self):
+        self.tokenizer = get_tokenizer(None)
+        self.template = ChatTemplate(self.tokenizer)
+        self.max_model_len = 8192
+        self.model_cfg = type("M", (), {"name": "fake"})()
+
+
+def _lcp(a, b):
+    n = 0
+    for x, y in zip(a, b):
+        if x != y:
+            break
+        n += 1
+    return n
+
+
+def _simulate(turns, sessions=12, seed=0):
+    h = NativeHandler(_Cfg(), engine=_FakeEngine())
+    cm = ConversationManager(max_history_length=50)
+    rng = random.Random(seed)
+    words = "the voice assistant should answer quickly about weather news music travel".split()
+    cached = total = 0
+    per_turn = []
+    prev = {}
+    for s in range(sessions):
+        cm.create_session(f"s{s}", "You are a helpful voice assistant.")
+    for t in range(turns):
+        turn_cached = turn_total = 0
+        for s in range(sessions):
+            sid = f"s{s}"
+            cm.add_user_message(sid, " ".join(rng.choice(words) for _ in range(40)) + "?")
+            msgs = cm.get_messages_for_generation(sid)
+            ids = h.build_prompt(msgs, 128, session_id=sid)
+            # the engine's prefix cache holds every earlier prompt + reply in full
+            # blocks (the system block is shared by all sessions)
+            hit = max([_lcp(ids, p) for p in prev.values()] + [0])
+            hit = (hit // BS) * BS
+            hit = min(hit, ((len(ids) - 1) // BS) * BS)
+            turn_cached += hit
+            turn_total += len(ids)
+            gen = [rng.randrange(1000, 60000) for _ in range(128)]
+            text = " ".join(rng.choice(words) for _ in range(100))
+            h._remember_reply(sid, gen, text)
+            prev[sid] = ids + gen
+            cm.add_assistant_message(sid, text, 128)
+            # the window never holds more than the API history (a suffix of it)
+            st = h._sessions[sid]
+            assert len(st.fps) <= len(cm.get_messages_for_generation(sid))
+        per_turn.append(turn_cached / turn_total)
+        cached += turn_cached
+        total += turn_total
+    return cached / total, per_turn
+
+
+def test_history_window_keeps_prefix_cache_over_40_turns():
+    ratio, per_turn = _simulate(40)
+    assert ratio >= 0.95, ratio
+    # every session reaches the cap on the same turn once (all re-prefill a cut
+    # window together); after that the jittered keep sizes spread the cuts out
+    low = [t for t, r in enumerate(per_turn) if t > 0 and r < 0.6]
+    assert len(low) <= 1, per_turn
+
+
+def test_window_is_suffix_of_api_history_and_cuts_in_chunks():
+    h = NativeHandler(_Cfg(), engine=_FakeEngine())
+    cm = ConversationManager(max_history_length=50)
+    cm.create_session("a", "sys")
+    cuts = 0
+    last = None
+    for t in range(60):
+        cm.add_user_message("a", f"question {t}")
+        msgs = cm.get_messages_for_generation("a")
+        h.build_prompt(msgs, 64, session_id="a")
+        st = h._sessions["a"]
+        n = len(st.fps)
+        if last is not None and n < last:
+            cuts += 1
+            assert last - n >= 10  # a chunk, not one message per turn
+        last = n
+        # the engine window is exactly the tail of what the API would send
+        api = msgs
+        assert n <= len(api)
+        h._remember_reply("a", [5, 6, 7], f"answer {t}")
+        cm.add_assistant_message("a", f"answer {t}", 3)
+    assert 1 <= cuts <= 4, cuts

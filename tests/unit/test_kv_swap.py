@@ -133,3 +133,51 @@ def test_tiny_cpu_swap_matches_unconstrained(temperature):
     assert small.scheduler.num_swap_out > 0
     assert small.scheduler.num_preemptions == small.scheduler.num_swap_out
     assert got == ref
+
+
+def test_failed_step_finishes_swapped_sequences():
+    """a step failure (e.g. in the swap copy) must also end the swapped
+    sequences with an error and give their host slots back -- they must never
+    resume on KV that was not copied."""
+    eng = _engine(8, 32, max_num_seqs=8, max_num_batched_tokens=64)
+    done = {}
+    for i in range(4):
+        eng.add_request(f"r{i}", [i + 1] * 6, SamplingParams(max_tokens=40, ignore_eos=True),
+                        on_output=lambda o: done.__setitem__(o.request_id, o) if o.finished else None)
+    s = eng.scheduler
+    for _ in range(60):
+        eng.step()
+        if s.swapped:
+            break
+    assert s.swapped
+    victims = [q.request_id for q in s.swapped]
+    eng.fail_unfinished("FT_FAULT: swap copy failed")
+    assert not eng.has_work()
+    assert all(done[v].finish_reason == "error" for v in victims)
+    assert eng.bm.num_free() == eng.bm.num_blocks and s.host.num_free() == s.host.num_blocks
+
+
+def test_swapped_in_blocks_return_to_the_prefix_cache():
+    """blocks restored by a swap-in are committed again, so a follow-up
+    turn that shares the prefix hits the cache."""
+    eng = _engine(12, 32, max_num_seqs=8, max_num_batched_tokens=64)
+    for i in range(5):
+        eng.add_request(f"r{i}", [i + 1] * 6, SamplingParams(max_tokens=12, ignore_eos=True))
+    s = eng.scheduler
+    resumed = None
+    for _ in range(200):
+        n_in = s.num_swap_in
+        before = {q.request_id for q in s.swapped}
+        eng.step()
+        if s.num_swap_in > n_in:
+            resumed = [q for q in s.running if q.request_id in before]
+            break
+    assert resumed, "no swap-in happened"
+    eng.step()  # post_step of the next step commits what the resumed blocks hold
+    for seq in resumed:
+        nfull = seq.num_computed // BS
+        hit = eng.bm.match_prefix(seq.tokens, nfull)
+        try:
+            assert list(hit) == list(seq.block_ids[:nfull])
+        finally:
+            eng.bm.free(list(hit))
