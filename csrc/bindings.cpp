@@ -62,6 +62,9 @@ int ft_ar_allreduce(void* out, const void* x, long n, const uint64_t* peers_dev,
                     size_t max_bytes, unsigned spin_budget, hipStream_t stream);
 int ft_skinny_gemm_pk(const void* x, int x_stride, int M, const void* wpk, int N, int K, float* ws,
                       void* out, int out_stride, int splits, int nt, hipStream_t stream);
+int ft_skinny_gemm_pkd(const void* x, int x_stride, int M, const void* wpk, int N, int K,
+                       float* ws, void* out, int out_stride, int splits, int nt, int depth,
+                       hipStream_t stream);
 int ft_pkr_gemm(const void* x, int x_stride, int M, const void* wpk, int N, int K, float* ws,
                 void* out, int out_stride, void* residual, int res_stride, int* tickets,
                 int splits, int nt, int depth, int epi, int norm, int wn, float eps,
@@ -359,7 +362,8 @@ void w4_dequant(at::Tensor wq, at::Tensor sz, at::Tensor out) {
 }
 
 void skinny_gemm(at::Tensor x, at::Tensor w, c10::optional<at::Tensor> out,
-                 c10::optional<at::Tensor> ws, int64_t splits, int64_t nt, int64_t u) {
+                 c10::optional<at::Tensor> ws, int64_t splits, int64_t nt, int64_t u,
+                 int64_t depth) {
   check_bf16(x, "x");
   check_bf16(w, "w");
   check_rows(x, "x");
@@ -383,7 +387,11 @@ void skinny_gemm(at::Tensor x, at::Tensor w, c10::optional<at::Tensor> out,
     op = out->data_ptr();
     ostride = (int)out->stride(0);
   }
-  if (u == -3)  // pre-packed weights (w is the packed [N/16][K/64][2][64][8] image)
+  if (u == -5)  // pre-packed weights, deep weight ring
+    check_rc(ft_skinny_gemm_pkd(x.data_ptr(), (int)x.stride(0), M, w.data_ptr(), N, K, wsp, op,
+                                ostride, (int)splits, (int)nt, (int)depth, cur_stream()),
+             "skinny_gemm_pkd");
+  else if (u == -3)  // pre-packed weights (w is the packed [N/16][K/64][2][64][8] image)
     check_rc(ft_skinny_gemm_pk(x.data_ptr(), (int)x.stride(0), M, w.data_ptr(), N, K, wsp, op,
                                ostride, (int)splits, (int)nt, cur_stream()),
              "skinny_gemm_pk");
@@ -613,7 +621,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("nt") = 1);
   m.def("w4_dequant", &w4_dequant);
   m.def("skinny_gemm", &skinny_gemm, py::arg("x"), py::arg("w"), py::arg("out") = py::none(),
-        py::arg("ws") = py::none(), py::arg("splits") = 1, py::arg("nt") = 1, py::arg("u") = 2);
+        py::arg("ws") = py::none(), py::arg("splits") = 1, py::arg("nt") = 1, py::arg("u") = 2,
+        py::arg("depth") = 4);
   m.def("pkr_gemm", &pkr_gemm, py::arg("x"), py::arg("w"), py::arg("out") = py::none(),
         py::arg("ws") = py::none(), py::arg("residual") = py::none(),
         py::arg("tickets") = py::none(), py::arg("splits") = 1, py::arg("nt") = 2,

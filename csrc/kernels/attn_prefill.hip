@@ -12,10 +12,15 @@
 //     (chunk ^ (row & 15)) so the B-operand reads (16 different rows, same
 //     column) are bank-conflict free (guide T2).
 //   * V blocks are stored transposed in the cache ([D][block_size], see
-//     rope_kv.hip), so the tile is staged as a [D][64 tok] image (rows padded to
-//     72 elements against bank conflicts) with whole-row 16-B copies, and the
-//     PV B operand (k = 8 consecutive tokens, n = one head dim) is one plain
-//     ds_read_b128 per MFMA.
+//     rope_kv.hip), so the tile is staged as a [D][64 tok] image with whole
+//     16-B copies, chunk c of dim row r at slot c ^ ((r >> 1) & 7) (the 16
+//     rows one ds_read_b128 lane group touches land on 16 distinct bank
+//     quads), and the PV B operand (k = 8 consecutive tokens, n = one head
+//     dim) is one plain ds_read_b128 per MFMA.
+//   * Pipelined staging (split STAGE_LOAD / STAGE_WRITE): the next tile's K and
+//     V^T global loads are issued into registers before the current tile's
+//     MFMAs and written to LDS after the barrier that retires them, so HBM/L2
+//     latency hides behind the QK^T / softmax / PV work.
 //   * S = Q K^T with v_mfma_f32_16x16x32_bf16 (Q fragments live in registers for
 //     the whole kernel), causal + length mask, online softmax in the log2
 //     domain, P goes through a per-wave LDS tile to become the A operand of
@@ -34,7 +39,6 @@ __device__ __forceinline__ bf16x8_t as_frag(const uint4& v) {
 
 constexpr int kPrefillBK = 64;   // kv tokens per tile
 constexpr int kPStride = 72;     // per-wave P tile row stride
-constexpr int kVtStride = 72;    // V^T image row stride (64 tokens + 8 pad)
 
 template <int D, int G>
 __global__ __launch_bounds__(256) void prefill_attn_kernel(
@@ -50,7 +54,7 @@ __global__ __launch_bounds__(256) void prefill_attn_kernel(
   constexpr int SWZ = (NCH >= 16) ? 15 : (NCH - 1);
 
   __shared__ __attribute__((aligned(16))) uint16_t Ks[kPrefillBK * D];
-  __shared__ __attribute__((aligned(16))) uint16_t Vs[D * kVtStride];   // V^T [D][64 tok]
+  __shared__ __attribute__((aligned(16))) uint16_t Vs[D * kPrefillBK];   // V^T [D][64 tok], swizzled
   __shared__ __attribute__((aligned(16))) uint16_t Ps[4][16 * kPStride];
 
   const int tile = blockIdx.x;
@@ -101,42 +105,58 @@ __global__ __launch_bounds__(256) void prefill_attn_kernel(
   const int* bt = block_tables + (size_t)b * bt_stride;
   const size_t head_off = (size_t)kvh * block_size * D;
   const size_t blk_stride = (size_t)nkv * block_size * D;
-  const int vt_tb = min(block_size, kPrefillBK);   // tokens of one block inside a tile
-  const int vt_cpr = vt_tb / 8;                     // 16-B chunks per V^T row and block
+  const int bs_shift = __builtin_ctz(block_size);
+  const int bmask = block_size - 1;
+  // V^T staging: item = (block j of the tile, dim d, 8-token chunk cc), cc fastest,
+  // so consecutive lanes read consecutive 16 B of one transposed block
+  const int tb_shift = min(bs_shift, 6);          // log2 tokens of one block inside a tile
+  const int cpr_shift = tb_shift - 3;             // log2 16-B chunks per block row
+  constexpr int IT = kPrefillBK * NCH / 256;      // staged 16-B items per thread (K and V each)
+  uint4 kreg[IT], vreg[IT];
+  auto stage_load = [&](int kbase) {
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int idx = threadIdx.x + it * 256;
+      {  // K row t, chunk ch
+        const int t = idx / NCH, ch = idx - (idx / NCH) * NCH;
+        const int p = kbase + t;
+        kreg[it] = make_uint4(0, 0, 0, 0);
+        if (p < kv_end)
+          kreg[it] = *reinterpret_cast<const uint4*>(k_cache + bt[p >> bs_shift] * blk_stride +
+                                                     head_off + (size_t)(p & bmask) * D + ch * 8);
+      }
+      {  // V^T dim d, tokens t .. t+7
+        const int cc = idx & ((1 << cpr_shift) - 1), rest = idx >> cpr_shift;
+        const int d = rest % D, j = rest / D;
+        const int p = kbase + (j << tb_shift) + cc * 8;
+        vreg[it] = make_uint4(0, 0, 0, 0);
+        if (p < kv_end)
+          vreg[it] = *reinterpret_cast<const uint4*>(v_cache + bt[p >> bs_shift] * blk_stride +
+                                                     head_off + (size_t)d * block_size + (p & bmask));
+      }
+    }
+  };
+  auto stage_write = [&]() {
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int idx = threadIdx.x + it * 256;
+      const int t = idx / NCH, ch = idx - (idx / NCH) * NCH;
+      reinterpret_cast<uint4*>(Ks + t * D)[ch ^ (t & SWZ)] = kreg[it];
+      const int cc = idx & ((1 << cpr_shift) - 1), rest = idx >> cpr_shift;
+      const int d = rest % D, j = rest / D;
+      const int c = ((j << tb_shift) >> 3) + cc;   // 16-B chunk (8 tokens) within the row
+      reinterpret_cast<uint4*>(Vs + d * kPrefillBK)[c ^ ((d >> 1) & 7)] = vreg[it];
+    }
+  };
 
+  if (ntiles > 0) {
+    stage_load(0);
+    stage_write();
+  }
+  __syncthreads();
   for (int kt = 0; kt < ntiles; ++kt) {
     const int kbase = kt * kPrefillBK;
-    // ---- stage K (swizzled rows) and V^T (padded dim rows) ---------------------------
-    for (int idx = threadIdx.x; idx < kPrefillBK * NCH; idx += 256) {
-      const int t = idx / NCH, ch = idx - (idx / NCH) * NCH;
-      const int p = kbase + t;
-      uint4 kv = make_uint4(0, 0, 0, 0);
-      if (p < kv_end) {
-        const int blk = bt[p / block_size];
-        const int off = p - (p / block_size) * block_size;
-        kv = *reinterpret_cast<const uint4*>(k_cache + blk * blk_stride + head_off +
-                                             (size_t)off * D + ch * 8);
-      }
-      reinterpret_cast<uint4*>(Ks + t * D)[ch ^ (t & SWZ)] = kv;
-    }
-    // V^T: item = (block j of the tile, dim d, 8-token chunk cc); consecutive lanes
-    // read consecutive 16 B of a transposed block
-    for (int idx = threadIdx.x; idx < kPrefillBK * NCH; idx += 256) {
-      const int cc = idx % vt_cpr, rest = idx / vt_cpr;
-      const int d = rest % D, j = rest / D;
-      const int t = j * vt_tb + cc * 8;  // first token of the chunk within the tile
-      const int p = kbase + t;
-      uint4 vv = make_uint4(0, 0, 0, 0);
-      if (p < kv_end) {
-        const int blk = bt[p / block_size];
-        const int off = p - (p / block_size) * block_size;
-        vv = *reinterpret_cast<const uint4*>(v_cache + blk * blk_stride + head_off +
-                                             (size_t)d * block_size + off);
-      }
-      *reinterpret_cast<uint4*>(Vs + d * kVtStride + t) = vv;
-    }
-    __syncthreads();
-
+    if (kt + 1 < ntiles) stage_load(kbase + kPrefillBK);  // in flight during this tile's math
     // ---- S = Q K^T -----------------------------------------------------------------
     floatx4_t s[4];
 #pragma unroll
@@ -198,12 +218,17 @@ __global__ __launch_bounds__(256) void prefill_attn_kernel(
 #pragma unroll
       for (int nd = 0; nd < ND; ++nd) {
         // B operand: tokens kc*32 + 8 lg .. +8 of head dim nd*16 + l15
-        const uint4 vb = *reinterpret_cast<const uint4*>(Vs + (nd * 16 + l15) * kVtStride +
-                                                         kc * 32 + 8 * lg);
+        const int row = nd * 16 + l15;
+        const uint4 vb = reinterpret_cast<const uint4*>(Vs + row * kPrefillBK)[
+            (kc * 4 + lg) ^ ((row >> 1) & 7)];
         o[nd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(pa), as_frag(vb), o[nd], 0, 0, 0);
       }
     }
-    __syncthreads();
+    __syncthreads();   // every wave is done with this tile's Ks / Vs / Ps
+    if (kt + 1 < ntiles) {
+      stage_write();
+      __syncthreads();
+    }
   }
 
   // ---- normalise + store -------------------------------------------------------------

@@ -606,6 +606,119 @@ __global__ __launch_bounds__(256) void skinny_pk_kernel(
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// Variant "pkd" (packed, deep weight ring): pk's decomposition (16*NT columns
+// per workgroup, the 4 waves split the K range by k-step) with the weight stream
+// in an R-deep register ring -- R-1 k-steps (R-1 x NT x 2 KiB per wave) stay in
+// flight while one feeds the MFMAs -- and x (L2-resident, shorter latency)
+// double-buffered on its own.  At decode shapes every CU holds 1-3 of these
+// workgroups, so bytes in flight per CU, not MFMA or VALU, set the rate (pk keeps
+// one k-step in flight per wave: ~32 KiB per CU at 1 workgroup/CU).
+template <int MT, int NT, int R>
+__global__ __launch_bounds__(256) void skinny_pkd_kernel(
+    const uint16_t* __restrict__ x, int x_stride, int M, const uint16_t* __restrict__ wpk, int K,
+    float* __restrict__ ws, uint16_t* __restrict__ out, int out_stride, int N, int k_slice) {
+  static_assert(R % 2 == 0, "the x ring is indexed by step parity");
+  __shared__ float s_red[4][MT * NT * 4][64];
+  const int lane = lane_id(), wave = wave_id();
+  const int l15 = lane & 15, g = lane >> 4;
+  const int n0 = blockIdx.x * (16 * NT);
+  const int s = blockIdx.y;
+  const int kbeg = s * k_slice;
+  const int ksteps_total = K >> 6;
+  const int step0 = kbeg >> 6;
+
+  const uint16_t* wp[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j)
+    wp[j] = wpk + ((size_t)(n0 / 16 + j) * ksteps_total + step0) * 1024 + lane * 8;
+  const uint16_t* xp[MT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+    const int r = min(16 * i + l15, M - 1);
+    xp[i] = x + (size_t)r * x_stride + kbeg + 16 * g;
+  }
+
+  sk_floatx4 acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = sk_floatx4{0.f, 0.f, 0.f, 0.f};
+
+  const int nsteps = k_slice >> 6;
+  const int my_steps = nsteps > wave ? (nsteps - wave + 3) >> 2 : 0;
+  const int last = my_steps - 1;
+  auto kst = [&](int t) { return wave + 4 * min(t, last); };  // past the end: re-load the last
+  uint4 wr[R][NT][2];
+  uint4 xr[2][MT][2];
+  auto load_w = [&](uint4 (&st)[NT][2], int t) {
+    const size_t off = (size_t)kst(t) * 1024;
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      st[j][0] = nt_load16(wp[j] + off);
+      st[j][1] = nt_load16(wp[j] + off + 512);
+    }
+  };
+  auto load_x = [&](uint4 (&st)[MT][2], int t) {
+    const int k = kst(t) * 64;
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      const uint4* p = reinterpret_cast<const uint4*>(xp[i] + k);
+      st[i][0] = p[0];
+      st[i][1] = p[1];
+    }
+  };
+  if (my_steps > 0) {
+#pragma unroll
+    for (int r = 0; r + 1 < R; ++r) load_w(wr[r], r);
+    load_x(xr[0], 0);
+    for (int t = 0; t < my_steps; t += R) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        load_w(wr[(r + R - 1) % R], t + r + R - 1);
+        load_x(xr[(r + 1) & 1], t + r + 1);
+        __builtin_amdgcn_sched_barrier(0);
+        if (t + r < my_steps) {
+#pragma unroll
+          for (int i = 0; i < MT; ++i)
+#pragma unroll
+            for (int j = 0; j < NT; ++j) {
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                  sk_frag(xr[r & 1][i][0]), sk_frag(wr[r][j][0]), acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                  sk_frag(xr[r & 1][i][1]), sk_frag(wr[r][j][1]), acc[i][j], 0, 0, 0);
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  }
+
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) s_red[wave][(i * NT + j) * 4 + r][lane] = acc[i][j][r];
+  __syncthreads();
+  constexpr int NREG = MT * NT * 4;
+  const int ln = threadIdx.x & 63;
+  float* slab = ws + (size_t)s * M * N;
+  for (int reg = threadIdx.x >> 6; reg < NREG; reg += 4) {
+    const float v = s_red[0][reg][ln] + s_red[1][reg][ln] + s_red[2][reg][ln] + s_red[3][reg][ln];
+    const int i = reg / (NT * 4), j = (reg / 4) % NT, r = reg & 3;
+    const int m = 16 * i + (ln >> 4) * 4 + r;
+    const int n = n0 + 16 * j + (ln & 15);
+    if (m < M) {
+      if (gridDim.y == 1)
+        out[(size_t)m * out_stride + n] = f32_to_bf16(v);
+      else
+        slab[(size_t)m * N + n] = v;
+    }
+  }
+}
+
 }  // namespace ft
 
 // Returns 0 on success.  Requirements (checked): M <= 64, N % (16*nt) == 0,
@@ -760,5 +873,34 @@ extern "C" int ft_skinny_gemm_pk(const void* x, int x_stride, int M, const void*
   FT_PK_NT(4)
 #undef FT_PK_NT
 #undef FT_PK
+  return -5;
+}
+
+// Pre-packed-weight variant with an R-deep weight ring (depth 2, 4 or 6).
+// Requirements (checked): M <= 64, N % (16*nt) == 0, K % (64*splits) == 0.
+extern "C" int ft_skinny_gemm_pkd(const void* x, int x_stride, int M, const void* wpk, int N,
+                                  int K, float* ws, void* out, int out_stride, int splits, int nt,
+                                  int depth, hipStream_t stream) {
+  if (M <= 0) return 0;
+  if (M > 64 || splits < 1) return -1;
+  if (N % (16 * nt) != 0) return -2;
+  if (K % (64 * splits) != 0) return -3;
+  if (splits > 1 && ws == nullptr) return -4;
+  const int mt = (M + 15) / 16;
+  dim3 grid(N / (16 * nt), splits), block(256);
+  const int k_slice = K / splits;
+#define FT_PKD(MT_, NT_, R_)                                                                 \
+  if (mt == MT_ && nt == NT_ && depth == R_) {                                               \
+    hipLaunchKernelGGL((ft::skinny_pkd_kernel<MT_, NT_, R_>), grid, block, 0, stream,        \
+                       (const uint16_t*)x, x_stride, M, (const uint16_t*)wpk, K, ws,         \
+                       (uint16_t*)out, out_stride, N, k_slice);                              \
+    return static_cast<int>(hipGetLastError());                                              \
+  }
+#define FT_PKD_MT(NT_, R_) FT_PKD(1, NT_, R_) FT_PKD(2, NT_, R_) FT_PKD(3, NT_, R_) FT_PKD(4, NT_, R_)
+  FT_PKD_MT(1, 2) FT_PKD_MT(1, 4) FT_PKD_MT(1, 6)
+  FT_PKD_MT(2, 2) FT_PKD_MT(2, 4) FT_PKD_MT(2, 6)
+  FT_PKD_MT(4, 2) FT_PKD_MT(4, 4)
+#undef FT_PKD_MT
+#undef FT_PKD
   return -5;
 }

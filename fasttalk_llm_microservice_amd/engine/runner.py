@@ -490,7 +490,12 @@ class ModelRunner:
         ops.sample(logits, self.d_temp[:nb], self.d_top_p[:nb], self.d_top_k[:nb],
                    self.d_seeds[:nb], self.d_steps[:nb], out=self.d_out[:nb])
 
+    @torch.inference_mode()
     def _capture(self, nb: int):
+        """Captures the decode graph of batch bucket ``nb``.  Always under
+        inference mode, whichever path triggers it (pipelined launches run outside
+        ``execute``): the CUDA generator's graph-safe RNG state is created by the
+        first capture and must be of the same kind for every later one."""
         t0 = time.time()
         # inputs must be valid for the warm-up/capture run: no KV writes, empty contexts
         saved = (self.d_slots[:nb].clone(), self.d_seq_lens[:nb].clone())

@@ -227,7 +227,7 @@ def kv_swap(caches, ptrs, ids: torch.Tensor, staging: torch.Tensor, to_staging: 
 SKINNY_CONFIGS = [(1, 2), (1, 4), (2, 2), (2, 4), (4, 1), (4, 2), (1, 0), (2, 0), (4, 0),
                   (1, -1), (2, -1), (4, -1), (1, -2), (2, -2), (1, -3), (2, -3), (4, -3),
                   (1, -4), (2, -4)]
-PACKED_VARIANTS = (-3, -4)
+PACKED_VARIANTS = (-3, -4, -5)
 
 
 def pack_weight(w: torch.Tensor) -> torch.Tensor:
@@ -245,12 +245,13 @@ def skinny_gemm_supported(m: int, n: int, k: int) -> bool:
     return 0 < m <= 64 and n % 16 == 0 and k % 128 == 0
 
 
-def skinny_gemm(x, w, out=None, ws=None, splits: int = 1, nt: int = 1, u: int = 2):
+def skinny_gemm(x, w, out=None, ws=None, splits: int = 1, nt: int = 1, u: int = 2, depth: int = 4):
     """y = x w^T (M <= 64).  splits > 1 leaves fp32 partial slabs in ``ws``
-    ([splits, M, N]) for a fused epilogue; otherwise writes bf16 ``out``."""
+    ([splits, M, N]) for a fused epilogue; otherwise writes bf16 ``out``.
+    u = -5: packed weights with a ``depth``-stage weight ring (2, 4 or 6)."""
     if splits == 1 and out is None:
         out = torch.empty(x.shape[0], w.shape[0], dtype=x.dtype, device=x.device)
-    native().skinny_gemm(x, w, out, ws, splits, nt, u)
+    native().skinny_gemm(x, w, out, ws, splits, nt, u, depth)
     return out if splits == 1 else ws
 
 
