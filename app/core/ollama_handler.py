@@ -8,6 +8,7 @@ it from a worker thread so it never blocks the event loop (Appendix D Q7).
 """
 from __future__ import annotations
 
+import codecs
 import json
 import logging
 import time
@@ -68,13 +69,16 @@ class OllamaHandler:
             with self._requests_lock:
                 self._active_requests[req_id] = {"stream": resp, "start_time": time.time()}
             buf = ""
+            # incremental: a multi-byte UTF-8 character split across HTTP chunks is
+            # completed by the next chunk instead of becoming U+FFFD
+            dec = codecs.getincrementaldecoder("utf-8")(errors="replace")
             for raw in resp.iter_content(chunk_size=None):
                 with self._requests_lock:
                     if req_id not in self._active_requests:
                         break
                 if not raw:
                     continue
-                buf += raw.decode("utf-8", errors="replace")
+                buf += dec.decode(raw)
                 done = False
                 while "\n" in buf:
                     line, buf = buf.split("\n", 1)

@@ -26,7 +26,9 @@ def register_openai_routes(app, handler) -> None:
     @app.post("/v1/chat/completions")
     async def chat_completions(request: Request):
         from fasttalk_llm_microservice_amd.engine.guided import GuidedSpec
-        from fasttalk_llm_microservice_amd.engine.tool_parser import parse_tool_calls
+        from fasttalk_llm_microservice_amd.engine.tool_parser import (StreamingToolCallParser,
+                                                                       StreamingToolDetector,
+                                                                       parse_tool_calls)
 
         try:
             body = await request.json()
@@ -66,25 +68,37 @@ def register_openai_routes(app, handler) -> None:
 
         if body.get("stream"):
             async def gen():
+                """With ``tools``, the first visible characters decide (like vLLM's
+                auto tool choice): speech streams as ``content`` deltas at once; a
+                tool call streams as ``tool_calls`` deltas -- id + name as soon as
+                the name is complete, then argument fragments as they decode."""
                 yield chunk({"role": "assistant", "content": ""})
-                parts, finish = [], "stop"
+                finish = "stop"
+                det = StreamingToolDetector() if tools else None
+                tcp = StreamingToolCallParser() if tools else None
+                any_call = False
                 async for out in handler.stream_events(messages, request_id=rid, **kw):
                     if out.finished:
                         finish = out.finish_reason
-                    if out.text:
-                        if tools:
-                            parts.append(out.text)
-                        else:
-                            yield chunk({"content": out.text})
-                if tools:
-                    text = "".join(parts)
-                    calls, rest = parse_tool_calls(text)
-                    if calls:
-                        yield chunk({"tool_calls": [dict(c.to_openai(), index=i)
-                                                    for i, c in enumerate(calls)]})
-                        finish = "tool_calls"
-                    elif text:
-                        yield chunk({"content": text})
+                    if not out.text:
+                        continue
+                    if det is None:
+                        yield chunk({"content": out.text})
+                        continue
+                    mode, emit = det.feed(out.text)
+                    if mode == "text":
+                        if emit:
+                            yield chunk({"content": emit})
+                    elif mode == "tool":
+                        held, det.buf = det.buf, ""   # the parser owns the tool text now
+                        deltas = tcp.feed(held)
+                        if deltas:
+                            any_call = True
+                            yield chunk({"tool_calls": deltas})
+                if det is not None and det.mode is None and det.buf:
+                    yield chunk({"content": det.buf})   # never became a tool call
+                if any_call:
+                    finish = "tool_calls"
                 yield chunk({}, finish if finish in ("stop", "length", "tool_calls") else "stop")
                 yield "data: [DONE]\n\n"
 

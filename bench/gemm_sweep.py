@@ -69,10 +69,10 @@ def main():
         out = torch.empty(M, n, device=dev).bfloat16()
         for nt, u in ops.SKINNY_CONFIGS:
             for splits in (1, 2, 4, 8, 16):
-                kstep = (512 if u in (-2, -4) else 64 * (u if u > 0 else 1)) * splits
+                kstep = (512 if u == -4 else 64) * splits
                 if n % (16 * nt) or k % kstep or splits * M * n > ws.numel():
                     continue
-                cols = 16 * nt if u in (0, -3) else 64 * nt
+                cols = 16 * nt if u == -3 else 64 * nt
                 blocks = (n // cols) * splits
                 if blocks < 128 or blocks > 16384:
                     continue
@@ -96,7 +96,7 @@ def main():
                     del packed
         rows.sort()
         for t, nt, u, splits, blocks, err in rows[: a.top]:
-            print(f"   {({0: 'ks', -1: 'xs', -2: 'xc', -3: 'pk', -4: 'xcp'}).get(u, 'cs')} nt={nt} u={u} splits={splits:2d} blocks={blocks:5d}: "
+            print(f"   {({-3: 'pk', -4: 'xcp'}).get(u, '?')} nt={nt} u={u} splits={splits:2d} blocks={blocks:5d}: "
                   f"{t:7.2f} us ({n * k * 2 / t / 1e3:5.0f} GB/s) err={err:.4f}", flush=True)
         bad = [r for r in rows if r[5] > 0.05]
         if bad:

@@ -68,9 +68,11 @@ def main():
         W = torch.randn(n, k, device=dev).bfloat16() * 0.02
         xx = torch.randn(B, k, device=dev).bfloat16()
         rep(f"hipblaslt {name} [{B}x{k}]x[{k}x{n}]", timeit(lambda: F.linear(xx, W)), n * k * 2)
-        if hasattr(ops, "skinny_gemm") and ops.skinny_gemm_supported(B, n, k):
+        if B <= 64 and n % 64 == 0 and k % 64 == 0:
             out = torch.empty(B, n, device=dev).bfloat16()
-            rep(f"skinny   {name}", timeit(lambda: ops.skinny_gemm(xx, W, out=out)), n * k * 2)
+            Wp = ops.pack_weight(W)
+            rep(f"packed   {name}", timeit(lambda: ops.skinny_gemm(xx, Wp, out=out, nt=2, u=-3)),
+                n * k * 2)
             ref = F.linear(xx, W).float()
             err = (out.float() - ref).abs().max().item()
             print(f"   max err vs hipblaslt {err:.4f}")

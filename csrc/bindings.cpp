@@ -41,14 +41,8 @@ int ft_w4_gemm(const void* x, int x_stride, int M, const uint32_t* wq, const voi
 int ft_w4_dequant(const uint32_t* wq, const void* sz, void* out, int N, int K, hipStream_t stream);
 int ft_kv_swap(const uint64_t* ptrs_dev, int ncache, const int* ids_dev, int n, void* staging,
                long block_elems, int to_staging, hipStream_t stream);
-int ft_skinny_gemm(const void* x, int x_stride, int M, const void* w, int N, int K, float* ws,
-                   void* out, int out_stride, int splits, int nt, int u, hipStream_t stream);
-int ft_skinny_gemm_ks(const void* x, int x_stride, int M, const void* w, int N, int K, float* ws,
-                      void* out, int out_stride, int splits, int nt, hipStream_t stream);
-int ft_skinny_gemm_xs(const void* x, int x_stride, int M, const void* w, int N, int K, float* ws,
-                      void* out, int out_stride, int splits, int nt, hipStream_t stream);
 int ft_skinny_gemm_xc(const void* x, int x_stride, int M, const void* w, int N, int K, float* ws,
-                      void* out, int out_stride, int splits, int nt, int packed, hipStream_t stream);
+                      void* out, int out_stride, int splits, int nt, hipStream_t stream);
 int ft_embed_rmsnorm(void* out, void* residual, const int* ids, const void* table, const void* w,
                      int rows, int hidden, int vocab, float eps, hipStream_t stream);
 size_t ft_ar_header_bytes();
@@ -62,9 +56,6 @@ int ft_ar_allreduce(void* out, const void* x, long n, const uint64_t* peers_dev,
                     size_t max_bytes, unsigned spin_budget, hipStream_t stream);
 int ft_skinny_gemm_pk(const void* x, int x_stride, int M, const void* wpk, int N, int K, float* ws,
                       void* out, int out_stride, int splits, int nt, hipStream_t stream);
-int ft_skinny_gemm_pkd(const void* x, int x_stride, int M, const void* wpk, int N, int K,
-                       float* ws, void* out, int out_stride, int splits, int nt, int depth,
-                       hipStream_t stream);
 int ft_pkr_gemm(const void* x, int x_stride, int M, const void* wpk, int N, int K, float* ws,
                 void* out, int out_stride, void* residual, int res_stride, int* tickets,
                 int splits, int nt, int depth, int epi, int norm, int wn, float eps,
@@ -231,6 +222,8 @@ void prefill_attention(at::Tensor out, at::Tensor q, at::Tensor k_cache, at::Ten
   check_i32(seq_lens, "seq_lens");
   check_i32(q_start_loc, "q_start_loc");
   check_i32(tile_info, "tile_info");
+  // the prefill kernel stages a sequence's block-table row in LDS (4096 entries)
+  TORCH_CHECK(block_tables.size(1) <= 4096, "prefill: at most 4096 KV blocks per sequence");
   TORCH_CHECK(tile_info.numel() >= 2 * num_tiles, "tile_info too small");
   check_rc(ft_prefill_attention(out.data_ptr(), (int)out.stride(0), q.data_ptr(),
                                 (int)q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
@@ -362,16 +355,16 @@ void w4_dequant(at::Tensor wq, at::Tensor sz, at::Tensor out) {
 }
 
 void skinny_gemm(at::Tensor x, at::Tensor w, c10::optional<at::Tensor> out,
-                 c10::optional<at::Tensor> ws, int64_t splits, int64_t nt, int64_t u,
-                 int64_t depth) {
+                 c10::optional<at::Tensor> ws, int64_t splits, int64_t nt, int64_t u) {
   check_bf16(x, "x");
   check_bf16(w, "w");
   check_rows(x, "x");
-  TORCH_CHECK(w.dim() == 2 && w.is_contiguous(), "w must be contiguous [N, K]");
+  TORCH_CHECK(w.dim() == 2 && w.is_contiguous(), "w must be the packed [N, K] image");
   const int M = (int)x.size(0), K = (int)x.size(1), N = (int)w.size(0);
   TORCH_CHECK(w.size(1) == K, "K mismatch");
   TORCH_CHECK(M <= 64, "skinny_gemm supports M <= 64");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0, "w alignment");
+  TORCH_CHECK(u == -3 || u == -4, "skinny_gemm variant: -3 (pk) or -4 (xc), packed weights");
   float* wsp = nullptr;
   void* op = nullptr;
   int ostride = 0;
@@ -387,30 +380,14 @@ void skinny_gemm(at::Tensor x, at::Tensor w, c10::optional<at::Tensor> out,
     op = out->data_ptr();
     ostride = (int)out->stride(0);
   }
-  if (u == -5)  // pre-packed weights, deep weight ring
-    check_rc(ft_skinny_gemm_pkd(x.data_ptr(), (int)x.stride(0), M, w.data_ptr(), N, K, wsp, op,
-                                ostride, (int)splits, (int)nt, (int)depth, cur_stream()),
-             "skinny_gemm_pkd");
-  else if (u == -3)  // pre-packed weights (w is the packed [N/16][K/64][2][64][8] image)
+  if (u == -3)  // w is the packed [N/16][K/64][2][64][8] image (ops.pack_weight)
     check_rc(ft_skinny_gemm_pk(x.data_ptr(), (int)x.stride(0), M, w.data_ptr(), N, K, wsp, op,
                                ostride, (int)splits, (int)nt, cur_stream()),
              "skinny_gemm_pk");
-  else if (u == -2 || u == -4)  // x-chunk variant (-4: pre-packed weights)
-    check_rc(ft_skinny_gemm_xc(x.data_ptr(), (int)x.stride(0), M, w.data_ptr(), N, K, wsp, op,
-                               ostride, (int)splits, (int)nt, u == -4 ? 1 : 0, cur_stream()),
-             "skinny_gemm_xc");
-  else if (u < 0)  // x-in-LDS variant
-    check_rc(ft_skinny_gemm_xs(x.data_ptr(), (int)x.stride(0), M, w.data_ptr(), N, K, wsp, op,
-                               ostride, (int)splits, (int)nt, cur_stream()),
-             "skinny_gemm_xs");
-  else if (u == 0)  // K-split-wave variant
-    check_rc(ft_skinny_gemm_ks(x.data_ptr(), (int)x.stride(0), M, w.data_ptr(), N, K, wsp, op,
-                               ostride, (int)splits, (int)nt, cur_stream()),
-             "skinny_gemm_ks");
   else
-    check_rc(ft_skinny_gemm(x.data_ptr(), (int)x.stride(0), M, w.data_ptr(), N, K, wsp, op, ostride,
-                            (int)splits, (int)nt, (int)u, cur_stream()),
-             "skinny_gemm");
+    check_rc(ft_skinny_gemm_xc(x.data_ptr(), (int)x.stride(0), M, w.data_ptr(), N, K, wsp, op,
+                               ostride, (int)splits, (int)nt, cur_stream()),
+             "skinny_gemm_xc");
 }
 
 // Ring-pipelined packed decode GEMM with fused epilogues (csrc/kernels/skinny_pkr.hip).
@@ -621,8 +598,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("nt") = 1);
   m.def("w4_dequant", &w4_dequant);
   m.def("skinny_gemm", &skinny_gemm, py::arg("x"), py::arg("w"), py::arg("out") = py::none(),
-        py::arg("ws") = py::none(), py::arg("splits") = 1, py::arg("nt") = 1, py::arg("u") = 2,
-        py::arg("depth") = 4);
+        py::arg("ws") = py::none(), py::arg("splits") = 1, py::arg("nt") = 1, py::arg("u") = -3);
   m.def("pkr_gemm", &pkr_gemm, py::arg("x"), py::arg("w"), py::arg("out") = py::none(),
         py::arg("ws") = py::none(), py::arg("residual") = py::none(),
         py::arg("tickets") = py::none(), py::arg("splits") = 1, py::arg("nt") = 2,

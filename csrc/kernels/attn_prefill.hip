@@ -1,31 +1,34 @@
 // K5: varlen causal prefill attention over the paged KV cache (new tokens +
 // cached prefix, i.e. multi-turn history reuse) on MFMA.  SURVEY.md §2.4 K5.
 //
-// Work decomposition (GQA-aware): a workgroup owns one (query tile, kv head).
-// Its 64 MFMA rows are (token, q-head) pairs flattened token-major, row r ->
-// token r / G, head r % G, so the G query heads that share a kv head share
-// every K/V tile the workgroup stages (each K/V byte is read once per tile of
-// 64/G query tokens).  4 waves x 16 rows.
+// Built for the serving regime of a voice chat: every turn prefills a short new
+// chunk (tens of tokens) on top of a long cached history (thousands), so the
+// kernel is a KV stream like decode, and what matters is reading each K/V byte
+// ONCE per (sequence, kv head) and keeping bytes in flight.
 //
-// Per 64-token KV tile:
-//   * K is staged row-major into LDS with a 16-B-chunk XOR swizzle
-//     (chunk ^ (row & 15)) so the B-operand reads (16 different rows, same
-//     column) are bank-conflict free (guide T2).
-//   * V blocks are stored transposed in the cache ([D][block_size], see
-//     rope_kv.hip), so the tile is staged as a [D][64 tok] image with whole
-//     16-B copies, chunk c of dim row r at slot c ^ ((r >> 1) & 7) (the 16
-//     rows one ds_read_b128 lane group touches land on 16 distinct bank
-//     quads), and the PV B operand (k = 8 consecutive tokens, n = one head
-//     dim) is one plain ds_read_b128 per MFMA.
-//   * Pipelined staging (split STAGE_LOAD / STAGE_WRITE): the next tile's K and
-//     V^T global loads are issued into registers before the current tile's
-//     MFMAs and written to LDS after the barrier that retires them, so HBM/L2
-//     latency hides behind the QK^T / softmax / PV work.
-//   * S = Q K^T with v_mfma_f32_16x16x32_bf16 (Q fragments live in registers for
-//     the whole kernel), causal + length mask, online softmax in the log2
-//     domain, P goes through a per-wave LDS tile to become the A operand of
-//     O += P V (16x16x32 again).  Running max/sum stay per lane; the sum is
-//     reduced across the 16 lanes of a row group only once at the end.
+// * Work: a workgroup owns (query block, kv head); its 256 MFMA rows are (token,
+//   q-head) pairs flattened token-major (row r -> token r / G, head r % G), so
+//   the G query heads of the kv head share every staged K/V tile and a block
+//   holds 256 / G tokens (64 at GQA 4: a typical turn is one block).  8 waves x
+//   2 m-tiles of 16 rows (512 threads, 2 waves per SIMD, one workgroup per CU).
+// * Transposed formulation, everything lane-local:
+//     S^T[64 kv x 16 q]  = K . Q^T      A = K rows from LDS, B = Q^T (registers)
+//     O^T[D x 16 q]     += V^T . P^T    A = V^T rows from LDS, B = P^T = S^T's
+//                                       C layout converted to bf16 in place
+//   A lane owns one query column of each m-tile: its running max / sum / rescale
+//   need no cross-lane traffic except one 4-lane max per tile, and P never goes
+//   through LDS.  The PV k-slots of a lane are tokens {4g..4g+3, 16+4g..16+4g+3}
+//   of each 32-token half (the S^T C layout); the V^T A operand uses the same
+//   permutation (two 8-B reads of the V^T image).
+// * Staging: K rows (16-B chunk XOR swizzle, conflict-free A reads) and V^T rows
+//   (V blocks are stored transposed in the cache, [D][block_size], rope_kv.hip;
+//   chunk c of dim row r at slot c ^ ((r >> 1) & 7)) in LDS, shared by the 8
+//   waves.  Tiles stream by LDS-DMA (global_load_lds_dwordx4) into a 4-slot
+//   ring: the swizzles are applied on the per-lane SOURCE address (the DMA's LDS
+//   destination is lane-linear), tiles t+1..t+3 stay in flight while tile t
+//   computes (counted vmcnt + raw s_barrier; a __syncthreads would drain the
+//   DMA).  The block-table entries of the KV range are copied to LDS once, so
+//   issuing a tile never waits on a table read.
 #include "ft_common.h"
 
 namespace ft {
@@ -38,24 +41,92 @@ __device__ __forceinline__ bf16x8_t as_frag(const uint4& v) {
 }
 
 constexpr int kPrefillBK = 64;   // kv tokens per tile
-constexpr int kPStride = 72;     // per-wave P tile row stride
+constexpr int kPrefillRows = 256; // query rows (token x head) per workgroup
+constexpr int kPrefillMaxBlocks = 4096;  // block-table entries staged in LDS (checked on the host)
+
+// max over aligned groups of 4 lanes that differ in bits 4..5 (the k groups)
+__device__ __forceinline__ float kgroup_max(float v) {
+  v = fmaxf(v, __shfl_xor(v, 16, 64));
+  return fmaxf(v, __shfl_xor(v, 32, 64));
+}
+__device__ __forceinline__ float kgroup_sum(float v) {
+  v += __shfl_xor(v, 16, 64);
+  return v + __shfl_xor(v, 32, 64);
+}
+
+// LDS reads in inline asm: with LDS-DMA (global_load_lds) in flight hipcc cannot
+// tell a ds_read from the DMA's destination and waits vmcnt(0) before every LDS
+// read, draining the prefetch.  These reads are invisible to its waitcnt pass, so
+// the kernel orders them itself: lgkm_wait<N>() (N reads may stay outstanding)
+// followed by dep() on each value it is about to consume.
+__device__ __forceinline__ uint32_t lds_off(const void* p) {
+  return (uint32_t)reinterpret_cast<uintptr_t>(p);
+}
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint4 ds_read16(uint32_t a) {
+  u32x4_t v;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(a));
+  return __builtin_bit_cast(uint4, v);
+}
+__device__ __forceinline__ uint2 ds_read8(uint32_t a) {
+  u32x2_t v;
+  asm volatile("ds_read_b64 %0, %1" : "=v"(v) : "v"(a));
+  return __builtin_bit_cast(uint2, v);
+}
+// global_load_lds_dwordx4 in inline asm (guide idiom): M0 = the wave-uniform LDS
+// destination, lanes land at M0 + 16 * lane.  hipcc's waitcnt pass does not see it
+// (it would otherwise treat the address VGPRs as pending and wait vmcnt(0) at their
+// reuse); the kernel waits for it with explicit counted vmcnt.
+__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_dst) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(lds_dst))
+      : "memory");
+}
+
+template <int N>
+__device__ __forceinline__ void lgkm_wait() {
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory");
+}
+__device__ __forceinline__ void dep(uint4& v) {
+  u32x4_t t = __builtin_bit_cast(u32x4_t, v);
+  asm volatile("" : "+v"(t));
+  v = __builtin_bit_cast(uint4, t);
+}
+__device__ __forceinline__ void dep(uint2& v) {
+  u32x2_t t = __builtin_bit_cast(u32x2_t, v);
+  asm volatile("" : "+v"(t));
+  v = __builtin_bit_cast(uint2, t);
+}
 
 template <int D, int G>
-__global__ __launch_bounds__(256) void prefill_attn_kernel(
+__global__ __launch_bounds__(512, 1) void prefill_attn_kernel(
     uint16_t* __restrict__ out, int out_stride, const uint16_t* __restrict__ q, int q_stride,
     const uint16_t* __restrict__ k_cache, const uint16_t* __restrict__ v_cache,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ seq_lens,
     const int* __restrict__ q_start_loc, const int* __restrict__ tile_info, int nkv,
     int block_size, float scale_log2) {
-  constexpr int NCH = D / 8;          // 16-B chunks per row
-  constexpr int KC = D / 32;          // k-chunks of the QK^T product
-  constexpr int ND = D / 16;          // 16-wide output column tiles
-  constexpr int TQ = 64 / G;          // query tokens per tile
+  constexpr int NCH = D / 8;          // 16-B chunks per K row
+  constexpr int KC = D / 32;          // k-steps of S^T = K Q^T
+  constexpr int ND = D / 16;          // 16-row dim tiles of O^T
+  constexpr int NW = 8;               // waves per workgroup
+  constexpr int MT = kPrefillRows / (16 * NW);  // 16-query m-tiles per wave
+  constexpr int QB = kPrefillRows / G;  // query tokens per workgroup
   constexpr int SWZ = (NCH >= 16) ? 15 : (NCH - 1);
 
-  __shared__ __attribute__((aligned(16))) uint16_t Ks[kPrefillBK * D];
-  __shared__ __attribute__((aligned(16))) uint16_t Vs[D * kPrefillBK];   // V^T [D][64 tok], swizzled
-  __shared__ __attribute__((aligned(16))) uint16_t Ps[4][16 * kPStride];
+  // one LDS array (guide §5 item 4a): [NSLOT slots][K image | V^T image], then the table
+  constexpr int NSLOT = 4;
+  constexpr int KIMG = kPrefillBK * D, VIMG = D * kPrefillBK;   // bf16 elements
+  constexpr int SLOT = KIMG + VIMG;
+  __shared__ __attribute__((aligned(16))) uint16_t smem[NSLOT * SLOT + 2 * kPrefillMaxBlocks];
+  int* s_bt = reinterpret_cast<int*>(smem + NSLOT * SLOT);
 
   const int tile = blockIdx.x;
   const int kvh = blockIdx.y;
@@ -65,190 +136,257 @@ __global__ __launch_bounds__(256) void prefill_attn_kernel(
   const int q0 = q_start_loc[b];
   const int qlen = q_start_loc[b + 1] - q0;
   const int ctx0 = L - qlen;  // position of the first new token
-  const int ntok = min(TQ, qlen - qs);
+  const int ntok = min(QB, qlen - qs);
 
   const int lane = lane_id(), wave = wave_id();
   const int l15 = lane & 15, lg = lane >> 4;
-  const int nq = nkv * G;
 
-  // ---- Q fragments (A operand): row = lane & 15 of this wave's 16 rows ----------
-  uint4 qa[KC];
-  {
-    const int r = wave * 16 + l15;
+  // ---- Q^T fragments (B operand) + the query column each lane owns ----------------
+  uint4 qb[MT][KC];
+  int qpos[MT];   // position of this lane's query column (-1: padding row)
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    const int r = (wave * MT + m) * 16 + l15;
     const int tq = r / G, g = r - (r / G) * G;
-    const bool valid = (r < TQ * G) && (tq < ntok);
+    const bool valid = (r < QB * G) && (tq < ntok);
+    qpos[m] = valid ? ctx0 + qs + tq : -1;
     const uint16_t* qp = q + (size_t)(q0 + qs + (valid ? tq : 0)) * q_stride + (kvh * G + g) * D;
 #pragma unroll
     for (int kc = 0; kc < KC; ++kc)
-      qa[kc] = valid ? reinterpret_cast<const uint4*>(qp + kc * 32 + 8 * lg)[0]
-                     : make_uint4(0, 0, 0, 0);
-  }
-  // query position of the 4 C-layout rows this lane holds
-  int qpos[4];
-  bool rvalid[4];
-#pragma unroll
-  for (int rr = 0; rr < 4; ++rr) {
-    const int r = wave * 16 + lg * 4 + rr;
-    const int tq = r / G;
-    rvalid[rr] = (r < TQ * G) && (tq < ntok);
-    qpos[rr] = ctx0 + qs + tq;
+      qb[m][kc] = valid ? reinterpret_cast<const uint4*>(qp + kc * 32 + 8 * lg)[0]
+                        : make_uint4(0, 0, 0, 0);
   }
 
-  floatx4_t o[ND];
+  // retire the Q loads here, outside the tile loop: a compiler-inserted wait at
+  // their first use inside the loop would be a vmcnt(0) that drains the K/V DMA
 #pragma unroll
-  for (int i = 0; i < ND; ++i) o[i] = floatx4_t{0.f, 0.f, 0.f, 0.f};
-  float m_run[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
-  float l_run[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc) dep(qb[m][kc]);
+
+  floatx4_t o[MT][ND];   // O^T: lane (l15 = query, lg) rows = dims 16 nd + 4 lg + i
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int i = 0; i < ND; ++i) o[m][i] = floatx4_t{0.f, 0.f, 0.f, 0.f};
+  float m_run[MT], l_run[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    m_run[m] = -INFINITY;
+    l_run[m] = 0.f;
+  }
 
   const int kv_end = min(L, ctx0 + qs + ntok);  // exclusive
   const int ntiles = (kv_end + kPrefillBK - 1) / kPrefillBK;
+  const int first_q = ctx0 + qs;                // lowest query position of the block
   const int* bt = block_tables + (size_t)b * bt_stride;
   const size_t head_off = (size_t)kvh * block_size * D;
   const size_t blk_stride = (size_t)nkv * block_size * D;
   const int bs_shift = __builtin_ctz(block_size);
   const int bmask = block_size - 1;
+  const int nblk = (kv_end + block_size - 1) >> bs_shift;
   // V^T staging: item = (block j of the tile, dim d, 8-token chunk cc), cc fastest,
   // so consecutive lanes read consecutive 16 B of one transposed block
   const int tb_shift = min(bs_shift, 6);          // log2 tokens of one block inside a tile
   const int cpr_shift = tb_shift - 3;             // log2 16-B chunks per block row
-  constexpr int IT = kPrefillBK * NCH / 256;      // staged 16-B items per thread (K and V each)
-  uint4 kreg[IT], vreg[IT];
-  auto stage_load = [&](int kbase) {
+  // LDS-DMA of one tile into ring slot `slot`: 16 KiB K image + 16 KiB V^T image (D
+  // = 128) = 32 wave-instructions of 1 KiB, 4 per wave.  Lanes past kv_end re-read
+  // a valid chunk (finite data; those keys are masked, their P is 0).
+  constexpr int KI = KIMG * 2 / 1024, VI = VIMG * 2 / 1024;   // 1-KiB pieces per image
+  constexpr int PER_WAVE = (KI + VI) / NW;
+  auto issue_tile = [&](int kt, int slot) {
+    const int kbase = kt * kPrefillBK;
+    uint16_t* kimg = smem + slot * SLOT;
+    uint16_t* vimg = kimg + KIMG;
+    auto blk_of = [&](int p) { return s_bt[p >> bs_shift]; };
 #pragma unroll
-    for (int it = 0; it < IT; ++it) {
-      const int idx = threadIdx.x + it * 256;
-      {  // K row t, chunk ch
-        const int t = idx / NCH, ch = idx - (idx / NCH) * NCH;
-        const int p = kbase + t;
-        kreg[it] = make_uint4(0, 0, 0, 0);
-        if (p < kv_end)
-          kreg[it] = *reinterpret_cast<const uint4*>(k_cache + bt[p >> bs_shift] * blk_stride +
-                                                     head_off + (size_t)(p & bmask) * D + ch * 8);
+    for (int r = 0; r < PER_WAVE; ++r) {
+      const int piece = wave + r * NW;
+      const uint16_t* src;
+      uint16_t* dst;
+      if (piece < KI) {           // K rows: lane -> (row t, LDS slot) ; source chunk = slot ^ swz
+        const int e = piece * 64 + lane;             // 16-B element of the K image
+        const int t = e / NCH, sl = e - (e / NCH) * NCH;
+        const int p = min(kbase + t, kv_end - 1);
+        src = k_cache + (size_t)blk_of(p) * blk_stride + head_off +
+              (size_t)(p & bmask) * D + (sl ^ (t & SWZ)) * 8;
+        dst = kimg + piece * 512;
+      } else {                    // V^T rows: lane -> (dim d, LDS slot); source chunk = slot ^ swz
+        const int e = (piece - KI) * 64 + lane;      // 16-B element of the V^T image
+        const int d = e >> 3, sl = e & 7;
+        const int p = min(kbase + ((sl ^ ((d >> 1) & 7)) << 3), (kv_end - 1) & ~7);
+        src = v_cache + (size_t)blk_of(p) * blk_stride + head_off +
+              (size_t)d * block_size + (p & bmask);
+        dst = vimg + (piece - KI) * 512;
       }
-      {  // V^T dim d, tokens t .. t+7
-        const int cc = idx & ((1 << cpr_shift) - 1), rest = idx >> cpr_shift;
-        const int d = rest % D, j = rest / D;
-        const int p = kbase + (j << tb_shift) + cc * 8;
-        vreg[it] = make_uint4(0, 0, 0, 0);
-        if (p < kv_end)
-          vreg[it] = *reinterpret_cast<const uint4*>(v_cache + bt[p >> bs_shift] * blk_stride +
-                                                     head_off + (size_t)d * block_size + (p & bmask));
-      }
+      glds16(src, lds_off(dst));
     }
   };
-  auto stage_write = [&]() {
-#pragma unroll
-    for (int it = 0; it < IT; ++it) {
-      const int idx = threadIdx.x + it * 256;
-      const int t = idx / NCH, ch = idx - (idx / NCH) * NCH;
-      reinterpret_cast<uint4*>(Ks + t * D)[ch ^ (t & SWZ)] = kreg[it];
-      const int cc = idx & ((1 << cpr_shift) - 1), rest = idx >> cpr_shift;
-      const int d = rest % D, j = rest / D;
-      const int c = ((j << tb_shift) >> 3) + cc;   // 16-B chunk (8 tokens) within the row
-      reinterpret_cast<uint4*>(Vs + d * kPrefillBK)[c ^ ((d >> 1) & 7)] = vreg[it];
-    }
+  // 4 tokens (8 B) of V^T row `row` starting at token t (t % 4 == 0)
+  const uint16_t* Ks = smem;          // current slot's images (set per tile)
+  const uint16_t* Vs = smem + KIMG;
+  // LDS byte address of 4 tokens (8 B) of V^T row `row` starting at token t (t % 4 == 0)
+  auto vt4 = [&](int row, int t) -> uint32_t {
+    return lds_off(Vs + row * kPrefillBK) + (((t >> 3) ^ ((row >> 1) & 7)) << 4) + (((t >> 2) & 1) << 3);
   };
 
-  if (ntiles > 0) {
-    stage_load(0);
-    stage_write();
-  }
-  __syncthreads();
-  for (int kt = 0; kt < ntiles; ++kt) {
+
+  auto tile_math = [&](int kt) {
     const int kbase = kt * kPrefillBK;
-    if (kt + 1 < ntiles) stage_load(kbase + kPrefillBK);  // in flight during this tile's math
-    // ---- S = Q K^T -----------------------------------------------------------------
-    floatx4_t s[4];
+    // ---- S^T = K Q^T: lane (l15 = query of m-tile m, lg) holds kv 16 n + 4 lg + i ----
+    floatx4_t s[MT][4];
 #pragma unroll
-    for (int n = 0; n < 4; ++n) {
-      s[n] = floatx4_t{0.f, 0.f, 0.f, 0.f};
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int n = 0; n < 4; ++n) s[m][n] = floatx4_t{0.f, 0.f, 0.f, 0.f};
+    // K A-fragments: 4 reads per 16-kv n-tile, the next n-tile's in flight
+    auto kread = [&](uint4 (&kf)[KC], int n) {
       const int row = n * 16 + l15;
 #pragma unroll
+      for (int kc = 0; kc < KC; ++kc)
+        kf[kc] = ds_read16(lds_off(Ks + row * D) + ((((kc * 4 + lg) ^ (row & SWZ))) << 4));
+    };
+    uint4 kf[2][KC];
+    kread(kf[0], 0);
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      if (n + 1 < 4) {
+        kread(kf[(n + 1) & 1], n + 1);
+        lgkm_wait<KC>();
+      } else {
+        lgkm_wait<0>();
+      }
+#pragma unroll
       for (int kc = 0; kc < KC; ++kc) {
-        const int ch = kc * 4 + lg;
-        const uint4 kb = reinterpret_cast<const uint4*>(Ks + row * D)[ch ^ (row & SWZ)];
-        s[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(qa[kc]), as_frag(kb), s[n], 0, 0,
-                                                        0);
+        dep(kf[n & 1][kc]);
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+          s[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(kf[n & 1][kc]), as_frag(qb[m][kc]),
+                                                             s[m][n], 0, 0, 0);
       }
     }
-    // ---- mask + online softmax (log2 domain) ---------------------------------------
-    float alpha[4];
+    // ---- mask + online softmax (log2 domain), one query column per lane ---------------
+    const bool edge = kbase + kPrefillBK > kv_end || kbase + kPrefillBK - 1 > first_q;
+    float alpha[MT];
 #pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
+    for (int m = 0; m < MT; ++m) {
       float mt = -INFINITY;
 #pragma unroll
-      for (int n = 0; n < 4; ++n) {
-        const int kp = kbase + n * 16 + l15;
-        float v = s[n][rr] * scale_log2;
-        if (!rvalid[rr] || kp > qpos[rr] || kp >= kv_end) v = -INFINITY;
-        s[n][rr] = v;
-        mt = fmaxf(mt, v);
-      }
-      mt = group_max<16>(mt);
-      const float mn = fmaxf(m_run[rr], mt);
+      for (int n = 0; n < 4; ++n)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float v = s[m][n][i] * scale_log2;
+          if (edge) {
+            const int kp = kbase + n * 16 + lg * 4 + i;
+            if (kp > qpos[m] || kp >= kv_end) v = -INFINITY;
+          }
+          s[m][n][i] = v;
+          mt = fmaxf(mt, v);
+        }
+      mt = kgroup_max(mt);
+      const float mn = fmaxf(m_run[m], mt);
       const float base = (mn == -INFINITY) ? 0.f : mn;
-      alpha[rr] = exp2f(m_run[rr] - base);
-      m_run[rr] = mn;
+      alpha[m] = exp2f(m_run[m] - base);
+      m_run[m] = mn;
       float ls = 0.f;
 #pragma unroll
-      for (int n = 0; n < 4; ++n) {
-        const float p = exp2f(s[n][rr] - base);
-        s[n][rr] = p;
-        ls += p;
-      }
-      l_run[rr] = l_run[rr] * alpha[rr] + ls;
+      for (int n = 0; n < 4; ++n)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float p = exp2f(s[m][n][i] - base);
+          s[m][n][i] = p;
+          ls += p;
+        }
+      l_run[m] = l_run[m] * alpha[m] + ls;
+#pragma unroll
+      for (int nd = 0; nd < ND; ++nd)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[m][nd][i] *= alpha[m];
     }
-#pragma unroll
-    for (int nd = 0; nd < ND; ++nd)
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) o[nd][rr] *= alpha[rr];
 
-    // ---- P (C layout) -> LDS -> A layout ------------------------------------------
-    uint16_t* pw = Ps[wave];
-#pragma unroll
-    for (int n = 0; n < 4; ++n)
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) pw[(lg * 4 + rr) * kPStride + n * 16 + l15] = f32_to_bf16(s[n][rr]);
-    __syncthreads();
-
-    // ---- O += P V ------------------------------------------------------------------
+    // ---- O^T += V^T P^T: k-slots of lane (., lg) = tokens {4lg.., 16+4lg..} + 32 kc ----
 #pragma unroll
     for (int kc = 0; kc < 2; ++kc) {
-      const uint4 pa = *reinterpret_cast<const uint4*>(pw + l15 * kPStride + kc * 32 + 8 * lg);
+      uint4 pb[MT];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        const floatx4_t& lo = s[m][2 * kc];
+        const floatx4_t& hi = s[m][2 * kc + 1];
+        pb[m] = make_uint4(pack2(lo[0], lo[1]), pack2(lo[2], lo[3]), pack2(hi[0], hi[1]),
+                           pack2(hi[2], hi[3]));
+      }
+      // V^T A-fragments: 2 reads per dim tile, the next tile's in flight
+      auto vread = [&](uint2 (&vv)[2], int nd) {
+        const int row = nd * 16 + l15;
+        vv[0] = ds_read8(vt4(row, kc * 32 + 4 * lg));
+        vv[1] = ds_read8(vt4(row, kc * 32 + 16 + 4 * lg));
+      };
+      uint2 vv[2][2];
+      vread(vv[0], 0);
 #pragma unroll
       for (int nd = 0; nd < ND; ++nd) {
-        // B operand: tokens kc*32 + 8 lg .. +8 of head dim nd*16 + l15
-        const int row = nd * 16 + l15;
-        const uint4 vb = reinterpret_cast<const uint4*>(Vs + row * kPrefillBK)[
-            (kc * 4 + lg) ^ ((row >> 1) & 7)];
-        o[nd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(pa), as_frag(vb), o[nd], 0, 0, 0);
+        if (nd + 1 < ND) {
+          vread(vv[(nd + 1) & 1], nd + 1);
+          lgkm_wait<2>();
+        } else {
+          lgkm_wait<0>();
+        }
+        dep(vv[nd & 1][0]);
+        dep(vv[nd & 1][1]);
+        const uint4 vf = make_uint4(vv[nd & 1][0].x, vv[nd & 1][0].y, vv[nd & 1][1].x,
+                                    vv[nd & 1][1].y);
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+          o[m][nd] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(vf), as_frag(pb[m]),
+                                                              o[m][nd], 0, 0, 0);
       }
     }
-    __syncthreads();   // every wave is done with this tile's Ks / Vs / Ps
-    if (kt + 1 < ntiles) {
-      stage_write();
-      __syncthreads();
-    }
+  };
+
+  // block-table entries of the KV range (LDS reads never wait on the DMA's vmcnt)
+  for (int i = threadIdx.x; i < nblk; i += blockDim.x) s_bt[i] = bt[i];
+  __syncthreads();
+
+#pragma unroll
+  for (int t = 0; t < NSLOT - 1; ++t)
+    if (t < ntiles) issue_tile(t, t);
+  for (int kt = 0; kt < ntiles; ++kt) {
+    const int slot = kt % NSLOT;
+    const int ahead = min(ntiles - 1 - kt, NSLOT - 1);   // tiles in flight behind tile kt
+    if (kt + NSLOT - 1 < ntiles)
+      issue_tile(kt + NSLOT - 1, (kt + NSLOT - 1) % NSLOT);  // slot of tile kt-1, retired
+    if (ahead >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * PER_WAVE) : "memory");
+    else if (ahead == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER_WAVE) : "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_WAVE) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();          // every wave's pieces of tile kt have landed
+    Ks = smem + slot * SLOT;
+    Vs = Ks + KIMG;
+    tile_math(kt);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();          // slot kt % NSLOT may be refilled
   }
 
-  // ---- normalise + store -------------------------------------------------------------
+  // ---- normalise + store: lane (l15 = query, lg) writes dims 16 nd + 4 lg .. +3 -------
 #pragma unroll
-  for (int rr = 0; rr < 4; ++rr) {
-    const float l = group_sum<16>(l_run[rr]);
-    if (!rvalid[rr]) continue;
-    const int r = wave * 16 + lg * 4 + rr;
+  for (int m = 0; m < MT; ++m) {
+    const float l = kgroup_sum(l_run[m]);
+    if (qpos[m] < 0) continue;
+    const int r = (wave * MT + m) * 16 + l15;
     const int tq = r / G, g = r - (r / G) * G;
     const float inv = l > 0.f ? 1.f / l : 0.f;
-    uint16_t* op = out + (size_t)(q0 + qs + tq) * out_stride + (kvh * G + g) * D;
+    uint16_t* op = out + (size_t)(q0 + qs + tq) * out_stride + (kvh * G + g) * D + 4 * lg;
 #pragma unroll
-    for (int nd = 0; nd < ND; ++nd) op[nd * 16 + l15] = f32_to_bf16(o[nd][rr] * inv);
+    for (int nd = 0; nd < ND; ++nd)
+      *reinterpret_cast<uint2*>(op + nd * 16) =
+          make_uint2(pack2(o[m][nd][0] * inv, o[m][nd][1] * inv),
+                     pack2(o[m][nd][2] * inv, o[m][nd][3] * inv));
   }
-  (void)nq;
 }
 
 }  // namespace ft
 
-extern "C" int ft_prefill_tile_tokens(int nq, int nkv) { return 64 / (nq / nkv); }
+extern "C" int ft_prefill_tile_tokens(int nq, int nkv) { return ft::kPrefillRows / (nq / nkv); }
 
 extern "C" int ft_prefill_attention(void* out, int out_stride, const void* q, int q_stride,
                                     const void* k_cache, const void* v_cache,
@@ -260,7 +398,7 @@ extern "C" int ft_prefill_attention(void* out, int out_stride, const void* q, in
   if (nq % nkv != 0) return -1;
   const int G = nq / nkv;
   const float scale_log2 = scale * 1.4426950408889634f;
-  dim3 grid(num_tiles, nkv), block(256);
+  dim3 grid(num_tiles, nkv), block(512);
 #define FT_PF_CASE(DD, GG)                                                                   \
   if (head_dim == DD && G == GG) {                                                           \
     hipLaunchKernelGGL((ft::prefill_attn_kernel<DD, GG>), grid, block, 0, stream,            \

@@ -129,3 +129,140 @@ class StreamingToolDetector:
         self.mode = "text"
         out, self.buf = self.buf, ""
         return "text", out
+
+
+_NAME_RE = re.compile(r'"name"\s*:\s*"((?:[^"\\]|\\.)*)"')
+_ARGS_RE = re.compile(r'"(?:parameters|arguments)"\s*:\s*')
+
+
+class StreamingToolCallParser:
+    """Incremental OpenAI ``delta.tool_calls`` from a llama3_json / hermes stream
+    (what vLLM's ``--enable-auto-tool-choice`` streams and the reference's
+    ``VLLMWithToolsHandler`` accumulates, ``/root/reference/app/core/vllm_handler.py:389-408``).
+
+    ``feed(delta)`` returns the tool-call deltas that became known: for each call
+    first ``{index, id, type, function: {name, arguments: ""}}``, then argument
+    fragments ``{index, function: {arguments}}`` as the JSON of the arguments
+    object streams in.  The concatenated fragments of a call are exactly the
+    arguments' JSON text as the model wrote it."""
+
+    def __init__(self):
+        self.buf = ""
+        self.obj_start: Optional[int] = None   # offset of the current call's '{'
+        self.header_sent = False
+        self.args_start: Optional[int] = None  # offset of the arguments value
+        self.args_sent = 0                     # chars of the value already emitted
+        self.args_end: Optional[int] = None
+        self.index = -1
+        self.call_id = ""
+        self.scan = 0                          # next offset to look for a call at
+        self.ncalls = 0
+
+    def _value_end(self, start: int) -> Optional[int]:
+        """End offset (exclusive) of the JSON value at ``start`` if complete."""
+        s = self.buf
+        if start >= len(s):
+            return None
+        if s[start] not in "{[":
+            if s[start] == '"':
+                i, esc = start + 1, False
+                while i < len(s):
+                    c = s[i]
+                    if esc:
+                        esc = False
+                    elif c == "\\":
+                        esc = True
+                    elif c == '"':
+                        return i + 1
+                    i += 1
+                return None
+            m = re.match(r"[^,}\]\s]+", s[start:])
+            return start + m.end() if m and start + m.end() < len(s) else None
+        depth, i, in_str, esc = 0, start, False, False
+        while i < len(s):
+            c = s[i]
+            if in_str:
+                if esc:
+                    esc = False
+                elif c == "\\":
+                    esc = True
+                elif c == '"':
+                    in_str = False
+            elif c == '"':
+                in_str = True
+            elif c in "{[":
+                depth += 1
+            elif c in "}]":
+                depth -= 1
+                if depth == 0:
+                    return i + 1
+            i += 1
+        return None
+
+    def _obj_end(self) -> Optional[int]:
+        return self._value_end(self.obj_start)
+
+    def feed(self, delta: str) -> List[Dict[str, Any]]:
+        self.buf += delta
+        out: List[Dict[str, Any]] = []
+        while True:
+            if self.obj_start is None:
+                i = self.buf.find("{", self.scan)
+                if i < 0:
+                    return out
+                self.obj_start = i
+                self.header_sent, self.args_start, self.args_sent, self.args_end = False, None, 0, None
+            seg = self.buf[self.obj_start:]
+            if not self.header_sent:
+                m = _NAME_RE.search(seg)
+                if m is None:
+                    return out
+                self.index = self.ncalls
+                self.ncalls += 1
+                self.call_id = f"call_{uuid.uuid4().hex[:12]}"
+                out.append({"index": self.index, "id": self.call_id, "type": "function",
+                            "function": {"name": json.loads('"' + m.group(1) + '"'), "arguments": ""}})
+                self.header_sent = True
+            if self.args_start is None:
+                m = _ARGS_RE.search(seg)
+                if m is None:
+                    end = self._obj_end()
+                    if end is None:
+                        return out
+                    out.append({"index": self.index, "function": {"arguments": "{}"}})
+                    self.obj_start, self.scan = None, end
+                    continue
+                self.args_start = self.obj_start + m.end()
+            while self.args_sent == 0 and self.args_start < len(self.buf) and \
+                    self.buf[self.args_start] in " \t\r\n":
+                self.args_start += 1  # the key's regex may have matched before the blanks arrived
+            if self.args_start >= len(self.buf):
+                return out
+            end = self.args_end if self.args_end is not None else self._value_end(self.args_start)
+            if end is not None:
+                self.args_end = end
+                raw = self.buf[self.args_start:end]
+                if raw.startswith('"'):  # arguments given as a JSON-encoded string
+                    try:
+                        raw = json.loads(raw)
+                    except json.JSONDecodeError:
+                        pass
+                    frag = raw[self.args_sent:] if self.args_sent == 0 else ""
+                else:
+                    frag = raw[self.args_sent:]
+                if frag:
+                    out.append({"index": self.index, "function": {"arguments": frag}})
+                self.args_sent = len(raw)
+                obj_end = self._obj_end()
+                if obj_end is None:
+                    return out
+                self.obj_start, self.scan = None, obj_end
+                continue
+            # arguments still streaming: emit what is certainly part of an object value
+            avail = self.buf[self.args_start:]
+            if avail.startswith("{") or avail.startswith("["):
+                frag = avail[self.args_sent:]
+                if frag:
+                    out.append({"index": self.index, "function": {"arguments": frag}})
+                    self.args_sent = len(avail)
+            return out

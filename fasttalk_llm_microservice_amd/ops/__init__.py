@@ -125,7 +125,8 @@ def decode_workspace(batch: int, nq: int, nkv: int, head_dim: int, waves: Option
 
 
 def prefill_tile_tokens(nq: int, nkv: int) -> int:
-    return 64 // (nq // nkv)
+    """Query tokens per prefill workgroup (256 MFMA rows of token x GQA head)."""
+    return 256 // (nq // nkv)
 
 
 def decode_attention(out, q, k_cache, v_cache, block_tables, seq_lens, tmp_out, tmp_ml, nq, nkv,
@@ -220,14 +221,10 @@ def kv_swap(caches, ptrs, ids: torch.Tensor, staging: torch.Tensor, to_staging: 
 # decode-shape (M <= 64) weight-streaming GEMM + fused row epilogues
 # ---------------------------------------------------------------------------------
 
-# (nt, u) instantiated; u == 0 selects the K-split-wave variant (skinny_ks_kernel),
-# u == -1 the x-in-LDS variant (skinny_xs_kernel), u == -2 the x-chunk variant (skinny_xc_kernel),
-# u == -3 pre-packed weights (skinny_pk_kernel; pass pack_weight(w) as w), u == -4 the x-chunk
-# variant on pre-packed weights
-SKINNY_CONFIGS = [(1, 2), (1, 4), (2, 2), (2, 4), (4, 1), (4, 2), (1, 0), (2, 0), (4, 0),
-                  (1, -1), (2, -1), (4, -1), (1, -2), (2, -2), (1, -3), (2, -3), (4, -3),
-                  (1, -4), (2, -4)]
-PACKED_VARIANTS = (-3, -4, -5)
+# (nt, u) instantiated: u == -3 the "pk" kernel, u == -4 the "xc" kernel, both on
+# pre-packed weights (pass pack_weight(w) as w)
+SKINNY_CONFIGS = [(1, -3), (2, -3), (4, -3), (1, -4), (2, -4)]
+PACKED_VARIANTS = (-3, -4)
 
 
 def pack_weight(w: torch.Tensor) -> torch.Tensor:
@@ -241,17 +238,13 @@ def pack_weight(w: torch.Tensor) -> torch.Tensor:
     return p.view(n, k)
 
 
-def skinny_gemm_supported(m: int, n: int, k: int) -> bool:
-    return 0 < m <= 64 and n % 16 == 0 and k % 128 == 0
-
-
-def skinny_gemm(x, w, out=None, ws=None, splits: int = 1, nt: int = 1, u: int = 2, depth: int = 4):
-    """y = x w^T (M <= 64).  splits > 1 leaves fp32 partial slabs in ``ws``
-    ([splits, M, N]) for a fused epilogue; otherwise writes bf16 ``out``.
-    u = -5: packed weights with a ``depth``-stage weight ring (2, 4 or 6)."""
+def skinny_gemm(x, w, out=None, ws=None, splits: int = 1, nt: int = 1, u: int = -3):
+    """y = x w^T (M <= 64) on a pack_weight() image.  splits > 1 leaves fp32 partial
+    slabs in ``ws`` ([splits, M, N]) for a fused epilogue; otherwise writes bf16
+    ``out``.  u = -3: "pk" kernel, u = -4: "xc" kernel."""
     if splits == 1 and out is None:
         out = torch.empty(x.shape[0], w.shape[0], dtype=x.dtype, device=x.device)
-    native().skinny_gemm(x, w, out, ws, splits, nt, u, depth)
+    native().skinny_gemm(x, w, out, ws, splits, nt, u)
     return out if splits == 1 else ws
 
 

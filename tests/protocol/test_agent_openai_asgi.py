@@ -145,6 +145,57 @@ def test_openai_chat_completions(monkeypatch, engine):
     assert c.post("/v1/chat/completions", json={"messages": []}).status_code == 400
 
 
+def _sse(text):
+    out = []
+    for x in text.split("\n\n"):
+        if x.startswith("data: ") and x != "data: [DONE]":
+            out.append(json.loads(x[6:]))
+    return out
+
+
+def test_openai_streams_with_tools(monkeypatch, engine):
+    """with ``tools`` the facade streams -- speech as content deltas
+    before finish_reason, tool calls as incremental delta.tool_calls (id + name
+    first, then argument fragments), like vLLM's auto tool choice that the
+    reference consumes (/root/reference/app/core/vllm_handler.py:389-408)."""
+    from app.core.websocket_server_vllm import WebSocketLLMServer
+    from app.utils.config import Config
+
+    monkeypatch.setenv("LLM_PROVIDER", "native")
+    monkeypatch.setenv("ENABLE_PYDANTIC_AI", "false")
+    c = TestClient(WebSocketLLMServer(Config(), engine=engine).app)
+    tools = [{"type": "function", "function": {"name": "get_weather", "parameters": {
+        "type": "object", "properties": {"city": {"type": "string", "maxLength": 12}}}}}]
+    # tool call: forced by tool_choice, streamed incrementally
+    s = c.post("/v1/chat/completions", json={
+        "messages": [{"role": "user", "content": "weather?"}], "tools": tools,
+        "tool_choice": "required", "max_tokens": 48, "seed": 3, "stream": True})
+    chunks = _sse(s.text)
+    tc = [ch["choices"][0]["delta"]["tool_calls"] for ch in chunks
+          if "tool_calls" in ch["choices"][0]["delta"]]
+    assert len(tc) >= 2, "tool call must stream in more than one chunk"
+    first = tc[0][0]
+    assert first["index"] == 0 and first["id"].startswith("call_")
+    assert first["function"]["name"] == "get_weather" and first["function"]["arguments"] == ""
+    args = "".join(d["function"]["arguments"] for deltas in tc for d in deltas if d["index"] == 0)
+    assert "city" in json.loads(args)
+    assert chunks[-1]["choices"][0]["finish_reason"] == "tool_calls"
+    # speech: content chunks arrive one by one, before the finishing chunk
+    s = c.post("/v1/chat/completions", json={
+        "messages": [{"role": "user", "content": "say hi"}], "tools": tools,
+        "max_tokens": 12, "temperature": 0, "ignore_eos": True, "stream": True})
+    chunks = _sse(s.text)
+    deltas = [ch["choices"][0]["delta"] for ch in chunks]
+    fin = [i for i, ch in enumerate(chunks) if ch["choices"][0]["finish_reason"]]
+    assert fin == [len(chunks) - 1]
+    content = [i for i, d in enumerate(deltas) if d.get("content")]
+    calls = [i for i, d in enumerate(deltas) if d.get("tool_calls")]
+    # random weights decide whether the first characters look like a tool call;
+    # either way the reply streams in several chunks before finish_reason
+    assert len(content) >= 2 or len(calls) >= 1
+    assert all(i < fin[0] for i in content + calls)
+
+
 # ----------------------------------------------------------------------------- ASGI over aiohttp
 def test_aiohttp_asgi_transport_serves_ws_and_http(monkeypatch, engine):
     import aiohttp

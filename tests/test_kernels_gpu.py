@@ -358,17 +358,20 @@ def test_w4_gemm_matches_fp32(m, n, k, nt, splits):
 # ----------------------------------------------------------------------------------
 
 @pytest.mark.parametrize("m", [1, 7, 16, 33, 64])
-@pytest.mark.parametrize("nt,u,splits", [(1, 2, 1), (2, 2, 4), (4, 1, 16), (4, 2, 8), (1, 4, 2)])
+@pytest.mark.parametrize("nt,u,splits", [(1, -3, 1), (2, -3, 4), (4, -3, 2), (1, -4, 1), (2, -4, 2)])
 def test_skinny_gemm(m, nt, u, splits):
+    """Packed-weight decode GEMMs ("pk" u=-3, "xc" u=-4) vs fp32, bf16 out and
+    split-K fp32 slabs."""
     n, k = 1024, 4096
     w = (torch.randn(n, k, device=DEV) * 0.05).bfloat16()
     x = torch.randn(m, k, device=DEV).bfloat16()
     ref_y = x.float() @ w.float().t()
+    wp = ops.pack_weight(w)
     if splits == 1:
-        y = ops.skinny_gemm(x, w, nt=nt, u=u).float()
+        y = ops.skinny_gemm(x, wp, nt=nt, u=u).float()
     else:
         ws = torch.empty(splits * m * n, device=DEV)
-        ops.skinny_gemm(x, w, ws=ws, splits=splits, nt=nt, u=u)
+        ops.skinny_gemm(x, wp, ws=ws, splits=splits, nt=nt, u=u)
         y = ws.view(splits, m, n).sum(0)
     _close(y, ref_y, atol=3e-2, rtol=1e-2, msg="skinny_gemm")
 
@@ -378,7 +381,7 @@ def test_skinny_gemm_strided_x():
     w = (torch.randn(n, k, device=DEV) * 0.05).bfloat16()
     big = torch.randn(m, k + 512, device=DEV).bfloat16()
     x = big[:, :k]
-    y = ops.skinny_gemm(x, w, nt=2, u=2)
+    y = ops.skinny_gemm(x, ops.pack_weight(w), nt=2, u=-3)
     _close(y, x.float() @ w.float().t(), atol=3e-2, rtol=1e-2, msg="strided")
 
 
