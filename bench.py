@@ -67,9 +67,15 @@ def main():
     ap.add_argument("--device", default="cuda", help="TP mode only: cpu runs the same path over gloo")
     ap.add_argument("--quant", default="", choices=["", "w4", "awq"],
                     help="W4A16 layer weights (the reference's AWQ-INT4 model); default bf16")
+    ap.add_argument("--agent-tools", type=float, default=-1.0, metavar="FRAC",
+                    help="BASELINE config 5: agent with JSON-guided tool calls, FRAC of the turns "
+                         "ask for a web search (stub backend); e.g. 0.2")
     a = ap.parse_args()
     if a.quant:
         os.environ["ENGINE_QUANTIZATION"] = a.quant
+    if a.agent_tools >= 0:
+        os.environ["AGENT_GUIDED_TOOL_CALLS"] = "true"
+        os.environ.setdefault("WEB_SEARCH_BACKEND", "stub")
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -89,7 +95,7 @@ def main():
     parent_conn, child_conn = ctx.Pipe()
     client = ctx.Process(target=client_process, daemon=True,
                          args=(child_conn, f"ws://127.0.0.1:{port}/ws/llm", a.sessions, sess_cfg,
-                               a.words, rank))
+                               a.words, rank, a.agent_tools))
     client.start()
 
     # ---- service stack on this rank's GPU ------------------------------------------
@@ -186,7 +192,9 @@ def main():
     metrics = engine.engine.metrics()
     if rank == 0:
         out = {
-            "metric": "output tokens/sec (node) + p50 TTFT over WebSocket, Llama-3-8B at 50 sessions",
+            "metric": "output tokens/sec (node) + p50 TTFT over WebSocket, Llama-3-8B at 50 sessions"
+                      + (f" (agent, guided tool calls on {a.agent_tools:.0%} of turns)"
+                         if a.agent_tools >= 0 else ""),
             "value": round(value, 2),
             "unit": "tokens/s",
             "n_gpus": world,

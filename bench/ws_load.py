@@ -28,13 +28,28 @@ WORDS = ("the voice assistant should answer quickly and naturally about weather 
          "meeting schedule reminder question answer story idea project update please thanks").split()
 
 
-def user_text(rng: random.Random, words: int) -> str:
-    return " ".join(rng.choice(WORDS) for _ in range(words)).capitalize() + "?"
+# words that never trigger the agent's tool heuristics (app/agents/voice_agent.py _TOOL_HINTS)
+PLAIN_WORDS = tuple(w for w in WORDS if w not in ("news", "weather", "question", "answer",
+                                                  "schedule", "reminder", "update"))
+
+
+def user_text(rng: random.Random, words: int, tool_frac: float = -1.0) -> str:
+    """A synthetic user turn.  ``tool_frac >= 0`` (agent tool-calling bench, BASELINE
+    config 5): that fraction of turns asks for a web search, the rest are plain
+    chat with no tool-hint words."""
+    if tool_frac < 0:
+        return " ".join(rng.choice(WORDS) for _ in range(words)).capitalize() + "?"
+    if rng.random() < tool_frac:
+        topic = " ".join(rng.choice(PLAIN_WORDS) for _ in range(max(1, words // 4)))
+        return f"Search the web for the latest news about {topic}?"
+    return " ".join(rng.choice(PLAIN_WORDS) for _ in range(words)).capitalize() + "."
 
 
 class Session:
-    def __init__(self, idx: int, url: str, cfg: Dict[str, Any], words: int, seed: int):
+    def __init__(self, idx: int, url: str, cfg: Dict[str, Any], words: int, seed: int,
+                 tool_frac: float = -1.0):
         self.idx = idx
+        self.tool_frac = tool_frac
         self.url = url
         self.cfg = cfg
         self.words = words
@@ -54,7 +69,8 @@ class Session:
 
     async def turn(self) -> Dict[str, Any]:
         t0 = time.perf_counter()
-        await self.ws.send_json({"type": "user_message", "text": user_text(self.rng, self.words)})
+        await self.ws.send_json({"type": "user_message",
+                                 "text": user_text(self.rng, self.words, self.tool_frac)})
         first = None
         frames = 0
         while True:
@@ -90,7 +106,9 @@ class Session:
 
 
 class LoadClient:
-    def __init__(self, url: str, sessions: int, cfg: Dict[str, Any], words: int = 40, seed: int = 0):
+    def __init__(self, url: str, sessions: int, cfg: Dict[str, Any], words: int = 40, seed: int = 0,
+                 tool_frac: float = -1.0):
+        self.tool_frac = tool_frac
         self.url = url
         self.n = sessions
         self.cfg = cfg
@@ -103,7 +121,8 @@ class LoadClient:
         import aiohttp
 
         self.http = aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=None))
-        self.sessions = [Session(i, self.url, self.cfg, self.words, self.seed) for i in range(self.n)]
+        self.sessions = [Session(i, self.url, self.cfg, self.words, self.seed, self.tool_frac)
+                         for i in range(self.n)]
         await asyncio.gather(*[s.open(self.http) for s in self.sessions])
 
     async def run_turns(self, turns: int) -> Dict[str, Any]:
@@ -132,11 +151,12 @@ class LoadClient:
             await self.http.close()
 
 
-def client_process(conn, url: str, sessions: int, cfg: Dict[str, Any], words: int, seed: int):
+def client_process(conn, url: str, sessions: int, cfg: Dict[str, Any], words: int, seed: int,
+                   tool_frac: float = -1.0):
     """Child-process entry: commands over a pipe ('open', ('run', n), 'close')."""
     loop = asyncio.new_event_loop()
     asyncio.set_event_loop(loop)
-    lc = LoadClient(url, sessions, cfg, words, seed)
+    lc = LoadClient(url, sessions, cfg, words, seed, tool_frac)
     try:
         while True:
             cmd = conn.recv()

@@ -129,6 +129,14 @@ class ModelRunner:
         self.stg = [_Staging(mb, self.max_blocks_per_seq, pin, self.is_gpu) for _ in range(2)]
         self._stg_next = 0
         self.h_out = torch.zeros(mb, dtype=i32, pin_memory=pin)  # eager-step sampler output
+        # guided decoding (E19): the token allow-mask is a STATIC input of every
+        # decode graph -- all-ones rows for unguided sequences -- so a batch with
+        # one tool-calling session stays on the graph path (it only loses the
+        # one-step-ahead pipelining: the next mask depends on this step's token)
+        self.mask_words = (model_cfg.vocab_size + 31) // 32
+        self.d_mask = torch.full((mb, self.mask_words), -1, dtype=i32, device=dv) if self.is_gpu else None
+        self.h_mask = torch.full((mb, self.mask_words), -1, dtype=i32, pin_memory=pin) if self.is_gpu else None
+        self._mask_rows = 0   # leading rows of d_mask that may hold a non-trivial mask
         self.d_logits_idx = torch.arange(mb, dtype=torch.int64, device=dv)
         # decode-attention partials: one slot per (sequence, kv head) + one per wave
         # of the kernel's grid (any step has at most max_num_seqs decode rows)
@@ -365,15 +373,15 @@ class ModelRunner:
     def _decode(self, batch: ScheduledBatch, masks) -> List[int]:
         seqs = batch.decode_seqs
         n = len(seqs)
-        bucket = self._bucket(n) if (self.use_graphs and masks is None) else None
+        bucket = self._bucket(n) if self.use_graphs else None
         if bucket is None:
             return self._decode_eager(seqs, masks)
-        return self.decode_collect(self.decode_launch(seqs))
+        return self.decode_collect(self.decode_launch(seqs, masks=masks))
 
     def can_pipeline(self, n: int) -> bool:
         return self.use_graphs and self._bucket(n) is not None
 
-    def decode_launch(self, seqs, ahead: int = 0) -> DecodeHandle:
+    def decode_launch(self, seqs, ahead: int = 0, masks: Optional[np.ndarray] = None) -> DecodeHandle:
         """Fills a staging set and queues a graph-replayed decode step (returns at
         once).  ``ahead=1`` launches the step AFTER the one in flight: positions
         are one further and the input ids are the in-flight step's sampled ids,
@@ -386,9 +394,27 @@ class ModelRunner:
         if self.bcast is not None:
             self.bcast.send(("graph", {"nb": nb, "n": n, "small": st.hs.copy(),
                                        "bt": st.hbt[:nb, :maxblk].copy(), "f32": st.hf.copy(),
-                                       "seeds": st.hseed.copy(), "from_device": bool(ahead)}, None))
+                                       "seeds": st.hseed.copy(), "from_device": bool(ahead)}, masks))
+        self._set_masks(masks, n)
         self._decode_enqueue(st, nb, n, from_device=bool(ahead))
         return DecodeHandle(st, n, nb)
+
+    def _set_masks(self, masks: Optional[np.ndarray], n: int):
+        """Uploads the step's allow-masks into the graph's static mask rows (stream
+        ordered before the replay); resets rows a previous guided step dirtied."""
+        if self.d_mask is None:
+            return
+        if masks is None:
+            if self._mask_rows:
+                self.d_mask[:self._mask_rows].fill_(-1)
+                self._mask_rows = 0
+            return
+        rows = max(n, self._mask_rows)
+        hm = self.h_mask.numpy()
+        hm[:n, : masks.shape[1]] = masks[:n]
+        hm[n:rows] = -1
+        self.d_mask[:rows].copy_(self.h_mask[:rows], non_blocking=True)
+        self._mask_rows = n
 
     def decode_collect(self, h: DecodeHandle) -> List[int]:
         self._wait(h.stage.event)
@@ -460,6 +486,7 @@ class ModelRunner:
             self._mixed_run(host, masks)
         elif kind == "graph":
             nb, n = host["nb"], host["n"]
+            self._set_masks(masks, n)
             st = self.stg[0]
             st.hs[:] = host["small"]
             bt = host["bt"]
@@ -488,7 +515,8 @@ class ModelRunner:
         h = self.model.forward(self.d_input_ids[:nb], meta, self.kv)
         logits = self.model.compute_logits(h)
         ops.sample(logits, self.d_temp[:nb], self.d_top_p[:nb], self.d_top_k[:nb],
-                   self.d_seeds[:nb], self.d_steps[:nb], out=self.d_out[:nb])
+                   self.d_seeds[:nb], self.d_steps[:nb], out=self.d_out[:nb],
+                   mask=self.d_mask[:nb] if self.d_mask is not None else None)
 
     @torch.inference_mode()
     def _capture(self, nb: int):

@@ -181,3 +181,33 @@ def test_w4_engine_graph_matches_eager():
     outs = [_engine(model="tiny-2k", quantization="w4", enforce_eager=e).generate(prompts, sp)
             for e in (False, True)]
     assert outs[0] == outs[1]
+
+
+def test_guided_rows_stay_on_the_decode_graph():
+    """a JSON-guided (tool-call) sequence inside a batch of plain
+    ones keeps every decode step on the hipGraph path -- the allow-mask is a static
+    graph input, all-ones for unguided rows -- and still yields schema-valid JSON."""
+    import json
+
+    from fasttalk_llm_microservice_amd.engine.guided import GuidedSpec
+
+    eng = _engine(max_num_seqs=16)
+    spec = GuidedSpec.json_schema({"type": "object", "properties": {
+        "city": {"type": "string", "maxLength": 8}, "n": {"type": "integer"}},
+        "required": ["city", "n"]})
+    prompts = _prompts(6, [12, 20, 28, 9, 33, 17], seed=4)
+    res = {}
+    for i, p in enumerate(prompts):
+        sp = SamplingParams(temperature=0.7, seed=10 + i, max_tokens=40,
+                            guided=spec if i == 2 else None, ignore_eos=i != 2)
+        eng.add_request(f"g{i}", p, sp, on_output=lambda o, i=i: res.setdefault(i, []).extend(o.token_ids))
+    while eng.has_work():
+        eng.step()
+    st = eng.runner.stats
+    assert st["eager_decode"] == 0 and st["graph_replays"] > 0, st
+    text = eng.tokenizer.decode(res[2])
+    obj = json.loads(text)
+    assert set(obj) == {"city", "n"} and isinstance(obj["n"], int)
+    assert all(len(res[i]) == 40 for i in range(6) if i != 2)
+    # the mask rows a guided step dirtied are reset for the next plain steps
+    assert eng.runner._mask_rows == 0 or eng.scheduler.has_work()
