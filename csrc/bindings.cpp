@@ -53,7 +53,10 @@ int ft_ar_ipc_open(const char* in64, void** ptr);
 int ft_ar_ipc_close(void* ptr);
 int ft_ar_read_error(void* mine, int* err);
 int ft_ar_allreduce(void* out, const void* x, long n, const uint64_t* peers_dev, int rank, int world,
-                    size_t max_bytes, unsigned spin_budget, hipStream_t stream);
+                    size_t max_bytes, unsigned spin_budget, int two_shot, hipStream_t stream);
+int ft_ar_allgather(void* out, const void* x, long rows, long row_elems, const uint64_t* peers_dev,
+                    int rank, int world, size_t max_bytes, unsigned spin_budget, hipStream_t stream);
+int ft_ar_export_error(int* dst, const uint64_t* peers_dev, int world, hipStream_t stream);
 int ft_skinny_gemm_pk(const void* x, int x_stride, int M, const void* wpk, int N, int K, float* ws,
                       void* out, int out_stride, int splits, int nt, hipStream_t stream);
 int ft_pkr_gemm(const void* x, int x_stride, int M, const void* wpk, int N, int K, float* ws,
@@ -465,15 +468,38 @@ int64_t custom_ar_error(int64_t p) {
   return e;
 }
 void custom_ar_allreduce(at::Tensor out, at::Tensor x, at::Tensor peers, int64_t rank, int64_t world,
-                         int64_t max_bytes, int64_t spin_budget) {
+                         int64_t max_bytes, int64_t spin_budget, bool two_shot) {
   check_bf16(out, "out");
   check_bf16(x, "x");
   TORCH_CHECK(x.is_contiguous() && out.is_contiguous() && out.numel() == x.numel(), "contiguous");
   TORCH_CHECK(peers.scalar_type() == at::kLong && peers.is_cuda() && peers.numel() == world, "peers");
+  TORCH_CHECK(x.numel() % 8 == 0 && x.numel() * 2 <= max_bytes, "custom_ar_allreduce: size");
   check_rc(ft_ar_allreduce(out.data_ptr(), x.data_ptr(), (long)x.numel(),
                            reinterpret_cast<const uint64_t*>(peers.data_ptr<int64_t>()), (int)rank,
-                           (int)world, (size_t)max_bytes, (unsigned)spin_budget, cur_stream()),
+                           (int)world, (size_t)max_bytes, (unsigned)spin_budget, two_shot ? 1 : 0,
+                           cur_stream()),
            "custom_ar_allreduce");
+}
+// x: [rows, shard] bf16 -> out: [rows, world * shard]
+void custom_ar_allgather(at::Tensor out, at::Tensor x, at::Tensor peers, int64_t rank, int64_t world,
+                         int64_t max_bytes, int64_t spin_budget) {
+  check_bf16(out, "out");
+  check_bf16(x, "x");
+  TORCH_CHECK(x.dim() == 2 && out.dim() == 2 && x.is_contiguous() && out.is_contiguous(), "2-D contiguous");
+  TORCH_CHECK(out.size(0) == x.size(0) && out.size(1) == x.size(1) * world, "allgather shapes");
+  TORCH_CHECK(x.size(1) % 8 == 0 && x.numel() * 2 <= max_bytes, "custom_ar_allgather: size");
+  TORCH_CHECK(peers.scalar_type() == at::kLong && peers.is_cuda() && peers.numel() == world, "peers");
+  check_rc(ft_ar_allgather(out.data_ptr(), x.data_ptr(), (long)x.size(0), (long)x.size(1),
+                           reinterpret_cast<const uint64_t*>(peers.data_ptr<int64_t>()), (int)rank,
+                           (int)world, (size_t)max_bytes, (unsigned)spin_budget, cur_stream()),
+           "custom_ar_allgather");
+}
+void custom_ar_export_error(at::Tensor dst, at::Tensor peers, int64_t world) {
+  TORCH_CHECK(dst.is_cuda() && dst.scalar_type() == at::kInt && dst.numel() >= 1, "dst: int32 device");
+  TORCH_CHECK(peers.scalar_type() == at::kLong && peers.is_cuda() && peers.numel() == world, "peers");
+  check_rc(ft_ar_export_error(dst.data_ptr<int>(), reinterpret_cast<const uint64_t*>(peers.data_ptr<int64_t>()),
+                              (int)world, cur_stream()),
+           "custom_ar_export_error");
 }
 
 // residual = table[ids]; out = rmsnorm(residual) * w  (embedding + first RMSNorm)
@@ -616,6 +642,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("custom_ar_close", &custom_ar_close);
   m.def("custom_ar_error", &custom_ar_error);
   m.def("custom_ar_allreduce", &custom_ar_allreduce);
+  m.def("custom_ar_allgather", &custom_ar_allgather);
+  m.def("custom_ar_export_error", &custom_ar_export_error);
   m.def("slab_silu", &slab_silu);
   m.def("slab_store", &slab_store);
   m.def("slab_rope_kv", &slab_rope_kv, py::arg("ws"), py::arg("splits"), py::arg("rows"),

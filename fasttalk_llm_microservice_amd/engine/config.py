@@ -52,7 +52,9 @@ class EngineConfig:
     graph_batch_sizes: Tuple[int, ...] = (1, 2, 4, 8, 16, 24, 32, 48, 64, 80, 96, 128, 160, 192, 224, 256)
     async_output: bool = True          # overlap detokenize/streaming with the next GPU step
     separate_process: bool = False     # run the step loop in its own process (no GIL sharing)
-    custom_allreduce: bool = False     # TP: one-shot xGMI all-reduce for decode-size messages
+    custom_allreduce: bool = False     # TP: xGMI one/two-shot all-reduce for decode-size messages
+    tp_share_device: bool = False      # TP ranks all on device_base (tests: gloo control + IPC data)
+    max_restarts: int = 3              # separate-process engines: respawns after a replica dies
     quantization: Optional[str] = None  # None | "awq" | "w4" (W4A16, group 128; --quantization awq)
 
     def resolved_device(self) -> str:
@@ -97,12 +99,18 @@ class EngineConfig:
             swap_space_gb=_env(["ENGINE_SWAP_SPACE", "VLLM_SWAP_SPACE"], 4.0, float),
             enable_prefix_caching=_env(["ENGINE_PREFIX_CACHING"], True, _bool),
             enforce_eager=_env(["ENGINE_ENFORCE_EAGER", "VLLM_ENFORCE_EAGER"], False, _bool),
-            separate_process=_env(["ENGINE_SEPARATE_PROCESS"], False, _bool),
+            separate_process=_env(["ENGINE_SEPARATE_PROCESS"], None, _bool),
             custom_allreduce=_env(["ENGINE_CUSTOM_ALLREDUCE"], False, _bool),
+            tp_share_device=_env(["ENGINE_TP_SHARE_DEVICE"], False, _bool),
+            max_restarts=_env(["ENGINE_MAX_RESTARTS"], 3, int),
             quantization=_env(["ENGINE_QUANTIZATION", "VLLM_QUANTIZATION"], None) or None,
         )
         for k, v in overrides.items():
             setattr(c, k, v)
+        if c.separate_process is None:
+            # a TP group runs in its own process by default: when a worker dies the
+            # supervisor (parallel/dp_router.py) can tear the group down and respawn it
+            c.separate_process = c.tp_size > 1
         if c.quantization is None and "awq" in c.model.lower():
             # the reference's default model (hugging-quants/...-AWQ-INT4) runs W4A16
             c.quantization = "awq"

@@ -458,8 +458,14 @@ class AsyncEngine:
         self.engine.shutdown()
 
     def is_healthy(self, stall_s: float = 120.0) -> bool:
-        """Watchdog: the step loop must be alive and, when busy, making progress."""
+        """Watchdog: the step loop must be alive and, when busy, making progress;
+        every tensor-parallel worker process must be running (a dead worker leaves
+        rank 0 blocked in a collective: /health turns 503 at once, not after the
+        stall timeout)."""
         if self.error is not None or self._thread is None or not self._thread.is_alive():
+            return False
+        group = getattr(self.engine, "tp_group", None)
+        if group is not None and hasattr(group, "alive") and not group.alive():
             return False
         if self.engine.has_work() and time.time() - self.heartbeat > stall_s:
             return False
@@ -529,6 +535,10 @@ class AsyncEngine:
         device OOM (torch.cuda.OutOfMemoryError) and sticky HIP faults are fatal,
         so /health turns unhealthy instead of every later step failing silently."""
         if isinstance(e, MemoryError):
+            return False
+        from ..parallel.shm_broadcast import PeerDied
+
+        if isinstance(e, PeerDied):  # a TP worker is gone: the group cannot step again
             return False
         try:
             import torch

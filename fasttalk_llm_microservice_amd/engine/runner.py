@@ -11,6 +11,7 @@ from __future__ import annotations
 
 import logging
 import math
+import os
 import time
 from typing import Dict, List, Optional, Tuple
 
@@ -25,6 +26,11 @@ from .config import EngineConfig
 from .scheduler import ScheduledBatch
 
 log = logging.getLogger("fasttalk.engine.runner")
+
+
+class CommFault(RuntimeError):
+    """A tensor-parallel collective of this step timed out (custom all-reduce spin
+    budget): the step's tokens are discarded and the group now runs on RCCL."""
 
 
 def _pow2_ceil(x: int) -> int:
@@ -42,6 +48,8 @@ class _Staging:
         self.h_f32 = torch.zeros(2 * mb, dtype=torch.float32, pin_memory=pin)
         self.h_seeds = torch.zeros(mb, dtype=torch.int64, pin_memory=pin)
         self.h_out = torch.zeros(mb, dtype=i32, pin_memory=pin)
+        self.h_err = torch.zeros(1, dtype=i32, pin_memory=pin)  # TP collective error flag
+        self.err_armed = False
         self.hs = self.h_small.numpy()
         self.hbt = self.h_bt.numpy()
         self.hf = self.h_f32.numpy()
@@ -129,6 +137,9 @@ class ModelRunner:
         self.stg = [_Staging(mb, self.max_blocks_per_seq, pin, self.is_gpu) for _ in range(2)]
         self._stg_next = 0
         self.h_out = torch.zeros(mb, dtype=i32, pin_memory=pin)  # eager-step sampler output
+        self.h_err = torch.zeros(1, dtype=i32, pin_memory=pin)
+        # TP rank 0 decides about collective faults; workers only follow its messages
+        self.checks_comm = comm.world_size > 1 and comm.rank == 0
         # guided decoding (E19): the token allow-mask is a STATIC input of every
         # decode graph -- all-ones rows for unguided sequences -- so a batch with
         # one tool-calling session stays on the graph path (it only loses the
@@ -148,7 +159,15 @@ class ModelRunner:
         self._done_event = torch.cuda.Event() if self.is_gpu else None
         self.graphs: Dict[int, torch.cuda.CUDAGraph] = {}
         self.graph_pool = None
-        self.use_graphs = self.is_gpu and not cfg.enforce_eager
+        self.use_graphs = self.is_gpu and not cfg.enforce_eager and comm.graph_safe()
+        # FT_FAULT_TP_STALL="<n>:<seconds>" (TP workers): before executing the n-th
+        # decode graph message, stall until rank 0's custom all-reduce has run out of
+        # spin budget (its error word is set; at most <seconds>) -- the fault test
+        # of the collective timeout contract
+        stall = os.environ.get("FT_FAULT_TP_STALL", "") if comm.rank > 0 else ""
+        self._stall_at, self._stall_s = (int(stall.split(":")[0]), float(stall.split(":")[1])) \
+            if stall else (None, 0.0)
+        self._graph_msgs = 0
         self.stats = {"graph_replays": 0, "eager_decode": 0, "prefill_steps": 0, "captures": 0}
         self.bcast = None  # TP rank 0: parallel.shm_broadcast.ShmBroadcast writer
 
@@ -361,14 +380,51 @@ class ModelRunner:
         if not self.is_gpu:
             return out.tolist()
         n = out.shape[0]
+        flag = self._arm_comm_check()
+        if flag is not None:
+            self.h_err.copy_(flag, non_blocking=True)
         if n <= self.h_out.shape[0]:
             self.h_out[:n].copy_(out, non_blocking=True)
             self._wait()
-            return self.h_out[:n].tolist()
-        host = torch.empty(n, dtype=out.dtype, pin_memory=True)
-        host.copy_(out, non_blocking=True)
-        self._wait()
+            host = self.h_out[:n]
+        else:
+            host = torch.empty(n, dtype=out.dtype, pin_memory=True)
+            host.copy_(out, non_blocking=True)
+            self._wait()
+        if flag is not None and int(self.h_err[0]):
+            self._comm_fault()
         return host.tolist()
+
+    # ------------------------------------------------------------------ TP fault contract
+    def _arm_comm_check(self) -> Optional[torch.Tensor]:
+        """Queues the fold of every rank's collective error word into the device
+        flag (eager steps; decode graphs carry it) and returns the flag, or None
+        when this rank does not check (single GPU, workers, RCCL only)."""
+        flag = self.comm.error_flag
+        if flag is None or not self.checks_comm:
+            return None
+        self.comm.export_error()
+        return flag
+
+    def _comm_fault(self):
+        """Rank 0 saw a timed-out custom collective: every rank drops to RCCL (in
+        message order, so the collectives stay matched) and the step fails."""
+        if self.bcast is not None:
+            self.bcast.send(("comm_fault", None, None))
+        self._drop_custom_collectives()
+        raise CommFault("tensor-parallel all-reduce timed out waiting for a peer; "
+                        "step discarded, group switched to RCCL")
+
+    def _drop_custom_collectives(self):
+        if self.is_gpu:
+            torch.cuda.synchronize(self.device)  # no graph of the old kind still running
+        self.comm.disable_custom("custom collective timed out")
+        self.graphs.clear()  # they captured the custom kernels; recaptured on demand
+        if not self.comm.graph_safe():
+            self.use_graphs = False
+        for st in self.stg:
+            st.err_armed = False
+            st.h_err.zero_()
 
     def _decode(self, batch: ScheduledBatch, masks) -> List[int]:
         seqs = batch.decode_seqs
@@ -417,8 +473,11 @@ class ModelRunner:
         self._mask_rows = n
 
     def decode_collect(self, h: DecodeHandle) -> List[int]:
-        self._wait(h.stage.event)
-        return h.stage.h_out[:h.n].tolist()
+        st = h.stage
+        self._wait(st.event)
+        if st.err_armed and int(st.h_err[0]):
+            self._comm_fault()
+        return st.h_out[:h.n].tolist()
 
     def _decode_fill(self, seqs, nb: int, st: "_Staging", ahead: int = 0) -> int:
         """Writes a decode step's inputs into a pinned staging set."""
@@ -472,6 +531,10 @@ class ModelRunner:
         g.replay()
         self.stats["graph_replays"] += 1
         st.h_out[:n].copy_(self.d_out[:n], non_blocking=True)
+        flag = self.comm.error_flag if self.checks_comm else None
+        st.err_armed = flag is not None
+        if flag is not None:  # the graph folded the ranks' error words into it
+            st.h_err.copy_(flag, non_blocking=True)
         st.event.record()
 
     # ------------------------------------------------------------------ TP workers
@@ -485,6 +548,13 @@ class ModelRunner:
         if kind == "mixed":
             self._mixed_run(host, masks)
         elif kind == "graph":
+            self._graph_msgs += 1
+            if self._stall_at is not None and self._graph_msgs == self._stall_at:
+                log.warning("FT_FAULT_TP_STALL: rank %d stalls", self.comm.rank)
+                t_end = time.time() + self._stall_s
+                while time.time() < t_end and not (self.comm.custom is not None
+                                                   and self.comm.custom.peer_error(0)):
+                    time.sleep(0.01)
             nb, n = host["nb"], host["n"]
             self._set_masks(masks, n)
             st = self.stg[0]
@@ -499,6 +569,8 @@ class ModelRunner:
             self.warmup(host)
         elif kind == "swap":
             self._swap(*host)
+        elif kind == "comm_fault":
+            self._drop_custom_collectives()
         else:
             raise ValueError(f"unknown TP message {kind!r}")
         return True
@@ -517,6 +589,8 @@ class ModelRunner:
         ops.sample(logits, self.d_temp[:nb], self.d_top_p[:nb], self.d_top_k[:nb],
                    self.d_seeds[:nb], self.d_steps[:nb], out=self.d_out[:nb],
                    mask=self.d_mask[:nb] if self.d_mask is not None else None)
+        if self.checks_comm:
+            self.comm.export_error()
 
     @torch.inference_mode()
     def _capture(self, nb: int):

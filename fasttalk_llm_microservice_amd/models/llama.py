@@ -278,6 +278,8 @@ class LlamaModel:
         full unsharded tensors on the host from one seed and slices them, so TP=N
         equals TP=1 exactly; otherwise every shard is drawn on the device."""
         cfg = self.cfg
+        if consistent is None and os.environ.get("FT_CONSISTENT_INIT"):
+            consistent = os.environ["FT_CONSISTENT_INIT"] == "1"  # TP-vs-TP=1 tests
         if consistent is None:
             consistent = cfg.num_params() < 2_000_000_000 and self.device.type == "cpu" or \
                 cfg.num_params() < 300_000_000

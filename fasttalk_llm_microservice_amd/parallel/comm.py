@@ -24,18 +24,34 @@ class TPComm:
         self.world_size = world_size
         self.custom = None  # CustomAllReduce, optional
         self.custom_max_bytes = 8 << 20
+        self._host_staged: Optional[bool] = None
 
     @property
     def enabled(self) -> bool:
         return self.world_size > 1
 
+    def _custom_on(self) -> bool:
+        return self.custom is not None and not self.custom.failed
+
+    def _via_host(self, x: torch.Tensor) -> bool:
+        """gloo carries device tensors through host memory (ranks sharing one GPU in
+        tests, where RCCL refuses duplicate devices); never graph-capturable."""
+        if self._host_staged is None:
+            self._host_staged = dist.get_backend(self.group) != "nccl"
+        return self._host_staged and x.is_cuda
+
     def all_reduce(self, x: torch.Tensor) -> torch.Tensor:
         if self.world_size == 1:
             return x
-        if (self.custom is not None and x.is_cuda
+        if (self._custom_on() and x.is_cuda
                 and x.numel() * x.element_size() <= self.custom_max_bytes
                 and self.custom.can_handle(x)):
             return self.custom.all_reduce(x)
+        if self._via_host(x):
+            h = x.float().cpu()
+            dist.all_reduce(h, group=self.group)
+            x.copy_(h)
+            return x
         dist.all_reduce(x, group=self.group)
         return x
 
@@ -43,9 +59,40 @@ class TPComm:
         """Concatenate rank shards along the last dim."""
         if self.world_size == 1:
             return x
+        if self._custom_on() and x.is_cuda and self.custom.can_gather(x):
+            return self.custom.all_gather_last(x)
+        if self._via_host(x):
+            h = x.cpu()
+            parts = [torch.empty_like(h) for _ in range(self.world_size)]
+            dist.all_gather(parts, h.contiguous(), group=self.group)
+            return torch.cat(parts, dim=-1).to(x.device)
         parts = [torch.empty_like(x) for _ in range(self.world_size)]
         dist.all_gather(parts, x.contiguous(), group=self.group)
         return torch.cat(parts, dim=-1)
+
+    # ---------------------------------------------------------------- fault contract
+    @property
+    def error_flag(self) -> Optional[torch.Tensor]:
+        """Device int32 flag the custom collectives' timeouts land in (None when the
+        custom path is off): the runner copies it to the host with each step's
+        sampled ids and fails the step when it is set."""
+        return self.custom.err_flag if self._custom_on() else None
+
+    def export_error(self):
+        if self._custom_on():
+            self.custom.export_error()
+
+    def disable_custom(self, reason: str = ""):
+        if self.custom is not None:
+            self.custom.disable(reason)
+
+    def graph_safe(self) -> bool:
+        """Can this group's collectives be captured in a hipGraph?"""
+        if self.world_size == 1:
+            return True
+        if self._host_staged is None:
+            self._host_staged = dist.get_backend(self.group) != "nccl"
+        return not self._host_staged or self._custom_on()
 
     def min_int(self, v: int) -> int:
         """Smallest value of ``v`` over the group (e.g. KV blocks every rank can hold)."""

@@ -1,7 +1,8 @@
-"""One-shot all-reduce over xGMI peer mappings (SURVEY.md §2.5 X1/X2, §2.7
-``custom_allreduce``), for the decode-size activations tensor parallelism
-reduces twice per layer.  The kernel and its signalling protocol are in
-``csrc/kernels/custom_ar.hip``; this module owns the IPC plumbing:
+"""All-reduce / all-gather over xGMI peer mappings (SURVEY.md §2.5 X1/X2/X4,
+§2.7 ``custom_allreduce``), for the decode-size activations tensor parallelism
+reduces twice per layer and the vocab-sharded logits it gathers once per step.
+The kernels and their signalling protocol are in ``csrc/kernels/custom_ar.hip``;
+this module owns the IPC plumbing and the fault contract:
 
 * every rank allocates one uncached device region (``hipDeviceMallocUncached``:
   epoch/error/arrival words, 8 signal slots, 2 staging buffers of
@@ -10,8 +11,20 @@ reduces twice per layer.  The kernel and its signalling protocol are in
   and opened with ``hipIpcOpenMemHandle``; the W base pointers live in a device
   int64 tensor, so the all-reduce is one kernel with fixed arguments and can be
   captured in the decode hipGraph;
-* a wait that runs past the spin budget sets an error word instead of hanging
-  the GPU; :meth:`healthy` reads it and the communicator then falls back to RCCL.
+* one-shot (every rank reads all W inputs) below ``two_shot_bytes``, two-shot
+  (reduce-scatter + all-gather, 2(W-1)/W of the remote bytes, one more
+  barrier) above it.  W=2 is always one-shot (both move n remote bytes).  The
+  default crossover (512 KiB at W=8, 1 MiB at W=4; ``ENGINE_CUSTOM_AR_TWO_SHOT``)
+  comes from the link model -- 7 xGMI links per GPU, a few microseconds per
+  cross-rank barrier -- not from a measurement: no multi-GPU box was available;
+* a wait that runs past the spin budget sets a sticky error word instead of
+  hanging the GPU, and the kernel returns with ``out`` NOT reduced.  Every
+  later collective on that rank returns at once.  :meth:`export_error` (in
+  every decode graph and after every eager step) folds all W error words into
+  :attr:`err_flag`, which the runner copies to the host with the sampled ids:
+  a set flag fails the step -- its tokens are discarded, never emitted -- and
+  the whole group switches to RCCL (:meth:`disable` on every rank, graphs
+  recaptured).
 
 Opt-in (``ENGINE_CUSTOM_ALLREDUCE=1``): messages above ``max_bytes`` (prefill)
 always go through RCCL.
@@ -19,6 +32,7 @@ always go through RCCL.
 from __future__ import annotations
 
 import logging
+import os
 from typing import List, Optional
 
 import torch
@@ -31,7 +45,8 @@ class CustomAllReduce:
     SUPPORTED_WORLD = (2, 4, 8)
 
     def __init__(self, group, rank: int, world: int, device: torch.device,
-                 max_bytes: int = 8 << 20, spin_budget: int = 1 << 26):
+                 max_bytes: int = 8 << 20, spin_budget: Optional[int] = None,
+                 two_shot_bytes: Optional[int] = None):
         from .. import ops
 
         if world not in self.SUPPORTED_WORLD:
@@ -39,7 +54,13 @@ class CustomAllReduce:
         self._C = ops.native()
         self.rank, self.world = rank, world
         self.max_bytes = int(max_bytes)
+        if spin_budget is None:
+            spin_budget = int(os.environ.get("ENGINE_CUSTOM_AR_SPIN", str(1 << 23)))  # ~1.6 s (0.19 us/spin measured)
         self.spin_budget = int(spin_budget)
+        if two_shot_bytes is None:
+            env = os.environ.get("ENGINE_CUSTOM_AR_TWO_SHOT")
+            two_shot_bytes = int(env) if env else {8: 512 << 10, 4: 1 << 20}.get(world, 1 << 62)
+        self.two_shot_bytes = int(two_shot_bytes)
         size = int(self._C.custom_ar_header_bytes()) + 2 * self.max_bytes
         self.base = int(self._C.custom_ar_alloc(size))
         handle = self._C.custom_ar_handle(self.base)
@@ -55,6 +76,7 @@ class CustomAllReduce:
                 self._opened.append(p)
                 ptrs.append(p)
         self.peers = torch.tensor(ptrs, dtype=torch.int64, device=device)
+        self.err_flag = torch.zeros(1, dtype=torch.int32, device=device)
         self.failed = False
         log.info("custom all-reduce ready: rank %d/%d, %d MiB staging", rank, world,
                  self.max_bytes >> 20)
@@ -64,15 +86,42 @@ class CustomAllReduce:
                 and x.numel() % 8 == 0 and x.numel() * 2 <= self.max_bytes)
 
     def all_reduce(self, x: torch.Tensor) -> torch.Tensor:
+        two = x.numel() * 2 >= self.two_shot_bytes
         self._C.custom_ar_allreduce(x, x, self.peers, self.rank, self.world, self.max_bytes,
-                                    self.spin_budget)
+                                    self.spin_budget, two)
         return x
 
+    def can_gather(self, x: torch.Tensor) -> bool:
+        return (not self.failed and x.dtype == torch.bfloat16 and x.dim() == 2
+                and x.is_contiguous() and x.shape[1] % 8 == 0
+                and x.numel() * 2 <= self.max_bytes)
+
+    def all_gather_last(self, x: torch.Tensor) -> torch.Tensor:
+        """[rows, shard] -> [rows, W * shard] in rank order."""
+        out = torch.empty(x.shape[0], self.world * x.shape[1], dtype=x.dtype, device=x.device)
+        self._C.custom_ar_allgather(out, x, self.peers, self.rank, self.world, self.max_bytes,
+                                    self.spin_budget)
+        return out
+
+    def export_error(self):
+        """err_flag <- OR of every rank's error word (stream ordered, graph-safe)."""
+        self._C.custom_ar_export_error(self.err_flag, self.peers, self.world)
+
+    def disable(self, reason: str = ""):
+        if not self.failed:
+            log.error("custom all-reduce disabled on rank %d (%s); the group uses RCCL from now on",
+                      self.rank, reason or "peer timeout")
+        self.failed = True
+
+    def peer_error(self, r: int) -> int:
+        """Host read of rank r's error word through its mapping (tests, diagnostics)."""
+        ptr = self.base if r == self.rank else int(self.peers[r].item())
+        return int(self._C.custom_ar_error(ptr))
+
     def healthy(self) -> bool:
-        """Synchronising check of the error word (call outside hot loops)."""
+        """Synchronising check of this rank's error word (call outside hot loops)."""
         if not self.failed and int(self._C.custom_ar_error(self.base)):
-            log.error("custom all-reduce timed out waiting for a peer; falling back to RCCL")
-            self.failed = True
+            self.disable("timed out waiting for a peer")
         return not self.failed
 
     def close(self):

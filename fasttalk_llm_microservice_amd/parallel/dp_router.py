@@ -13,6 +13,13 @@ so :class:`app.core.native_handler.NativeHandler` cannot tell the difference.
 Replica protocol (``multiprocessing`` pipe, both directions pickled):
   router -> replica: ("add", rid, prompt_ids, params) | ("abort", rid) | ("stop",)
   replica -> router: ("ready", info) | ("out", [RequestOutput...], metrics) | ("dead", err)
+
+Failure handling (SURVEY.md §5 "TP worker death -> health 503 + engine
+restart"): a replica whose engine cannot step again -- a TP worker process died,
+the step loop stalled, a fatal device error -- reports ``dead`` and exits (its
+TP workers follow their parent).  The router fails that replica's requests, is
+unhealthy (``/health`` 503) while it respawns the replica in a fresh process
+(``max_restarts`` times), and routes new conversations to live replicas.
 """
 from __future__ import annotations
 
@@ -36,9 +43,39 @@ from ..models.config import resolve_model
 log = logging.getLogger("fasttalk.dp")
 
 
+def _replica_watchdog(eng, send, beat, stall_s: float):
+    """Replica-side liveness: exits the process (after reporting ``dead``) when a
+    TP worker died, the step loop has been stuck for ``stall_s`` while busy, or
+    the router process is gone.  A step stuck inside a collective cannot notice
+    any of these itself."""
+    ppid = os.getppid()
+
+    def watch():
+        while True:
+            time.sleep(0.5)
+            why = None
+            group = getattr(eng, "tp_group", None)
+            if group is not None and hasattr(group, "alive") and not group.alive():
+                why = "a tensor-parallel worker process died"
+            elif beat[1] and time.time() - beat[0] > stall_s:
+                why = f"engine step stalled for more than {stall_s:.0f}s"
+            elif os.getppid() != ppid:
+                os._exit(3)
+            if why:
+                log.error("replica: %s; exiting for a restart", why)
+                try:
+                    send(("dead", why))
+                finally:
+                    os._exit(3)
+
+    threading.Thread(target=watch, name="fasttalk-replica-watch", daemon=True).start()
+
+
 def _replica_main(index: int, cfg, conn, device_base: int = 0):
     """Replica process: one engine (TP group when cfg.tp_size > 1) + step loop."""
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    from ..engine.engine import AsyncEngine
+
     try:
         base = device_base + index * max(1, cfg.tp_size)
         if cfg.resolved_device() == "cuda":
@@ -58,11 +95,21 @@ def _replica_main(index: int, cfg, conn, device_base: int = 0):
     except BaseException as e:  # pragma: no cover - reported to the router
         conn.send(("dead", repr(e)))
         return
-    conn.send(("ready", {"num_blocks": eng.bm.num_blocks, "max_model_len": eng.max_model_len}))
+    lock = threading.Lock()
+
+    def send(msg):
+        with lock:
+            conn.send(msg)
+
+    send(("ready", {"num_blocks": eng.bm.num_blocks, "max_model_len": eng.max_model_len}))
+    beat = [time.time(), False]  # last loop iteration, busy
+    _replica_watchdog(eng, send, beat, float(os.environ.get("ENGINE_STALL_S", "120")))
     outs: List[RequestOutput] = []
     last_metrics = 0.0
+    streak = 0
     try:
         while True:
+            beat[0], beat[1] = time.time(), eng.has_work()
             timeout = 0.0 if eng.has_work() else 0.05
             while conn.poll(timeout):
                 cmd = conn.recv()
@@ -79,14 +126,26 @@ def _replica_main(index: int, cfg, conn, device_base: int = 0):
                 elif cmd[0] == "stop":
                     return
             if eng.has_work():
-                eng.step()
+                try:
+                    eng.step()
+                    streak = 0
+                except Exception as e:  # same contract as AsyncEngine._run
+                    log.exception("replica step failed")
+                    eng.fail_unfinished(str(e))  # error outputs land in `outs`
+                    streak += 1
+                    if not AsyncEngine._recoverable(e) or streak >= int(
+                            os.environ.get("ENGINE_MAX_FAIL_STREAK", "3")):
+                        if outs:
+                            send(("out", list(outs), None))
+                        send(("dead", repr(e)))
+                        return
             now = time.time()
             metrics = None
             if now - last_metrics > 0.5:
                 metrics = eng.metrics()
                 last_metrics = now
             if outs or metrics is not None:
-                conn.send(("out", list(outs), metrics))
+                send(("out", list(outs), metrics))
                 outs.clear()  # the sequences' on_output callbacks append to this list
     finally:
         eng.shutdown()
@@ -96,8 +155,11 @@ class _Replica:
     def __init__(self, index: int, cfg, ctx, device_base: int = 0):
         self.index = index
         self.conn, child = ctx.Pipe()
+        # not a daemon: a TP replica spawns its worker processes.  The replica exits
+        # by itself when the router process is gone (_replica_watchdog) and the
+        # router stops it at interpreter exit (MultiGPUEngine.start registers that)
         self.proc = ctx.Process(target=_replica_main, args=(index, cfg, child, device_base),
-                                daemon=True, name=f"fasttalk-dp{index}")
+                                daemon=False, name=f"fasttalk-dp{index}")
         self.proc.start()
         child.close()
         self.lock = threading.Lock()
@@ -165,28 +227,74 @@ class MultiGPUEngine:
         self._ids = itertools.count()
         self._readers: List[threading.Thread] = []
         self._stop = False
+        self.restarts = 0
 
     # ------------------------------------------------------------------ lifecycle
+    @staticmethod
+    def _await_ready(r: _Replica, timeout: float):
+        t0 = time.time()
+        while not r.conn.poll(1.0):
+            if not r.proc.is_alive() or time.time() - t0 > timeout:
+                raise EngineError(f"DP replica {r.index} failed to start")
+        kind, payload = r.conn.recv()
+        if kind != "ready":
+            raise EngineError(f"DP replica {r.index} failed: {payload}")
+        r.info = payload
+
+    def _start_reader(self, r: _Replica):
+        th = threading.Thread(target=self._reader, args=(r,), daemon=True,
+                              name=f"fasttalk-dp-reader{r.index}")
+        th.start()
+        self._readers.append(th)
+
     def start(self, timeout: float = 1800.0):
+        import atexit
+
+        atexit.register(self.shutdown)
         self.replicas = [_Replica(i, self.cfg, self.ctx, self.device_base) for i in range(self.dp)]
         t0 = time.time()
         for r in self.replicas:
-            while not r.conn.poll(1.0):
-                if not r.proc.is_alive() or time.time() - t0 > timeout:
-                    raise EngineError(f"DP replica {r.index} failed to start")
-            kind, payload = r.conn.recv()
-            if kind != "ready":
-                raise EngineError(f"DP replica {r.index} failed: {payload}")
-            r.info = payload
+            self._await_ready(r, timeout)
         for r in self.replicas:
-            th = threading.Thread(target=self._reader, args=(r,), daemon=True,
-                                  name=f"fasttalk-dp-reader{r.index}")
-            th.start()
-            self._readers.append(th)
+            self._start_reader(r)
         log.info("DP engine: %d replicas ready in %.1fs", self.dp, time.time() - t0)
         return self
 
+    def _replica_down(self, r: _Replica):
+        """Fails the replica's requests and respawns it in a fresh process (the old
+        one, and with it its TP workers, exits); unhealthy until the new one is ready."""
+        self._fail_replica(r)
+        if self._stop or self.restarts >= max(0, int(getattr(self.cfg, "max_restarts", 0))):
+            return
+        self.restarts += 1
+        threading.Thread(target=self._restart, args=(r,), daemon=True,
+                         name=f"fasttalk-dp-restart{r.index}").start()
+
+    def _restart(self, old: _Replica, timeout: float = 1800.0):
+        old.proc.join(timeout=10)
+        if old.proc.is_alive():
+            old.proc.kill()
+            old.proc.join(timeout=10)
+        time.sleep(float(os.environ.get("ENGINE_RESTART_DELAY", "2")))  # workers' exit frees the GPU
+        if self._stop:
+            return
+        log.warning("restarting DP replica %d (restart %d/%d) after: %s", old.index, self.restarts,
+                    self.cfg.max_restarts, old.error)
+        new = _Replica(old.index, self.cfg, self.ctx, self.device_base)
+        try:
+            self._await_ready(new, timeout)
+        except Exception as e:
+            new.error = str(e)
+            self.replicas[old.index] = new
+            log.error("DP replica %d did not come back: %s", old.index, e)
+            return
+        self.replicas[old.index] = new
+        self._start_reader(new)
+        log.warning("DP replica %d is back", old.index)
+
     def shutdown(self):
+        if self._stop:
+            return
         self._stop = True
         for r in self.replicas:
             try:
@@ -208,8 +316,8 @@ class MultiGPUEngine:
             try:
                 msg = r.conn.recv()
             except (EOFError, OSError):
-                r.error = "replica exited"
-                self._fail_replica(r)
+                r.error = r.error or "replica exited"
+                self._replica_down(r)
                 return
             if msg[0] == "out":
                 _, outs, metrics = msg
@@ -227,7 +335,7 @@ class MultiGPUEngine:
                         pass
             elif msg[0] == "dead":
                 r.error = msg[1]
-                self._fail_replica(r)
+                self._replica_down(r)
                 return
 
     def _fail_replica(self, r: _Replica):

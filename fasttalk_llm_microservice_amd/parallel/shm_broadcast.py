@@ -69,6 +69,10 @@ class _Seg:
             pass
 
 
+class PeerDied(RuntimeError):
+    """The other side of the broadcast ring is gone (TP worker or rank 0 died)."""
+
+
 class ShmBroadcast:
     def __init__(self, num_readers: int, name: Optional[str] = None, create: bool = True,
                  reader_index: int = -1, num_slots: int = 8, slot_bytes: int = 4 << 20):
@@ -89,6 +93,7 @@ class ShmBroadcast:
             self.name = name
             self.shm = _Seg(name)
         self.owner = create
+        self.liveness = None  # optional () -> bool, polled while blocked (~1/s)
         self._hdr = np.ndarray((1 + num_readers,), dtype=np.int64, buffer=self.shm.buf, offset=0)
         self._seq = int(self._hdr[0])
         # messages are numbered from 1; a reader's ack is the last one it consumed
@@ -101,14 +106,17 @@ class ShmBroadcast:
     def _slot_hdr(self, i: int) -> np.ndarray:
         return np.ndarray((2,), dtype=np.int64, buffer=self.shm.buf, offset=self._slot_off(i))
 
-    @staticmethod
-    def _spin(cond, timeout: Optional[float]):
+    def _spin(self, cond, timeout: Optional[float]):
         t0 = time.perf_counter()
         n = 0
         while not cond():
             n += 1
             if n > 200:
                 time.sleep(5e-5 if n < 20000 else 1e-3)
+                # a dead peer never acks / never sends: ask the owner's liveness
+                # probe about once a second instead of spinning forever
+                if n >= 20000 and n % 1000 == 0 and self.liveness is not None and not self.liveness():
+                    raise PeerDied("shm broadcast peer process died")
             if timeout is not None and time.perf_counter() - t0 > timeout:
                 raise TimeoutError("shm broadcast timed out")
 

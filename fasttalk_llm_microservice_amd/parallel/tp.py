@@ -25,6 +25,8 @@ import logging
 import multiprocessing as mp
 import os
 import socket
+import threading
+import time
 from typing import List, Optional
 
 import torch
@@ -42,13 +44,34 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def _backend(device: str) -> str:
-    return "nccl" if device == "cuda" else "gloo"
+def _backend(device: str, cfg=None) -> str:
+    """RCCL on GPUs.  ``tp_share_device`` (tests: every rank on ONE GPU, which RCCL
+    refuses) runs control over gloo and the data path over the custom xGMI/IPC
+    collectives, with gloo host staging as the fallback."""
+    if device == "cuda" and not (cfg is not None and cfg.tp_share_device):
+        return "nccl"
+    return "gloo"
 
 
 def _set_device(device: str, index: int):
     if device == "cuda":
         torch.cuda.set_device(index)
+
+
+def _exit_with_parent(what: str):
+    """Workers die with the rank-0 process that spawned them even when they are
+    stuck inside a collective that will never complete (the step loop cannot
+    notice then): a daemon thread polls the parent pid once a second."""
+    ppid = os.getppid()
+
+    def watch():
+        while True:
+            time.sleep(1.0)
+            if os.getppid() != ppid:
+                log.error("%s: rank 0 (pid %d) is gone; exiting", what, ppid)
+                os._exit(3)
+
+    threading.Thread(target=watch, name="fasttalk-tp-parent-watch", daemon=True).start()
 
 
 def _maybe_custom_ar(cfg, comm: TPComm, device: str):
@@ -84,12 +107,14 @@ def worker_loop(cfg, comm: TPComm, bcast: ShmBroadcast):
 def _spawned_worker(rank: int, world: int, port: int, bcast_name: str, cfg, device: str,
                     device_base: int):
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    _set_device(device, device_base + rank)
+    _exit_with_parent(f"TP worker {rank}")
+    dev_index = device_base + (0 if cfg.tp_share_device else rank)
+    _set_device(device, dev_index)
     kw = {}
-    if device == "cuda":
-        kw["device_id"] = torch.device(f"cuda:{device_base + rank}")
-    dist.init_process_group(_backend(device), init_method=f"tcp://127.0.0.1:{port}", rank=rank,
-                            world_size=world, **kw)
+    if device == "cuda" and not cfg.tp_share_device:
+        kw["device_id"] = torch.device(f"cuda:{dev_index}")
+    dist.init_process_group(_backend(device, cfg), init_method=f"tcp://127.0.0.1:{port}",
+                            rank=rank, world_size=world, **kw)
     comm = TPComm(dist.group.WORLD, rank, world)
     _maybe_custom_ar(cfg, comm, device)
     bcast = ShmBroadcast(world - 1, name=bcast_name, create=False, reader_index=rank - 1)
@@ -110,6 +135,7 @@ class TPGroup:
         self.device_base = device_base
         self.port = _free_port()
         self.bcast = ShmBroadcast(self.world - 1)
+        self.bcast.liveness = self.alive
         ctx = mp.get_context("spawn")
         self.procs: List[mp.Process] = []
         for r in range(1, self.world):
@@ -120,9 +146,10 @@ class TPGroup:
             self.procs.append(p)
         _set_device(self.device, device_base)
         kw = {}
-        if self.device == "cuda":
+        if self.device == "cuda" and not cfg.tp_share_device:
             kw["device_id"] = torch.device(f"cuda:{device_base}")
-        dist.init_process_group(_backend(self.device), init_method=f"tcp://127.0.0.1:{self.port}",
+        dist.init_process_group(_backend(self.device, cfg),
+                                init_method=f"tcp://127.0.0.1:{self.port}",
                                 rank=0, world_size=self.world, **kw)
         self.comm = TPComm(dist.group.WORLD, 0, self.world)
         _maybe_custom_ar(cfg, self.comm, self.device)
@@ -147,6 +174,7 @@ class TPGroup:
             dist.destroy_process_group()
 
     def alive(self) -> bool:
+        """Every worker process still running (wired into the engine's health)."""
         return all(p.is_alive() for p in self.procs)
 
 

@@ -1,8 +1,12 @@
-"""Custom one-shot all-reduce (csrc/kernels/custom_ar.hip) with two ranks that
-share ONE MI355X: two processes, IPC-mapped uncached regions of the same device,
-the same signalling protocol the TP group runs over xGMI.  Checks sums against a
-fp32 host reference, eager and captured in a hipGraph (fixed kernel arguments,
-epochs advance on the device), and that no wait ran out of spin budget."""
+"""Custom xGMI collectives (csrc/kernels/custom_ar.hip) with two ranks that share
+ONE MI355X: two processes, IPC-mapped uncached regions of the same device, the
+same signalling protocol the TP group runs over xGMI.  Checks one-shot and
+two-shot sums and the interleaved all-gather against fp32 host references,
+eager and captured in a hipGraph (fixed kernel arguments, epochs advance on the
+device), that no wait ran out of spin budget -- and the timeout contract: a
+rank whose peer never arrives gets its error word set after the spin budget,
+leaves its input unreduced, skips later calls at once, and the exported flag
+shows it (the time per spin is printed: it sizes ENGINE_CUSTOM_AR_SPIN)."""
 import multiprocessing as mp
 import os
 import socket
@@ -62,7 +66,47 @@ def _worker(rank, world, port, q):
         g.replay()
         torch.cuda.synchronize()
         errs.append((buf.float().cpu() - sum(x.float() for x in xs)).abs().max().item())
-    q.put((rank, errs, ar.healthy()))
+    # two-shot (reduce-scatter + all-gather), forced at every size
+    ar.two_shot_bytes = 0
+    for trial, n in enumerate([64 * 4096, 8 * 4096, 8 * 3, 50 * 4096], start=20):
+        xs = _inputs(trial, world, n)
+        x = xs[rank].cuda()
+        ar.all_reduce(x)
+        torch.cuda.synchronize()
+        errs.append((x.float().cpu() - sum(v.float() for v in xs)).abs().max().item())
+    ar.two_shot_bytes = 1 << 62
+    # all-gather of vocab-sharded logits: [rows, shard] -> [rows, W * shard]
+    for trial, (rows, shard) in enumerate([(50, 4008), (1, 64), (64, 4096)], start=30):
+        shards = [torch.randn(rows, shard, generator=torch.Generator().manual_seed(100 * trial + r))
+                  .bfloat16() for r in range(world)]
+        got = ar.all_gather_last(shards[rank].cuda())
+        torch.cuda.synchronize()
+        errs.append((got.float().cpu() - torch.cat(shards, dim=-1).float()).abs().max().item())
+    healthy = ar.healthy()
+    ar.export_error()
+    flag_ok = int(ar.err_flag.item()) == 0
+    dist.barrier()
+    # timeout contract: rank 1 skips a call, rank 0 waits out a small spin budget
+    spin_us = None
+    left_unreduced = skipped_fast = flagged = None
+    if rank == 0:
+        import time
+
+        budget = 1 << 16
+        x = torch.full((4096,), 1.0, device="cuda").bfloat16()
+        t0 = time.perf_counter()
+        ar._C.custom_ar_allreduce(x, x, ar.peers, ar.rank, ar.world, ar.max_bytes, budget, False)
+        torch.cuda.synchronize()
+        spin_us = (time.perf_counter() - t0) * 1e6 / budget
+        left_unreduced = bool((x.float() == 1.0).all().item())
+        t0 = time.perf_counter()
+        ar.all_reduce(x)  # sticky error: returns at once, no second wait
+        torch.cuda.synchronize()
+        skipped_fast = time.perf_counter() - t0 < 0.05
+        ar.export_error()
+        flagged = int(ar.err_flag.item()) == 1 and not ar.healthy()
+        print(f"custom AR timeout: {spin_us:.3f} us per spin (budget {budget})", flush=True)
+    q.put((rank, errs, healthy and flag_ok, spin_us, left_unreduced, skipped_fast, flagged))
     dist.barrier()
     ar.close()
     dist.destroy_process_group()
@@ -82,6 +126,11 @@ def test_custom_allreduce_two_ranks_one_gpu():
             p.join(timeout=60)
             if p.is_alive():
                 p.kill()
-    for rank, errs, healthy in results:
+    for rank, errs, healthy, spin_us, unreduced, fast, flagged in results:
         assert healthy, f"rank {rank}: a wait ran out of spin budget"
         assert max(errs) < 0.06, f"rank {rank}: max abs err {max(errs)} ({errs})"
+        if rank == 0:
+            print(f"spin cost {spin_us:.3f} us")
+            assert unreduced, "a timed-out all-reduce must leave its input as it was"
+            assert fast, "a rank with its error word set must skip later calls at once"
+            assert flagged, "the exported error flag must show the timeout"

@@ -105,3 +105,78 @@ def test_dp2_router_session_affinity_and_outputs():
         assert eng.engine.metrics()["replicas"] == 2
     finally:
         eng.shutdown()
+
+
+def test_tp_worker_death_turns_health_red():
+    """SURVEY §5 "TP worker death -> health 503": AsyncEngine.is_healthy consults
+    TPGroup.alive(), so /health flips as soon as a worker process is gone (rank 0
+    may be blocked in a collective that never completes)."""
+    from fasttalk_llm_microservice_amd.engine.engine import AsyncEngine
+    from fasttalk_llm_microservice_amd.parallel.shm_broadcast import PeerDied
+    from fasttalk_llm_microservice_amd.parallel.tp import spawn_tp_engine
+
+    eng = spawn_tp_engine(_cfg(tp_size=2))
+    ae = AsyncEngine(eng).start()
+    try:
+        assert ae.is_healthy()
+        worker = eng.tp_group.procs[0]
+        worker.kill()
+        worker.join(timeout=30)
+        assert not ae.is_healthy()
+        # a dead peer is fatal for the group (not a per-request failure)
+        assert not AsyncEngine._recoverable(PeerDied("x"))
+    finally:
+        ae._stop = True
+        ae._wake.set()
+        eng.tp_group.bcast.liveness = lambda: False  # shutdown must not wait for the dead worker
+        eng.shutdown()
+
+
+def test_separate_process_tp_engine_restarts_after_worker_death(monkeypatch):
+    """A TP group in its own process (the default for tp_size > 1): when a worker
+    dies the replica reports itself dead and exits, the router is unhealthy, fails
+    the replica's requests, respawns the group in a fresh process and serves the
+    same tokens again."""
+    import asyncio
+
+    import psutil
+
+    from fasttalk_llm_microservice_amd.parallel.dp_router import MultiGPUEngine
+
+    monkeypatch.setenv("ENGINE_RESTART_DELAY", "0.2")
+    rng = np.random.default_rng(5)
+    prompts = [rng.integers(0, 120000, n).tolist() for n in (12, 31)]
+    sp = SamplingParams(temperature=0, max_tokens=5, ignore_eos=True)
+    ref = LLMEngine(_cfg()).generate(prompts, sp)
+    cfg = _cfg(tp_size=2)
+    assert cfg.separate_process is False  # dataclass default; from_env defaults TP to True
+    from fasttalk_llm_microservice_amd.engine.config import EngineConfig
+
+    monkeypatch.setenv("ENGINE_TP_SIZE", "2")
+    assert EngineConfig.from_env(model="tiny").separate_process is True
+    eng = MultiGPUEngine(cfg).start()
+
+    async def one(p, rid):
+        ids = []
+        async for o in eng.generate(p, sp, request_id=rid):
+            ids.extend(o.token_ids)
+        return ids
+
+    try:
+        assert asyncio.run(one(prompts[0], "a#0")) == ref[0]
+        rep = eng.replicas[0]
+        kids = [c for c in psutil.Process(rep.proc.pid).children()
+                if "resource_tracker" not in " ".join(c.cmdline())]
+        assert kids, "the replica must own its TP worker process"
+        for c in kids:
+            c.kill()
+        t0 = time.time()
+        while eng.is_healthy() and time.time() - t0 < 30:
+            time.sleep(0.1)
+        assert not eng.is_healthy(), "a dead TP worker must make the engine unhealthy"
+        while not eng.is_healthy() and time.time() - t0 < 240:
+            time.sleep(0.2)
+        assert eng.is_healthy() and eng.restarts == 1 and eng.replicas[0] is not rep
+        assert asyncio.run(one(prompts[1], "b#0")) == ref[1]
+    finally:
+        eng.shutdown()
