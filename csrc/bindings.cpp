@@ -59,6 +59,8 @@ int ft_ar_allgather(void* out, const void* x, long rows, long row_elems, const u
 int ft_ar_export_error(int* dst, const uint64_t* peers_dev, int world, hipStream_t stream);
 int ft_skinny_gemm_pk(const void* x, int x_stride, int M, const void* wpk, int N, int K, float* ws,
                       void* out, int out_stride, int splits, int nt, hipStream_t stream);
+int ft_packed_gemm(const void* x, int x_stride, int M, const void* wpk, int N, int K, int splits,
+                   int epi, int cfg, void* out, int out_stride, float* ws, hipStream_t stream);
 int ft_pkr_gemm(const void* x, int x_stride, int M, const void* wpk, int N, int K, float* ws,
                 void* out, int out_stride, void* residual, int res_stride, int* tickets,
                 int splits, int nt, int depth, int epi, int norm, int wn, float eps,
@@ -365,7 +367,7 @@ void skinny_gemm(at::Tensor x, at::Tensor w, c10::optional<at::Tensor> out,
   TORCH_CHECK(w.dim() == 2 && w.is_contiguous(), "w must be the packed [N, K] image");
   const int M = (int)x.size(0), K = (int)x.size(1), N = (int)w.size(0);
   TORCH_CHECK(w.size(1) == K, "K mismatch");
-  TORCH_CHECK(M <= 64, "skinny_gemm supports M <= 64");
+  TORCH_CHECK(M <= (u == -4 ? 128 : 64), "skinny_gemm supports M <= 64 (pk) / 128 (xc)");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0, "w alignment");
   TORCH_CHECK(u == -3 || u == -4, "skinny_gemm variant: -3 (pk) or -4 (xc), packed weights");
   float* wsp = nullptr;
@@ -391,6 +393,42 @@ void skinny_gemm(at::Tensor x, at::Tensor w, c10::optional<at::Tensor> out,
     check_rc(ft_skinny_gemm_xc(x.data_ptr(), (int)x.stride(0), M, w.data_ptr(), N, K, wsp, op,
                                ostride, (int)splits, (int)nt, cur_stream()),
              "skinny_gemm_xc");
+}
+
+// Packed-image GEMM for M > 64 rows (csrc/kernels/packed_gemm.hip).
+// epi: 0 bf16 out [M, N], 1 fp32 slabs ws [splits, M, N], 2 SiLU-mul out [M, N/2]
+// (interleaved gate/up image).
+void packed_gemm(at::Tensor x, at::Tensor w, c10::optional<at::Tensor> out,
+                 c10::optional<at::Tensor> ws, int64_t splits, int64_t epi, int64_t cfg) {
+  check_bf16(x, "x");
+  check_bf16(w, "w");
+  check_rows(x, "x");
+  TORCH_CHECK(w.dim() == 2 && w.is_contiguous(), "w must be the packed [N, K] image");
+  const int M = (int)x.size(0), K = (int)x.size(1), N = (int)w.size(0);
+  TORCH_CHECK(w.size(1) == K, "K mismatch");
+  TORCH_CHECK(N % 16 == 0 && K % 64 == 0, "packed_gemm: N % 16, K % 64");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && x.stride(0) % 8 == 0,
+              "x rows must be 16-B aligned");
+  TORCH_CHECK(epi >= 0 && epi <= 2 && (epi == 1) == (splits > 1), "packed_gemm: epi/splits");
+  float* wsp = nullptr;
+  void* op = nullptr;
+  int ostride = 0;
+  if (epi == 1) {
+    TORCH_CHECK(ws.has_value(), "splits > 1 needs a workspace");
+    check_ws(*ws, (int64_t)splits * M * N);
+    wsp = ws->data_ptr<float>();
+  } else {
+    TORCH_CHECK(out.has_value(), "needs out");
+    check_bf16(*out, "out");
+    const int64_t cols = epi == 2 ? N / 2 : N;
+    TORCH_CHECK(out->dim() == 2 && out->stride(1) == 1 && out->size(0) >= M && out->size(1) >= cols,
+                "out shape");
+    op = out->data_ptr();
+    ostride = (int)out->stride(0);
+  }
+  check_rc(ft_packed_gemm(x.data_ptr(), (int)x.stride(0), M, w.data_ptr(), N, K, (int)splits,
+                          (int)epi, (int)cfg, op, ostride, wsp, cur_stream()),
+           "packed_gemm");
 }
 
 // Ring-pipelined packed decode GEMM with fused epilogues (csrc/kernels/skinny_pkr.hip).
@@ -642,6 +680,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("custom_ar_close", &custom_ar_close);
   m.def("custom_ar_error", &custom_ar_error);
   m.def("custom_ar_allreduce", &custom_ar_allreduce);
+  m.def("packed_gemm", &packed_gemm);
   m.def("custom_ar_allgather", &custom_ar_allgather);
   m.def("custom_ar_export_error", &custom_ar_export_error);
   m.def("slab_silu", &slab_silu);

@@ -30,6 +30,7 @@
 //   DMA).  The block-table entries of the KV range are copied to LDS once, so
 //   issuing a tile never waits on a table read.
 #include "ft_common.h"
+#include "ft_lds.h"
 
 namespace ft {
 
@@ -52,58 +53,6 @@ __device__ __forceinline__ float kgroup_max(float v) {
 __device__ __forceinline__ float kgroup_sum(float v) {
   v += __shfl_xor(v, 16, 64);
   return v + __shfl_xor(v, 32, 64);
-}
-
-// LDS reads in inline asm: with LDS-DMA (global_load_lds) in flight hipcc cannot
-// tell a ds_read from the DMA's destination and waits vmcnt(0) before every LDS
-// read, draining the prefetch.  These reads are invisible to its waitcnt pass, so
-// the kernel orders them itself: lgkm_wait<N>() (N reads may stay outstanding)
-// followed by dep() on each value it is about to consume.
-__device__ __forceinline__ uint32_t lds_off(const void* p) {
-  return (uint32_t)reinterpret_cast<uintptr_t>(p);
-}
-typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
-typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ uint4 ds_read16(uint32_t a) {
-  u32x4_t v;
-  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(a));
-  return __builtin_bit_cast(uint4, v);
-}
-__device__ __forceinline__ uint2 ds_read8(uint32_t a) {
-  u32x2_t v;
-  asm volatile("ds_read_b64 %0, %1" : "=v"(v) : "v"(a));
-  return __builtin_bit_cast(uint2, v);
-}
-// global_load_lds_dwordx4 in inline asm (guide idiom): M0 = the wave-uniform LDS
-// destination, lanes land at M0 + 16 * lane.  hipcc's waitcnt pass does not see it
-// (it would otherwise treat the address VGPRs as pending and wait vmcnt(0) at their
-// reuse); the kernel waits for it with explicit counted vmcnt.
-__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_dst) {
-  uint32_t keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %2\n\t"
-      "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, off\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(lds_dst))
-      : "memory");
-}
-
-template <int N>
-__device__ __forceinline__ void lgkm_wait() {
-  asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory");
-}
-__device__ __forceinline__ void dep(uint4& v) {
-  u32x4_t t = __builtin_bit_cast(u32x4_t, v);
-  asm volatile("" : "+v"(t));
-  v = __builtin_bit_cast(uint4, t);
-}
-__device__ __forceinline__ void dep(uint2& v) {
-  u32x2_t t = __builtin_bit_cast(u32x2_t, v);
-  asm volatile("" : "+v"(t));
-  v = __builtin_bit_cast(uint2, t);
 }
 
 template <int D, int G>

@@ -1,5 +1,6 @@
 // K3/K7/K8/K10/K11 at decode shapes: y[M, N] = x[M, K] . W[N, K]^T with M <= 64
-// (one token per running sequence), bf16 in, fp32 accumulate.
+// (one token per running sequence; "xc" also 65..128 rows: small mixed
+// decode + prefill steps, still a weight stream), bf16 in, fp32 accumulate.
 //
 // At M <= 64 every projection is a weight stream (Llama-3-8B: 16 GB of weights
 // per step vs < 1 MB of activations), so the kernels are built around the HBM
@@ -71,7 +72,8 @@ template <int MT, int NT>
 __global__ __launch_bounds__(256) void skinny_xc_kernel(
     const uint16_t* __restrict__ x, int x_stride, int M, const uint16_t* __restrict__ w, int K,
     float* __restrict__ ws, uint16_t* __restrict__ out, int out_stride, int N, int k_slice) {
-  constexpr int KC = 512;                          // k per chunk (8 MFMA k-steps of 64)
+  constexpr int KC = MT <= 4 ? 512 : 256;          // k per chunk (8 / 4 MFMA k-steps of 64)
+  constexpr int KS = KC / 64;
   constexpr int ROWS = 16 * MT;
   constexpr int CPR = KC / 8;                      // 16-B chunks per x row per chunk (64)
   constexpr int XL = ROWS * CPR / 256;             // x loads per thread per chunk
@@ -108,9 +110,9 @@ __global__ __launch_bounds__(256) void skinny_xc_kernel(
       xr[p] = *reinterpret_cast<const uint4*>(x + (size_t)min(row, M - 1) * x_stride + kbeg + kc +
                                               ch * 8);
     }
-    uint4 wr[8][NT][2];
+    uint4 wr[KS][NT][2];
 #pragma unroll
-    for (int st = 0; st < 8; ++st)
+    for (int st = 0; st < KS; ++st)
 #pragma unroll
       for (int j = 0; j < NT; ++j) {
         const uint16_t* p = wp[j] + (size_t)((kc >> 6) + st) * 1024;
@@ -128,7 +130,7 @@ __global__ __launch_bounds__(256) void skinny_xc_kernel(
     __syncthreads();
     if (active) {
 #pragma unroll
-      for (int st = 0; st < 8; ++st) {
+      for (int st = 0; st < KS; ++st) {
 #pragma unroll
         for (int i = 0; i < MT; ++i) {
           const int row = 16 * i + l15;
@@ -277,15 +279,16 @@ __global__ __launch_bounds__(256) void skinny_pk_kernel(
 
 
 
-// x-chunk variant.  Requirements (checked): M <= 64, N % (16*nt) == 0,
-// K % (512*splits) == 0.
+// x-chunk variant.  Requirements (checked): M <= 128, N % (16*nt) == 0,
+// K % (512*splits) == 0 (M <= 64) or K % (256*splits) == 0 (65..128 rows: the x
+// chunk halves so 128 rows still fit 64 KiB of LDS).
 extern "C" int ft_skinny_gemm_xc(const void* x, int x_stride, int M, const void* w, int N, int K,
                                  float* ws, void* out, int out_stride, int splits, int nt,
                                  hipStream_t stream) {
   if (M <= 0) return 0;
-  if (M > 64 || splits < 1) return -1;
+  if (M > 128 || splits < 1) return -1;
   if (N % (16 * nt) != 0) return -2;
-  if (K % (512 * splits) != 0) return -3;
+  if (K % ((M > 64 ? 256 : 512) * splits) != 0) return -3;
   if (splits > 1 && ws == nullptr) return -4;
   const int mt = (M + 15) / 16;
   const int cols = 4 * 16 * nt;
@@ -298,7 +301,8 @@ extern "C" int ft_skinny_gemm_xc(const void* x, int x_stride, int M, const void*
                        (uint16_t*)out, out_stride, N, k_slice);                              \
     return static_cast<int>(hipGetLastError());                                              \
   }
-#define FT_XC_NT(NT_) FT_XC(1, NT_) FT_XC(2, NT_) FT_XC(3, NT_) FT_XC(4, NT_)
+#define FT_XC_NT(NT_) FT_XC(1, NT_) FT_XC(2, NT_) FT_XC(3, NT_) FT_XC(4, NT_) \
+  FT_XC(5, NT_) FT_XC(6, NT_) FT_XC(7, NT_) FT_XC(8, NT_)
   FT_XC_NT(1)
   FT_XC_NT(2)
 #undef FT_XC_NT

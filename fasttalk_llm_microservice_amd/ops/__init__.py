@@ -248,6 +248,18 @@ def skinny_gemm(x, w, out=None, ws=None, splits: int = 1, nt: int = 1, u: int = 
     return out if splits == 1 else ws
 
 
+def packed_gemm(x, w, out=None, ws=None, splits: int = 1, epi: str = "store", cfg: int = 0):
+    """y = x w^T for any M on a pack_weight() image (csrc/kernels/packed_gemm.hip).
+    epi "store": bf16 [M, N]; "slab": fp32 slabs [splits, M, N] in ``ws``; "silu":
+    silu(gate) * up of an interleave_gate_up(w, 1) image -> [M, N / 2]."""
+    code = {"store": 0, "slab": 1, "silu": 2}[epi]
+    if code != 1 and out is None:
+        cols = w.shape[0] // 2 if code == 2 else w.shape[0]
+        out = torch.empty(x.shape[0], cols, dtype=x.dtype, device=x.device)
+    native().packed_gemm(x, w, out, ws, splits, code, cfg)
+    return ws if code == 1 else out
+
+
 def embed_rmsnorm(ids: torch.Tensor, table: torch.Tensor, w: torch.Tensor, eps: float):
     """(rmsnorm(table[ids]) * w, table[ids]): the embedding gather fused with the
     first layer's input norm; the second tensor starts the residual stream."""
