@@ -42,6 +42,8 @@ def main():
     ap.add_argument("--rows", default="80,128,256,512,1024,4096")
     ap.add_argument("--only", default="")
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--cfgs", default="0,1,2,3,4")
+    ap.add_argument("--splits", default="1,2,4,8,16")
     a = ap.parse_args()
     torch.manual_seed(0)
     for name, (n, k) in SHAPES.items():
@@ -65,16 +67,17 @@ def main():
                             continue
                         cands.append((f"xc{nt}/{sp}", lambda nt=nt, sp=sp: ops.native().skinny_gemm(
                             x, wp, out, ws, sp, nt, -4), sp))
-            for cfg in (0, 1, 2, 3):
-                bm, bn = [(256, 256), (128, 256), (256, 128), (256, 256)][cfg]
+            for cfg in [int(c) for c in a.cfgs.split(",")]:
+                bm, bn = [(256, 256), (128, 256), (256, 128), (256, 256), (256, 256)][cfg]
                 tiles = -(-m // bm) * -(-n // bn)
-                for sp in (1, 2, 4, 8, 16):
+                for sp in [int(v) for v in a.splits.split(",")]:
                     if k % (64 * sp) or (sp > 1 and tiles * sp > 2048) or (sp > 1 and tiles >= 512):
                         continue
                     cands.append((f"pg{cfg}/{sp}", lambda cfg=cfg, sp=sp: ops.native().packed_gemm(
                         x, wp, out, ws if sp > 1 else None, sp, 1 if sp > 1 else 0, cfg), sp))
             best = None
             xbest = None
+            times = {}
             for label, fn, sp in cands:
                 if sp > 1 and sp * m * n > ws.numel():
                     continue
@@ -88,10 +91,12 @@ def main():
                 if err > 0.1:
                     res.append(f"!!{label} err {err:.3f}")
                 us = timeit(f, a.iters)
+                times[label] = us
                 if best is None or us < best[1]:
                     best = (label, us)
                 if label.startswith("xc") and (xbest is None or us < xbest[1]):
                     xbest = (label, us)
+            res.append(" ".join(f"{l}={t:.1f}" for l, t in sorted(times.items())))
             res.append(f"best {best[0]:9s} {best[1]:7.1f} us  {fl / best[1] / 1e6:6.0f} TF  "
                        f"vs blas {blas / best[1]:.2f}x")
             if xbest:

@@ -13,7 +13,7 @@ int ft_rmsnorm(void* out, const void* x, const void* w, int rows, int hidden, in
                int out_stride, float eps, hipStream_t stream);
 int ft_fused_add_rmsnorm(void* out, const void* x, void* residual, const void* w, int rows,
                          int hidden, int x_stride, int out_stride, float eps, hipStream_t stream);
-int ft_silu_mul(void* out, const void* gu, int rows, int inter, hipStream_t stream);
+int ft_silu_mul(void* out, const void* gu, int rows, int inter, int il, hipStream_t stream);
 int ft_rope_kv_write(void* qkv, int qkv_stride, const int* positions, const float* cos_sin,
                      const int* slot_mapping, void* k_cache, void* v_cache, int tokens, int nq,
                      int nkv, int head_dim, int block_size, hipStream_t stream);
@@ -68,7 +68,7 @@ int ft_pkr_gemm(const void* x, int x_stride, int M, const void* wpk, int N, int 
 int ft_row_rmsnorm(const void* x, int x_stride, const float* ws, int splits, void* out,
                    int out_stride, void* residual, const void* w, int rows, int hidden, float eps,
                    hipStream_t stream);
-int ft_slab_silu(const float* ws, int splits, int rows, int inter, void* out, int out_stride,
+int ft_slab_silu(const float* ws, int splits, int rows, int inter, void* out, int out_stride, int il,
                  hipStream_t stream);
 int ft_slab_store(const float* ws, int splits, int rows, int cols, void* out, int out_stride,
                   hipStream_t stream);
@@ -147,14 +147,15 @@ void fused_add_rmsnorm(at::Tensor out, at::Tensor x, at::Tensor residual, at::Te
            "fused_add_rmsnorm");
 }
 
-void silu_mul(at::Tensor out, at::Tensor gu) {
+void silu_mul(at::Tensor out, at::Tensor gu, bool il) {
   check_bf16(out, "out");
   check_bf16(gu, "gate_up");
   TORCH_CHECK(gu.is_contiguous() && out.is_contiguous(), "contiguous tensors required");
   TORCH_CHECK(gu.dim() == 2 && out.dim() == 2 && gu.size(0) == out.size(0) &&
                   gu.size(1) == 2 * out.size(1),
               "silu_mul shapes");
-  check_rc(ft_silu_mul(out.data_ptr(), gu.data_ptr(), (int)out.size(0), (int)out.size(1),
+  TORCH_CHECK(!il || out.size(1) % 16 == 0, "interleaved silu_mul: inter % 16");
+  check_rc(ft_silu_mul(out.data_ptr(), gu.data_ptr(), (int)out.size(0), (int)out.size(1), il ? 1 : 0,
                        cur_stream()),
            "silu_mul");
 }
@@ -591,13 +592,14 @@ void row_rmsnorm(at::Tensor out, c10::optional<at::Tensor> x, c10::optional<at::
   }
 }
 
-void slab_silu(at::Tensor ws, int64_t splits, int64_t rows, int64_t inter, at::Tensor out) {
+void slab_silu(at::Tensor ws, int64_t splits, int64_t rows, int64_t inter, at::Tensor out, bool il) {
   check_ws(ws, splits * rows * 2 * inter);
   check_bf16(out, "out");
   check_rows(out, "out");
   TORCH_CHECK(out.size(0) >= rows && out.size(1) >= inter, "out shape");
+  TORCH_CHECK(!il || inter % 16 == 0, "interleaved slab_silu: inter % 16");
   check_rc(ft_slab_silu(ws.data_ptr<float>(), (int)splits, (int)rows, (int)inter, out.data_ptr(),
-                        (int)out.stride(0), cur_stream()), "slab_silu");
+                        (int)out.stride(0), il ? 1 : 0, cur_stream()), "slab_silu");
 }
 
 void slab_store(at::Tensor ws, int64_t splits, int64_t rows, int64_t cols, at::Tensor out) {

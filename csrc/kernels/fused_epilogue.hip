@@ -110,15 +110,17 @@ __global__ __launch_bounds__(256) void row_add_rmsnorm_kernel(Src src, uint16_t*
 // ---------------------------------------------------------------------------------
 // SiLU-and-mul / store over split-K slabs (grid-stride, 8 outputs per thread)
 // ---------------------------------------------------------------------------------
+// il: interleaved gate/up columns (groups of 16, see silu_mul_kernel)
 __global__ __launch_bounds__(256) void slab_silu_kernel(SrcSlab src, uint16_t* __restrict__ out,
-                                                        int out_stride, int rows, int inter) {
+                                                        int out_stride, int rows, int inter, int il) {
   const int vec = inter / 8;
   const long total = (long)rows * vec;
   for (long idx = (long)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (long)gridDim.x * 256) {
     const int r = (int)(idx / vec), c = (int)(idx - (long)r * vec) * 8;
     float g[8], u[8];
-    src.load8(r, c, g);
-    src.load8(r, inter + c, u);
+    const int gc = il ? ((c >> 4) << 5) + (c & 15) : c;
+    src.load8(r, gc, g);
+    src.load8(r, il ? gc + 16 : inter + c, u);
 #pragma unroll
     for (int j = 0; j < 8; ++j) g[j] = g[j] / (1.f + __expf(-g[j])) * u[j];
     *reinterpret_cast<uint4*>(out + (size_t)r * out_stride + c) = store8(g);
@@ -261,7 +263,7 @@ extern "C" int ft_row_rmsnorm(const void* x, int x_stride, const float* ws, int 
 }
 
 extern "C" int ft_slab_silu(const float* ws, int splits, int rows, int inter, void* out,
-                            int out_stride, hipStream_t stream) {
+                            int out_stride, int il, hipStream_t stream) {
   if (rows <= 0) return 0;
   if (inter % 8) return -1;
   ft::SrcSlab src{ws, splits, rows, 2 * inter};
@@ -269,7 +271,7 @@ extern "C" int ft_slab_silu(const float* ws, int splits, int rows, int inter, vo
   int grid = (int)((total + 255) / 256);
   if (grid > 4096) grid = 4096;
   hipLaunchKernelGGL(ft::slab_silu_kernel, dim3(grid), dim3(256), 0, stream, src, (uint16_t*)out,
-                     out_stride, rows, inter);
+                     out_stride, rows, inter, il);
   return static_cast<int>(hipGetLastError());
 }
 

@@ -155,9 +155,12 @@ __global__ __launch_bounds__(256) void embed_rmsnorm_kernel(uint16_t* __restrict
 // ----------------------------------------------------------------------------
 // SiLU-and-mul: out[t, i] = silu(gu[t, i]) * gu[t, I + i]
 // ----------------------------------------------------------------------------
+// il: gate/up rows interleaved in groups of 16 (ops.interleave_gate_up(w, 1), the
+// single gate_up image of the packed model): gate column c sits at
+// (c / 16) * 32 + c % 16, its up column 16 further.
 __global__ __launch_bounds__(256) void silu_mul_kernel(uint16_t* __restrict__ out,
                                                        const uint16_t* __restrict__ gu, int rows,
-                                                       int inter) {
+                                                       int inter, int il) {
   const int vec_per_row = inter / 8;
   const long total = (long)rows * vec_per_row;
   for (long idx = (long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
@@ -166,8 +169,9 @@ __global__ __launch_bounds__(256) void silu_mul_kernel(uint16_t* __restrict__ ou
     const int c = (int)(idx - r * vec_per_row);
     const uint4* g4 = reinterpret_cast<const uint4*>(gu + r * 2 * (long)inter);
     float g[8], u[8];
-    load8(g4[c], g);
-    load8(g4[vec_per_row + c], u);
+    const int gi = il ? ((c >> 1) << 2) + (c & 1) : c;       // uint4 index of the gate chunk
+    load8(g4[gi], g);
+    load8(g4[il ? gi + 2 : vec_per_row + c], u);
 #pragma unroll
     for (int j = 0; j < 8; ++j) g[j] = g[j] / (1.f + __expf(-g[j])) * u[j];
     reinterpret_cast<uint4*>(out + r * (long)inter)[c] = store8(g);
@@ -191,14 +195,15 @@ extern "C" int ft_fused_add_rmsnorm(void* out, const void* x, void* residual, co
                                   stream);
 }
 
-extern "C" int ft_silu_mul(void* out, const void* gu, int rows, int inter, hipStream_t stream) {
+extern "C" int ft_silu_mul(void* out, const void* gu, int rows, int inter, int il,
+                           hipStream_t stream) {
   if (rows <= 0) return 0;
   if (inter % 8 != 0) return -1;
   const long total = (long)rows * (inter / 8);
   int grid = (int)((total + 255) / 256);
   if (grid > 256 * 16) grid = 256 * 16;
   hipLaunchKernelGGL(ft::silu_mul_kernel, dim3(grid), dim3(256), 0, stream, (uint16_t*)out,
-                     (const uint16_t*)gu, rows, inter);
+                     (const uint16_t*)gu, rows, inter, il);
   return static_cast<int>(hipGetLastError());
 }
 

@@ -54,14 +54,14 @@ __device__ __forceinline__ void pg_wait_ahead(int ahead) {
 }
 
 template <int WM, int WN, int MT, int NT, int S, int EPI>
-__global__ __launch_bounds__(512, 1) void packed_gemm_kernel(
+__global__ __launch_bounds__(WM * WN * 64, 1) void packed_gemm_kernel(
     const uint16_t* __restrict__ x, int x_stride, int M, const uint16_t* __restrict__ wpk, int N,
     int K, int k_slice, uint16_t* __restrict__ out, int out_stride, float* __restrict__ ws) {
   constexpr int NW = WM * WN;
-  static_assert(NW == 8, "8 waves");
+  static_assert(NW == 8 || NW == 4, "4 or 8 waves");
   constexpr int BM = WM * MT * 16, BN = WN * NT * 16;
-  constexpr int A_PW = BM / 64;         // x DMA instructions per wave per stage (8 rows each)
-  constexpr int B_PW = BN / 64;         // W DMA instructions per wave per stage (1 KiB each)
+  constexpr int A_PW = BM / (8 * NW);   // x DMA instructions per wave per stage (8 rows each)
+  constexpr int B_PW = BN * 2 / (16 * NW);  // W DMA instructions per wave per stage (1 KiB each)
   constexpr int PW = A_PW + B_PW;
   constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128;
   constexpr int STAGE = A_BYTES + B_BYTES;
@@ -474,10 +474,11 @@ extern "C" int ft_packed_gemm(const void* x, int x_stride, int M, const void* wp
     case 1: bm = 128; bn = 256; break;
     case 2: bm = 256; bn = 128; break;
     case 3: bm = 256; bn = 256; break;
+    case 4: bm = 256; bn = 256; break;
     default: return -5;
   }
   const int tiles = ((M + bm - 1) / bm) * ((N + bn - 1) / bn);
-  dim3 grid(tiles, splits), block(512);
+  dim3 grid(tiles, splits), block(cfg == 4 ? 256 : 512);
 #define FT_PG(CFG, WM, WN, MT, NT, S)                                                          \
   if (cfg == CFG) {                                                                            \
     if (epi == 0)                                                                              \
@@ -510,6 +511,7 @@ extern "C" int ft_packed_gemm(const void* x, int x_stride, int M, const void* wp
     return static_cast<int>(hipGetLastError());
   }
   FT_PG(0, 2, 4, 8, 4, 2)
+  FT_PG(4, 2, 2, 8, 8, 2)
   FT_PG(1, 2, 4, 4, 4, 3)
   FT_PG(2, 4, 2, 4, 4, 3)
 #undef FT_PG

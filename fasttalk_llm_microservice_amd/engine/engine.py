@@ -512,12 +512,12 @@ class AsyncEngine:
                 eng.step()
             except Exception as e:  # surfaced through health / streams (FT_FAULT_* tests)
                 log.exception("engine step failed")
-                self.error = e
-                eng.fail_unfinished(str(e))
-                self._flush()
                 self._fail_streak += 1
                 fatal = not self._recoverable(e) or self._fail_streak >= self.max_fail_streak
-                self.error = e if fatal else None
+                if fatal:  # set before the error outputs go out: no new request slips in
+                    self.error = e
+                eng.fail_unfinished(str(e))
+                self._flush()
                 continue
             self._fail_streak = 0
             self._flush()

@@ -97,7 +97,9 @@ _ATTR = {"qkv": "wqkv", "o": "wo", "gu": "wgu", "down": "wd"}
 PACKED_ROWS = 64
 _M_BUCKETS = (1, 8, 16, 32, 64)
 PACKED_PLAN = {
-    "qkv": {1: (1, -3, 1), 8: (2, -3, 1), 16: (2, -3, 1)},
+    # qkv 32 / 64: split-K slabs reduced by slab_rope_kv (the bf16 image is the only
+    # copy of the weights, so there is no hipBLASLt fallback)
+    "qkv": {1: (1, -3, 1), 8: (2, -3, 1), 16: (2, -3, 1), 32: (2, -3, 4), 64: (2, -3, 4)},
     "o": {1: (1, -3, 2), 8: (2, -3, 2), 16: (2, -3, 2), 32: (2, -3, 2), 64: (2, -3, 2)},
     # gu 64: split-K slabs reduced by slab_silu (engine A/B at 50 rows: 5.47 vs 5.54 ms/step)
     "gu": {1: (1, -3, 1), 8: (1, -3, 1), 16: (4, -3, 1), 32: (4, -3, 1), 64: (2, -4, 2)},
@@ -105,6 +107,34 @@ PACKED_PLAN = {
     "lm": {1: (1, -3, 1), 8: (2, -3, 1), 16: (4, -3, 1), 32: (1, -4, 1), 64: (2, -4, 1)},
 }
 MAX_SPLITS = 4
+
+# Above PACKED_ROWS rows: packed_gemm.hip on the same image, (row limit, tile cfg,
+# split-K) per projection from bench/pg_probe.py on MI355X vs hipBLASLt on row-major
+# weights (profiles/packed_gemm_*_r02.log): split-K fills the chip at mixed-step
+# sizes (80-256 rows: 0.8-1.7x hipBLASLt), whole tiles above.
+PG_PLAN = {
+    "qkv": ((128, 1, 8), (256, 2, 4), (512, 2, 2), (1 << 30, 2, 1)),
+    "o": ((128, 2, 8), (256, 1, 8), (512, 2, 4), (1024, 2, 2), (1 << 30, 0, 1)),
+    "gu": ((128, 1, 2), (256, 2, 1), (1 << 30, 0, 1)),
+    "down": ((128, 1, 16), (256, 1, 8), (512, 0, 8), (1024, 0, 4), (1 << 30, 3, 1)),
+    "lm": ((128, 1, 1), (256, 3, 1), (1 << 30, 0, 1)),
+}
+PG_MAX_SLAB_ROWS = 1024
+
+
+def pg_cfg(proj: str, rows: int, k: int) -> Tuple[int, int]:
+    for lim, cfg, sp in PG_PLAN[proj]:
+        if rows <= lim:
+            break
+    while sp > 1 and k % (64 * sp):
+        sp //= 2
+    return cfg, sp
+
+
+def _cfg_fits(c, n: int, k: int) -> bool:
+    nt, u, sp = c
+    kq = 512 if u == -4 else 64
+    return n % (16 * nt) == 0 and k % (kq * sp) == 0 and (u != -4 or n % 64 == 0)
 
 
 def _overlay_packed_plan(spec: str):
@@ -266,6 +296,8 @@ class LlamaModel:
         self._w4_scratch: Optional[torch.Tensor] = None
         self.fused = False
         self.gu_nt = 2
+        self.gu_il = False        # gate_up image interleaved in groups of 16 (packed bf16)
+        self.w4_slab: dict = {}   # W4 projections that leave split-K slabs
         self.tickets: Optional[torch.Tensor] = None
 
     # ------------------------------------------------------------------ weights
@@ -388,129 +420,167 @@ class LlamaModel:
             self._w4_scratch = torch.empty(max(need, big), dtype=self.dtype, device=self.device)
         return Q.w4_dequant(w, out=self._w4_scratch[:need].view(w.n, w.k))
 
-    def _proj(self, x: torch.Tensor, L: LayerWeights, proj: str) -> torch.Tensor:
-        """bf16 y = x W^T for one layer projection (W4, packed bf16 or hipBLASLt)."""
-        q = L.q4.get(proj) if L.q4 else None
-        if q is None:
-            attr = _ATTR[proj]
-            return self._gemm(x, getattr(L, attr), getattr(L, attr + "_pk"), proj)
-        if x.shape[0] <= W4_ROWS:
-            nt, _ = w4_cfg(proj, x.shape[0])
-            return Q.w4_gemm(x, q, nt=nt)
-        return F.linear(x, self._w4_dense(q))
-
-    def _proj_slab(self, x: torch.Tensor, L: LayerWeights, proj: str) -> int:
-        """Split-K projection into self.ws fp32 slabs; returns the split count (0: not taken)."""
-        q = L.q4.get(proj) if L.q4 else None
-        if q is None:
-            if proj == "qkv":  # bf16 qkv: split-K slabs only where its plan splits K
-                c = packed_cfg(proj, x.shape[0])
-                if c is None or c[2] == 1:
-                    return 0
-            return self._gemm_slab(x, getattr(L, _ATTR[proj] + "_pk"), proj)
-        if self.ws is None or x.shape[0] > W4_ROWS:
-            return 0
-        nt, sp = w4_cfg(proj, x.shape[0])
-        Q.w4_gemm(x, q, ws=self.ws, splits=sp, nt=nt)
-        return sp
-
-    def _gu_slab(self, x: torch.Tensor, L: LayerWeights) -> int:
-        """gate_up as split-K fp32 slabs where its plan splits K (bf16 weights);
-        returns the split count (0: not taken)."""
-        if L.q4 or L.wgu_pk is None or self.ws is None:
-            return 0
-        c = packed_cfg("gu", x.shape[0])
-        if c is None or c[2] == 1:
-            return 0
-        nt, u, sp = c
-        ops.skinny_gemm(x, L.wgu_pk, ws=self.ws, splits=sp, nt=nt, u=u)
-        return sp
-
     def _prepare_packed(self):
-        """Adds the packed copies the decode GEMMs stream (one more copy of the
-        layer weights and the LM head: ~16 GB for Llama-3-8B, of 288 GB)."""
+        """ONE weight image on the GPU (bf16): every layer projection and the LM head
+        are re-laid out into the MFMA-fragment image the decode kernels stream
+        (ops.pack_weight) and the row-major originals are dropped; prefill and large
+        batches run packed_gemm.hip on the same bytes.  The input RMSNorm weights are
+        folded into the QKV / gate_up images (W diag(ln)) -- the GPU norms then run
+        with unit weights -- and gate_up is interleaved in groups of 16 rows so the
+        fused SiLU epilogues see gate and up side by side.  Resident weights = the
+        model size (+ the embedding table when it is not tied)."""
         if not self.use_packed or not self.layers:
             return
-        H = self.cfg.hidden_size
-        L0 = self.layers[0]
-        # o / down leave split-K slabs for the fused add+RMSNorm: TP=1 only (under
-        # TP the row-parallel outputs are all-reduced first) and hidden % 2048
-        slab_ok = self.tp == 1 and H % 2048 == 0
-        use = {}
-        need_ws = MAX_SPLITS * PACKED_ROWS * H
-        for proj, attr in _ATTR.items():  # split-K slabs of every planned config
-            w = getattr(L0, attr)
-            if w is not None:
-                need_ws = max(need_ws, max((sp * b * w.shape[0] for b, (_, _, sp)
-                                            in PACKED_PLAN[proj].items()), default=0))
-        for proj, attr in _ATTR.items():
-            w = getattr(L0, attr)
-            if w is None:  # W4: the slab path depends on the shape rules only
-                q = L0.q4[proj]
-                sp_max = max(sp for _, sp in W4_PLAN[proj].values())
-                use[proj] = proj in ("qkv", "o", "down") and slab_ok \
-                    and q.k % (128 * sp_max) == 0 \
-                    and all(q.n % (16 * nt) == 0 for nt, _ in W4_PLAN[proj].values())
-                if use[proj]:
-                    need_ws = max(need_ws, max(sp * b * q.n for b, (_, sp) in W4_PLAN[proj].items()))
-                continue
-            use[proj] = _packable(*w.shape, proj) and (proj in ("qkv", "gu") or slab_ok)
+        cfg = self.cfg
+        H = cfg.hidden_size
+        fold = self.quant is None
+        one = torch.ones(H, dtype=self.dtype, device=self.device)
         for L in self.layers:
-            for proj, attr in _ATTR.items():
-                w = getattr(L, attr)
-                setattr(L, attr + "_pk", ops.pack_weight(w) if use[proj] and w is not None else None)
-        if self.lm_head is not None and _packable(*self.lm_head.shape, "lm"):
+            if L.wqkv is not None:
+                w = _fold_norm(L.wqkv, L.ln1) if fold else L.wqkv
+                L.wqkv_pk, L.wqkv = ops.pack_weight(w), None
+            if L.wo is not None:
+                L.wo_pk, L.wo = ops.pack_weight(L.wo), None
+            if L.wgu is not None:
+                w = _fold_norm(L.wgu, L.ln2) if fold else L.wgu
+                L.wgu_pk, L.wgu = ops.pack_weight(ops.interleave_gate_up(w, 1)), None
+            if L.wd is not None:
+                L.wd_pk, L.wd = ops.pack_weight(L.wd), None
+            if fold:
+                L.ln1 = L.ln2 = one
+        self.gu_il = self.layers[0].wgu_pk is not None
+        if self.lm_head is not None:
             self.lm_head_pk = ops.pack_weight(self.lm_head)
-        if use["o"] or use["down"] or use["qkv"] and L0.q4:
-            self.ws = torch.empty(need_ws, dtype=torch.float32, device=self.device)
+            self.lm_head = None
+        # split-K slab workspace: the largest [splits, rows, N] any plan may write
+        L0 = self.layers[0]
+        ns = {"qkv": (self.nq + 2 * self.nkv) * self.d, "o": H,
+              "gu": 2 * cfg.intermediate_size // self.tp, "down": H}
+        need = MAX_SPLITS * PACKED_ROWS * H
+        for proj, n in ns.items():
+            need = max(need, max(sp * b * n for b, (_, _, sp) in PACKED_PLAN[proj].items()))
+            need = max(need, max((sp * min(lim, PG_MAX_SLAB_ROWS) * n
+                                  for lim, _, sp in PG_PLAN[proj] if sp > 1), default=0))
+        slab_w4 = self.tp == 1 and H % 2048 == 0
+        for proj in ("qkv", "o", "down"):  # W4: the slab path depends on the shape rules only
+            q = L0.q4.get(proj) if L0.q4 else None
+            if q is None:
+                continue
+            sp_max = max(sp for _, sp in W4_PLAN[proj].values())
+            self.w4_slab[proj] = slab_w4 and q.k % (128 * sp_max) == 0 and \
+                all(q.n % (16 * nt) == 0 for nt, _ in W4_PLAN[proj].values())
+            if self.w4_slab[proj]:
+                need = max(need, max(sp * b * q.n for b, (_, sp) in W4_PLAN[proj].items()))
+        self.ws = torch.empty(need, dtype=torch.float32, device=self.device)
+        torch.cuda.empty_cache()
         self._prepare_fused()
 
     def _prepare_fused(self):
-        """Weights of the fused decode layer: QKV and gate_up packed with ln1 / ln2
-        folded in (the kernels scale by the row RMS only), gate_up interleaved for
-        the SiLU epilogue.  Above FUSED_ROWS rows the unfused layer runs; it keeps
-        its unfolded QKV / gate_up packs only where PACKED_PLAN uses them there."""
+        """The fused decode layer (<= FUSED_ROWS rows) streams the same images: QKV /
+        gate_up already carry ln1 / ln2 and gate_up is interleaved for nt = 2."""
         self.fused = False
         cfg = self.cfg
         H, I = cfg.hidden_size, cfg.intermediate_size
         nqkv = (self.nq + 2 * self.nkv) * self.d
-        self.gu_nt = FUSED_PLAN["gu"][fused_bucket(FUSED_ROWS)][0]
+        self.gu_nt = 2
+        L0 = self.layers[0]
         if (self.quant or self.tp != 1 or os.environ.get("FT_FUSED_DECODE", "1") == "0"
-                or self.layers[0].wqkv is None or H % 64 or I % 64 or nqkv % 16
-                or I % (8 * self.gu_nt)):
+                or L0.wqkv_pk is None or L0.wgu_pk is None or H % 64 or I % 64 or nqkv % 16):
             return
         for L in self.layers:
-            L.fqkv = ops.pack_weight(_fold_norm(L.wqkv, L.ln1))
-            L.fgu = ops.pack_weight(ops.interleave_gate_up(_fold_norm(L.wgu, L.ln2),
-                                                           self.gu_nt // 2))
-            L.fo = L.wo_pk if L.wo_pk is not None else ops.pack_weight(L.wo)
-            L.fd = L.wd_pk if L.wd_pk is not None else ops.pack_weight(L.wd)
-            if not any(b > FUSED_ROWS for b in PACKED_PLAN["qkv"]):
-                L.wqkv_pk = None
-            if not any(b > FUSED_ROWS for b in PACKED_PLAN["gu"]):
-                L.wgu_pk = None
+            L.fqkv, L.fo, L.fgu, L.fd = L.wqkv_pk, L.wo_pk, L.wgu_pk, L.wd_pk
         need = MAX_FUSED_SPLITS * FUSED_ROWS * max(nqkv, H)
         if self.ws is None or self.ws.numel() < need:
             self.ws = torch.empty(need, dtype=torch.float32, device=self.device)
         self.tickets = torch.zeros(max(4096, H // 16), dtype=torch.int32, device=self.device)
         self.fused = True
 
-    def _gemm(self, x: torch.Tensor, w: torch.Tensor, w_pk: Optional[torch.Tensor], proj: str):
-        """bf16 y = x w^T: packed decode GEMM when the plan has a split-1 config."""
-        c = packed_cfg(proj, x.shape[0]) if w_pk is not None else None
-        if c is None or c[2] != 1:
-            return F.linear(x, w)
-        nt, u, _ = c
-        return ops.skinny_gemm(x, w_pk, splits=1, nt=nt, u=u)
+    def resident_weight_bytes(self) -> int:
+        """Bytes of weights held on the device (every layer tensor, embedding, head)."""
+        seen, total = set(), 0
 
-    def _gemm_slab(self, x: torch.Tensor, w_pk: Optional[torch.Tensor], proj: str) -> int:
-        """Split-K packed GEMM into self.ws; returns the split count (0: not taken)."""
-        c = packed_cfg(proj, x.shape[0]) if (w_pk is not None and self.ws is not None) else None
-        if c is None:
-            return 0
-        nt, u, sp = c
-        ops.skinny_gemm(x, w_pk, ws=self.ws, splits=sp, nt=nt, u=u)
-        return sp
+        def add(t):
+            nonlocal total
+            if isinstance(t, torch.Tensor) and t.device.type == self.device.type and \
+                    t.data_ptr() not in seen:
+                seen.add(t.data_ptr())
+                total += t.numel() * t.element_size()
+        for L in self.layers:
+            for f in dataclasses.fields(L):
+                v = getattr(L, f.name)
+                if isinstance(v, dict):
+                    for q in v.values():
+                        for t in vars(q).values():
+                            add(t)
+                else:
+                    add(v)
+        for t in (self.embed, self.norm, self.lm_head, self.lm_head_pk):
+            add(t)
+        return total
+
+    # ------------------------------------------------------------------ projections
+    def _slab_ok(self, proj: str) -> bool:
+        """May this projection leave split-K fp32 slabs for its consumer?  qkv ->
+        slab_rope_kv, gate_up -> slab_silu (both rank-local); o / down -> the
+        residual add + RMSNorm, which is TP=1 only (under TP the row-parallel
+        outputs are all-reduced first) and needs hidden % 2048."""
+        if proj in ("qkv", "gu"):
+            return True
+        return self.tp == 1 and self.cfg.hidden_size % 2048 == 0
+
+    def _lin(self, x: torch.Tensor, L: LayerWeights, proj: str) -> Tuple[int, Optional[torch.Tensor]]:
+        """One layer projection y = x W^T.  Returns (splits, None) when the result
+        is left as ``splits`` fp32 slabs in self.ws for the fused consumer, else
+        (0, y).  For "gu" y is already h = silu(gate) * up."""
+        rows = x.shape[0]
+        q = L.q4.get(proj) if L.q4 else None
+        if q is not None:  # W4A16
+            if self.ws is not None and rows <= W4_ROWS and self.w4_slab.get(proj):
+                nt, sp = w4_cfg(proj, rows)
+                Q.w4_gemm(x, q, ws=self.ws, splits=sp, nt=nt)
+                return sp, None
+            if rows <= W4_ROWS:
+                y = Q.w4_gemm(x, q, nt=w4_cfg(proj, rows)[0])
+            else:
+                y = F.linear(x, self._w4_dense(q))
+            return 0, (ops.silu_mul(y) if proj == "gu" else y)
+        attr = _ATTR[proj]
+        wp = getattr(L, attr + "_pk")
+        if wp is None:  # row-major weights: CPU backend, or FT_PACKED_GEMM=0
+            y = F.linear(x, getattr(L, attr))
+            return 0, (ops.silu_mul(y) if proj == "gu" else y)
+        return self._packed(x, wp, proj)
+
+    def _packed(self, x: torch.Tensor, wp: torch.Tensor, proj: str) -> Tuple[int, Optional[torch.Tensor]]:
+        """y = x W^T on the packed image: the decode kernels up to PACKED_ROWS rows
+        (skinny_gemm.hip), the tiled MFMA GEMM above (packed_gemm.hip)."""
+        rows = x.shape[0]
+        n, k = wp.shape
+        gu = proj == "gu"
+        slab_ok = self._slab_ok(proj) and self.ws is not None
+        c = packed_cfg(proj, rows) if proj in PACKED_PLAN else None
+        if c is not None and _cfg_fits(c, n, k):
+            nt, u, sp = c
+            if sp > 1 and not (slab_ok and sp * rows * n <= self.ws.numel()):
+                sp = 1
+            if sp > 1:
+                ops.skinny_gemm(x, wp, ws=self.ws, splits=sp, nt=nt, u=u)
+                return sp, None
+            y = ops.skinny_gemm(x, wp, splits=1, nt=nt, u=u)
+            return 0, (ops.silu_mul(y, interleaved=True) if gu else y)
+        cfg, sp = pg_cfg(proj, rows, k)
+        if sp > 1 and (self.ws is None or sp * rows * n > self.ws.numel()):
+            sp = 1
+        if sp > 1:
+            ops.packed_gemm(x, wp, ws=self.ws, splits=sp, epi="slab", cfg=cfg)
+            if slab_ok:
+                return sp, None
+            y = torch.empty(rows, n, dtype=x.dtype, device=x.device)  # TP / odd hidden
+            ops.slab_store(self.ws, sp, rows, n, y)
+            return 0, y
+        if gu:
+            return 0, ops.packed_gemm(x, wp, epi="silu", cfg=cfg)
+        return 0, ops.packed_gemm(x, wp, cfg=cfg)
 
     # ------------------------------------------------------------------ KV cache
     def kv_cache_shape(self, num_blocks: int, block_size: int) -> Tuple[int, ...]:
@@ -605,34 +675,31 @@ class LlamaModel:
             else:
                 ops.fused_add_rmsnorm(x, residual, L.ln1, eps)
             kc, vc = kv_caches[li]
-            sq = self._proj_slab(x, L, "qkv")
+            sq, qkv = self._lin(x, L, "qkv")
             if sq:  # split-K slabs -> RoPE'd q and the paged K/V write in one kernel
                 qkv = torch.empty(t, (nq + 2 * nkv) * d, dtype=self.dtype, device=self.device)
                 ops.slab_rope_kv(self.ws, sq, t, qkv.shape[1], qkv, meta.positions, self.cos_sin,
                                  meta.slot_mapping, kc, vc, nq, nkv, d)
             else:
-                qkv = self._proj(x, L, "qkv")
                 ops.rope_kv_write(qkv, meta.positions, self.cos_sin, meta.slot_mapping, kc, vc,
                                   nq, nkv, d)
             attn = self._attention(qkv, meta, kc, vc)
-            so = self._proj_slab(attn, L, "o")
+            so, y = self._lin(attn, L, "o")
             if so:
                 x = torch.empty(t, H, dtype=self.dtype, device=self.device)
                 ops.row_rmsnorm(x, L.ln2, eps, t, ws=self.ws, splits=so, residual=residual)
             else:
-                x = self._proj(attn, L, "o")
+                x = y
                 self.comm.all_reduce(x)
                 ops.fused_add_rmsnorm(x, residual, L.ln2, eps)
-            sg = self._gu_slab(x, L)
+            sg, h = self._lin(x, L, "gu")
             if sg:  # split-K gate_up slabs -> SiLU-mul reduces them
                 h = torch.empty(t, cfg.intermediate_size // self.tp, dtype=self.dtype,
                                 device=self.device)
-                ops.slab_silu(self.ws, sg, t, h.shape[1], h)
-            else:
-                h = ops.silu_mul(self._proj(x, L, "gu"))
-            slab = self._proj_slab(h, L, "down")
+                ops.slab_silu(self.ws, sg, t, h.shape[1], h, interleaved=self.gu_il)
+            slab, y = self._lin(h, L, "down")
             if not slab:
-                x = self._proj(h, L, "down")
+                x = y
                 self.comm.all_reduce(x)
         if slab:
             x = torch.empty(t, H, dtype=self.dtype, device=self.device)
@@ -648,5 +715,8 @@ class LlamaModel:
 
     def compute_logits(self, h: torch.Tensor) -> torch.Tensor:
         """[B, H] -> [B, V] logits (bf16 on GPU; vocab-parallel shards gathered)."""
-        logits = self._gemm(h, self.lm_head, self.lm_head_pk, "lm")
+        if self.lm_head_pk is not None:
+            logits = self._packed(h, self.lm_head_pk, "lm")[1]
+        else:
+            logits = F.linear(h, self.lm_head)
         return self.comm.all_gather_last(logits)

@@ -87,12 +87,18 @@ def fused_add_rmsnorm(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, 
     return x, residual
 
 
-def silu_mul(gu: torch.Tensor, out: Optional[torch.Tensor] = None):
+def silu_mul(gu: torch.Tensor, out: Optional[torch.Tensor] = None, interleaved: bool = False):
+    """silu(gate) * up of [M, 2I] gate_up rows: halves [gate | up], or ``interleaved``
+    groups of 16 (interleave_gate_up(w, 1), the packed model's gate_up image)."""
     if gu.is_cuda:
         if out is None:
             out = torch.empty(gu.shape[0], gu.shape[1] // 2, dtype=gu.dtype, device=gu.device)
-        native().silu_mul(out, gu)
+        native().silu_mul(out, gu, interleaved)
         return out
+    if interleaved:
+        m, two_i = gu.shape
+        v = gu.reshape(m, two_i // 32, 2, 16)
+        gu = torch.cat([v[:, :, 0].reshape(m, -1), v[:, :, 1].reshape(m, -1)], dim=1)
     r = ref.silu_mul(gu)
     if out is not None:
         out.copy_(r)
@@ -278,8 +284,8 @@ def row_rmsnorm(out, w, eps, rows, x=None, ws=None, splits=1, residual=None):
     return out
 
 
-def slab_silu(ws, splits, rows, inter, out):
-    native().slab_silu(ws, splits, rows, inter, out)
+def slab_silu(ws, splits, rows, inter, out, interleaved: bool = False):
+    native().slab_silu(ws, splits, rows, inter, out, interleaved)
     return out
 
 

@@ -3,6 +3,7 @@ import numpy as np
 import pytest
 import torch
 
+from fasttalk_llm_microservice_amd import ops
 from fasttalk_llm_microservice_amd.engine.config import EngineConfig
 from fasttalk_llm_microservice_amd.engine.engine import LLMEngine
 from fasttalk_llm_microservice_amd.engine.sampling_params import SamplingParams
@@ -211,3 +212,92 @@ def test_guided_rows_stay_on_the_decode_graph():
     assert all(len(res[i]) == 40 for i in range(6) if i != 2)
     # the mask rows a guided step dirtied are reset for the next plain steps
     assert eng.runner._mask_rows == 0 or eng.scheduler.has_work()
+
+
+def test_single_weight_image_llama3_8b():
+    """the GPU holds ONE image of the weights (packed, with the
+    input norms folded in); resident weights <= 1.1x the model's bf16 size."""
+    cfg = MODELS["llama3-8b"]
+    m = LlamaModel(cfg, torch.device("cuda"), torch.bfloat16, max_model_len=2048).init_random(0)
+    torch.cuda.synchronize()
+    resident = m.resident_weight_bytes()
+    model_bytes = cfg.num_params() * 2
+    print(f"resident {resident / 2**30:.2f} GiB vs model {model_bytes / 2**30:.2f} GiB")
+    assert resident <= 1.1 * model_bytes, (resident, model_bytes)
+    L0 = m.layers[0]
+    assert L0.wqkv is None and L0.wgu is None and L0.wqkv_pk is not None
+    assert m.fused and L0.fqkv is L0.wqkv_pk and L0.fgu is L0.wgu_pk
+    del m
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("rows", [20, 50, 100])
+def test_llama3_8b_shape_decode_matches_cpu_fp32(rows):
+    """a 2-layer Llama-3-8B-shaped model (H 4096, I 14336, GQA 4)
+    decoding `rows` sequences with ragged contexts up to 6k over random KV caches
+    -- the fused layer (20 rows), the unfused split-K/slab plan of the 64 bucket
+    (50 rows) and the packed GEMM (100 rows) -- eager and replayed from a hipGraph,
+    against the fp32 CPU model on the same weights and cache contents."""
+    import dataclasses as dc
+
+    cfg = dc.replace(MODELS["llama3-8b"], name="llama3-8b-2l", num_layers=2)
+    g = LlamaModel(cfg, torch.device("cuda"), torch.bfloat16, max_model_len=8192)
+    g.init_random(5, consistent=True)
+    c = LlamaModel(cfg, torch.device("cpu"), torch.float32, max_model_len=8192)
+    c.init_random(5, consistent=True)
+    rng = np.random.default_rng(rows)
+    lens = rng.integers(64, 6000, rows)
+    lens[0] = 6000
+    bs = 16
+    nblk = [int(-(-n // bs)) for n in lens]
+    perm = torch.from_numpy(rng.permutation(sum(nblk)).astype(np.int32))
+    bt = torch.zeros(rows, max(nblk), dtype=torch.int32)
+    o = 0
+    for i, nb in enumerate(nblk):
+        bt[i, :nb] = perm[o:o + nb]
+        o += nb
+    total = sum(nblk)
+    kv_g = g.allocate_kv_cache(total, bs)
+    kv_c = c.allocate_kv_cache(total, bs)
+    for (kg, vg), (kc, vc) in zip(kv_g, kv_c):
+        kc.copy_(torch.randn(kc.shape).bfloat16().float())
+        vc.copy_(torch.randn(vc.shape).bfloat16().float())
+        kg.copy_(kc.bfloat16())
+        vg.copy_(vc.bfloat16())
+    ids = torch.from_numpy(rng.integers(0, 120000, rows).astype(np.int32))
+    pos = torch.from_numpy((lens - 1).astype(np.int32))
+    slots = torch.tensor([int(bt[i, (lens[i] - 1) // bs]) * bs + (lens[i] - 1) % bs
+                          for i in range(rows)], dtype=torch.int32)
+
+    def meta(dev, tmp=None):
+        m = AttnMeta(positions=pos.to(dev), slot_mapping=slots.to(dev),
+                     logits_indices=torch.arange(rows, device=dev), num_decode=rows,
+                     dec_block_tables=bt.to(dev), dec_seq_lens=(pos + 1).to(dev))
+        if tmp is not None:
+            m.tmp_out, m.tmp_ml = tmp
+        return m
+
+    n_out, n_ml = ops.decode_workspace(rows, g.nq, g.nkv, g.d)
+    tmp = (torch.empty(n_out, device="cuda"), torch.empty(n_ml, device="cuda"))
+    ref = c.compute_logits(c.forward(ids, meta("cpu"), kv_c)).float()
+    mg = meta("cuda", tmp)
+    idg = ids.cuda()
+    eager = g.compute_logits(g.forward(idg, mg, kv_g)).float().cpu()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        g.compute_logits(g.forward(idg, mg, kv_g))
+    torch.cuda.current_stream().wait_stream(s)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        out = g.compute_logits(g.forward(idg, mg, kv_g))
+    graph.replay()
+    torch.cuda.synchronize()
+    replayed = out.float().cpu()
+    for name, a in (("eager", eager), ("graph", replayed)):
+        cos = torch.nn.functional.cosine_similarity(a, ref, dim=-1)
+        agree = (a.argmax(-1) == ref.argmax(-1)).float().mean().item()
+        print(f"rows {rows} {name}: min cos {cos.min().item():.5f} argmax agree {agree:.3f}")
+        assert cos.min().item() > 0.99, (name, cos.min().item())
+        assert agree >= 0.9, (name, agree)
+    assert torch.equal(eager, replayed)

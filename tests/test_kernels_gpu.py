@@ -557,3 +557,44 @@ def test_slab_rope_kv_residual_norm():
     _close(q_out, qkv[:, : nq * d], atol=3e-2, rtol=2e-2, msg="q")
     _close(k1, k2, atol=3e-2, rtol=2e-2, msg="k")
     _close(v1, v2, atol=3e-2, rtol=2e-2, msg="v")
+
+
+@pytest.mark.parametrize("m", [65, 80, 200, 256, 300, 700])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
+def test_packed_gemm_matches_fp32(m, cfg):
+    """packed_gemm.hip (any M, on the decode kernels' packed image) vs fp32
+    x W^T: bf16 store, split-K slabs (+ slab_store), odd N tails (N % 256 != 0)."""
+    torch.manual_seed(m + cfg)
+    for n, k in [(768, 512), (1040, 1024)]:
+        w = (torch.randn(n, k, device="cuda") * 0.05).bfloat16()
+        x = torch.randn(m, k, device="cuda").bfloat16()
+        ref = x.float() @ w.float().t()
+        wp = ops.pack_weight(w)
+        _close(ops.packed_gemm(x, wp, cfg=cfg), ref, atol=3e-2, rtol=2e-2, msg=f"pg cfg{cfg}")
+        ws = torch.empty(4 * m * n, device="cuda")
+        ops.packed_gemm(x, wp, ws=ws, splits=4, epi="slab", cfg=cfg)
+        out = torch.empty(m, n, device="cuda").bfloat16()
+        ops.slab_store(ws, 4, m, n, out)
+        _close(out, ref, atol=3e-2, rtol=2e-2, msg=f"pg cfg{cfg} split-K")
+
+
+@pytest.mark.parametrize("cfg", [0, 1, 3])
+def test_packed_gemm_silu_epilogue_and_interleaved_silu(cfg):
+    """gate_up in the single-image layout (interleave_gate_up(w, 1)): the GEMM's
+    SiLU epilogue, silu_mul(interleaved) on its dense output and slab_silu on
+    split-K slabs all equal silu(x Wg^T) * (x Wu^T)."""
+    torch.manual_seed(cfg)
+    inter, k, m = 1024, 512, 150
+    w = (torch.randn(2 * inter, k, device="cuda") * 0.05).bfloat16()
+    x = torch.randn(m, k, device="cuda").bfloat16()
+    g, u = (x.float() @ w.float().t()).chunk(2, dim=-1)
+    ref = torch.nn.functional.silu(g) * u
+    wp = ops.pack_weight(ops.interleave_gate_up(w, 1))
+    _close(ops.packed_gemm(x, wp, epi="silu", cfg=cfg), ref, atol=3e-2, rtol=2e-2, msg="silu epi")
+    dense = ops.packed_gemm(x, wp, cfg=cfg)
+    _close(ops.silu_mul(dense, interleaved=True), ref, atol=3e-2, rtol=2e-2, msg="silu_mul il")
+    ws = torch.empty(2 * m * 2 * inter, device="cuda")
+    ops.packed_gemm(x, wp, ws=ws, splits=2, epi="slab", cfg=cfg)
+    h = torch.empty(m, inter, device="cuda").bfloat16()
+    ops.slab_silu(ws, 2, m, inter, h, interleaved=True)
+    _close(h, ref, atol=3e-2, rtol=2e-2, msg="slab_silu il")
