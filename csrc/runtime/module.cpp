@@ -11,7 +11,9 @@ using namespace ftrt;
 
 void register_json_fsm(py::module_& m);
 
-PYBIND11_MODULE(_rt, m) {
+// The bindings are a plain function so csrc/tools/rt_sanitize.cpp can register the
+// same module inside an ASan/UBSan-instrumented executable that embeds Python.
+void ftrt_register(py::module_& m) {
   m.doc() = "FastTalk native engine runtime (block manager, detokenizer, token FSM)";
 
   py::class_<BlockManager>(m, "BlockManager")
@@ -71,3 +73,7 @@ PYBIND11_MODULE(_rt, m) {
 
   register_json_fsm(m);
 }
+
+#ifndef FTRT_EMBEDDED
+PYBIND11_MODULE(_rt, m) { ftrt_register(m); }
+#endif

@@ -14,6 +14,12 @@ def rt():
     if _rt is not None:
         return _rt
     with _lock:
+        if _rt is None and os.environ.get("FT_RT_MODULE"):
+            # a differently built copy of the same bindings, e.g. the ASan/UBSan
+            # executable's embedded module (tests/unit/test_sanitizers.py)
+            import importlib
+
+            _rt = importlib.import_module(os.environ["FT_RT_MODULE"])
         if _rt is None:
             try:
                 from .. import _rt as mod  # type: ignore

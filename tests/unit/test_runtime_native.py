@@ -205,3 +205,12 @@ def test_tool_call_grammar():
         if obj["name"] == "duckduckgo_search":
             assert isinstance(obj["parameters"]["query"], str)
     assert g.num_allowed(g.initial()) > 0
+
+
+def test_runtime_module_identity():
+    """Under tests/unit/test_sanitizers.py the instrumented build is the one in use."""
+    import os
+
+    want = os.environ.get("FT_RT_MODULE")
+    if want:
+        assert rt().__name__ == want
