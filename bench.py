@@ -190,9 +190,11 @@ def main():
     p = lambda q: ttfts[min(len(ttfts) - 1, int(round(q * (len(ttfts) - 1))))] if ttfts else 0.0  # noqa
     value = tokens / t_max
     metrics = engine.engine.metrics()
+    mlabel = _model_label(a.model)
     if rank == 0:
         out = {
-            "metric": "output tokens/sec (node) + p50 TTFT over WebSocket, Llama-3-8B at 50 sessions"
+            "metric": f"output tokens/sec (node) + p50 TTFT over WebSocket, {mlabel} at "
+                      f"{a.sessions} session{'s' if a.sessions != 1 else ''}"
                       + (f" (agent, guided tool calls on {a.agent_tools:.0%} of turns)"
                          if a.agent_tools >= 0 else ""),
             "value": round(value, 2),
@@ -205,9 +207,9 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "w4a16 (bf16 compute)" if a.quant else "bf16",
-            "data": "synthetic (random-init Llama-3-8B weights, synthetic English prompts, "
+            "data": f"synthetic (random-init {mlabel} weights, synthetic English prompts, "
                     "synthetic Llama-3 tokenizer)",
-            "config": {"model": "Llama-3-8B", "global_batch": a.sessions * world,
+            "config": {"model": mlabel, "global_batch": a.sessions * world,
                        "seq_len": engine.engine.max_model_len, "parallelism": f"dp{world}",
                        "sessions_per_gpu": a.sessions, "tokens_per_turn": a.gen,
                        "path": "ws/llm -> " + ("direct engine" if a.no_agent else "voice agent") +
@@ -217,7 +219,9 @@ def main():
             "p50_server_ttft_ms": _p50([x for r in allr for x in r["server_ttft"]]),
             "p50_engine_ttft_ms": _p50([x for r in allr for x in r["engine_ttft"]]),
             "per_session_tok_s": round(value / (a.sessions * world), 2),
-            "reference_anchor": "8B single stream ~50-80 tok/s, ~200 ms TTFT on RTX 3090 (README.md:567)",
+            "reference_anchor": ("70B ~20 tok/s, ~1 s TTFT, multi-GPU (README.md:474,568)"
+                                 if "70B" in mlabel else
+                                 "8B single stream ~50-80 tok/s, ~200 ms TTFT on RTX 3090 (README.md:567)"),
             "prefix_cache_hit_tokens": sum(r["cached"] for r in allr),
             "prompt_tokens": sum(r["prompt"] for r in allr),
             "engine_decode_step_ms": round(metrics.get("decode_step_ms_avg", 0.0), 3),
@@ -236,6 +240,16 @@ def main():
         pass
     loop.call_soon_threadsafe(loop.stop)
     engine.shutdown()
+
+
+def _model_label(name: str) -> str:
+    """BASELINE.json's model names for the configs it quotes (Llama-3-8B / -70B)."""
+    from fasttalk_llm_microservice_amd.models.config import resolve_model
+
+    n = resolve_model(name).name
+    return {"llama3-8b": "Llama-3-8B", "llama3.1-8b": "Llama-3.1-8B", "llama3-70b": "Llama-3-70B",
+            "llama3.1-70b": "Llama-3.1-70B", "llama3.2-1b": "Llama-3.2-1B",
+            "llama3.2-3b": "Llama-3.2-3B"}.get(n, n)
 
 
 def bench_tp(a, rank: int, world: int, local_rank: int):

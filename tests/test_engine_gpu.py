@@ -231,16 +231,18 @@ def test_single_weight_image_llama3_8b():
     torch.cuda.empty_cache()
 
 
-@pytest.mark.parametrize("rows", [20, 50, 100])
-def test_llama3_8b_shape_decode_matches_cpu_fp32(rows):
-    """a 2-layer Llama-3-8B-shaped model (H 4096, I 14336, GQA 4)
-    decoding `rows` sequences with ragged contexts up to 6k over random KV caches
-    -- the fused layer (20 rows), the unfused split-K/slab plan of the 64 bucket
-    (50 rows) and the packed GEMM (100 rows) -- eager and replayed from a hipGraph,
-    against the fp32 CPU model on the same weights and cache contents."""
+@pytest.mark.parametrize("model,rows", [("llama3-8b", 1), ("llama3-8b", 20), ("llama3-8b", 50),
+                                        ("llama3-8b", 100), ("llama3-70b", 1), ("llama3-70b", 72)])
+def test_llama3_shape_decode_matches_cpu_fp32(model, rows):
+    """a 2-layer Llama-3-8B-shaped model (H 4096, I 14336, GQA 4) -- and
+    a 70B-shaped one (H 8192, I 28672, GQA 8) -- decoding `rows` sequences with ragged
+    contexts up to 6k over random KV caches: the fused layer (1 / 20 rows), the
+    unfused split-K/slab plan of the 64 bucket (50 rows) and the packed GEMM (72 /
+    100 rows), eager and replayed from a hipGraph, against the fp32 CPU model on the
+    same weights and cache contents."""
     import dataclasses as dc
 
-    cfg = dc.replace(MODELS["llama3-8b"], name="llama3-8b-2l", num_layers=2)
+    cfg = dc.replace(MODELS[model], name=f"{model}-2l", num_layers=2)
     g = LlamaModel(cfg, torch.device("cuda"), torch.bfloat16, max_model_len=8192)
     g.init_random(5, consistent=True)
     c = LlamaModel(cfg, torch.device("cpu"), torch.float32, max_model_len=8192)
@@ -297,7 +299,7 @@ def test_llama3_8b_shape_decode_matches_cpu_fp32(rows):
     for name, a in (("eager", eager), ("graph", replayed)):
         cos = torch.nn.functional.cosine_similarity(a, ref, dim=-1)
         agree = (a.argmax(-1) == ref.argmax(-1)).float().mean().item()
-        print(f"rows {rows} {name}: min cos {cos.min().item():.5f} argmax agree {agree:.3f}")
+        print(f"{model} rows {rows} {name}: min cos {cos.min().item():.5f} argmax agree {agree:.3f}")
         assert cos.min().item() > 0.99, (name, cos.min().item())
         assert agree >= 0.9, (name, agree)
     assert torch.equal(eager, replayed)
