@@ -9,6 +9,7 @@ from __future__ import annotations
 import asyncio
 import collections
 import itertools
+import os
 import logging
 import queue
 import threading
@@ -56,11 +57,16 @@ class LLMEngine:
         self.detok = R.Detokenizer(self.tokenizer.id_to_bytes)
         self.scheduler = Scheduler(self.bm, cfg.block_size, cfg.max_num_seqs,
                                    cfg.max_num_batched_tokens, self.max_model_len,
-                                   host_blocks=getattr(runner, "num_host_blocks", 0))
+                                   host_blocks=getattr(runner, "num_host_blocks", 0),
+                                   prefill_chunk=cfg.prefill_chunk)
         self.stop_ids = set(self.tokenizer.stop_ids) | set(self.model_cfg.eos_token_ids)
         self._trie = None
         self.stats = collections.Counter()
         self.step_times = collections.deque(maxlen=512)
+        # FT_STEP_TRACE=<path>: per-step timeline (kind, rows, tokens, start/end) and
+        # request arrivals, written at shutdown -- what the GPU waits on between turns
+        self._trace_path = os.environ.get("FT_STEP_TRACE") or None
+        self._trace: List[tuple] = []
         self.host_prof = collections.Counter()
         self._inflight = None          # (batch, DecodeHandle) of a queued decode step
         self._last_complete = 0.0
@@ -81,6 +87,8 @@ class LLMEngine:
             raise EngineError(f"prompt of {len(prompt_ids)} tokens exceeds max_model_len "
                               f"{self.max_model_len}")
         seq = Sequence(request_id, prompt_ids, params, on_output, meta)
+        if self._trace_path:
+            self._trace.append(("arrive", time.perf_counter(), len(prompt_ids)))
         seq.detok_stream = self.detok.new_stream()
         if params.guided is not None:
             seq.grammar = params.guided.grammar(self)
@@ -163,6 +171,8 @@ class LLMEngine:
         dt = t2 - self._last_complete if self._last_complete else t2 - t0
         self._last_complete = t2
         self.step_times.append((False, len(batch.decode_seqs), len(batch.decode_seqs), dt))
+        if self._trace_path:
+            self._trace.append(("decode_p", t0, t2, len(batch.decode_seqs), 0, 0))
         self.stats["decode_steps"] += 1
         self.stats["pipelined_steps"] += 1
         hp = self.host_prof
@@ -246,6 +256,10 @@ class LLMEngine:
             hp["process"] += t2 - t1
             hp["steps"] += 1
         self.step_times.append((batch.has_prefill, len(batch.decode_seqs), batch.total_tokens, dt))
+        if self._trace_path:
+            self._trace.append(("mixed" if batch.has_prefill else "decode", ts, t2,
+                                len(batch.decode_seqs), sum(batch.prefill_tokens),
+                                len(batch.prefill_seqs)))
         self.stats["mixed_steps" if batch.has_prefill else "decode_steps"] += 1
         self.stats["generated_tokens"] += len(sampled_seqs)
         self.stats["prefill_tokens"] += sum(batch.prefill_tokens)
@@ -366,8 +380,16 @@ class LLMEngine:
                         done.add(o.request_id)
         return [results[r] for r in ids]
 
+    def write_trace(self):
+        if self._trace_path and self._trace:
+            import json
+
+            with open(self._trace_path, "w") as f:
+                json.dump(self._trace, f)
+
     def shutdown(self):
         """Stops tensor-parallel workers (if any)."""
+        self.write_trace()
         g = getattr(self, "tp_group", None)
         if g is not None:
             g.shutdown()

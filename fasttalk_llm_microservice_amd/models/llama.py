@@ -120,6 +120,12 @@ PG_PLAN = {
     "lm": ((128, 1, 1), (256, 3, 1), (1 << 30, 0, 1)),
 }
 PG_MAX_SLAB_ROWS = 1024
+# At prefill-burst sizes hipBLASLt's tiles beat packed_gemm (1.35-1.66 vs 1.1-1.2
+# PF/s at M = 4096, profiles/packed_gemm_*_r02.log) by more than it costs to unpack
+# the layer's weight into a transient row-major copy (one read + one write of the
+# weight, ~0.17 ms per 8B layer): from this many rows up the projection unpacks and
+# calls the library.  The resident weights stay single-image.  0 disables.
+PG_BLAS_ROWS = int(os.environ.get("FT_PG_BLAS_ROWS", "2048"))
 
 
 def pg_cfg(proj: str, rows: int, k: int) -> Tuple[int, int]:
@@ -298,6 +304,8 @@ class LlamaModel:
         self.gu_nt = 2
         self.gu_il = False        # gate_up image interleaved in groups of 16 (packed bf16)
         self.w4_slab: dict = {}   # W4 projections that leave split-K slabs
+        self._unpack_buf: Optional[torch.Tensor] = None  # transient row-major weight (prefill)
+        self._unpack_need = 0
         self.tickets: Optional[torch.Tensor] = None
 
     # ------------------------------------------------------------------ weights
@@ -449,6 +457,9 @@ class LlamaModel:
             if fold:
                 L.ln1 = L.ln2 = one
         self.gu_il = self.layers[0].wgu_pk is not None
+        self._unpack_need = max((w.numel() for w in (self.layers[0].wqkv_pk, self.layers[0].wo_pk,
+                                                      self.layers[0].wgu_pk, self.layers[0].wd_pk)
+                                 if w is not None), default=0)
         if self.lm_head is not None:
             self.lm_head_pk = ops.pack_weight(self.lm_head)
             self.lm_head = None
@@ -567,6 +578,12 @@ class LlamaModel:
                 ops.skinny_gemm(x, wp, ws=self.ws, splits=sp, nt=nt, u=u)
                 return sp, None
             y = ops.skinny_gemm(x, wp, splits=1, nt=nt, u=u)
+            return 0, (ops.silu_mul(y, interleaved=True) if gu else y)
+        if PG_BLAS_ROWS and rows >= PG_BLAS_ROWS and proj != "lm":
+            if self._unpack_buf is None or self._unpack_buf.numel() < n * k:
+                self._unpack_buf = torch.empty(max(n * k, self._unpack_need), dtype=wp.dtype,
+                                               device=wp.device)
+            y = F.linear(x, ops.unpack_weight(wp, out=self._unpack_buf))
             return 0, (ops.silu_mul(y, interleaved=True) if gu else y)
         cfg, sp = pg_cfg(proj, rows, k)
         if sp > 1 and (self.ws is None or sp * rows * n > self.ws.numel()):

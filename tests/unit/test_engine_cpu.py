@@ -135,6 +135,26 @@ def test_continuous_batching_and_chunked_prefill():
     assert eng.bm.num_free() == eng.bm.num_blocks
 
 
+def test_soft_prefill_chunk_splits_bursts_not_lone_prompts():
+    """prefill_chunk: a lone long prompt still prefills in one step (up to the hard
+    budget); a burst of short prompts is spread over steps of <= prefill_chunk
+    prefill tokens, so the first of them start decoding early."""
+    eng = _fake_engine(max_num_seqs=16, max_num_batched_tokens=256, prefill_chunk=32,
+                       num_blocks=512)
+    long = list(range(1, 201))
+    assert eng.generate([long], SamplingParams(temperature=0, max_tokens=2, ignore_eos=True)) == \
+        [_expected(long, 2)]
+    assert eng.runner.batches[0] == (0, [200])          # one step, beyond the soft budget
+    eng.runner.batches.clear()
+    burst = [list(range(1000 + 20 * i, 1020 + 20 * i)) for i in range(6)]
+    outs = eng.generate(burst, SamplingParams(temperature=0, max_tokens=3, ignore_eos=True))
+    assert outs == [_expected(p, 3) for p in burst]
+    first = eng.runner.batches[0]
+    assert sum(first[1]) <= 32 and first[1][0] == 20     # 20 + a 12-token head of the next
+    assert all(sum(pre) <= 32 for _, pre in eng.runner.batches)
+    assert eng.bm.num_free() == eng.bm.num_blocks
+
+
 def test_preemption_under_kv_pressure_completes_everything():
     eng = _fake_engine(num_blocks=12, max_num_seqs=8, max_num_batched_tokens=64)
     prompts = [[i + 1] * 6 for i in range(5)]
