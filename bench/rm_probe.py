@@ -31,8 +31,12 @@ def main():
     ap.add_argument("--rows", default="1,8,16,32,50,64")
     ap.add_argument("--only", default="")
     ap.add_argument("--iters", type=int, default=30)
+    ap.add_argument("--configs", default="", help="nt:u:splits,... (default: the built-in list)")
+    ap.add_argument("--packed-only", action="store_true")
     a = ap.parse_args()
     rows = [int(r) for r in a.rows.split(",")]
+    configs = [tuple(int(v) for v in c.split(":")) for c in a.configs.split(",")] if a.configs \
+        else CONFIGS
     res = {}
     torch.manual_seed(0)
     for name, (n, k) in SHAPES.items():
@@ -42,16 +46,17 @@ def main():
         copies = max(2, -(-(600 << 20) // nbytes))
         ws_rm = [torch.randn(n, k, device="cuda").bfloat16() * 0.02 for _ in range(copies)]
         ws_pk = [ops.pack_weight(w) for w in ws_rm]
-        ws = torch.empty(4 * 64 * max(n, 4096), device="cuda")
+        ws = torch.empty(16 * 64 * max(n, 4096), device="cuda")
         for m in rows:
             x = torch.randn(m, k, device="cuda").bfloat16()
             ref = F.linear(x, ws_rm[0]).float()
             best = {}
-            for nt, u, sp in CONFIGS:
+            per_cfg = {}
+            for nt, u, sp in configs:
                 kq = 512 if u == -4 else 64
                 if n % (16 * nt) or k % (kq * sp) or (u == -4 and n % 64):
                     continue
-                for rm in (False, True):
+                for rm in ((False,) if a.packed_only else (False, True)):
                     uu = u - 10 if rm else u
                     imgs = ws_rm if rm else ws_pk
                     out = torch.empty(m, n, device="cuda").bfloat16()
@@ -74,6 +79,8 @@ def main():
                     torch.cuda.synchronize()
                     us = s.elapsed_time(e) * 1e3 / a.iters
                     key = "rm" if rm else "pk"
+                    if not rm:
+                        per_cfg[(nt, u, sp)] = us
                     if key not in best or us < best[key][0]:
                         best[key] = (us, (nt, u, sp))
             # hipBLASLt on the row-major copies
@@ -87,6 +94,11 @@ def main():
             e.record()
             torch.cuda.synchronize()
             blas = s.elapsed_time(e) * 1e3 / a.iters
+            if a.packed_only:
+                print(f"{name:5s} m={m:3d} blas {blas:6.2f} " + " ".join(
+                    f"{c[0]}/{c[1]}/{c[2]}={t:.1f}" for c, t in sorted(per_cfg.items(), key=lambda kv: kv[1])),
+                    flush=True)
+                continue
             pk, rm = best.get("pk", (0, None)), best.get("rm", (0, None))
             line = (f"{name:5s} m={m:3d}  packed {pk[0]:7.2f} us {str(pk[1]):14s} "
                     f"row-major {rm[0]:7.2f} us {str(rm[1]):14s} hipblaslt {blas:7.2f} us  "

@@ -99,8 +99,11 @@ _M_BUCKETS = (1, 8, 16, 32, 64)
 PACKED_PLAN = {
     # qkv 32 / 64: split-K slabs reduced by slab_rope_kv (the bf16 image is the only
     # copy of the weights, so there is no hipBLASLt fallback)
-    "qkv": {1: (1, -3, 1), 8: (2, -3, 1), 16: (2, -3, 1), 32: (2, -3, 4), 64: (2, -3, 4)},
-    "o": {1: (1, -3, 2), 8: (2, -3, 2), 16: (2, -3, 2), 32: (2, -3, 2), 64: (2, -3, 2)},
+    # 32 / 64 rows: "xc" with 8 splits (x chunk staged once per workgroup in LDS, 384
+    # workgroups): qkv 14.7 vs 18.2 us, o 12.4 vs 13.1 us at 50-64 rows, engine A/B
+    # 8.05 vs 8.22 ms/step (profiles/ab_decode_plan_xc8_r02.log)
+    "qkv": {1: (1, -3, 1), 8: (2, -3, 1), 16: (2, -3, 1), 32: (2, -4, 8), 64: (2, -4, 8)},
+    "o": {1: (1, -3, 2), 8: (2, -3, 2), 16: (2, -3, 2), 32: (2, -3, 2), 64: (2, -4, 8)},
     # gu 64: split-K slabs reduced by slab_silu (engine A/B at 50 rows: 5.47 vs 5.54 ms/step)
     "gu": {1: (1, -3, 1), 8: (1, -3, 1), 16: (4, -3, 1), 32: (4, -3, 1), 64: (2, -4, 2)},
     "down": {1: (1, -3, 2), 8: (2, -3, 4), 16: (4, -3, 4), 32: (4, -3, 4), 64: (4, -3, 4)},
