@@ -18,8 +18,10 @@
 //   * top-p: exact rejection -- a drawn token s is accepted iff the mass of
 //     strictly more likely kept tokens is < top_p * Z (i.e. s is in the
 //     nucleus); accepted draws are distributed exactly as the renormalised
-//     nucleus.  Acceptance >= top_p per round, 8 rounds max, then argmax
-//     (always in the nucleus).  Each round costs one pass.
+//     nucleus.  Acceptance >= top_p per round, 8 rounds max; if all miss
+//     (<= (1 - top_p)^8), the nucleus threshold is found by a 4-ary search on
+//     the key and the draw repeats restricted to it -- exact in every case.
+//     Each round costs one pass.
 //   * RNG: splitmix64(seed, step, round) -> one uniform per round per row, so
 //     sampling is reproducible per (seed, step) and graph-capturable.
 //   * allow-bitmask (1 bit / vocab id) implements the JSON token FSM (E19).
@@ -249,44 +251,48 @@ __global__ __launch_bounds__(kSampThreads) void sample_kernel(
   }
 
   // ---- per-chunk masses of kept tokens (LDS), per-thread totals -------------------------
-  float mass = 0.f;
+  float mass = 0.f, excl = 0.f, Z = 0.f;
+  auto masses = [&](uint32_t th) {
+    mass = 0.f;
 #pragma unroll 8
-  for (int c = 0; c < kChunks; ++c) {
-    uint32_t key[8];
-    load_keys8<T>(x, mrow, chunk_base(c), vocab, key);
-    float cm = 0.f;
+    for (int c = 0; c < kChunks; ++c) {
+      uint32_t key[8];
+      load_keys8<T>(x, mrow, chunk_base(c), vocab, key);
+      float cm = 0.f;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) cm += key[j] >= thr ? exp2f((key_to_f32(key[j]) - M) * cexp) : 0.f;
-    chunk_mass[c * kSampThreads + tid] = cm;
-    mass += cm;
-  }
-  // block exclusive scan of per-thread masses
-  float incl = mass;
+      for (int j = 0; j < 8; ++j) cm += key[j] >= th ? exp2f((key_to_f32(key[j]) - M) * cexp) : 0.f;
+      chunk_mass[c * kSampThreads + tid] = cm;
+      mass += cm;
+    }
+    // block exclusive scan of per-thread masses
+    float incl = mass;
 #pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const float y = __shfl_up(incl, o, 64);
-    if (lane_id() >= o) incl += y;
-  }
-  __syncthreads();
-  if (lane_id() == 63) sh.scan[wave_id()] = incl;
-  __syncthreads();
-  float wbase = 0.f, Z = 0.f;
+    for (int o = 1; o < 64; o <<= 1) {
+      const float y = __shfl_up(incl, o, 64);
+      if (lane_id() >= o) incl += y;
+    }
+    __syncthreads();
+    if (lane_id() == 63) sh.scan[wave_id()] = incl;
+    __syncthreads();
+    float wbase = 0.f;
+    Z = 0.f;
 #pragma unroll
-  for (int w = 0; w < kSampWaves; ++w) {
-    const float t = sh.scan[w];
-    if (w < wave_id()) wbase += t;
-    Z += t;
-  }
-  const float excl = wbase + incl - mass;
+    for (int w = 0; w < kSampWaves; ++w) {
+      const float t = sh.scan[w];
+      if (w < wave_id()) wbase += t;
+      Z += t;
+    }
+    excl = wbase + incl - mass;
+  };
+  masses(thr);
 
   const float tp = top_p[row];
   const uint64_t s0 =
       splitmix64((uint64_t)seeds[row] ^ (0x632BE59BD9B4E019ull * (uint64_t)(steps[row] + 1)));
-  int chosen = besti;
+  int chosen = -1;
   const int rounds = (tp < 1.f) ? 8 : 1;
-  for (int r = 0; r < rounds; ++r) {
-    const uint64_t h = splitmix64(s0 + (uint64_t)r * 0xD1B54A32D192ED03ull);
-    const float u = ((float)(h >> 40) + 0.5f) * (1.0f / 16777216.0f);
+  // inverse CDF over the kept ids (key >= th) whose chunk masses masses(th) left
+  auto draw = [&](uint32_t th, float u) -> int {
     const float target = u * Z;
     __syncthreads();
     if (tid == 0) sh.found = 0;
@@ -319,7 +325,7 @@ __global__ __launch_bounds__(kSampThreads) void sample_kernel(
         load_keys8<T>(x, mrow, chunk_base(cc), vocab, key);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          if (key[j] >= thr) {
+          if (key[j] >= th) {
             const float pj = exp2f((key_to_f32(key[j]) - M) * cexp);
             pick = chunk_base(cc) + j;
             if (acc + pj > target) break;
@@ -330,7 +336,12 @@ __global__ __launch_bounds__(kSampThreads) void sample_kernel(
       if (pick >= 0 && atomicCAS(&sh.found, 0, 1) == 0) sh.winner = pick;
     }
     __syncthreads();
-    const int s = sh.found ? sh.winner : besti;
+    return sh.found ? sh.winner : besti;
+  };
+  for (int r = 0; r < rounds; ++r) {
+    const uint64_t h = splitmix64(s0 + (uint64_t)r * 0xD1B54A32D192ED03ull);
+    const float u = ((float)(h >> 40) + 0.5f) * (1.0f / 16777216.0f);
+    const int s = draw(thr, u);
     if (tp >= 1.f) {
       chosen = s;
       break;
@@ -356,6 +367,40 @@ __global__ __launch_bounds__(kSampThreads) void sample_kernel(
       chosen = s;
       break;
     }
+  }
+  if (chosen < 0) {
+    // every rejection round missed (probability <= (1 - top_p)^8): draw exactly from
+    // the nucleus instead of falling back to the argmax.  Nucleus = kept ids with
+    // key >= t*, t* = the smallest key t whose strictly-more-likely mass
+    // f(t) = mass(key > t) is < top_p * Z; 4-ary search, 3 masses per pass.
+    const float tgt = tp * Z;
+    uint32_t lo = 0u;   // invariant: f(lo) >= tgt (f(0) = Z)
+    for (int shift = 14; shift >= 0; shift -= 2) {
+      const uint32_t t1 = lo + (1u << shift), t2 = lo + (2u << shift), t3 = lo + (3u << shift);
+      float f1 = 0.f, f2 = 0.f, f3 = 0.f;
+#pragma unroll 8
+      for (int c = 0; c < kChunks; ++c) {
+        uint32_t key[8];
+        load_keys8<T>(x, mrow, chunk_base(c), vocab, key);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          if (key[j] >= thr && key[j] > t1) {
+            const float pj = exp2f((key_to_f32(key[j]) - M) * cexp);
+            f1 += pj;
+            f2 += key[j] > t2 ? pj : 0.f;
+            f3 += key[j] > t3 ? pj : 0.f;
+          }
+        }
+      }
+      f1 = block_sum_f(f1, sh);
+      f2 = block_sum_f(f2, sh);
+      f3 = block_sum_f(f3, sh);
+      lo = (f3 >= tgt) ? t3 : (f2 >= tgt) ? t2 : (f1 >= tgt) ? t1 : lo;
+    }
+    const uint32_t tstar = lo + 1u;
+    masses(tstar > thr ? tstar : thr);
+    const uint64_t h = splitmix64(s0 + 8ull * 0xD1B54A32D192ED03ull);
+    chosen = draw(tstar > thr ? tstar : thr, ((float)(h >> 40) + 0.5f) * (1.0f / 16777216.0f));
   }
   if (tid == 0) out_tokens[row] = chosen;
 }

@@ -235,8 +235,20 @@ class Scheduler:
         seqs, ntok, samp, rejected = [], [], [], []
         retried = None
         used = 0
+        # the soft budget is for latency when the backlog is short (one turn of every
+        # session: short new messages); a backlog of more than a full step (many long
+        # prompts at once, e.g. every session re-rendering its history window) runs
+        # full steps instead, for throughput
+        soft = self.prefill_chunk
+        if soft:
+            backlog = 0
+            for w in self.waiting:
+                backlog += w.n_tokens - w.num_computed
+                if backlog > budget:
+                    soft = 0
+                    break
         while self.waiting and budget > 0 and n_decode + len(seqs) < self.max_num_seqs:
-            if seqs and self.prefill_chunk and used >= self.prefill_chunk:
+            if seqs and soft and used >= soft:
                 break
             seq = self.waiting[0]
             if seq.num_computed == 0 and not seq.block_ids:
@@ -249,8 +261,7 @@ class Scheduler:
                         seq.num_committed_blocks = len(hit)
                         seq.num_cached_tokens = seq.num_computed
             remaining = seq.n_tokens - seq.num_computed
-            limit = budget if not seqs or not self.prefill_chunk else \
-                min(budget, self.prefill_chunk - used)
+            limit = budget if not seqs or not soft else min(budget, soft - used)
             chunk = min(remaining, limit)
             need = self._blocks_needed(seq, seq.num_computed + chunk)
             if need and not self.bm.can_allocate(need):

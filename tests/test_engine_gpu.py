@@ -284,22 +284,27 @@ def test_llama3_shape_decode_matches_cpu_fp32(model, rows):
     ref = c.compute_logits(c.forward(ids, meta("cpu"), kv_c)).float()
     mg = meta("cuda", tmp)
     idg = ids.cuda()
-    eager = g.compute_logits(g.forward(idg, mg, kv_g)).float().cpu()
-    s = torch.cuda.Stream()
-    s.wait_stream(torch.cuda.current_stream())
-    with torch.cuda.stream(s):
-        g.compute_logits(g.forward(idg, mg, kv_g))
-    torch.cuda.current_stream().wait_stream(s)
-    graph = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(graph):
-        out = g.compute_logits(g.forward(idg, mg, kv_g))
-    graph.replay()
-    torch.cuda.synchronize()
-    replayed = out.float().cpu()
+    # graph capture under inference mode, like the engine's (ModelRunner._capture): the
+    # CUDA generator's graph-safe state must be of one kind for the whole process
+    with torch.inference_mode():
+        eager = g.compute_logits(g.forward(idg, mg, kv_g)).float().cpu()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            g.compute_logits(g.forward(idg, mg, kv_g))
+        torch.cuda.current_stream().wait_stream(s)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            out = g.compute_logits(g.forward(idg, mg, kv_g))
+        graph.replay()
+        torch.cuda.synchronize()
+        replayed = out.float().cpu()
     for name, a in (("eager", eager), ("graph", replayed)):
         cos = torch.nn.functional.cosine_similarity(a, ref, dim=-1)
         agree = (a.argmax(-1) == ref.argmax(-1)).float().mean().item()
         print(f"{model} rows {rows} {name}: min cos {cos.min().item():.5f} argmax agree {agree:.3f}")
-        assert cos.min().item() > 0.99, (name, cos.min().item())
-        assert agree >= 0.9, (name, agree)
+        # random weights leave near-ties in the logits: cosine is the tight check,
+        # argmax agreement only a coarse one
+        assert cos.min().item() > 0.9995, (name, cos.min().item())
+        assert agree >= 0.8, (name, agree)
     assert torch.equal(eager, replayed)

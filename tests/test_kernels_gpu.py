@@ -259,6 +259,35 @@ def test_sample_distribution():
     assert (emp - expect).abs().max().item() < 0.01
 
 
+def test_sample_topp_distribution_is_exact():
+    """top_p = 0.3 on a flat-tailed distribution: acceptance per rejection round is
+    only ~0.3, so ~6% of rows exhaust the 8 rounds and take the exact nucleus
+    fallback -- the draws must still follow the renormalised nucleus (ADVICE r1:
+    the old argmax fallback biased them towards greedy)."""
+    v = 64
+    base = torch.linspace(2.0, -2.0, v)   # distinct logits (no ties at the nucleus edge)
+    rows = 4096
+    logits = base.to(DEV).repeat(rows, 1)
+    t = torch.ones(rows, device=DEV)
+    p = torch.full((rows,), 0.3, device=DEV)
+    k = torch.zeros(rows, dtype=torch.int32, device=DEV)
+    s = torch.arange(rows, dtype=torch.int64, device=DEV) * 7919 + 3
+    counts = torch.zeros(v)
+    for step in range(8):
+        st = torch.full((rows,), step, dtype=torch.int32, device=DEV)
+        out = ops.sample(logits, t, p, k, s, st).long().cpu()
+        counts += torch.bincount(out, minlength=v).float()
+    probs = torch.softmax(base, -1)
+    order = probs.argsort(descending=True)
+    above = torch.cumsum(probs[order], 0) - probs[order]     # strictly more likely mass
+    nucleus = order[above < 0.3]
+    expect = torch.zeros(v)
+    expect[nucleus] = probs[nucleus] / probs[nucleus].sum()
+    emp = counts / counts.sum()
+    assert counts[[i for i in range(v) if i not in set(nucleus.tolist())]].sum() == 0
+    assert (emp - expect).abs().max().item() < 0.012, (emp[nucleus], expect[nucleus])
+
+
 def test_sample_mask():
     v = 1000
     logits = torch.randn(8, v, device=DEV)
