@@ -235,18 +235,12 @@ class Scheduler:
         seqs, ntok, samp, rejected = [], [], [], []
         retried = None
         used = 0
-        # the soft budget is for latency when the backlog is short (one turn of every
-        # session: short new messages); a backlog of more than a full step (many long
-        # prompts at once, e.g. every session re-rendering its history window) runs
-        # full steps instead, for throughput
+        # the soft budget is for latency when the queue head is short (one turn of
+        # every session: short new messages on a cached history); when the head
+        # itself needs more than the soft budget (a long first prompt, or every
+        # session re-rendering its history window at once) the step is filled to the
+        # hard budget instead, for throughput
         soft = self.prefill_chunk
-        if soft:
-            backlog = 0
-            for w in self.waiting:
-                backlog += w.n_tokens - w.num_computed
-                if backlog > budget:
-                    soft = 0
-                    break
         while self.waiting and budget > 0 and n_decode + len(seqs) < self.max_num_seqs:
             if seqs and soft and used >= soft:
                 break
@@ -261,6 +255,8 @@ class Scheduler:
                         seq.num_committed_blocks = len(hit)
                         seq.num_cached_tokens = seq.num_computed
             remaining = seq.n_tokens - seq.num_computed
+            if not seqs and remaining >= soft:
+                soft = 0
             limit = budget if not seqs or not soft else min(budget, soft - used)
             chunk = min(remaining, limit)
             need = self._blocks_needed(seq, seq.num_computed + chunk)

@@ -153,9 +153,9 @@ def test_soft_prefill_chunk_splits_bursts_not_lone_prompts():
     assert sum(first[1]) <= 32 and first[1][0] == 20     # 20 + a 12-token head of the next
     assert all(sum(pre) <= 32 for _, pre in eng.runner.batches)
     assert eng.bm.num_free() == eng.bm.num_blocks
-    # a backlog beyond one full step (many long prompts at once) runs full steps
+    # a queue headed by a prompt longer than the soft budget runs full steps
     eng.runner.batches.clear()
-    many = [list(range(3000 + 70 * i, 3070 + 70 * i)) for i in range(5)]   # 350 > 256 tokens
+    many = [list(range(3000 + 70 * i, 3070 + 70 * i)) for i in range(5)]   # 70 > 32 tokens each
     outs = eng.generate(many, SamplingParams(temperature=0, max_tokens=2, ignore_eos=True))
     assert outs == [_expected(p, 2) for p in many]
     assert sum(eng.runner.batches[0][1]) == 256
