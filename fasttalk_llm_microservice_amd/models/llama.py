@@ -115,14 +115,17 @@ MAX_SPLITS = 4
 # split-K) per projection from bench/pg_probe.py on MI355X vs hipBLASLt on row-major
 # weights (profiles/packed_gemm_*_r02.log): split-K fills the chip at mixed-step
 # sizes (80-256 rows: 0.8-1.7x hipBLASLt), whole tiles above.
+# Up to 2047 rows (the soft prefill chunk of 1024 tokens + decode rows lands at
+# ~1.1k) the M = 1024 measurements rule: split-K keeps o / down at 512 workgroups
+# (whole tiles there: 80 workgroups on 256 CUs, 2-3x slower).
 PG_PLAN = {
-    "qkv": ((128, 1, 8), (256, 2, 4), (512, 2, 2), (1 << 30, 2, 1)),
-    "o": ((128, 2, 8), (256, 1, 8), (512, 2, 4), (1024, 2, 2), (1 << 30, 0, 1)),
+    "qkv": ((128, 1, 8), (256, 2, 4), (512, 2, 2), (2047, 0, 2), (1 << 30, 2, 1)),
+    "o": ((128, 2, 8), (256, 1, 8), (512, 2, 4), (2047, 1, 2), (1 << 30, 0, 1)),
     "gu": ((128, 1, 2), (256, 2, 1), (1 << 30, 0, 1)),
-    "down": ((128, 1, 16), (256, 1, 8), (512, 0, 8), (1024, 0, 4), (1 << 30, 3, 1)),
+    "down": ((128, 1, 16), (256, 1, 8), (512, 0, 8), (2047, 0, 4), (1 << 30, 3, 1)),
     "lm": ((128, 1, 1), (256, 3, 1), (1 << 30, 0, 1)),
 }
-PG_MAX_SLAB_ROWS = 1024
+PG_MAX_SLAB_ROWS = 2048
 # At prefill-burst sizes hipBLASLt's tiles beat packed_gemm (1.35-1.66 vs 1.1-1.2
 # PF/s at M = 4096, profiles/packed_gemm_*_r02.log) by more than it costs to unpack
 # the layer's weight into a transient row-major copy (one read + one write of the
