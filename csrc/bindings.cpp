@@ -23,7 +23,7 @@ int ft_paged_decode_attention(void* out, int out_stride, float* tmp_out, float* 
                               const void* q, int q_stride, const void* k_cache,
                               const void* v_cache, const int* block_tables, int bt_stride,
                               const int* seq_lens, int batch, int nq, int nkv, int head_dim,
-                              int block_size, float scale, hipStream_t stream);
+                              int block_size, float scale, int* counters, hipStream_t stream);
 int ft_prefill_tile_tokens(int nq, int nkv);
 int ft_prefill_attention(void* out, int out_stride, const void* q, int q_stride,
                          const void* k_cache, const void* v_cache, const int* block_tables,
@@ -186,7 +186,7 @@ void rope_kv_write(at::Tensor qkv, at::Tensor positions, at::Tensor cos_sin,
 void paged_decode_attention(at::Tensor out, at::Tensor q, at::Tensor k_cache, at::Tensor v_cache,
                             at::Tensor block_tables, at::Tensor seq_lens, at::Tensor tmp_out,
                             at::Tensor tmp_ml, int64_t nq, int64_t nkv, int64_t head_dim,
-                            double scale) {
+                            double scale, c10::optional<at::Tensor> counters) {
   check_bf16(out, "out");
   check_bf16(q, "q");
   check_rows(out, "out");
@@ -206,12 +206,18 @@ void paged_decode_attention(at::Tensor out, at::Tensor q, at::Tensor k_cache, at
   TORCH_CHECK(tmp_out.numel() >= slots * (nq / nkv) * head_dim &&
                   tmp_ml.numel() >= slots * (nq / nkv) * 2,
               "decode workspace too small (ops.decode_workspace)");
+  int* cnt = nullptr;
+  if (counters.has_value()) {  // fused combine: zeroed int32 [>= batch * nkv], left zeroed
+    check_i32(*counters, "counters");
+    TORCH_CHECK(counters->numel() >= (int64_t)batch * nkv, "decode counters too small");
+    cnt = counters->data_ptr<int>();
+  }
   check_rc(ft_paged_decode_attention(out.data_ptr(), (int)out.stride(0), tmp_out.data_ptr<float>(),
                                      tmp_ml.data_ptr<float>(), q.data_ptr(), (int)q.stride(0),
                                      k_cache.data_ptr(), v_cache.data_ptr(),
                                      block_tables.data_ptr<int>(), (int)block_tables.stride(0),
                                      seq_lens.data_ptr<int>(), batch, (int)nq, (int)nkv,
-                                     (int)head_dim, (int)k_cache.size(2), (float)scale,
+                                     (int)head_dim, (int)k_cache.size(2), (float)scale, cnt,
                                      cur_stream()),
            "paged_decode_attention");
 }

@@ -28,7 +28,17 @@
 //   (R-1 tiles in flight while one computes).  A segment that one wave covers
 //   whole is written as bf16 at once; pieces of shared segments leave fp32
 //   (acc, m, l) partials at slot = segment + wave (collision-free: consecutive
-//   segments share at most one wave) for paged_decode_combine.
+//   segments share at most one wave).
+// * Combine in the same launch (counters != null): a wave that leaves a partial
+//   stores it write-through (agent-scope atomic stores = sc1), drains its stores
+//   and counts itself in the segment's counter; the wave that draws the last
+//   ticket merges the segment's partials (sc1 loads) into bf16 and resets the
+//   counter for the next call.  This is the guide's sc1 hand-off (§6 Guideline
+//   16): no fences, correct for any wave -> XCD placement.  Measured at 50
+//   sessions it LOSES to the separate paged_decode_combine kernel (12.3 vs 10.9 ms
+//   per decode step: the last arriver's sc1 loads of the partials are serial
+//   memory round trips), so the engine launches the combine kernel unless
+//   FT_DECODE_FUSED_COMBINE=1.
 #include "ft_common.h"
 
 #include <stdlib.h>
@@ -93,7 +103,7 @@ __global__ __launch_bounds__(256, R == 2 ? 3 : 2) void paged_decode_kernel(
     float* __restrict__ tmp_ml, const uint16_t* __restrict__ q, int q_stride,
     const uint16_t* __restrict__ k_cache, const uint16_t* __restrict__ v_cache,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ seq_lens,
-    int batch, int nkv, int bs_shift, float scale_log2) {
+    int batch, int nkv, int bs_shift, float scale_log2, int* __restrict__ counters) {
   static_assert(G >= 1 && G <= 16, "GQA group must fit the 16 MFMA columns");
   constexpr int KC = D / 32, ND = D / 16;
   __shared__ int s_pre[kDecMaxBatch + 1];
@@ -102,6 +112,17 @@ __global__ __launch_bounds__(256, R == 2 ? 3 : 2) void paged_decode_kernel(
   const int total = nkv * s_pre[batch];
   const int nw = dec_num_waves(total, gridDim.x * 4);
   const int w = wave_id() * gridDim.x + blockIdx.x;  // spreads low wave ids over CUs
+  if (counters != nullptr && blockIdx.x == 0) {
+    // fused-combine mode has no combine kernel to define empty sequences' outputs
+    // (the padded rows of a decode graph bucket): one thread per empty segment
+    for (int seg = threadIdx.x; seg < batch * nkv; seg += blockDim.x) {
+      const int b = seg / nkv;
+      if (s_pre[b + 1] == s_pre[b]) {
+        uint4* o = reinterpret_cast<uint4*>(out + (size_t)b * out_stride + (seg - b * nkv) * G * D);
+        for (int i = 0; i < G * D / 8; ++i) o[i] = make_uint4(0u, 0u, 0u, 0u);
+      }
+    }
+  }
   if (total == 0 || w >= nw) return;
   int f = (int)(((long long)w * total) / nw);
   const int f1 = (int)(((long long)(w + 1) * total) / nw);
@@ -243,12 +264,62 @@ __global__ __launch_bounds__(256, R == 2 ? 3 : 2) void paged_decode_kernel(
         const float mr = __shfl(m_run, r & 15, 64);
         if (r < G) {
           float* dst = tmp_out + (slot * G + r) * D + n;
+          if (counters != nullptr) {   // write-through: read by another wave in this launch
 #pragma unroll
-          for (int nd = 0; nd < ND; ++nd) dst[nd * 16] = o[nd][i4];
-          if (n == 0) {
-            tmp_ml[(slot * G + r) * 2] = mr;
-            tmp_ml[(slot * G + r) * 2 + 1] = lr;
+            for (int nd = 0; nd < ND; ++nd)
+              __hip_atomic_store(dst + nd * 16, o[nd][i4], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (n == 0) {
+              __hip_atomic_store(tmp_ml + (slot * G + r) * 2, mr, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+              __hip_atomic_store(tmp_ml + (slot * G + r) * 2 + 1, lr, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+            }
+          } else {
+#pragma unroll
+            for (int nd = 0; nd < ND; ++nd) dst[nd * 16] = o[nd][i4];
+            if (n == 0) {
+              tmp_ml[(slot * G + r) * 2] = mr;
+              tmp_ml[(slot * G + r) * 2 + 1] = lr;
+            }
           }
+        }
+      }
+      if (counters != nullptr) {
+        // publish (every partial store of this wave retired), then take a ticket
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        int prev = 0;
+        if (lane == 0)
+          prev = __hip_atomic_fetch_add(counters + seg, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        prev = __shfl(prev, 0, 64);
+        // waves sharing the segment: the first and last whose tile range meets it
+        const int S = nkv * s_pre[b] + h * nb, E = S + nb;
+        const int wf = (int)(((long long)(S + 1) * nw - 1) / total);
+        const int wl = (int)(((long long)E * nw - 1) / total);
+        const int np = wl - wf + 1;
+        if (prev == np - 1) {   // last arriver: merge the np partials of this segment
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keep the loads below the ticket
+          const size_t base = (size_t)(seg + wf);
+          uint16_t* op = out + (size_t)b * out_stride + h * G * D;
+          for (int i = lane; i < G * D; i += 64) {
+            const int r = i / D, d = i - r * D;
+            float M = -INFINITY;
+            for (int k = 0; k < np; ++k)
+              M = fmaxf(M, __hip_atomic_load(tmp_ml + ((base + k) * G + r) * 2, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT));
+            float den = 0.f, acc = 0.f;
+            for (int k = 0; k < np; ++k) {
+              const size_t sl = (base + k) * G + r;
+              const float e = exp2f(__hip_atomic_load(tmp_ml + sl * 2, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT) - M);
+              den += e * __hip_atomic_load(tmp_ml + sl * 2 + 1, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+              acc += e * __hip_atomic_load(tmp_out + sl * D + d, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+            }
+            op[i] = f32_to_bf16(acc / den);
+          }
+          if (lane == 0)
+            __hip_atomic_store(counters + seg, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
       }
     }
@@ -343,7 +414,7 @@ extern "C" int ft_paged_decode_attention(void* out, int out_stride, float* tmp_o
                                          const void* v_cache, const int* block_tables,
                                          int bt_stride, const int* seq_lens, int batch, int nq,
                                          int nkv, int head_dim, int block_size, float scale,
-                                         hipStream_t stream) {
+                                         int* counters, hipStream_t stream) {
   if (batch <= 0) return 0;
   if (nq % nkv != 0) return -1;
   if (batch > ft::kDecMaxBatch) return -5;
@@ -365,10 +436,12 @@ extern "C" int ft_paged_decode_attention(void* out, int out_stride, float* tmp_o
     hipLaunchKernelGGL((ft::paged_decode_kernel<DD, GG, RR>), dim3(nwg), dim3(256), 0, stream, \
                        (uint16_t*)out, out_stride, tmp_out, tmp_ml, (const uint16_t*)q,          \
                        q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache,             \
-                       block_tables, bt_stride, seq_lens, batch, nkv, bs_shift, scale_log2);     \
-    hipLaunchKernelGGL((ft::paged_decode_combine_kernel<DD, GG>), dim3(batch * nkv), dim3(256),  \
-                       0, stream, (uint16_t*)out, out_stride, tmp_out, tmp_ml, seq_lens, batch,  \
-                       nkv, nwg * 4);                                                            \
+                       block_tables, bt_stride, seq_lens, batch, nkv, bs_shift, scale_log2,      \
+                       counters);                                                                \
+    if (counters == nullptr)                                                                     \
+      hipLaunchKernelGGL((ft::paged_decode_combine_kernel<DD, GG>), dim3(batch * nkv), dim3(256),\
+                         0, stream, (uint16_t*)out, out_stride, tmp_out, tmp_ml, seq_lens, batch,\
+                         nkv, nwg * 4);                                                          \
     return static_cast<int>(hipGetLastError());                                                  \
   }
   if (ring == 2) { FT_DEC_CASE(128, 4, 2) }

@@ -156,6 +156,11 @@ class ModelRunner:
                                            waves=None if self.is_gpu else 0)
         self.tmp_out = torch.empty(max(1, n_out), dtype=torch.float32, device=dv)
         self.tmp_ml = torch.empty(max(1, n_ml), dtype=torch.float32, device=dv)
+        # in-launch combine tickets, opt-in (FT_DECODE_FUSED_COMBINE=1): measured slower
+        # than the separate combine kernel at 50 sessions (12.3 vs 10.9 ms/step: the last
+        # arriver's write-through (sc1) partial loads are latency-bound), kept for A/B
+        self.dec_counters = ops.decode_counters(self.max_decode_rows, self.model.nkv, dv) \
+            if self.is_gpu and os.environ.get("FT_DECODE_FUSED_COMBINE", "0") == "1" else None
         self._done_event = torch.cuda.Event() if self.is_gpu else None
         self.graphs: Dict[int, torch.cuda.CUDAGraph] = {}
         self.graph_pool = None
@@ -349,6 +354,7 @@ class ModelRunner:
             meta.dec_block_tables = t(host["d_bt"])
             meta.dec_seq_lens = t(host["d_sl"])
             meta.tmp_out, meta.tmp_ml = self.tmp_out, self.tmp_ml
+            meta.dec_counters = self.dec_counters
         input_ids = t(host["ids"])
         h = self.model.forward(input_ids, meta, self.kv)
         if len(host["lrows"]) == 0:
@@ -580,7 +586,7 @@ class ModelRunner:
         return AttnMeta(positions=self.d_positions[:nb], slot_mapping=self.d_slots[:nb],
                         logits_indices=self.d_logits_idx[:nb], num_decode=nb,
                         dec_block_tables=self.d_bt[:nb], dec_seq_lens=self.d_seq_lens[:nb],
-                        tmp_out=self.tmp_out, tmp_ml=self.tmp_ml)
+                        tmp_out=self.tmp_out, tmp_ml=self.tmp_ml, dec_counters=self.dec_counters)
 
     def _graph_body(self, nb: int):
         meta = self._decode_meta(nb)

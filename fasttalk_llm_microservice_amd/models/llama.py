@@ -44,6 +44,7 @@ class AttnMeta:
     dec_seq_lens: Optional[torch.Tensor] = None       # [num_decode]
     tmp_out: Optional[torch.Tensor] = None            # decode partials (ops.decode_workspace)
     tmp_ml: Optional[torch.Tensor] = None
+    dec_counters: Optional[torch.Tensor] = None       # in-launch combine tickets (ops.decode_counters)
     # prefill rows
     block_tables: Optional[torch.Tensor] = None       # [P, max_blocks]
     seq_lens: Optional[torch.Tensor] = None           # [P] kv length after this step
@@ -633,7 +634,7 @@ class LlamaModel:
         if nd > 0:
             ops.decode_attention(attn[:nd], qkv[:nd], kc, vc, meta.dec_block_tables,
                                  meta.dec_seq_lens, meta.tmp_out, meta.tmp_ml, nq, nkv, d,
-                                 self.scale)
+                                 self.scale, counters=meta.dec_counters)
         if t > nd:
             ops.prefill_attention(attn[nd:], qkv[nd:], kc, vc, meta.block_tables, meta.seq_lens,
                                   meta.q_start_loc, meta.tile_info, meta.num_tiles, nq, nkv, d,

@@ -135,13 +135,21 @@ def prefill_tile_tokens(nq: int, nkv: int) -> int:
     return 256 // (nq // nkv)
 
 
+def decode_counters(batch: int, nkv: int, device) -> torch.Tensor:
+    """Zeroed int32 tickets of the decode kernel's in-launch combine (one per
+    sequence x kv head; the kernel leaves them zeroed)."""
+    return torch.zeros(max(1, batch * nkv), dtype=torch.int32, device=device)
+
+
 def decode_attention(out, q, k_cache, v_cache, block_tables, seq_lens, tmp_out, tmp_ml, nq, nkv,
-                     head_dim, scale):
+                     head_dim, scale, counters: Optional[torch.Tensor] = None):
     """out[b] = attention of the single new query of sequence b (q: [B, >=nq*D] rows).
-    k_cache [blocks, nkv, bs, D]; v_cache [blocks, nkv, D, bs] (transposed blocks)."""
+    k_cache [blocks, nkv, bs, D]; v_cache [blocks, nkv, D, bs] (transposed blocks).
+    ``counters`` (decode_counters): merge shared segments inside the launch instead
+    of a second combine kernel."""
     if q.is_cuda:
         native().paged_decode_attention(out, q, k_cache, v_cache, block_tables, seq_lens, tmp_out,
-                                        tmp_ml, nq, nkv, head_dim, scale)
+                                        tmp_ml, nq, nkv, head_dim, scale, counters)
         return out
     b = q.shape[0]
     qq = q[:, : nq * head_dim].reshape(b, nq, head_dim)

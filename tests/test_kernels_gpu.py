@@ -92,7 +92,7 @@ def _random_tables(lens, bs, nblocks_total):
     return bt
 
 
-def _decode_case(lens, nq, nkv, d, bs=16, seed=0):
+def _decode_case(lens, nq, nkv, d, bs=16, seed=0, fused=True, calls=1):
     torch.manual_seed(seed)
     nblocks = sum((l + bs - 1) // bs for l in lens) + 4
     k, v = _alloc_cache(nblocks, nkv, bs, d)
@@ -105,7 +105,15 @@ def _decode_case(lens, nq, nkv, d, bs=16, seed=0):
     tmp_ml = torch.full((n_ml,), float("nan"), device=DEV)
     out = torch.full((b, nq * d), float("nan"), device=DEV).bfloat16()
     scale = d ** -0.5
-    ops.decode_attention(out, q, k, v, bt, sl, tmp_out, tmp_ml, nq, nkv, d, scale)
+    cnt = ops.decode_counters(b, nkv, DEV) if fused else None
+    for _ in range(calls):
+        first = out.clone()
+        ops.decode_attention(out, q, k, v, bt, sl, tmp_out, tmp_ml, nq, nkv, d, scale, counters=cnt)
+    if calls > 1:   # the in-launch combine's tickets reset: repeat calls agree bit for bit
+        assert torch.equal(first, out)
+    if cnt is not None:
+        torch.cuda.synchronize()
+        assert int(cnt.abs().sum()) == 0, "combine tickets must be left zeroed"
     expect = ref.paged_attention(q.view(b, nq, d), k, v, bt, sl,
                                  torch.arange(b + 1, dtype=torch.int32), scale).view(b, nq * d)
     return out, expect
@@ -113,9 +121,12 @@ def _decode_case(lens, nq, nkv, d, bs=16, seed=0):
 
 @pytest.mark.parametrize("nq,nkv,d", [(32, 8, 128), (64, 8, 128), (8, 8, 128), (24, 8, 128),
                                       (32, 8, 64), (8, 1, 128), (16, 8, 128)])
-def test_decode_attention(nq, nkv, d):
-    # lengths around tile / block edges; one long sequence spreads over many waves
-    out, expect = _decode_case([1, 17, 255, 256, 257, 1000, 2100], nq, nkv, d)
+@pytest.mark.parametrize("fused", [True, False])
+def test_decode_attention(nq, nkv, d, fused):
+    # lengths around tile / block edges; one long sequence spreads over many waves;
+    # fused = segments shared by several waves merged inside the launch (tickets)
+    out, expect = _decode_case([1, 17, 255, 256, 257, 1000, 2100], nq, nkv, d, fused=fused,
+                               calls=3)
     _close(out, expect, atol=2e-2, rtol=2e-2, msg="decode attention")
 
 
@@ -125,7 +136,7 @@ def test_decode_attention_serving_shapes(b, max_len):
     g = torch.Generator().manual_seed(b)
     lens = torch.randint(max(1, max_len // 4), max_len + 1, (b,), generator=g).tolist()
     lens[0] = max_len
-    out, expect = _decode_case(lens, 32, 8, 128, seed=b)
+    out, expect = _decode_case(lens, 32, 8, 128, seed=b, calls=2)
     assert torch.isfinite(out.float()).all()
     _close(out, expect, atol=2e-2, rtol=2e-2, msg=f"decode attention b={b}")
 
