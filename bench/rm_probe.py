@@ -53,19 +53,25 @@ def main():
             best = {}
             per_cfg = {}
             for nt, u, sp in configs:
-                kq = 512 if u == -4 else 64
+                kq = {-4: 512, -5: 512 if nt == 2 else 256, -6: 512}.get(u, 64)
                 if n % (16 * nt) or k % (kq * sp) or (u == -4 and n % 64):
                     continue
-                for rm in ((False,) if a.packed_only else (False, True)):
+                if u == -6 and (sp != 1 or nt != 2 or name != "gu"):
+                    continue
+                for rm in ((False,) if a.packed_only or u <= -5 else (False, True)):
                     uu = u - 10 if rm else u
                     imgs = ws_rm if rm else ws_pk
-                    out = torch.empty(m, n, device="cuda").bfloat16()
+                    out = torch.empty(m, n // 2 if u == -6 else n, device="cuda").bfloat16()
 
                     def run(i):
                         ops.native().skinny_gemm(x, imgs[i % copies], out, ws, sp, nt, uu)
                     if sp == 1:
                         run(0)
-                        err = (out.float() - ref).abs().max().item()
+                        r = ref
+                        if u == -6:  # gate/up interleaved in 16-column groups -> silu(g) * u
+                            r4 = ref.view(m, n // 32, 2, 16)
+                            r = (F.silu(r4[:, :, 0]) * r4[:, :, 1]).reshape(m, n // 2)
+                        err = (out.float() - r).abs().max().item()
                         if err > 0.05:
                             print(f"  !! {name} m={m} nt={nt} u={uu} err {err}", flush=True)
                     for i in range(5):

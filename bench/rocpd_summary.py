@@ -56,6 +56,27 @@ def busy(db: str, last_ms: float = 0.0) -> str:
             f"{sum(g for g in gaps if g > 50e3) / 1e6:.2f} ms")
 
 
+def gaps_by_kernel(db: str, last_ms: float, top: int = 15) -> str:
+    """Idle time before each kernel (previous kernel's end -> this start) over
+    the last ``last_ms`` ms, summed per kernel name: where a step's gaps sit."""
+    c = sqlite3.connect(db)
+    rows = sorted(c.execute("select start, end, name from kernels").fetchall())
+    t1 = max(e for _, e, _ in rows)
+    t0 = t1 - last_ms * 1e6
+    agg, prev_e = {}, None
+    for s, e, n in rows:
+        if prev_e is not None and s >= t0:
+            g = max(0, s - prev_e)
+            a = agg.setdefault(n[:90], [0, 0])
+            a[0] += g
+            a[1] += 1
+        prev_e = e if prev_e is None else max(prev_e, e)
+    out = [f"{'gap_us':>10} {'n':>6} {'avg':>7}  next kernel"]
+    for n, (g, k) in sorted(agg.items(), key=lambda kv: -kv[1][0])[:top]:
+        out.append(f"{g / 1e3:10.0f} {k:6d} {g / 1e3 / k:7.2f}  {n}")
+    return "\n".join(out)
+
+
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("db")
@@ -67,3 +88,5 @@ if __name__ == "__main__":
     print(summarize(a.db, a.top, a.per_step))
     if a.busy_last_ms >= 0:
         print(busy(a.db, a.busy_last_ms))
+        if a.busy_last_ms > 0:
+            print(gaps_by_kernel(a.db, a.busy_last_ms))

@@ -59,6 +59,8 @@ int ft_ar_allgather(void* out, const void* x, long rows, long row_elems, const u
 int ft_ar_export_error(int* dst, const uint64_t* peers_dev, int world, hipStream_t stream);
 int ft_skinny_gemm_pk(const void* x, int x_stride, int M, const void* wpk, int N, int K, float* ws,
                       void* out, int out_stride, int splits, int nt, hipStream_t stream);
+int ft_skinny_gemm_xr(const void* x, int x_stride, int M, const void* w, int N, int K, float* ws,
+                      void* out, int out_stride, int splits, int nt, int silu, hipStream_t stream);
 int ft_packed_gemm(const void* x, int x_stride, int M, const void* wpk, int N, int K, int splits,
                    int epi, int cfg, void* out, int out_stride, float* ws, hipStream_t stream);
 int ft_unpack_weight(void* out, const void* wpk, int N, int K, hipStream_t stream);
@@ -375,9 +377,13 @@ void skinny_gemm(at::Tensor x, at::Tensor w, c10::optional<at::Tensor> out,
   TORCH_CHECK(w.dim() == 2 && w.is_contiguous(), "w must be the packed [N, K] image");
   const int M = (int)x.size(0), K = (int)x.size(1), N = (int)w.size(0);
   TORCH_CHECK(w.size(1) == K, "K mismatch");
-  TORCH_CHECK(M <= (u == -4 ? 128 : 64), "skinny_gemm supports M <= 64 (pk) / 128 (xc)");
+  TORCH_CHECK(M <= (u == -4 ? 128 : 64), "skinny_gemm supports M <= 64 (pk, xr) / 128 (xc)");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0, "w alignment");
-  TORCH_CHECK(u == -3 || u == -4, "skinny_gemm variant: -3 (pk) or -4 (xc), packed weights");
+  TORCH_CHECK(u >= -6 && u <= -3,
+              "skinny_gemm variant: -3 (pk), -4 (xc), -5 (xr), -6 (xr + SiLU), packed weights");
+  const bool silu = u == -6;
+  TORCH_CHECK(!silu || (splits == 1 && nt == 2 && N % 32 == 0),
+              "xr SiLU epilogue: one split, nt 2, interleaved gate_up image");
   float* wsp = nullptr;
   void* op = nullptr;
   int ostride = 0;
@@ -388,12 +394,17 @@ void skinny_gemm(at::Tensor x, at::Tensor w, c10::optional<at::Tensor> out,
   } else {
     TORCH_CHECK(out.has_value(), "splits == 1 needs out");
     check_bf16(*out, "out");
-    TORCH_CHECK(out->dim() == 2 && out->stride(1) == 1 && out->size(0) >= M && out->size(1) >= N,
+    TORCH_CHECK(out->dim() == 2 && out->stride(1) == 1 && out->size(0) >= M &&
+                    out->size(1) >= (silu ? N / 2 : N),
                 "out shape");
     op = out->data_ptr();
     ostride = (int)out->stride(0);
   }
-  if (u == -3)  // w is the packed [N/16][K/64][2][64][8] image (ops.pack_weight)
+  if (u <= -5)
+    check_rc(ft_skinny_gemm_xr(x.data_ptr(), (int)x.stride(0), M, w.data_ptr(), N, K, wsp, op,
+                               ostride, (int)splits, (int)nt, silu ? 1 : 0, cur_stream()),
+             "skinny_gemm_xr");
+  else if (u == -3)  // w is the packed [N/16][K/64][2][64][8] image (ops.pack_weight)
     check_rc(ft_skinny_gemm_pk(x.data_ptr(), (int)x.stride(0), M, w.data_ptr(), N, K, wsp, op,
                                ostride, (int)splits, (int)nt, cur_stream()),
              "skinny_gemm_pk");

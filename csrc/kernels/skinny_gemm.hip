@@ -21,6 +21,8 @@
 // over the packed image (profiles/pkd_sweep_r02.log: 5-20 % slower than pk/xc).
 #include "ft_common.h"
 
+#include <type_traits>
+
 namespace ft {
 
 typedef __bf16 sk_bf16x8 __attribute__((ext_vector_type(8)));
@@ -37,6 +39,10 @@ __device__ __forceinline__ sk_bf16x8 sk_frag(const uint4& v) {
 __device__ __forceinline__ uint4 nt_load16(const uint16_t* p) {
   const sk_u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const sk_u32x4*>(p));
   return __builtin_bit_cast(uint4, v);
+}
+
+__device__ __forceinline__ sk_u32x4 nt_load16v(const uint16_t* p) {
+  return __builtin_nontemporal_load(reinterpret_cast<const sk_u32x4*>(p));
 }
 
 // ---------------------------------------------------------------------------
@@ -154,6 +160,161 @@ __global__ __launch_bounds__(256) void skinny_xc_kernel(
     __syncthreads();
   }
   if (!active) return;
+  float* slab = ws + (size_t)s * M * N;
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = 16 * i + g * 4 + r;
+      if (m < M) {
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          const int n = n0 + 16 * j + l15;
+          if (gridDim.y == 1)
+            out[(size_t)m * out_stride + n] = f32_to_bf16(acc[i][j][r]);
+          else
+            slab[(size_t)m * N + n] = acc[i][j][r];
+        }
+      }
+    }
+}
+
+
+// ---------------------------------------------------------------------------
+// Variant "xr" (x chunks in LDS, weight RING across chunks): "xc" with the
+// chunk loop software-pipelined.  Measured (bench/xc_diag.py, 50 rows, cold):
+// xc drains its weight stream at every 512-wide chunk -- the next chunk's
+// loads are issued only after this chunk's MFMAs -- so a multi-chunk K slice
+// (gate_up without split-K: 8 chunks) ran at 3.5 TB/s against 6 TB/s for its
+// bare loads, which is why gate_up needed split-K slabs (+14.7 MB of fp32
+// written and re-read by slab_silu).  Here each k-step's weight registers are
+// refilled with the NEXT chunk's fragment right after their MFMAs, so every
+// wave keeps KS k-steps (NT * 16 KiB) in flight without extra registers, and x
+// is double-buffered in LDS (one barrier per chunk).  SILU: the gate_up image
+// is interleaved in 16-column groups (interleave_gate_up(w, 1)), so with NT = 2
+// a wave holds a gate tile and its up tile and writes h = silu(g) * u (bf16,
+// N/2 columns) itself -- no slabs, no slab_silu launch.
+template <int MT, int NT, int KC, bool SILU>
+__global__ __launch_bounds__(256, 1) void skinny_xr_kernel(
+    const uint16_t* __restrict__ x, int x_stride, int M, const uint16_t* __restrict__ w, int K,
+    float* __restrict__ ws, uint16_t* __restrict__ out, int out_stride, int N, int k_slice) {
+  constexpr int KS = KC / 64;
+  constexpr int ROWS = 16 * MT;
+  constexpr int CPR = KC / 8;
+  constexpr int XL = ROWS * CPR / 256;
+  static_assert(XL >= 1 && (ROWS * CPR) % 256 == 0, "x chunk must tile the workgroup");
+  static_assert(!SILU || NT == 2, "the SiLU epilogue pairs a gate tile with its up tile");
+  __shared__ __attribute__((aligned(16))) uint16_t s_x[2][ROWS * KC];
+  const int tid = threadIdx.x;
+  const int lane = lane_id(), wave = wave_id();
+  const int l15 = lane & 15, g = lane >> 4;
+  const int n0 = (blockIdx.x * 4 + wave) * (16 * NT);
+  const int s = blockIdx.y;
+  const int kbeg = s * k_slice;
+  const int nch = k_slice / KC;
+  const bool active = n0 < N;
+
+  const uint16_t* wp[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j)
+    wp[j] = w + ((size_t)(min(n0 + 16 * j, N - 16) / 16) * (K >> 6) + (kbeg >> 6)) * 1024 + lane * 8;
+  // this thread's x elements: row e / CPR, 16-B chunk e % CPR of each chunk, e = tid + 256 p
+  const uint16_t* xsrc[XL];
+#pragma unroll
+  for (int p = 0; p < XL; ++p) {
+    const int e = tid + 256 * p;
+    xsrc[p] = x + (size_t)min(e / CPR, M - 1) * x_stride + kbeg + (e % CPR) * 8;
+  }
+
+  sk_floatx4 acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = sk_floatx4{0.f, 0.f, 0.f, 0.f};
+
+  // native vector registers (the HIP uint4 struct defeats register promotion of
+  // arrays that stay live across the chunk loop: they went to scratch)
+  sk_u32x4 xr[XL];
+  sk_u32x4 wr[KS][NT][2];
+#pragma unroll
+  for (int p = 0; p < XL; ++p) xr[p] = *reinterpret_cast<const sk_u32x4*>(xsrc[p]);
+#pragma unroll
+  for (int st = 0; st < KS; ++st)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      wr[st][j][0] = nt_load16v(wp[j] + (size_t)st * 1024);
+      wr[st][j][1] = nt_load16v(wp[j] + (size_t)st * 1024 + 512);
+    }
+  // one chunk: x regs -> LDS buffer c&1, next chunk's x loads, barrier, MFMAs with
+  // each k-step's weight registers refilled from chunk c+1 right after use.
+  // MORE is a template constant (the last chunk is peeled) so the loop body is
+  // branch-free: with conditional loads the waitcnt pass drained vmcnt(0) at
+  // every chunk, which is the bubble this variant exists to remove.  Waves past
+  // N (clamped weight pointers) compute and discard.
+  auto chunk = [&](int c, auto more_tag) {
+    constexpr bool MORE = decltype(more_tag)::value;
+    uint16_t* sx = s_x[c & 1];
+#pragma unroll
+    for (int p = 0; p < XL; ++p) {
+      const int e = tid + 256 * p;
+      const int row = e / CPR, ch = e % CPR;
+      const int slot = (ch & ~7) | ((ch & 7) ^ (row & 7));
+      *reinterpret_cast<sk_u32x4*>(&sx[row * KC + slot * 8]) = xr[p];
+    }
+    if constexpr (MORE) {
+#pragma unroll
+      for (int p = 0; p < XL; ++p) xr[p] = *reinterpret_cast<const sk_u32x4*>(xsrc[p] + (c + 1) * KC);
+    }
+    __syncthreads();   // chunk c visible; every wave is past chunk c-1's reads of the other buffer
+    const size_t nxt = (size_t)(c + 1) * KS * 1024;
+#pragma unroll
+    for (int st = 0; st < KS; ++st) {
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        const int row = 16 * i + l15;
+        sk_u32x4 xf[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int ch = st * 8 + 2 * g + h;
+          const int slot = (ch & ~7) | ((ch & 7) ^ (row & 7));
+          xf[h] = *reinterpret_cast<const sk_u32x4*>(&sx[row * KC + slot * 8]);
+        }
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              __builtin_bit_cast(sk_bf16x8, xf[0]), __builtin_bit_cast(sk_bf16x8, wr[st][j][0]),
+              acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              __builtin_bit_cast(sk_bf16x8, xf[1]), __builtin_bit_cast(sk_bf16x8, wr[st][j][1]),
+              acc[i][j], 0, 0, 0);
+        }
+      }
+      if constexpr (MORE) {   // refill this k-step's registers with the next chunk's fragments
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          wr[st][j][0] = nt_load16v(wp[j] + nxt + (size_t)st * 1024);
+          wr[st][j][1] = nt_load16v(wp[j] + nxt + (size_t)st * 1024 + 512);
+        }
+      }
+    }
+  };
+  for (int c = 0; c + 1 < nch; ++c) chunk(c, std::true_type{});
+  chunk(nch - 1, std::false_type{});
+  if (!active) return;
+  if constexpr (SILU) {
+    const int col = (n0 >> 1) + l15;   // 16-column gate group n0/32 -> h columns
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = 16 * i + g * 4 + r;
+        if (m < M) {
+          const float gt = acc[i][0][r], up = acc[i][1][r];
+          out[(size_t)m * out_stride + col] = f32_to_bf16(gt / (1.f + __expf(-gt)) * up);
+        }
+      }
+    return;
+  }
   float* slab = ws + (size_t)s * M * N;
 #pragma unroll
   for (int i = 0; i < MT; ++i)
@@ -307,6 +468,41 @@ extern "C" int ft_skinny_gemm_xc(const void* x, int x_stride, int M, const void*
   FT_XC_NT(2)
 #undef FT_XC_NT
 #undef FT_XC
+  return -5;
+}
+
+// Ring-pipelined x-chunk variant.  Requirements (checked): M <= 64,
+// N % (16*nt) == 0, K % (kc*splits) == 0 with kc = 512 (nt 2) / 256 (nt 1; two
+// 64-column workgroups per CU); silu: nt == 2, splits == 1, out = [M, N/2].
+extern "C" int ft_skinny_gemm_xr(const void* x, int x_stride, int M, const void* w, int N, int K,
+                                 float* ws, void* out, int out_stride, int splits, int nt, int silu,
+                                 hipStream_t stream) {
+  if (M <= 0) return 0;
+  if (M > 64 || splits < 1) return -1;
+  if (nt != 1 && nt != 2) return -5;
+  if (N % (16 * nt) != 0) return -2;
+  const int kc = nt == 2 ? 512 : 256;
+  if (K % (kc * splits) != 0) return -3;
+  if (splits > 1 && ws == nullptr) return -4;
+  if (silu && (nt != 2 || splits != 1)) return -6;
+  const int mt = (M + 15) / 16;
+  const int cols = 4 * 16 * nt;
+  dim3 grid((N + cols - 1) / cols, splits), block(256);
+  const int k_slice = K / splits;
+#define FT_XR(MT_, NT_, KC_, S_)                                                             \
+  if (mt == MT_ && nt == NT_ && (silu != 0) == S_) {                                         \
+    hipLaunchKernelGGL((ft::skinny_xr_kernel<MT_, NT_, KC_, S_>), grid, block, 0, stream,    \
+                       (const uint16_t*)x, x_stride, M, (const uint16_t*)w, K, ws,           \
+                       (uint16_t*)out, out_stride, N, k_slice);                              \
+    return static_cast<int>(hipGetLastError());                                              \
+  }
+#define FT_XR_MT(MT_) FT_XR(MT_, 1, 256, false) FT_XR(MT_, 2, 512, false) FT_XR(MT_, 2, 512, true)
+  FT_XR_MT(1)
+  FT_XR_MT(2)
+  FT_XR_MT(3)
+  FT_XR_MT(4)
+#undef FT_XR_MT
+#undef FT_XR
   return -5;
 }
 

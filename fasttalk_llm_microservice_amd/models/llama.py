@@ -103,12 +103,17 @@ PACKED_PLAN = {
     # 32 / 64 rows: "xc" with 8 splits (x chunk staged once per workgroup in LDS, 384
     # workgroups): qkv 14.7 vs 18.2 us, o 12.4 vs 13.1 us at 50-64 rows, engine A/B
     # 8.05 vs 8.22 ms/step (profiles/ab_decode_plan_xc8_r02.log)
-    "qkv": {1: (1, -3, 1), 8: (2, -3, 1), 16: (2, -3, 1), 32: (2, -4, 8), 64: (2, -4, 8)},
-    "o": {1: (1, -3, 2), 8: (2, -3, 2), 16: (2, -3, 2), 32: (2, -3, 2), 64: (2, -4, 8)},
-    # gu 64: split-K slabs reduced by slab_silu (engine A/B at 50 rows: 5.47 vs 5.54 ms/step)
-    "gu": {1: (1, -3, 1), 8: (1, -3, 1), 16: (4, -3, 1), 32: (4, -3, 1), 64: (2, -4, 2)},
-    "down": {1: (1, -3, 2), 8: (2, -3, 4), 16: (4, -3, 4), 32: (4, -3, 4), 64: (4, -3, 4)},
-    "lm": {1: (1, -3, 1), 8: (2, -3, 1), 16: (4, -3, 1), 32: (1, -4, 1), 64: (2, -4, 1)},
+    # 33-64 rows: "xr" (xc with the chunk loop pipelined: no drain between 512-wide
+    # K chunks), so fewer splits pay: cold-cache us at 50 rows, xr vs the previous
+    # plan (profiles/xr_vs_xc_decode_gemm_r02.log): qkv 14.6 (2 splits) vs 15.2
+    # (xc, 8), o 10.9 (4) vs 13.1 (xc, 8), gate_up 44.7 with its own SiLU epilogue
+    # vs 47.9 + 6.3 (xc 2 splits + slab_silu), down 25.3 vs 26.3 (pk), LM head
+    # 181 vs ~195.  Fewer splits also shrink the slabs the next kernel re-reads.
+    "qkv": {1: (1, -3, 1), 8: (2, -3, 1), 16: (2, -3, 1), 32: (2, -4, 8), 64: (1, -5, 2)},
+    "o": {1: (1, -3, 2), 8: (2, -3, 2), 16: (2, -3, 2), 32: (2, -3, 2), 64: (1, -5, 4)},
+    "gu": {1: (1, -3, 1), 8: (1, -3, 1), 16: (4, -3, 1), 32: (4, -3, 1), 64: (2, -6, 1)},
+    "down": {1: (1, -3, 2), 8: (2, -3, 4), 16: (4, -3, 4), 32: (4, -3, 4), 64: (1, -5, 4)},
+    "lm": {1: (1, -3, 1), 8: (2, -3, 1), 16: (4, -3, 1), 32: (1, -4, 1), 64: (2, -5, 1)},
 }
 MAX_SPLITS = 4
 
@@ -146,7 +151,9 @@ def pg_cfg(proj: str, rows: int, k: int) -> Tuple[int, int]:
 
 def _cfg_fits(c, n: int, k: int) -> bool:
     nt, u, sp = c
-    kq = 512 if u == -4 else 64
+    kq = {-4: 512, -5: 512 if nt == 2 else 256, -6: 512}.get(u, 64)
+    if u == -6 and (nt != 2 or sp != 1 or n % 32):
+        return False
     return n % (16 * nt) == 0 and k % (kq * sp) == 0 and (u != -4 or n % 64 == 0)
 
 
@@ -585,6 +592,8 @@ class LlamaModel:
                 ops.skinny_gemm(x, wp, ws=self.ws, splits=sp, nt=nt, u=u)
                 return sp, None
             y = ops.skinny_gemm(x, wp, splits=1, nt=nt, u=u)
+            if u == -6:  # the xr kernel's own SiLU epilogue: y is already h
+                return 0, y
             return 0, (ops.silu_mul(y, interleaved=True) if gu else y)
         if PG_BLAS_ROWS and rows >= PG_BLAS_ROWS and proj != "lm":
             if self._unpack_buf is None or self._unpack_buf.numel() < n * k:

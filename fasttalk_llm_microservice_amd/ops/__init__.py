@@ -255,9 +255,12 @@ def pack_weight(w: torch.Tensor) -> torch.Tensor:
 def skinny_gemm(x, w, out=None, ws=None, splits: int = 1, nt: int = 1, u: int = -3):
     """y = x w^T (M <= 64) on a pack_weight() image.  splits > 1 leaves fp32 partial
     slabs in ``ws`` ([splits, M, N]) for a fused epilogue; otherwise writes bf16
-    ``out``.  u = -3: "pk" kernel, u = -4: "xc" kernel."""
+    ``out``.  u = -3: "pk" kernel, -4: "xc", -5: "xr" (chunk-pipelined xc),
+    -6: "xr" with the SiLU epilogue on an interleave_gate_up(w, 1) image (out is
+    h = silu(gate) * up, [M, N / 2])."""
     if splits == 1 and out is None:
-        out = torch.empty(x.shape[0], w.shape[0], dtype=x.dtype, device=x.device)
+        cols = w.shape[0] // 2 if u == -6 else w.shape[0]
+        out = torch.empty(x.shape[0], cols, dtype=x.dtype, device=x.device)
     native().skinny_gemm(x, w, out, ws, splits, nt, u)
     return out if splits == 1 else ws
 

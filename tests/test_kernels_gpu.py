@@ -398,10 +398,12 @@ def test_w4_gemm_matches_fp32(m, n, k, nt, splits):
 # ----------------------------------------------------------------------------------
 
 @pytest.mark.parametrize("m", [1, 7, 16, 33, 64])
-@pytest.mark.parametrize("nt,u,splits", [(1, -3, 1), (2, -3, 4), (4, -3, 2), (1, -4, 1), (2, -4, 2)])
+@pytest.mark.parametrize("nt,u,splits", [(1, -3, 1), (2, -3, 4), (4, -3, 2), (1, -4, 1), (2, -4, 2),
+                                         (2, -5, 1), (1, -5, 1), (2, -5, 4), (1, -5, 2)])
 def test_skinny_gemm(m, nt, u, splits):
-    """Packed-weight decode GEMMs ("pk" u=-3, "xc" u=-4) vs fp32, bf16 out and
-    split-K fp32 slabs."""
+    """Packed-weight decode GEMMs ("pk" u=-3, "xc" u=-4, chunk-pipelined "xr"
+    u=-5: 8 / 16 / 2 / 8 chunks per workgroup) vs fp32, bf16 out and split-K fp32
+    slabs."""
     n, k = 1024, 4096
     w = (torch.randn(n, k, device=DEV) * 0.05).bfloat16()
     x = torch.randn(m, k, device=DEV).bfloat16()
@@ -414,6 +416,21 @@ def test_skinny_gemm(m, nt, u, splits):
         ops.skinny_gemm(x, wp, ws=ws, splits=splits, nt=nt, u=u)
         y = ws.view(splits, m, n).sum(0)
     _close(y, ref_y, atol=3e-2, rtol=1e-2, msg="skinny_gemm")
+
+
+@pytest.mark.parametrize("m", [1, 29, 50, 64])
+@pytest.mark.parametrize("n,k", [(2048, 4096), (28672, 4096)])
+def test_skinny_gemm_xr_silu(m, n, k):
+    """xr with the SiLU epilogue on an interleave_gate_up(w, 1) image: h = silu(x Wg^T)
+    * (x Wu^T) straight from the GEMM (no slabs), vs fp32."""
+    wg = (torch.randn(n // 2, k, device=DEV) * 0.02).bfloat16()
+    wu = (torch.randn(n // 2, k, device=DEV) * 0.02).bfloat16()
+    x = torch.randn(m, k, device=DEV).bfloat16()
+    ref_h = torch.nn.functional.silu(x.float() @ wg.float().t()) * (x.float() @ wu.float().t())
+    wp = ops.pack_weight(ops.interleave_gate_up(torch.cat([wg, wu]), 1))
+    h = ops.skinny_gemm(x, wp, nt=2, u=-6)
+    assert h.shape == (m, n // 2)
+    _close(h.float(), ref_h, atol=3e-2, rtol=2e-2, msg="xr silu")
 
 
 def test_skinny_gemm_strided_x():
@@ -486,7 +503,9 @@ def test_embed_rmsnorm(hidden):
                                              (128256, 4096, 1, 2, -4), (6144, 4096, 8, 2, -4),
                                              (4096, 4096, 8, 1, -4), (6144, 4096, 1, 2, -3),
                                              (28672, 4096, 1, 1, -3), (4096, 4096, 2, 2, -3),
-                                             (4096, 14336, 2, 1, -3), (128256, 4096, 1, 4, -3)])
+                                             (4096, 14336, 2, 1, -3), (128256, 4096, 1, 4, -3),
+                                             (4096, 14336, 7, 2, -5), (4096, 14336, 4, 1, -5),
+                                             (28672, 4096, 1, 2, -5), (6144, 4096, 8, 2, -5)])
 @pytest.mark.parametrize("m", [1, 37, 64])
 def test_skinny_gemm_packed(m, n, k, splits, nt, u):
     """Packed-weight decode GEMMs vs fp32 torch (split-K slabs summed on the host)."""
