@@ -34,11 +34,12 @@
 //   and counts itself in the segment's counter; the wave that draws the last
 //   ticket merges the segment's partials (sc1 loads) into bf16 and resets the
 //   counter for the next call.  This is the guide's sc1 hand-off (§6 Guideline
-//   16): no fences, correct for any wave -> XCD placement.  Measured at 50
-//   sessions it LOSES to the separate paged_decode_combine kernel (12.3 vs 10.9 ms
-//   per decode step: the last arriver's sc1 loads of the partials are serial
-//   memory round trips), so the engine launches the combine kernel unless
-//   FT_DECODE_FUSED_COMBINE=1.
+//   16): no fences, correct for any wave -> XCD placement.  The partials are
+//   stored dim-permuted so every lane writes / reads contiguous 8-B words, and
+//   the last arriver batches all of a segment's partial loads (8 slots in
+//   flight) -- the first version's element-wise sc1 round trips made it lose to
+//   the separate combine kernel (12.3 vs 10.9 ms per decode step).  The engine
+//   launches the combine kernel unless FT_DECODE_FUSED_COMBINE=1.
 #include "ft_common.h"
 
 #include <stdlib.h>
@@ -86,15 +87,22 @@ template <int D>
 __device__ __forceinline__ void mt_load(MTile<D>& t, const uint16_t* __restrict__ k_cache,
                                         const uint16_t* __restrict__ v_cache, size_t kbase,
                                         size_t vbase, int koff, int voff, int bsz) {
-  // wave-uniform tile bases (SGPR pairs) + 32-bit lane offsets
+  // wave-uniform tile bases (SGPR pairs) + 32-bit lane offsets.  Non-temporal:
+  // the step's KV (0.4-1 GB at 50-64 sessions) is read once and far exceeds the
+  // 256 MiB Infinity Cache; the bare stream of this kernel's partition ran 5-7 %
+  // faster with nt than with the default policy (bench/attn_diag.py).
+  typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+  typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
   const uint16_t* kb = k_cache + kbase;
   const uint16_t* vb = v_cache + vbase;
 #pragma unroll
   for (int kc = 0; kc < D / 32; ++kc)
-    t.k[kc] = *reinterpret_cast<const uint4*>(kb + koff + kc * 32);
+    t.k[kc] = __builtin_bit_cast(
+        uint4, __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(kb + koff + kc * 32)));
 #pragma unroll
   for (int nd = 0; nd < D / 16; ++nd)
-    t.v[nd] = *reinterpret_cast<const uint2*>(vb + voff + nd * 16 * bsz);
+    t.v[nd] = __builtin_bit_cast(
+        uint2, __builtin_nontemporal_load(reinterpret_cast<const u32x2_t*>(vb + voff + nd * 16 * bsz)));
 }
 
 template <int D, int G, int R>
@@ -264,15 +272,21 @@ __global__ __launch_bounds__(256, R == 2 ? 3 : 2) void paged_decode_kernel(
         const float mr = __shfl(m_run, r & 15, 64);
         if (r < G) {
           float* dst = tmp_out + (slot * G + r) * D + n;
-          if (counters != nullptr) {   // write-through: read by another wave in this launch
+          if (counters != nullptr) {
+            // write-through (read by another wave in this launch), dims permuted to
+            // [n][nd] so each lane's ND values are contiguous: 8-B sc1 stores, and
+            // (m, l) as one 8-B store
+            uint64_t* dp = reinterpret_cast<uint64_t*>(tmp_out + (slot * G + r) * D + n * ND);
 #pragma unroll
-            for (int nd = 0; nd < ND; ++nd)
-              __hip_atomic_store(dst + nd * 16, o[nd][i4], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            for (int p2 = 0; p2 < ND / 2; ++p2) {
+              const uint64_t v = (uint64_t)__float_as_uint(o[2 * p2][i4]) |
+                                 ((uint64_t)__float_as_uint(o[2 * p2 + 1][i4]) << 32);
+              __hip_atomic_store(dp + p2, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
             if (n == 0) {
-              __hip_atomic_store(tmp_ml + (slot * G + r) * 2, mr, __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT);
-              __hip_atomic_store(tmp_ml + (slot * G + r) * 2 + 1, lr, __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT);
+              const uint64_t ml = (uint64_t)__float_as_uint(mr) | ((uint64_t)__float_as_uint(lr) << 32);
+              __hip_atomic_store(reinterpret_cast<uint64_t*>(tmp_ml + (slot * G + r) * 2), ml,
+                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
           } else {
 #pragma unroll
@@ -300,23 +314,47 @@ __global__ __launch_bounds__(256, R == 2 ? 3 : 2) void paged_decode_kernel(
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keep the loads below the ticket
           const size_t base = (size_t)(seg + wf);
           uint16_t* op = out + (size_t)b * out_stride + h * G * D;
-          for (int i = lane; i < G * D; i += 64) {
-            const int r = i / D, d = i - r * D;
-            float M = -INFINITY;
-            for (int k = 0; k < np; ++k)
-              M = fmaxf(M, __hip_atomic_load(tmp_ml + ((base + k) * G + r) * 2, __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT));
-            float den = 0.f, acc = 0.f;
-            for (int k = 0; k < np; ++k) {
-              const size_t sl = (base + k) * G + r;
-              const float e = exp2f(__hip_atomic_load(tmp_ml + sl * 2, __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_AGENT) - M);
-              den += e * __hip_atomic_load(tmp_ml + sl * 2 + 1, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
-              acc += e * __hip_atomic_load(tmp_out + sl * D + d, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
+          // lane (r, c): head r, dims c + 16 nd of the permuted partials; the
+          // partial slots are read in batches of 8 with every load of a batch in
+          // flight at once (8-B sc1 loads; slots past np re-read the last one and
+          // are masked), online-max merge
+          for (int q4 = lane; q4 < G * 16; q4 += 64) {
+            const int r = q4 >> 4, c = q4 & 15;
+            float M = -INFINITY, den = 0.f, acc[ND];
+#pragma unroll
+            for (int nd = 0; nd < ND; ++nd) acc[nd] = 0.f;
+            for (int k0 = 0; k0 < np; k0 += 8) {
+              uint64_t mlv[8], ov[8][ND / 2];
+#pragma unroll
+              for (int k = 0; k < 8; ++k) {
+                const size_t sl = (base + min(k0 + k, np - 1)) * G + r;
+                mlv[k] = __hip_atomic_load(reinterpret_cast<const uint64_t*>(tmp_ml + sl * 2),
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const uint64_t* sp = reinterpret_cast<const uint64_t*>(tmp_out + sl * D + c * ND);
+#pragma unroll
+                for (int p2 = 0; p2 < ND / 2; ++p2)
+                  ov[k][p2] = __hip_atomic_load(sp + p2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              }
+#pragma unroll
+              for (int k = 0; k < 8; ++k) {
+                if (k0 + k < np) {
+                  const float m = __uint_as_float((uint32_t)mlv[k]);
+                  const float l = __uint_as_float((uint32_t)(mlv[k] >> 32));
+                  const float mn = fmaxf(M, m);
+                  const float a = exp2f(M - mn), e = exp2f(m - mn);
+                  den = den * a + e * l;
+#pragma unroll
+                  for (int p2 = 0; p2 < ND / 2; ++p2) {
+                    acc[2 * p2] = acc[2 * p2] * a + e * __uint_as_float((uint32_t)ov[k][p2]);
+                    acc[2 * p2 + 1] = acc[2 * p2 + 1] * a + e * __uint_as_float((uint32_t)(ov[k][p2] >> 32));
+                  }
+                  M = mn;
+                }
+              }
             }
-            op[i] = f32_to_bf16(acc / den);
+            const float inv = 1.f / den;
+#pragma unroll
+            for (int nd = 0; nd < ND; ++nd) op[r * D + 16 * nd + c] = f32_to_bf16(acc[nd] * inv);
           }
           if (lane == 0)
             __hip_atomic_store(counters + seg, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
