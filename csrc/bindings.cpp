@@ -60,7 +60,8 @@ int ft_ar_export_error(int* dst, const uint64_t* peers_dev, int world, hipStream
 int ft_skinny_gemm_pk(const void* x, int x_stride, int M, const void* wpk, int N, int K, float* ws,
                       void* out, int out_stride, int splits, int nt, hipStream_t stream);
 int ft_skinny_gemm_xr(const void* x, int x_stride, int M, const void* w, int N, int K, float* ws,
-                      void* out, int out_stride, int splits, int nt, int silu, hipStream_t stream);
+                      void* out, int out_stride, int splits, int nt, int epi, int norm,
+                      void* residual, int res_stride, int* tickets, float eps, hipStream_t stream);
 int ft_packed_gemm(const void* x, int x_stride, int M, const void* wpk, int N, int K, int splits,
                    int epi, int cfg, void* out, int out_stride, float* ws, hipStream_t stream);
 int ft_unpack_weight(void* out, const void* wpk, int N, int K, hipStream_t stream);
@@ -402,7 +403,8 @@ void skinny_gemm(at::Tensor x, at::Tensor w, c10::optional<at::Tensor> out,
   }
   if (u <= -5)
     check_rc(ft_skinny_gemm_xr(x.data_ptr(), (int)x.stride(0), M, w.data_ptr(), N, K, wsp, op,
-                               ostride, (int)splits, (int)nt, silu ? 1 : 0, cur_stream()),
+                               ostride, (int)splits, (int)nt, silu ? 1 : 0, 0, nullptr, 0, nullptr,
+                               0.f, cur_stream()),
              "skinny_gemm_xr");
   else if (u == -3)  // w is the packed [N/16][K/64][2][64][8] image (ops.pack_weight)
     check_rc(ft_skinny_gemm_pk(x.data_ptr(), (int)x.stride(0), M, w.data_ptr(), N, K, wsp, op,
@@ -412,6 +414,58 @@ void skinny_gemm(at::Tensor x, at::Tensor w, c10::optional<at::Tensor> out,
     check_rc(ft_skinny_gemm_xc(x.data_ptr(), (int)x.stride(0), M, w.data_ptr(), N, K, wsp, op,
                                ostride, (int)splits, (int)nt, cur_stream()),
              "skinny_gemm_xc");
+}
+
+// "xr" decode GEMM with the fused epilogues (csrc/kernels/skinny_gemm.hip):
+// epi 1 SiLU (norm: x is the raw residual, rows RMS-scaled), epi 2 residual +=
+// x w^T with split-K reduced in the launch (ws + zeroed tickets).
+void skinny_gemm_xr(at::Tensor x, at::Tensor w, c10::optional<at::Tensor> out,
+                    c10::optional<at::Tensor> ws, int64_t splits, int64_t nt, int64_t epi,
+                    bool norm, c10::optional<at::Tensor> residual,
+                    c10::optional<at::Tensor> tickets, double eps) {
+  check_bf16(x, "x");
+  check_bf16(w, "w");
+  check_rows(x, "x");
+  TORCH_CHECK(w.dim() == 2 && w.is_contiguous(), "w must be the packed [N, K] image");
+  const int M = (int)x.size(0), K = (int)x.size(1), N = (int)w.size(0);
+  TORCH_CHECK(w.size(1) == K && M <= 64, "xr: K mismatch or M > 64");
+  void* op = nullptr;
+  int ostride = 0;
+  if (epi == 1 || (epi == 0 && splits == 1)) {
+    TORCH_CHECK(out.has_value(), "xr: out required");
+    check_bf16(*out, "out");
+    TORCH_CHECK(out->dim() == 2 && out->stride(1) == 1 && out->size(0) >= M &&
+                    out->size(1) >= (epi == 1 ? N / 2 : N), "xr: out shape");
+    op = out->data_ptr();
+    ostride = (int)out->stride(0);
+  }
+  float* wsp = nullptr;
+  if (splits > 1) {
+    TORCH_CHECK(ws.has_value(), "xr: splits > 1 needs a workspace");
+    check_ws(*ws, (int64_t)splits * N * 16 * ((M + 15) / 16));
+    check_ws(*ws, (int64_t)splits * M * N);
+    wsp = ws->data_ptr<float>();
+  }
+  void* rp = nullptr;
+  int rstride = 0;
+  if (epi == 2) {
+    TORCH_CHECK(residual.has_value(), "xr resid: residual required");
+    check_bf16(*residual, "residual");
+    TORCH_CHECK(residual->dim() == 2 && residual->stride(1) == 1 && residual->size(0) >= M &&
+                    residual->size(1) >= N, "xr resid: residual shape");
+    rp = residual->data_ptr();
+    rstride = (int)residual->stride(0);
+  }
+  int* tp = nullptr;
+  if (epi == 2 && splits > 1) {
+    TORCH_CHECK(tickets.has_value() && tickets->scalar_type() == at::kInt && tickets->is_cuda() &&
+                    tickets->numel() >= N / (16 * nt), "xr resid: int32 tickets >= N / (16 nt)");
+    tp = tickets->data_ptr<int>();
+  }
+  check_rc(ft_skinny_gemm_xr(x.data_ptr(), (int)x.stride(0), M, w.data_ptr(), N, K, wsp, op, ostride,
+                             (int)splits, (int)nt, (int)epi, norm ? 1 : 0, rp, rstride, tp, (float)eps,
+                             cur_stream()),
+           "skinny_gemm_xr");
 }
 
 // Packed-image GEMM for M > 64 rows (csrc/kernels/packed_gemm.hip).
@@ -691,6 +745,10 @@ PYBIND11_MODULE(_C, m) {
         py::arg("out") = py::none(), py::arg("ws") = py::none(), py::arg("splits") = 1,
         py::arg("nt") = 1);
   m.def("w4_dequant", &w4_dequant);
+  m.def("skinny_gemm_xr", &skinny_gemm_xr, py::arg("x"), py::arg("w"), py::arg("out") = py::none(),
+        py::arg("ws") = py::none(), py::arg("splits") = 1, py::arg("nt") = 2, py::arg("epi") = 0,
+        py::arg("norm") = false, py::arg("residual") = py::none(), py::arg("tickets") = py::none(),
+        py::arg("eps") = 1e-5);
   m.def("skinny_gemm", &skinny_gemm, py::arg("x"), py::arg("w"), py::arg("out") = py::none(),
         py::arg("ws") = py::none(), py::arg("splits") = 1, py::arg("nt") = 1, py::arg("u") = -3);
   m.def("pkr_gemm", &pkr_gemm, py::arg("x"), py::arg("w"), py::arg("out") = py::none(),
