@@ -124,15 +124,16 @@ __global__ __launch_bounds__(256, 2) void attn_loads(const uint16_t* __restrict_
 }  // namespace ftd
 
 extern "C" int attn_loads_launch(const void* k, const void* v, const int* bt, int bt_stride, const int* sl,
-                                 int batch, int nkv, int mode, int ring, unsigned* sink, hipStream_t stream) {
-  const int nwg = ft_num_cus() * 2;
+                                 int batch, int nkv, int mode, int ring, int wpc, int bs_shift,
+                                 unsigned* sink, hipStream_t stream) {
+  const int nwg = ft_num_cus() * wpc;
 #define L(MM, RR)                                                                                      \
   if (mode == MM && ring == RR) {                                                                      \
     hipLaunchKernelGGL((ftd::attn_loads<128, RR, MM>), dim3(nwg), dim3(256), 0, stream,                \
-                       (const uint16_t*)k, (const uint16_t*)v, bt, bt_stride, sl, batch, nkv, 4, sink); \
+                       (const uint16_t*)k, (const uint16_t*)v, bt, bt_stride, sl, batch, nkv, bs_shift, sink); \
     return (int)hipGetLastError();                                                                     \
   }
-  L(0, 3) L(1, 3) L(2, 3) L(0, 4) L(0, 6) L(3, 3) L(3, 4) L(4, 3) L(4, 4)
+  L(0, 3) L(1, 3) L(2, 3) L(0, 4) L(0, 6) L(3, 3) L(3, 4) L(4, 2) L(4, 3) L(4, 4)
 #undef L
   return -1;
 }

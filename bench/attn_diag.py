@@ -15,9 +15,13 @@ from fasttalk_llm_microservice_amd import ops  # noqa: E402
 from gemm_sweep import graph_time  # noqa: E402
 
 lib = ctypes.CDLL(os.path.join(os.path.dirname(os.path.abspath(__file__)), "libattndiag.so"))
-lib.attn_loads_launch.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int, ctypes.c_void_p] + [ctypes.c_int] * 4 + \
+lib.attn_loads_launch.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int, ctypes.c_void_p] + [ctypes.c_int] * 6 + \
     [ctypes.c_void_p, ctypes.c_void_p]
-nq, nkv, d, bs = 32, 8, 128, 16
+nq, nkv, d = 32, 8, 128
+bs = int(os.environ.get("BS", "16"))   # KV block size (tokens)
+STREAMS = [(0, 3, 2, "K+V r3"), (4, 3, 2, "K+V nt r3"), (4, 4, 2, "K+V nt r4"), (3, 3, 2, "contig r3")]
+if os.environ.get("SWEEP"):  # ring x workgroups-per-CU of the nt stream
+    STREAMS = [(4, r, w, f"nt r{r} w{w}") for r in (2, 3, 4) for w in (1, 2, 3, 4)]
 sink = torch.zeros(256, dtype=torch.int32, device="cuda")
 for B, ctx, uniform in [(50, 3000, False), (50, 4500, False), (64, 4096, True)]:
     nblk = math.ceil(ctx / bs)
@@ -33,7 +37,7 @@ for B, ctx, uniform in [(50, 3000, False), (50, 4500, False), (64, 4096, True)]:
         bt = torch.cat([bt, torch.arange(bt.numel(), B * nblk, device="cuda")]).int().view(B, nblk)
     else:
         bt = torch.randperm(nblocks, device="cuda")[: B * nblk].int().view(B, nblk)
-    print("block order", order, flush=True) if B == 50 and ctx == 3000 else None
+    print("block order", order, "bs", bs, flush=True) if B == 50 and ctx == 3000 else None
     sl = torch.full((B,), ctx, dtype=torch.int32, device="cuda") if uniform else \
         torch.randint(ctx // 2, ctx + 1, (B,), dtype=torch.int32, device="cuda")
     q = torch.randn(B, (nq + 2 * nkv) * d, device="cuda").bfloat16()
@@ -48,10 +52,11 @@ for B, ctx, uniform in [(50, 3000, False), (50, 4500, False), (64, 4096, True)]:
                                                                    d, d ** -0.5, counters=cnt) for i in range(8)])
     res = [f"B={B} ctx={ctx}{' uniform' if uniform else ''} {nbytes / 1e6:.0f} MB: full {full:7.1f} us "
            f"({nbytes / full / 1e3:.0f} GB/s) fused-combine {fused:7.1f}"]
-    for mode, ring, name in [(0, 3, "K+V r3"), (4, 3, "K+V nt r3"), (4, 4, "K+V nt r4"), (3, 3, "contig r3")]:
-        def call(kv, mode=mode, ring=ring):
+    for mode, ring, wpc, name in STREAMS:
+        def call(kv, mode=mode, ring=ring, wpc=wpc):
             return lambda: lib.attn_loads_launch(kv[0].data_ptr(), kv[1].data_ptr(), bt.data_ptr(), bt.stride(0),
-                                                 sl.data_ptr(), B, nkv, mode, ring, sink.data_ptr(),
+                                                 sl.data_ptr(), B, nkv, mode, ring, wpc, bs.bit_length() - 1,
+                                                 sink.data_ptr(),
                                                  torch.cuda.current_stream().cuda_stream)
         assert call(kvs[0])() == 0
         t = graph_time([call(kvs[i % 2]) for i in range(8)])

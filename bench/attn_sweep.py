@@ -5,7 +5,7 @@ unless --uniform; KV blocks are scattered (random permutation), like a pool
 that has served many sessions.
 
 python bench/attn_sweep.py [--nq 32 --nkv 8] [--uniform]
-FT_DECODE_RING=2|3|4 selects the kernel's register-ring depth (default 3).
+FT_DECODE_RING=2|3|4 selects the kernel's register-ring depth (default 2).
 """
 from __future__ import annotations
 
@@ -55,7 +55,7 @@ def main():
         us = timeit(lambda: ops.decode_attention(out, q, kc, vc, bt, sl, tmp_o, tmp_ml, nq, nkv, d,
                                                  d ** -0.5), iters=100, warmup=10)
         print(json.dumps({"B": B, "ctx": ctx, "uniform": a.uniform,
-                          "ring": int(os.environ.get("FT_DECODE_RING", "3")),
+                          "ring": int(os.environ.get("FT_DECODE_RING", "2")),
                           "us": round(us, 2), "GBps": round(nbytes / us / 1e3, 1)}), flush=True)
         del kc, vc
 

@@ -77,6 +77,29 @@ def gaps_by_kernel(db: str, last_ms: float, top: int = 15) -> str:
     return "\n".join(out)
 
 
+def timeline(db: str, last_ms: float, span_ms: float = 30.0, min_gap_us: float = 5.0) -> str:
+    """Dispatch sequence of a ``span_ms`` window starting ``last_ms`` before the end:
+    every dispatch preceded by an idle gap >= min_gap_us, with its predecessor, so
+    a step's bubbles can be placed (what ran before and after each)."""
+    c = sqlite3.connect(db)
+    rows = sorted(c.execute("select start, end, name from kernels").fetchall())
+    t1 = max(e for _, e, _ in rows)
+    t0 = t1 - last_ms * 1e6
+    out = [f"timeline {span_ms:.0f} ms from t-{last_ms:.0f} ms: gaps >= {min_gap_us:.0f} us"]
+    prev = None
+    for s, e, n in rows:
+        if s < t0:
+            prev = (s, e, n)
+            continue
+        if s > t0 + span_ms * 1e6:
+            break
+        if prev is not None and (s - prev[1]) / 1e3 >= min_gap_us:
+            out.append(f"  t={(prev[0] - t0) / 1e3:9.1f} us  {(prev[1] - prev[0]) / 1e3:7.1f} us  {prev[2][:70]}")
+            out.append(f"      gap {(s - prev[1]) / 1e3:8.1f} us -> {(e - s) / 1e3:7.1f} us  {n[:70]}")
+        prev = (s, e, n)
+    return "\n".join(out)
+
+
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("db")
@@ -90,3 +113,4 @@ if __name__ == "__main__":
         print(busy(a.db, a.busy_last_ms))
         if a.busy_last_ms > 0:
             print(gaps_by_kernel(a.db, a.busy_last_ms))
+            print(timeline(a.db, a.busy_last_ms / 2))

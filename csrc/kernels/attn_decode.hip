@@ -38,8 +38,10 @@
 //   stored dim-permuted so every lane writes / reads contiguous 8-B words, and
 //   the last arriver batches all of a segment's partial loads (8 slots in
 //   flight) -- the first version's element-wise sc1 round trips made it lose to
-//   the separate combine kernel (12.3 vs 10.9 ms per decode step).  The engine
-//   launches the combine kernel unless FT_DECODE_FUSED_COMBINE=1.
+//   the separate combine kernel (12.3 vs 10.9 ms per decode step).  At one
+//   workgroup per CU it matches or beats the combine kernel (85 vs 86 us at 50 x
+//   1.5-3k, 177 vs 182 us at 64 x 4k) and saves a launch per layer: the engine
+//   uses it unless FT_DECODE_FUSED_COMBINE=0.
 #include "ft_common.h"
 
 #include <stdlib.h>
@@ -83,30 +85,40 @@ struct MTile {
   uint2 v[D / 16];
 };
 
+// One tile's loads as buffer loads: the wave-uniform tile bases become SGPR
+// descriptors and each lane keeps ONE 32-bit byte offset per image; the K
+// k-steps are immediate offsets and the V^T dim tiles' stride (16 rows of the
+// transposed block) goes in soffset, so the ring costs no address VGPRs (with
+// 64-bit flat addresses the R = 3 kernel needed 204 VGPRs: 2 waves / SIMD).
+// aux 2 = nt: the step's KV (0.4-1 GB at 50-64 sessions) is read once and far
+// exceeds the 256 MiB Infinity Cache (the bare stream ran 5-7 % faster with nt).
+// a wave-uniform pointer the compiler can PROVE uniform (SGPR descriptor, no
+// waterfall loop around each buffer op: the tile indices derive from wave_id())
+__device__ __forceinline__ void* uniform_ptr(const void* p) {
+  const uint64_t a = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  return reinterpret_cast<void*>(((uint64_t)hi << 32) | lo);
+}
+
 template <int D>
 __device__ __forceinline__ void mt_load(MTile<D>& t, const uint16_t* __restrict__ k_cache,
                                         const uint16_t* __restrict__ v_cache, size_t kbase,
-                                        size_t vbase, int koff, int voff, int bsz) {
-  // wave-uniform tile bases (SGPR pairs) + 32-bit lane offsets.  Non-temporal:
-  // the step's KV (0.4-1 GB at 50-64 sessions) is read once and far exceeds the
-  // 256 MiB Infinity Cache; the bare stream of this kernel's partition ran 5-7 %
-  // faster with nt than with the default policy (bench/attn_diag.py).
-  typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
-  typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
-  const uint16_t* kb = k_cache + kbase;
-  const uint16_t* vb = v_cache + vbase;
+                                        size_t vbase, int koff_b, int voff_b, int vstep_b) {
+  const __amdgpu_buffer_rsrc_t kr = __builtin_amdgcn_make_buffer_rsrc(
+      uniform_ptr(k_cache + kbase), 0, 16 * D * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t vr = __builtin_amdgcn_make_buffer_rsrc(
+      uniform_ptr(v_cache + vbase), 0, 0x7fffffff, 0x00020000);
 #pragma unroll
   for (int kc = 0; kc < D / 32; ++kc)
-    t.k[kc] = __builtin_bit_cast(
-        uint4, __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(kb + koff + kc * 32)));
+    t.k[kc] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(kr, koff_b + kc * 64, 0, 2));
 #pragma unroll
   for (int nd = 0; nd < D / 16; ++nd)
-    t.v[nd] = __builtin_bit_cast(
-        uint2, __builtin_nontemporal_load(reinterpret_cast<const u32x2_t*>(vb + voff + nd * 16 * bsz)));
+    t.v[nd] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(vr, voff_b, nd * vstep_b, 2));
 }
 
-template <int D, int G, int R>
-__global__ __launch_bounds__(256, R == 2 ? 3 : 2) void paged_decode_kernel(
+template <int D, int G, int R, bool FC, int WPC>
+__global__ __launch_bounds__(256, WPC) void paged_decode_kernel(
     uint16_t* __restrict__ out, int out_stride, float* __restrict__ tmp_out,
     float* __restrict__ tmp_ml, const uint16_t* __restrict__ q, int q_stride,
     const uint16_t* __restrict__ k_cache, const uint16_t* __restrict__ v_cache,
@@ -120,7 +132,7 @@ __global__ __launch_bounds__(256, R == 2 ? 3 : 2) void paged_decode_kernel(
   const int total = nkv * s_pre[batch];
   const int nw = dec_num_waves(total, gridDim.x * 4);
   const int w = wave_id() * gridDim.x + blockIdx.x;  // spreads low wave ids over CUs
-  if (counters != nullptr && blockIdx.x == 0) {
+  if (FC && blockIdx.x == 0) {
     // fused-combine mode has no combine kernel to define empty sequences' outputs
     // (the padded rows of a decode graph bucket): one thread per empty segment
     for (int seg = threadIdx.x; seg < batch * nkv; seg += blockDim.x) {
@@ -142,8 +154,9 @@ __global__ __launch_bounds__(256, R == 2 ? 3 : 2) void paged_decode_kernel(
   const int bmask = bsz - 1;
   const size_t blk_stride = (size_t)nkv * bsz * D;
   // per-lane offsets inside a 16-token tile
-  const int koff = n * D + 8 * g;          // K row n, dims 8g.. (+32 kc)
-  const int voff = n * bsz + 4 * g;        // V^T row n (+16 nd), tokens 4g..4g+3
+  const int koff_b = 2 * (n * D + 8 * g);     // bytes: K row n, dims 8g.. (+32 kc)
+  const int voff_b = 2 * (n * bsz + 4 * g);   // bytes: V^T row n (+16 nd), tokens 4g..4g+3
+  const int vstep_b = 2 * 16 * bsz;           // bytes between the V^T dim tiles
 
   while (f < f1) {
     // segment (b, h) holding flattened tile f: b = last sequence with nkv * pre[b] <= f
@@ -188,7 +201,7 @@ __global__ __launch_bounds__(256, R == 2 ? 3 : 2) void paged_decode_kernel(
         const size_t blk = (size_t)(uint32_t)__builtin_amdgcn_readlane(my_blk, j);
         const int off = __builtin_amdgcn_readlane(my_off, j);
         const size_t hb = blk * blk_stride + (size_t)h * bsz * D;
-        mt_load<D>(t, k_cache, v_cache, hb + (size_t)off * D, hb + off, koff, voff, bsz);
+        mt_load<D>(t, k_cache, v_cache, hb + (size_t)off * D, hb + off, koff_b, voff_b, vstep_b);
       };
       auto consume = [&](const MTile<D>& t, int i) {
         const int valid = L - ((t0 + c0 + i) << 4);   // tokens of this tile inside the sequence
@@ -272,7 +285,7 @@ __global__ __launch_bounds__(256, R == 2 ? 3 : 2) void paged_decode_kernel(
         const float mr = __shfl(m_run, r & 15, 64);
         if (r < G) {
           float* dst = tmp_out + (slot * G + r) * D + n;
-          if (counters != nullptr) {
+          if (FC) {
             // write-through (read by another wave in this launch), dims permuted to
             // [n][nd] so each lane's ND values are contiguous: 8-B sc1 stores, and
             // (m, l) as one 8-B store
@@ -298,7 +311,7 @@ __global__ __launch_bounds__(256, R == 2 ? 3 : 2) void paged_decode_kernel(
           }
         }
       }
-      if (counters != nullptr) {
+      if (FC) {
         // publish (every partial store of this wave retired), then take a ticket
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         int prev = 0;
@@ -438,9 +451,21 @@ static int ft_num_cus() {
   return n;
 }
 
-// workgroups per CU (all resident): ring depth 2 fits 3 waves/SIMD (168 VGPRs),
-// deeper rings 2 waves/SIMD
-static int dec_wg_per_cu(int ring) { return ring == 2 ? 3 : 2; }
+// Workgroups per CU.  Fewer bytes in flight stream FASTER here: the bare load
+// stream of this partition (bench/attn_diag.py SWEEP=1, 50 x 1.5-3k ragged, random
+// blocks) ran 6.28 TB/s with one 4-wave workgroup per CU and one tile in flight
+// per wave, 5.77 TB/s at 2 workgroups x 2 tiles, 4.77 TB/s at 4 x 3 -- ~8 MB in
+// flight chip-wide is the sweet spot, more thrashes the HBM queues (the plain
+// streaming-read ceiling, bench/bw_read.py, peaks at the same 8 MB).
+// FT_DECODE_WPC (1-3) overrides for A/B runs.
+static int dec_wg_per_cu() {
+  static const int w = [] {
+    const char* e = getenv("FT_DECODE_WPC");
+    const int v = e ? atoi(e) : 1;
+    return (v >= 1 && v <= 3) ? v : 1;
+  }();
+  return w;
+}
 
 // upper bound on the waves of the decode grid: the workspace holds batch * nkv +
 // waves partial slots
@@ -464,35 +489,52 @@ extern "C" int ft_paged_decode_attention(void* out, int out_stride, float* tmp_o
   // the default for the A/B sweeps (bench/attn_sweep.py)
   static const int ring = [] {
     const char* e = getenv("FT_DECODE_RING");
-    const int r = e ? atoi(e) : 3;
-    return (r >= 2 && r <= 4) ? r : 3;
+    const int r = e ? atoi(e) : 2;
+    return (r >= 2 && r <= 4) ? r : 2;
   }();
+  // 1 workgroup per CU, or the register-limited maximum for the ring depth
+  const int wpc = dec_wg_per_cu() == 1 ? 1 : (ring == 2 ? 3 : 2);
   int nwg = 0;
+#define FT_DEC_LAUNCH(DD, GG, RR, FCC)                                                         \
+  if (wpc == 1)                                                                                \
+    hipLaunchKernelGGL((ft::paged_decode_kernel<DD, GG, RR, FCC, 1>), dim3(nwg), dim3(256), 0,  \
+                       stream, (uint16_t*)out, out_stride, tmp_out, tmp_ml, (const uint16_t*)q, \
+                       q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache,            \
+                       block_tables, bt_stride, seq_lens, batch, nkv, bs_shift, scale_log2,     \
+                       counters);                                                               \
+  else                                                                                         \
+  hipLaunchKernelGGL((ft::paged_decode_kernel<DD, GG, RR, FCC, (RR == 2 ? 3 : 2)>), dim3(nwg),  \
+                     dim3(256), 0, stream, (uint16_t*)out, out_stride, tmp_out, tmp_ml,          \
+                     (const uint16_t*)q, q_stride, (const uint16_t*)k_cache,                     \
+                     (const uint16_t*)v_cache, block_tables, bt_stride, seq_lens, batch, nkv,    \
+                     bs_shift, scale_log2, counters)
 #define FT_DEC_CASE(DD, GG, RR)                                                                \
   if (head_dim == DD && G == GG) {                                                             \
-    nwg = ft_num_cus() * dec_wg_per_cu(RR);                                                    \
-    hipLaunchKernelGGL((ft::paged_decode_kernel<DD, GG, RR>), dim3(nwg), dim3(256), 0, stream, \
-                       (uint16_t*)out, out_stride, tmp_out, tmp_ml, (const uint16_t*)q,          \
-                       q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache,             \
-                       block_tables, bt_stride, seq_lens, batch, nkv, bs_shift, scale_log2,      \
-                       counters);                                                                \
-    if (counters == nullptr)                                                                     \
+    nwg = ft_num_cus() * wpc;                                                    \
+    if (counters != nullptr) {                                                                 \
+      FT_DEC_LAUNCH(DD, GG, RR, true);                                                         \
+    } else {                                                                                   \
+      FT_DEC_LAUNCH(DD, GG, RR, false);                                                        \
       hipLaunchKernelGGL((ft::paged_decode_combine_kernel<DD, GG>), dim3(batch * nkv), dim3(256),\
                          0, stream, (uint16_t*)out, out_stride, tmp_out, tmp_ml, seq_lens, batch,\
                          nkv, nwg * 4);                                                          \
+    }                                                                                            \
     return static_cast<int>(hipGetLastError());                                                  \
   }
-  if (ring == 2) { FT_DEC_CASE(128, 4, 2) }
+  // ring 2 at one workgroup per CU: full kernel 86 vs 92 us (ring 3) at 50 x 1.5-3k,
+  // 125 vs 128 us at 50 x 2.2-4.5k (bench/attn_diag.py, profiles/attn_decode_w1_r02.log)
+  if (ring == 3) { FT_DEC_CASE(128, 4, 3) }
   if (ring == 4) { FT_DEC_CASE(128, 4, 4) }
-  FT_DEC_CASE(128, 1, 3)
-  FT_DEC_CASE(128, 2, 3)
-  FT_DEC_CASE(128, 3, 3)
-  FT_DEC_CASE(128, 4, 3)
-  FT_DEC_CASE(128, 8, 3)
-  FT_DEC_CASE(64, 1, 3)
-  FT_DEC_CASE(64, 2, 3)
-  FT_DEC_CASE(64, 4, 3)
-  FT_DEC_CASE(64, 8, 3)
+  FT_DEC_CASE(128, 1, 2)
+  FT_DEC_CASE(128, 2, 2)
+  FT_DEC_CASE(128, 3, 2)
+  FT_DEC_CASE(128, 4, 2)
+  FT_DEC_CASE(128, 8, 2)
+  FT_DEC_CASE(64, 1, 2)
+  FT_DEC_CASE(64, 2, 2)
+  FT_DEC_CASE(64, 4, 2)
+  FT_DEC_CASE(64, 8, 2)
 #undef FT_DEC_CASE
+#undef FT_DEC_LAUNCH
   return -2;
 }

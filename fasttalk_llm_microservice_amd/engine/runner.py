@@ -37,16 +37,85 @@ def _pow2_ceil(x: int) -> int:
     return 1 << max(0, (x - 1).bit_length())
 
 
+def input_words(mb: int, max_blocks: int) -> int:
+    return 10 * mb + mb * max_blocks
+
+
+def _input_views(buf: torch.Tensor, mb: int, max_blocks: int):
+    """(small int32 [6mb], f32 [2mb], seeds int64 [mb], block tables int32 [mb, max_blocks])
+    views of one int32 buffer of input_words() elements."""
+    return (buf[0:6 * mb], buf[6 * mb:8 * mb].view(torch.float32), buf[8 * mb:10 * mb].view(torch.int64),
+            buf[10 * mb:].view(mb, max_blocks))
+
+
+class _Uploader:
+    """Eager (mixed decode + prefill) step inputs in ONE host -> device copy: the
+    numpy arrays are packed into a pinned int32 image (64-B aligned fields, int64
+    and float32 bit-cast) and come back as typed device views.  Two images
+    alternate; an image is refilled only after its previous copy retired (event).
+    Replaces ~15 pageable ``torch.from_numpy(a).to(dev)`` copies per step, each a
+    blit launch with the GPU idle in front of it."""
+
+    ALIGN = 16  # int32 words
+
+    def __init__(self, device, pin: bool):
+        self.device = device
+        self.pin = pin
+        self.host = [torch.zeros(0, dtype=torch.int32) for _ in range(2)]
+        self.events = [None, None]
+        self.dev = torch.zeros(0, dtype=torch.int32, device=device)
+        self.k = 0
+
+    def __call__(self, arrays):
+        arrs = [np.ascontiguousarray(a) for a in arrays]
+        offs, n = [], 0
+        for a in arrs:
+            offs.append(n)
+            w = (a.nbytes + 3) // 4
+            n += (w + self.ALIGN - 1) // self.ALIGN * self.ALIGN
+        n = max(n, self.ALIGN)
+        k = self.k
+        self.k ^= 1
+        if self.events[k] is not None:
+            self.events[k].synchronize()
+        if self.host[k].numel() < n:
+            self.host[k] = torch.zeros(2 * n, dtype=torch.int32, pin_memory=self.pin)
+        if self.dev.numel() < n:
+            # the old buffer may still feed queued kernels: the caching allocator only
+            # reuses its memory after the stream has passed this point
+            self.dev = torch.zeros(2 * n, dtype=torch.int32, device=self.device)
+        hb = self.host[k].numpy().view(np.uint8)
+        for a, o in zip(arrs, offs):
+            hb[4 * o:4 * o + a.nbytes] = a.reshape(-1).view(np.uint8)
+        self.dev[:n].copy_(self.host[k][:n], non_blocking=True)
+        if self.pin:
+            ev = self.events[k] or torch.cuda.Event()
+            ev.record()
+            self.events[k] = ev
+        outs = []
+        for a, o in zip(arrs, offs):
+            w = (a.nbytes + 3) // 4
+            v = self.dev[o:o + w]
+            if a.dtype.itemsize == 8:
+                v = v.view(torch.int64 if a.dtype.kind in "iu" else torch.float64)
+            elif a.dtype == np.float32:
+                v = v.view(torch.float32)
+            elif a.dtype.itemsize != 4:
+                raise TypeError(f"upload: unsupported dtype {a.dtype}")
+            outs.append(v.view(a.shape) if a.ndim != 1 else v)
+        return outs
+
+
 class _Staging:
     """Pinned host mirror of the decode graph's device inputs + its output copy.
     int32 ``small`` fields: ids | pos | slots | seq_lens | top_k | steps."""
 
     def __init__(self, mb: int, max_blocks: int, pin: bool, gpu: bool):
         i32 = torch.int32
-        self.h_small = torch.zeros(6 * mb, dtype=i32, pin_memory=pin)
-        self.h_bt = torch.zeros(mb, max_blocks, dtype=i32, pin_memory=pin)
-        self.h_f32 = torch.zeros(2 * mb, dtype=torch.float32, pin_memory=pin)
-        self.h_seeds = torch.zeros(mb, dtype=torch.int64, pin_memory=pin)
+        # one pinned int32 image, laid out like the device inputs (_input_views), so a
+        # step's inputs go up in ONE copy: small | f32 | seeds (int64) | block tables
+        self.h_in = torch.zeros(input_words(mb, max_blocks), dtype=i32, pin_memory=pin)
+        self.h_small, self.h_f32, self.h_seeds, self.h_bt = _input_views(self.h_in, mb, max_blocks)
         self.h_out = torch.zeros(mb, dtype=i32, pin_memory=pin)
         self.h_err = torch.zeros(1, dtype=i32, pin_memory=pin)  # TP collective error flag
         self.err_armed = False
@@ -116,26 +185,28 @@ class ModelRunner:
         dv = self.device
         i32 = torch.int32
         pin = self.is_gpu
-        # Static graph inputs live in a few device buffers whose layout mirrors a
-        # pinned host staging copy, so a decode step refreshes all inputs with 4
-        # async H2D copies.  int32 fields: ids | pos | slots | seq_lens | top_k | steps
-        self.d_small = torch.zeros(6 * mb, dtype=i32, device=dv)
+        # Static graph inputs live in ONE device buffer whose layout mirrors a pinned
+        # host staging image, so a decode step refreshes all its inputs with one async
+        # H2D copy (each copy is a blit launch, and the GPU idled ~20 us in front of
+        # each of the four it used to take: profiles/prof_driver_config_r02b.txt).
+        # int32 fields: ids | pos | slots | seq_lens | top_k | steps, then temperature |
+        # top_p (f32), seeds (int64), block tables
+        self.d_in = torch.zeros(input_words(mb, self.max_blocks_per_seq), dtype=i32, device=dv)
+        self.d_small, self.d_f32, self.d_seeds, self.d_bt = _input_views(self.d_in, mb, self.max_blocks_per_seq)
         self.d_input_ids = self.d_small[0:mb]
         self.d_positions = self.d_small[mb:2 * mb]
         self.d_slots = self.d_small[2 * mb:3 * mb]
         self.d_seq_lens = self.d_small[3 * mb:4 * mb]
         self.d_top_k = self.d_small[4 * mb:5 * mb]
         self.d_steps = self.d_small[5 * mb:6 * mb]
-        self.d_bt = torch.zeros(mb, self.max_blocks_per_seq, dtype=i32, device=dv)
-        self.d_f32 = torch.zeros(2 * mb, dtype=torch.float32, device=dv)
         self.d_temp = self.d_f32[0:mb]
         self.d_top_p = self.d_f32[mb:2 * mb]
-        self.d_seeds = torch.zeros(mb, dtype=torch.int64, device=dv)
         self.d_out = torch.zeros(mb, dtype=i32, device=dv)
         # two pinned staging sets: while decode step n runs, step n+1 is filled
         # and queued behind it from the other set (pipelined decode)
         self.stg = [_Staging(mb, self.max_blocks_per_seq, pin, self.is_gpu) for _ in range(2)]
         self._stg_next = 0
+        self._upload = _Uploader(dv, pin) if self.is_gpu else None
         self.h_out = torch.zeros(mb, dtype=i32, pin_memory=pin)  # eager-step sampler output
         self.h_err = torch.zeros(1, dtype=i32, pin_memory=pin)
         # TP rank 0 decides about collective faults; workers only follow its messages
@@ -156,11 +227,11 @@ class ModelRunner:
                                            waves=None if self.is_gpu else 0)
         self.tmp_out = torch.empty(max(1, n_out), dtype=torch.float32, device=dv)
         self.tmp_ml = torch.empty(max(1, n_ml), dtype=torch.float32, device=dv)
-        # in-launch combine tickets, opt-in (FT_DECODE_FUSED_COMBINE=1): measured slower
-        # than the separate combine kernel at 50 sessions (12.3 vs 10.9 ms/step: the last
-        # arriver's write-through (sc1) partial loads are latency-bound), kept for A/B
+        # in-launch combine tickets (FT_DECODE_FUSED_COMBINE=0: separate combine kernel):
+        # with the kernel at one workgroup per CU the last-arriver merge matches or beats
+        # the combine kernel and saves a launch per layer (csrc/kernels/attn_decode.hip)
         self.dec_counters = ops.decode_counters(self.max_decode_rows, self.model.nkv, dv) \
-            if self.is_gpu and os.environ.get("FT_DECODE_FUSED_COMBINE", "0") == "1" else None
+            if self.is_gpu and os.environ.get("FT_DECODE_FUSED_COMBINE", "1") == "1" else None
         self._done_event = torch.cuda.Event() if self.is_gpu else None
         self.graphs: Dict[int, torch.cuda.CUDAGraph] = {}
         self.graph_pool = None
@@ -339,27 +410,40 @@ class ModelRunner:
     def _mixed_run(self, host: Dict[str, object], masks) -> List[int]:
         self.stats["prefill_steps"] += 1
         nd = host["nd"]
-        dv = self.device
-        t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dv, non_blocking=True)  # noqa: E731
         qsl = host["qsl"]
-        meta = AttnMeta(
-            positions=t(host["pos"]), slot_mapping=t(host["slots"]),
-            logits_indices=t(host["lrows"]), num_decode=nd,
-            block_tables=t(host["bt"]), seq_lens=t(host["seq_lens"]),
-            q_start_loc=t(qsl) if self.is_gpu else torch.from_numpy(qsl),
-            tile_info=t(host["tiles"]), num_tiles=host["num_tiles"])
+        names = ["pos", "slots", "lrows", "bt", "seq_lens", "qsl", "tiles", "ids"]
         if nd:
             if nd > self.max_decode_rows:
                 raise ValueError(f"{nd} decode rows exceed max_num_seqs {self.max_decode_rows}")
-            meta.dec_block_tables = t(host["d_bt"])
-            meta.dec_seq_lens = t(host["d_sl"])
+            names += ["d_bt", "d_sl"]
+        arrays = [host[k] for k in names]
+        has_logits = len(host["lrows"]) > 0
+        if has_logits:
+            arrays += list(host["sampling"])
+            if masks is not None:
+                arrays.append(masks)
+        if self.is_gpu:
+            dev = self._upload(arrays)
+        else:
+            dev = [torch.from_numpy(np.ascontiguousarray(a)) for a in arrays]
+        d = dict(zip(names, dev))
+        meta = AttnMeta(
+            positions=d["pos"], slot_mapping=d["slots"], logits_indices=d["lrows"], num_decode=nd,
+            block_tables=d["bt"], seq_lens=d["seq_lens"],
+            q_start_loc=d["qsl"] if self.is_gpu else torch.from_numpy(qsl),
+            tile_info=d["tiles"], num_tiles=host["num_tiles"])
+        if nd:
+            meta.dec_block_tables = d["d_bt"]
+            meta.dec_seq_lens = d["d_sl"]
             meta.tmp_out, meta.tmp_ml = self.tmp_out, self.tmp_ml
             meta.dec_counters = self.dec_counters
-        input_ids = t(host["ids"])
-        h = self.model.forward(input_ids, meta, self.kv)
-        if len(host["lrows"]) == 0:
+        h = self.model.forward(d["ids"], meta, self.kv)
+        if not has_logits:
             return []
-        return self._sample(h, host["sampling"], masks)
+        k = len(names)
+        samp = dev[k:k + 5]
+        dmask = dev[k + 5] if masks is not None else None
+        return self._sample(h, host["sampling"], masks, dev_sampling=samp, dev_mask=dmask)
 
     def _wait(self, ev=None):
         """Block until the GPU work queued so far (or up to ``ev``) is done WITHOUT
@@ -373,16 +457,18 @@ class ModelRunner:
             time.sleep(0.0001)
         self.stats["wait_ms"] = self.stats.get("wait_ms", 0.0) + 1e3 * (time.perf_counter() - t0)
 
-    def _sample(self, h, sampling, masks) -> List[int]:
+    def _sample(self, h, sampling, masks, dev_sampling=None, dev_mask=None) -> List[int]:
         logits = self.model.compute_logits(h)
-        temp, topp, topk, seeds, steps = sampling
-        dv = self.device
-        m = None
-        if masks is not None:
-            m = torch.from_numpy(masks).to(dv)
-        out = ops.sample(logits, torch.from_numpy(temp).to(dv), torch.from_numpy(topp).to(dv),
-                         torch.from_numpy(topk).to(dv), torch.from_numpy(seeds).to(dv),
-                         torch.from_numpy(steps).to(dv), mask=m)
+        if dev_sampling is None:
+            arrays = list(sampling) + ([masks] if masks is not None else [])
+            if self.is_gpu:
+                dev = self._upload(arrays)
+            else:
+                dev = [torch.from_numpy(np.ascontiguousarray(a)) for a in arrays]
+            dev_sampling = dev[:5]
+            dev_mask = dev[5] if masks is not None else None
+        temp, topp, topk, seeds, steps = dev_sampling
+        out = ops.sample(logits, temp, topp, topk, seeds, steps, mask=dev_mask)
         if not self.is_gpu:
             return out.tolist()
         n = out.shape[0]
@@ -525,10 +611,8 @@ class ModelRunner:
         return maxblk
 
     def _decode_enqueue(self, st: "_Staging", nb: int, n: int, from_device: bool = False):
-        self.d_small.copy_(st.h_small, non_blocking=True)
-        self.d_bt[:nb].copy_(st.h_bt[:nb], non_blocking=True)
-        self.d_f32.copy_(st.h_f32, non_blocking=True)
-        self.d_seeds.copy_(st.h_seeds, non_blocking=True)
+        nw = 10 * self.max_decode_batch + nb * self.max_blocks_per_seq
+        self.d_in[:nw].copy_(st.h_in[:nw], non_blocking=True)
         if from_device:  # the previous step's sampled ids feed this step
             self.d_input_ids[:nb].copy_(self.d_out[:nb])
         g = self.graphs.get(nb)
