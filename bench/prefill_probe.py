@@ -39,18 +39,25 @@ def main():
         qsl = torch.arange(0, S * Q + 1, Q, dtype=torch.int32)
         T = S * Q
         q = torch.randn(T, nq * d, device=dev).bfloat16()
-        tiles = ops.build_prefill_tiles([Q] * S, ops.prefill_tile_tokens(nq, nkv))
+        tiles, comb = ops.build_prefill_tiles([Q] * S, ops.prefill_tile_tokens(nq, nkv),
+                                              seq_lens=None if os.environ.get("NOSPLIT") else [L] * S,
+                                              nkv=nkv)
         ti = torch.tensor(tiles, dtype=torch.int32, device=dev).flatten()
+        n_po, n_pml = ops.prefill_partials(nkv, d)
+        po, pml = torch.empty(n_po, device=dev), torch.empty(n_pml, device=dev)
+        cb = torch.tensor(comb or [[0, 0, 0, 0]], dtype=torch.int32, device=dev).flatten()
+        npart = sum(c[3] for c in comb)
         out = torch.empty(T, nq * d, device=dev).bfloat16()
         qd = qsl.to(dev)
         us = timeit(lambda: ops.prefill_attention(out, q, kc, vc, bt, sl, qd, ti, len(tiles), nq, nkv,
-                                                  d, d ** -0.5), iters=20, warmup=3)
+                                                  d, d ** -0.5, po, pml, cb, len(comb), npart),
+                    iters=20, warmup=3)
         # causal FLOPs: each new token attends to C + its position in the chunk
         flops = 4 * d * nq * S * sum(C + i + 1 for i in range(Q))
         kv_bytes = S * L * nkv * d * 2 * 2
         print(json.dumps({"seqs": S, "new": Q, "ctx": C, "us": round(us, 1),
                           "TFLOPs": round(flops / us / 1e6, 1),
-                          "KV_GBps": round(kv_bytes / us / 1e3, 1), "wgs": len(tiles) * nkv}),
+                          "KV_GBps": round(kv_bytes / us / 1e3, 1), "wgs": len(tiles) * nkv, "splits": npart}),
               flush=True)
         del kc, vc
 

@@ -29,7 +29,8 @@ int ft_prefill_attention(void* out, int out_stride, const void* q, int q_stride,
                          const void* k_cache, const void* v_cache, const int* block_tables,
                          int bt_stride, const int* seq_lens, const int* q_start_loc,
                          const int* tile_info, int num_tiles, int nq, int nkv, int head_dim,
-                         int block_size, float scale, hipStream_t stream);
+                         int block_size, float scale, float* part_o, float* part_ml,
+                         const int* combine, int num_combine, hipStream_t stream);
 int ft_sample(int* out_tokens, const void* logits, int logits_is_bf16, long logit_stride,
               int batch, int vocab, const float* temperature, const float* top_p,
               const int* top_k, const long long* seeds, const int* steps,
@@ -228,7 +229,9 @@ void paged_decode_attention(at::Tensor out, at::Tensor q, at::Tensor k_cache, at
 void prefill_attention(at::Tensor out, at::Tensor q, at::Tensor k_cache, at::Tensor v_cache,
                        at::Tensor block_tables, at::Tensor seq_lens, at::Tensor q_start_loc,
                        at::Tensor tile_info, int64_t num_tiles, int64_t nq, int64_t nkv,
-                       int64_t head_dim, double scale) {
+                       int64_t head_dim, double scale, c10::optional<at::Tensor> part_o,
+                       c10::optional<at::Tensor> part_ml, c10::optional<at::Tensor> combine,
+                       int64_t num_combine, int64_t num_partials) {
   check_bf16(out, "out");
   check_bf16(q, "q");
   check_rows(out, "out");
@@ -240,13 +243,34 @@ void prefill_attention(at::Tensor out, at::Tensor q, at::Tensor k_cache, at::Ten
   check_i32(tile_info, "tile_info");
   // the prefill kernel stages a sequence's block-table row in LDS (4096 entries)
   TORCH_CHECK(block_tables.size(1) <= 4096, "prefill: at most 4096 KV blocks per sequence");
-  TORCH_CHECK(tile_info.numel() >= 2 * num_tiles, "tile_info too small");
+  // work items: (sequence, first query token, KV tile range, partial slot)
+  TORCH_CHECK(tile_info.numel() >= 4 * num_tiles, "tile_info too small");
+  float* po = nullptr;
+  float* pml = nullptr;
+  const int* cb = nullptr;
+  if (num_partials > 0 || num_combine > 0) {
+    TORCH_CHECK(part_o.has_value() && part_ml.has_value() && combine.has_value(),
+                "split-KV prefill needs part_o, part_ml and combine");
+    TORCH_CHECK(part_o->scalar_type() == at::kFloat && part_ml->scalar_type() == at::kFloat,
+                "partials fp32");
+    check_dev(*part_o, "part_o");
+    check_dev(*part_ml, "part_ml");
+    check_i32(*combine, "combine");
+    // partial slots hold 256 rows (token x GQA head) of D floats per kv head
+    TORCH_CHECK(part_o->numel() >= num_partials * nkv * 256 * head_dim, "part_o too small");
+    TORCH_CHECK(part_ml->numel() >= num_partials * nkv * 256 * 2, "part_ml too small");
+    TORCH_CHECK(combine->numel() >= 4 * num_combine, "combine too small");
+    po = part_o->data_ptr<float>();
+    pml = part_ml->data_ptr<float>();
+    cb = combine->data_ptr<int>();
+  }
   check_rc(ft_prefill_attention(out.data_ptr(), (int)out.stride(0), q.data_ptr(),
                                 (int)q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
                                 block_tables.data_ptr<int>(), (int)block_tables.stride(0),
                                 seq_lens.data_ptr<int>(), q_start_loc.data_ptr<int>(),
                                 tile_info.data_ptr<int>(), (int)num_tiles, (int)nq, (int)nkv,
-                                (int)head_dim, (int)k_cache.size(2), (float)scale, cur_stream()),
+                                (int)head_dim, (int)k_cache.size(2), (float)scale, po, pml, cb,
+                                (int)num_combine, cur_stream()),
            "prefill_attention");
 }
 

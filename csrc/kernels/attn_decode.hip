@@ -493,7 +493,7 @@ extern "C" int ft_paged_decode_attention(void* out, int out_stride, float* tmp_o
     return (r >= 2 && r <= 4) ? r : 2;
   }();
   // 1 workgroup per CU, or the register-limited maximum for the ring depth
-  const int wpc = dec_wg_per_cu() == 1 ? 1 : (ring == 2 ? 3 : 2);
+  const int wpc = min(dec_wg_per_cu(), ring == 2 ? 3 : 2);
   int nwg = 0;
 #define FT_DEC_LAUNCH(DD, GG, RR, FCC)                                                         \
   if (wpc == 1)                                                                                \

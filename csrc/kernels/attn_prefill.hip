@@ -29,6 +29,14 @@
 //   computes (counted vmcnt + raw s_barrier; a __syncthreads would drain the
 //   DMA).  The block-table entries of the KV range are copied to LDS once, so
 //   issuing a tile never waits on a table read.
+// * Split-KV (flash-decoding for prefill): a chat turn prefills ~100 tokens over a
+//   history of thousands, i.e. 2 query blocks per sequence -- a mixed step of ~10
+//   prompts was 160 workgroups on 256 CUs, each streaming the whole history alone
+//   (213 us per layer at the driver config, 0.25 PFLOP/s).  A work item is now
+//   (query block, KV tile range): long ranges are split over several workgroups
+//   (host plan, ops.build_prefill_tiles), each leaves fp32 (O, m, l) partials and
+//   prefill_combine_kernel merges them; items covering the whole range still
+//   write bf16 directly.
 #include "ft_common.h"
 #include "ft_lds.h"
 
@@ -61,7 +69,7 @@ __global__ __launch_bounds__(512, 1) void prefill_attn_kernel(
     const uint16_t* __restrict__ k_cache, const uint16_t* __restrict__ v_cache,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ seq_lens,
     const int* __restrict__ q_start_loc, const int* __restrict__ tile_info, int nkv,
-    int block_size, float scale_log2) {
+    int block_size, float scale_log2, float* __restrict__ part_o, float* __restrict__ part_ml) {
   constexpr int NCH = D / 8;          // 16-B chunks per K row
   constexpr int KC = D / 32;          // k-steps of S^T = K Q^T
   constexpr int ND = D / 16;          // 16-row dim tiles of O^T
@@ -79,8 +87,11 @@ __global__ __launch_bounds__(512, 1) void prefill_attn_kernel(
 
   const int tile = blockIdx.x;
   const int kvh = blockIdx.y;
-  const int b = tile_info[tile * 2];
-  const int qs = tile_info[tile * 2 + 1];
+  // work item: (sequence, first query token, KV tile range lo << 16 | hi, partial slot)
+  const int b = tile_info[tile * 4];
+  const int qs = tile_info[tile * 4 + 1];
+  const int krange = tile_info[tile * 4 + 2];
+  const int pslot = tile_info[tile * 4 + 3];   // < 0: the item covers the whole range
   const int L = seq_lens[b];
   const int q0 = q_start_loc[b];
   const int qlen = q_start_loc[b + 1] - q0;
@@ -126,7 +137,8 @@ __global__ __launch_bounds__(512, 1) void prefill_attn_kernel(
   }
 
   const int kv_end = min(L, ctx0 + qs + ntok);  // exclusive
-  const int ntiles = (kv_end + kPrefillBK - 1) / kPrefillBK;
+  const int kt_lo = krange >> 16;
+  const int ntiles = min((kv_end + kPrefillBK - 1) / kPrefillBK, krange & 0xffff);
   const int first_q = ctx0 + qs;                // lowest query position of the block
   const int* bt = block_tables + (size_t)b * bt_stride;
   const size_t head_off = (size_t)kvh * block_size * D;
@@ -298,8 +310,8 @@ __global__ __launch_bounds__(512, 1) void prefill_attn_kernel(
 
 #pragma unroll
   for (int t = 0; t < NSLOT - 1; ++t)
-    if (t < ntiles) issue_tile(t, t);
-  for (int kt = 0; kt < ntiles; ++kt) {
+    if (kt_lo + t < ntiles) issue_tile(kt_lo + t, (kt_lo + t) % NSLOT);
+  for (int kt = kt_lo; kt < ntiles; ++kt) {
     const int slot = kt % NSLOT;
     const int ahead = min(ntiles - 1 - kt, NSLOT - 1);   // tiles in flight behind tile kt
     if (kt + NSLOT - 1 < ntiles)
@@ -322,6 +334,16 @@ __global__ __launch_bounds__(512, 1) void prefill_attn_kernel(
     const float l = kgroup_sum(l_run[m]);
     if (qpos[m] < 0) continue;
     const int r = (wave * MT + m) * 16 + l15;
+    if (pslot >= 0) {   // split item: unnormalised fp32 O + (m, l) of row r
+      float* po = part_o + (((size_t)pslot * nkv + kvh) * kPrefillRows + r) * D + 4 * lg;
+#pragma unroll
+      for (int nd = 0; nd < ND; ++nd)
+        *reinterpret_cast<float4*>(po + nd * 16) = make_float4(o[m][nd][0], o[m][nd][1], o[m][nd][2], o[m][nd][3]);
+      if (lg == 0)
+        *reinterpret_cast<float2*>(part_ml + (((size_t)pslot * nkv + kvh) * kPrefillRows + r) * 2) =
+            make_float2(m_run[m], l);
+      continue;
+    }
     const int tq = r / G, g = r - (r / G) * G;
     const float inv = l > 0.f ? 1.f / l : 0.f;
     uint16_t* op = out + (size_t)(q0 + qs + tq) * out_stride + (kvh * G + g) * D + 4 * lg;
@@ -333,6 +355,60 @@ __global__ __launch_bounds__(512, 1) void prefill_attn_kernel(
   }
 }
 
+// Merges the split items of one (query block, kv head): combine entry = (sequence,
+// first query token, first partial slot, number of splits).  One thread per (row,
+// 4 dims): 256 / (D / 4) rows per workgroup, grid.z covers the 256 rows, so the
+// merge is a wide parallel pass (a wave per row with dependent split loads was
+// latency-bound at ~100 us).  Online-max merge, the next split's loads in flight.
+template <int D, int G>
+__global__ __launch_bounds__(256) void prefill_combine_kernel(
+    uint16_t* __restrict__ out, int out_stride, const float* __restrict__ part_o,
+    const float* __restrict__ part_ml, const int* __restrict__ q_start_loc,
+    const int* __restrict__ combine, int nkv) {
+  constexpr int QB = kPrefillRows / G;
+  constexpr int CH = D / 4;                 // float4 chunks per row
+  constexpr int RPB = 256 / CH;             // rows per workgroup
+  const int c = blockIdx.x, kvh = blockIdx.y;
+  const int b = combine[c * 4], qs = combine[c * 4 + 1], s0 = combine[c * 4 + 2], ns = combine[c * 4 + 3];
+  const int q0 = q_start_loc[b];
+  const int ntok = min(QB, q_start_loc[b + 1] - q0 - qs);
+  const int r = blockIdx.z * RPB + threadIdx.x / CH;
+  const int ch = threadIdx.x % CH;
+  if (r >= ntok * G) return;
+  const size_t stride = (size_t)nkv * kPrefillRows;          // rows between slots
+  size_t row = ((size_t)s0 * nkv + kvh) * kPrefillRows + r;
+  float M = -INFINITY, den = 0.f;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  float2 ml = *reinterpret_cast<const float2*>(part_ml + row * 2);
+  float4 v = *reinterpret_cast<const float4*>(part_o + row * D + 4 * ch);
+  for (int k = 0; k < ns; ++k) {
+    float2 ml_n = ml;
+    float4 v_n = v;
+    if (k + 1 < ns) {   // next split's loads before this one's math
+      const size_t rn = row + stride;
+      ml_n = *reinterpret_cast<const float2*>(part_ml + rn * 2);
+      v_n = *reinterpret_cast<const float4*>(part_o + rn * D + 4 * ch);
+    }
+    if (ml.x != -INFINITY) {   // a split wholly above this row's position adds nothing
+      const float mn = fmaxf(M, ml.x);
+      const float a = exp2f(M - mn), e = exp2f(ml.x - mn);
+      den = den * a + e * ml.y;
+      acc.x = acc.x * a + e * v.x;
+      acc.y = acc.y * a + e * v.y;
+      acc.z = acc.z * a + e * v.z;
+      acc.w = acc.w * a + e * v.w;
+      M = mn;
+    }
+    ml = ml_n;
+    v = v_n;
+    row += stride;
+  }
+  const float inv = den > 0.f ? 1.f / den : 0.f;
+  const int tq = r / G, g = r - (r / G) * G;
+  *reinterpret_cast<uint2*>(out + (size_t)(q0 + qs + tq) * out_stride + (kvh * G + g) * D + 4 * ch) =
+      make_uint2(pack2(acc.x * inv, acc.y * inv), pack2(acc.z * inv, acc.w * inv));
+}
+
 }  // namespace ft
 
 extern "C" int ft_prefill_tile_tokens(int nq, int nkv) { return ft::kPrefillRows / (nq / nkv); }
@@ -342,9 +418,11 @@ extern "C" int ft_prefill_attention(void* out, int out_stride, const void* q, in
                                     const int* block_tables, int bt_stride, const int* seq_lens,
                                     const int* q_start_loc, const int* tile_info, int num_tiles,
                                     int nq, int nkv, int head_dim, int block_size, float scale,
-                                    hipStream_t stream) {
+                                    float* part_o, float* part_ml, const int* combine,
+                                    int num_combine, hipStream_t stream) {
   if (num_tiles <= 0) return 0;
   if (nq % nkv != 0) return -1;
+  if (num_combine > 0 && (part_o == nullptr || part_ml == nullptr || combine == nullptr)) return -3;
   const int G = nq / nkv;
   const float scale_log2 = scale * 1.4426950408889634f;
   dim3 grid(num_tiles, nkv), block(512);
@@ -354,7 +432,12 @@ extern "C" int ft_prefill_attention(void* out, int out_stride, const void* q, in
                        (uint16_t*)out, out_stride, (const uint16_t*)q, q_stride,             \
                        (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables,     \
                        bt_stride, seq_lens, q_start_loc, tile_info, nkv, block_size,         \
-                       scale_log2);                                                          \
+                       scale_log2, part_o, part_ml);                                         \
+    if (num_combine > 0)                                                                     \
+      hipLaunchKernelGGL((ft::prefill_combine_kernel<DD, GG>),                               \
+                         dim3(num_combine, nkv, ft::kPrefillRows / (256 / (DD / 4))),         \
+                         dim3(256), 0, stream, (uint16_t*)out, out_stride, part_o, part_ml,  \
+                         q_start_loc, combine, nkv);                                         \
     return static_cast<int>(hipGetLastError());                                              \
   }
   FT_PF_CASE(128, 1)

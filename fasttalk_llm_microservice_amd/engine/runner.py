@@ -227,6 +227,14 @@ class ModelRunner:
                                            waves=None if self.is_gpu else 0)
         self.tmp_out = torch.empty(max(1, n_out), dtype=torch.float32, device=dv)
         self.tmp_ml = torch.empty(max(1, n_ml), dtype=torch.float32, device=dv)
+        # split-KV prefill partials (ops.build_prefill_tiles): 128 slots = 128 MiB fp32
+        # for Llama-3-8B; FT_PREFILL_SPLIT=0 keeps one workgroup per query block
+        self.num_cus = torch.cuda.get_device_properties(dv).multi_processor_count if self.is_gpu else 256
+        self.pf_part_o = self.pf_part_ml = None
+        if self.is_gpu and os.environ.get("FT_PREFILL_SPLIT", "1") == "1":
+            n_po, n_pml = ops.prefill_partials(self.model.nkv, d)
+            self.pf_part_o = torch.empty(n_po, dtype=torch.float32, device=dv)
+            self.pf_part_ml = torch.empty(n_pml, dtype=torch.float32, device=dv)
         # in-launch combine tickets (FT_DECODE_FUSED_COMBINE=0: separate combine kernel):
         # with the kernel at one workgroup per CU the last-arriver merge matches or beats
         # the combine kernel and saves a launch per layer (csrc/kernels/attn_decode.hip)
@@ -396,13 +404,18 @@ class ModelRunner:
             slots.append(blk[p // bs] * bs + p % bs)
             seq_lens[i] = a + n
             qsl[i + 1] = qsl[i] + n
-        tiles = ops.build_prefill_tiles(ntoks, ops.prefill_tile_tokens(self.model.nq, self.model.nkv))
+        tiles, combine = ops.build_prefill_tiles(
+            ntoks, ops.prefill_tile_tokens(self.model.nq, self.model.nkv),
+            seq_lens=seq_lens if self.pf_part_o is not None else None, nkv=self.model.nkv,
+            num_cus=self.num_cus)
         # logits rows: every decode row + the last row of each prompt that completes
         lrows = list(range(nd)) + [nd + int(qsl[i + 1]) - 1 for i, sm in enumerate(psamp) if sm]
         host.update(ids=np.concatenate(ids).astype(np.int32), pos=np.concatenate(pos).astype(np.int32),
                     slots=np.concatenate(slots).astype(np.int32), lrows=np.asarray(lrows, np.int64),
                     bt=bt, seq_lens=seq_lens, qsl=qsl, tiles=np.asarray(tiles, np.int32).reshape(-1),
-                    num_tiles=len(tiles))
+                    num_tiles=len(tiles), combine=np.asarray(combine, np.int32).reshape(-1),
+                    num_combine=len(combine),
+                    num_partials=sum(c[3] for c in combine))
         sseqs = dseqs + [s for s, sm in zip(pseqs, psamp) if sm]
         host["sampling"] = self._sampling_arrays(sseqs)
         return host
@@ -411,7 +424,7 @@ class ModelRunner:
         self.stats["prefill_steps"] += 1
         nd = host["nd"]
         qsl = host["qsl"]
-        names = ["pos", "slots", "lrows", "bt", "seq_lens", "qsl", "tiles", "ids"]
+        names = ["pos", "slots", "lrows", "bt", "seq_lens", "qsl", "tiles", "ids", "combine"]
         if nd:
             if nd > self.max_decode_rows:
                 raise ValueError(f"{nd} decode rows exceed max_num_seqs {self.max_decode_rows}")
@@ -432,6 +445,10 @@ class ModelRunner:
             block_tables=d["bt"], seq_lens=d["seq_lens"],
             q_start_loc=d["qsl"] if self.is_gpu else torch.from_numpy(qsl),
             tile_info=d["tiles"], num_tiles=host["num_tiles"])
+        if host.get("num_combine", 0):
+            meta.pf_part_o, meta.pf_part_ml = self.pf_part_o, self.pf_part_ml
+            meta.pf_combine, meta.pf_num_combine = d["combine"], host["num_combine"]
+            meta.pf_num_partials = host["num_partials"]
         if nd:
             meta.dec_block_tables = d["d_bt"]
             meta.dec_seq_lens = d["d_sl"]

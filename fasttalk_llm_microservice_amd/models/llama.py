@@ -49,8 +49,13 @@ class AttnMeta:
     block_tables: Optional[torch.Tensor] = None       # [P, max_blocks]
     seq_lens: Optional[torch.Tensor] = None           # [P] kv length after this step
     q_start_loc: Optional[torch.Tensor] = None        # [P+1], relative to row num_decode
-    tile_info: Optional[torch.Tensor] = None          # [num_tiles*2]
+    tile_info: Optional[torch.Tensor] = None          # [num_tiles*4] (ops.build_prefill_tiles)
     num_tiles: int = 0
+    pf_part_o: Optional[torch.Tensor] = None          # split-KV prefill partials + combine list
+    pf_part_ml: Optional[torch.Tensor] = None
+    pf_combine: Optional[torch.Tensor] = None
+    pf_num_combine: int = 0
+    pf_num_partials: int = 0
 
     @property
     def is_prefill(self) -> bool:
@@ -655,7 +660,8 @@ class LlamaModel:
         if t > nd:
             ops.prefill_attention(attn[nd:], qkv[nd:], kc, vc, meta.block_tables, meta.seq_lens,
                                   meta.q_start_loc, meta.tile_info, meta.num_tiles, nq, nkv, d,
-                                  self.scale)
+                                  self.scale, meta.pf_part_o, meta.pf_part_ml, meta.pf_combine,
+                                  meta.pf_num_combine, meta.pf_num_partials)
         return attn
 
     def _forward_fused(self, input_ids: torch.Tensor, meta: AttnMeta, kv_caches) -> torch.Tensor:

@@ -160,10 +160,16 @@ def decode_attention(out, q, k_cache, v_cache, block_tables, seq_lens, tmp_out, 
 
 
 def prefill_attention(out, q, k_cache, v_cache, block_tables, seq_lens, q_start_loc, tile_info,
-                      num_tiles, nq, nkv, head_dim, scale):
+                      num_tiles, nq, nkv, head_dim, scale, part_o=None, part_ml=None, combine=None,
+                      num_combine: int = 0, num_partials: int = 0):
+    """Varlen causal attention of the new tokens over their paged history.
+    ``tile_info``: the work items of build_prefill_tiles (4 int32 each); split-KV
+    items leave fp32 partials in ``part_o`` / ``part_ml`` (prefill_partials) that
+    the ``combine`` list merges (csrc/kernels/attn_prefill.hip)."""
     if q.is_cuda:
         native().prefill_attention(out, q, k_cache, v_cache, block_tables, seq_lens, q_start_loc,
-                                   tile_info, num_tiles, nq, nkv, head_dim, scale)
+                                   tile_info, num_tiles, nq, nkv, head_dim, scale, part_o, part_ml,
+                                   combine, num_combine, num_partials)
         return out
     t = q.shape[0]
     qq = q[:, : nq * head_dim].reshape(t, nq, head_dim)
@@ -172,13 +178,57 @@ def prefill_attention(out, q, k_cache, v_cache, block_tables, seq_lens, q_start_
     return out
 
 
-def build_prefill_tiles(q_lens, tile_tokens: int):
-    """Host-side tile list [(seq, q_offset)] for the prefill kernel grid."""
-    tiles = []
+PREFILL_BK = 64          # KV tokens per tile of the prefill kernel
+PREFILL_ROWS = 256       # MFMA rows (query token x GQA head) per work item
+PREFILL_MAX_PARTIALS = 128
+
+
+def prefill_partials(nkv: int, head_dim: int, max_partials: int = PREFILL_MAX_PARTIALS):
+    """(part_o, part_ml) fp32 element counts of the split-KV workspace."""
+    return max_partials * nkv * PREFILL_ROWS * head_dim, max_partials * nkv * PREFILL_ROWS * 2
+
+
+def build_prefill_tiles(q_lens, tile_tokens: int, seq_lens=None, nkv: int = 8, num_cus: int = 256,
+                        max_partials: int = PREFILL_MAX_PARTIALS, min_split_tiles: int = 4):
+    """Host plan of the prefill kernel grid: (items, combine).
+
+    items: [(seq, first query token, kv_lo_tile << 16 | kv_hi_tile, partial slot)],
+    one per (query block, KV range); combine: [(seq, first query token, first slot,
+    splits)] for query blocks whose KV range is split over several workgroups.
+    Without ``seq_lens`` (or when every block is its own workgroup anyway) no
+    range is split.  A chat turn prefills ~100 tokens over thousands of cached
+    ones: ~2 query blocks per prompt, so a 10-prompt step would be 160 workgroups
+    each streaming a whole history alone -- the ranges are cut so the grid has
+    about 2 workgroups per CU (at least ``min_split_tiles`` 64-token tiles each)."""
+    blocks = []
     for b, ql in enumerate(q_lens):
-        for s in range(0, int(ql), tile_tokens):
-            tiles.append((b, s))
-    return tiles
+        ql = int(ql)
+        for s in range(0, ql, tile_tokens):
+            if seq_lens is None:
+                nkt = 0
+            else:
+                L = int(seq_lens[b])
+                kv_end = min(L, L - ql + s + min(tile_tokens, ql - s))
+                nkt = (kv_end + PREFILL_BK - 1) // PREFILL_BK
+            blocks.append((b, s, nkt))
+    items, combine = [], []
+    target = max(1, 2 * num_cus // max(1, nkv))
+    total = sum(n for _, _, n in blocks)
+    chunk = 0
+    if seq_lens is not None and len(blocks) < target and total > 0:
+        chunk = max(min_split_tiles, -(-total // target))
+    slots = 0
+    for b, s, nkt in blocks:
+        ns = -(-nkt // chunk) if chunk else 1
+        if ns > 1 and slots + ns <= max_partials:
+            combine.append((b, s, slots, ns))
+            for j in range(ns):
+                lo, hi = j * nkt // ns, (j + 1) * nkt // ns
+                items.append((b, s, (lo << 16) | hi, slots + j))
+            slots += ns
+        else:
+            items.append((b, s, 0xFFFF, -1))
+    return items, combine
 
 
 # ---------------------------------------------------------------------------------

@@ -59,7 +59,7 @@ def test_gpu_logits_match_cpu_reference(model, quant, T, fused_rows, monkeypatch
             seq_lens=torch.tensor([T], dtype=torch.int32, device=dev),
             logits_indices=torch.arange(T, device=dev),
             q_start_loc=torch.tensor([0, T], dtype=torch.int32, device=dev if m is g else "cpu"),
-            tile_info=torch.tensor([[0, s] for s in range(0, T, 16)], dtype=torch.int32,
+            tile_info=torch.tensor([[0, s, 0xFFFF, -1] for s in range(0, T, 16)], dtype=torch.int32,
                                    device=dev).flatten(),
             num_tiles=len(range(0, T, 16)))
         h = m.forward(ids, meta, kv)

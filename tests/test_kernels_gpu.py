@@ -147,12 +147,11 @@ def test_decode_attention_block_sizes(bs):
     _close(out, expect, atol=2e-2, rtol=2e-2, msg=f"decode attention bs={bs}")
 
 
-@pytest.mark.parametrize("nq,nkv,d", [(32, 8, 128), (24, 8, 128), (64, 8, 128), (32, 8, 64),
-                                      (8, 8, 128)])
-def test_prefill_attention(nq, nkv, d):
+def _prefill_run(seqs, nq, nkv, d, split, num_cus=256, seed=0):
+    """(out, expect) of the prefill kernel over (new tokens, cached prefix) pairs;
+    split: plan split-KV items (partials + combine) with this many CUs."""
+    torch.manual_seed(seed)
     bs = 16
-    # (new tokens, cached prefix)
-    seqs = [(1, 0), (5, 0), (64, 0), (77, 33), (16, 300), (130, 1), (3, 500)]
     lens = [a + p for a, p in seqs]
     nblocks = sum((l + bs - 1) // bs for l in lens) + 4
     k, v = _alloc_cache(nblocks, nkv, bs, d)
@@ -162,13 +161,45 @@ def test_prefill_attention(nq, nkv, d):
     qsl = torch.tensor([0] + list(torch.tensor(qlens).cumsum(0)), dtype=torch.int32)
     t = int(qsl[-1])
     q = torch.randn(t, nq * d, device=DEV).bfloat16()
-    tiles = ops.build_prefill_tiles(qlens, ops.prefill_tile_tokens(nq, nkv))
+    tiles, comb = ops.build_prefill_tiles(qlens, ops.prefill_tile_tokens(nq, nkv),
+                                          seq_lens=lens if split else None, nkv=nkv, num_cus=num_cus,
+                                          min_split_tiles=1)
+    assert bool(comb) == bool(split), comb
     ti = torch.tensor(tiles, dtype=torch.int32, device=DEV).flatten()
     out = torch.zeros(t, nq * d, device=DEV).bfloat16()
     scale = d ** -0.5
-    ops.prefill_attention(out, q, k, v, bt, sl, qsl.to(DEV), ti, len(tiles), nq, nkv, d, scale)
+    if comb:
+        n_po, n_pml = ops.prefill_partials(nkv, d)
+        po = torch.full((n_po,), float("nan"), device=DEV)
+        pml = torch.full((n_pml,), float("nan"), device=DEV)
+        cb = torch.tensor(comb, dtype=torch.int32, device=DEV).flatten()
+        ops.prefill_attention(out, q, k, v, bt, sl, qsl.to(DEV), ti, len(tiles), nq, nkv, d, scale,
+                              po, pml, cb, len(comb), sum(c[3] for c in comb))
+    else:
+        ops.prefill_attention(out, q, k, v, bt, sl, qsl.to(DEV), ti, len(tiles), nq, nkv, d, scale)
     expect = ref.paged_attention(q.view(t, nq, d), k, v, bt, sl, qsl, scale).view(t, nq * d)
+    return out, expect
+
+
+@pytest.mark.parametrize("nq,nkv,d", [(32, 8, 128), (24, 8, 128), (64, 8, 128), (32, 8, 64),
+                                      (8, 8, 128)])
+def test_prefill_attention(nq, nkv, d):
+    # (new tokens, cached prefix)
+    seqs = [(1, 0), (5, 0), (64, 0), (77, 33), (16, 300), (130, 1), (3, 500)]
+    out, expect = _prefill_run(seqs, nq, nkv, d, split=False)
     _close(out, expect, atol=2e-2, rtol=2e-2, msg="prefill attention")
+
+
+@pytest.mark.parametrize("nq,nkv,d", [(32, 8, 128), (32, 8, 64), (8, 8, 128)])
+def test_prefill_attention_split_kv(nq, nkv, d):
+    """Split-KV work items (history ranges over several workgroups, fp32 partials
+    merged by the combine kernel): chat-turn shapes (~100 new tokens over long
+    cached histories), ranges cut at arbitrary tiles incl. ones entirely above a
+    query block's early rows (fully masked partials)."""
+    seqs = [(100, 2900), (37, 4000), (64, 0), (130, 700), (3, 1500), (1, 63)]
+    out, expect = _prefill_run(seqs, nq, nkv, d, split=True, num_cus=256)
+    assert torch.isfinite(out.float()).all()
+    _close(out, expect, atol=2e-2, rtol=2e-2, msg="prefill attention split-KV")
 
 
 def test_prefill_attention_strided_q():
@@ -181,7 +212,7 @@ def test_prefill_attention_strided_q():
     sl = torch.tensor(lens, dtype=torch.int32, device=DEV)
     qsl = torch.tensor([0, 40, 130], dtype=torch.int32)
     qkv = torch.randn(130, (nq + 2 * nkv) * d, device=DEV).bfloat16()
-    tiles = ops.build_prefill_tiles([40, 90], ops.prefill_tile_tokens(nq, nkv))
+    tiles, _ = ops.build_prefill_tiles([40, 90], ops.prefill_tile_tokens(nq, nkv))
     ti = torch.tensor(tiles, dtype=torch.int32, device=DEV).flatten()
     out = torch.zeros(130, nq * d, device=DEV).bfloat16()
     ops.prefill_attention(out, qkv, k, v, bt, sl, qsl.to(DEV), ti, len(tiles), nq, nkv, d, 0.088)

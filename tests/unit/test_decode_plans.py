@@ -62,3 +62,35 @@ def test_fused_plan_loader_validates(plans, tmp_path):
     assert llama.FUSED_PLAN["o"][8] == (2, 2, 2, 0)
     assert 7 not in llama.FUSED_PLAN["o"]  # not a bucket
     assert llama.FUSED_PLAN["down"][16] == before_down  # splits out of range
+
+
+def test_prefill_split_plan_covers_ranges():
+    """ops.build_prefill_tiles: every query block's KV tiles are covered exactly
+    once by its items; split blocks get consecutive partial slots listed in the
+    combine entries; short histories and an exhausted slot budget stay unsplit."""
+    from fasttalk_llm_microservice_amd import ops
+
+    q_lens = [100, 37, 64, 130, 3, 1]
+    seq_lens = [3000, 4037, 64, 830, 1503, 64]
+    items, comb = ops.build_prefill_tiles(q_lens, 64, seq_lens=seq_lens, nkv=8, num_cus=256)
+    assert comb and len(items) > 7
+    by_block = {}
+    for b, s, rng, slot in items:
+        by_block.setdefault((b, s), []).append((rng >> 16, rng & 0xFFFF, slot))
+    for (b, s), parts in by_block.items():
+        L, ql = seq_lens[b], q_lens[b]
+        nkt = -(-min(L, L - ql + s + min(64, ql - s)) // 64)
+        if len(parts) == 1:
+            assert parts[0] == (0, 0xFFFF, -1)
+            continue
+        parts.sort()
+        assert parts[0][0] == 0 and parts[-1][1] == nkt
+        assert all(a[1] == c[0] and a[0] < a[1] for a, c in zip(parts, parts[1:]))
+        (cb,) = [c for c in comb if (c[0], c[1]) == (b, s)]
+        assert [p[2] for p in parts] == list(range(cb[2], cb[2] + cb[3]))
+    # no seq_lens: one item per query block, nothing to combine
+    items, comb = ops.build_prefill_tiles(q_lens, 64)
+    assert comb == [] and all(r == 0xFFFF and sl == -1 for _, _, r, sl in items)
+    # slot budget: blocks that would exceed it run unsplit
+    items, comb = ops.build_prefill_tiles(q_lens, 64, seq_lens=seq_lens, num_cus=256, max_partials=4)
+    assert sum(c[3] for c in comb) <= 4
