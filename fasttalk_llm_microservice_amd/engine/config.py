@@ -52,6 +52,7 @@ class EngineConfig:
     enforce_eager: bool = False        # disable hipGraph decode capture
     graph_batch_sizes: Tuple[int, ...] = (1, 2, 4, 8, 16, 24, 32, 48, 64, 80, 96, 128, 160, 192, 224, 256)
     async_output: bool = True          # overlap detokenize/streaming with the next GPU step
+    pipeline_depth: int = 1            # decode steps queued on the GPU ahead of the one collected
     separate_process: bool = False     # run the step loop in its own process (no GIL sharing)
     custom_allreduce: bool = False     # TP: xGMI one/two-shot all-reduce for decode-size messages
     tp_share_device: bool = False      # TP ranks all on device_base (tests: gloo control + IPC data)
@@ -102,6 +103,7 @@ class EngineConfig:
             enable_prefix_caching=_env(["ENGINE_PREFIX_CACHING"], True, _bool),
             enforce_eager=_env(["ENGINE_ENFORCE_EAGER", "VLLM_ENFORCE_EAGER"], False, _bool),
             separate_process=_env(["ENGINE_SEPARATE_PROCESS"], None, _bool),
+            pipeline_depth=max(1, min(3, _env(["ENGINE_PIPELINE_DEPTH"], 1, int))),
             custom_allreduce=_env(["ENGINE_CUSTOM_ALLREDUCE"], False, _bool),
             tp_share_device=_env(["ENGINE_TP_SHARE_DEVICE"], False, _bool),
             max_restarts=_env(["ENGINE_MAX_RESTARTS"], 3, int),

@@ -68,7 +68,10 @@ class LLMEngine:
         self._trace_path = os.environ.get("FT_STEP_TRACE") or None
         self._trace: List[tuple] = []
         self.host_prof = collections.Counter()
-        self._inflight = None          # (batch, DecodeHandle) of a queued decode step
+        # queued decode steps, oldest first: [(batch, DecodeHandle)], at most
+        # cfg.pipeline_depth + 1 of them (ENGINE_PIPELINE_DEPTH)
+        self._inflight: List = []
+        self.pipeline_depth = max(1, int(getattr(cfg, "pipeline_depth", 1)))
         self._last_complete = 0.0
         from .debug import FaultInjector, StepProfiler
 
@@ -105,7 +108,7 @@ class LLMEngine:
         return True
 
     def has_work(self) -> bool:
-        return self._inflight is not None or self.scheduler.has_work()
+        return bool(self._inflight) or self.scheduler.has_work()
 
     # ------------------------------------------------------------------ helpers
     def token_trie(self):
@@ -137,37 +140,43 @@ class LLMEngine:
                 and self.runner.can_pipeline(len(batch.decode_seqs))
                 and all(s.grammar is None for s in batch.decode_seqs))
 
-    def _speculate(self, batch: ScheduledBatch):
-        """Queue the step after the in-flight one for the same sequences (same rows),
-        assuming none of them stops.  Rows of sequences that do stop are discarded;
-        their extra KV write lands in a block that is not in the prefix cache."""
+    def _speculate(self, batch: ScheduledBatch, ahead: int):
+        """Queue a step ``ahead`` steps after the collected state for the same
+        sequences (same rows), assuming none of them stops.  Rows of sequences that
+        do stop are discarded; their extra KV writes land in blocks beyond the
+        sequence's end, which are not in the prefix cache."""
         sched = self.scheduler
         seqs = batch.decode_seqs
         if sched.waiting or any(s.status == SeqStatus.FINISHED for s in seqs):
             return None
         need = 0
         for s in seqs:
-            if s.n_tokens + 1 >= self.max_model_len:
+            if s.n_tokens + ahead >= self.max_model_len:
                 return None
-            need += sched._blocks_needed(s, s.n_tokens + 1)
+            need += sched._blocks_needed(s, s.n_tokens + ahead)
         if need and not self.bm.can_allocate(need):
             return None
         for s in seqs:
-            k = sched._blocks_needed(s, s.n_tokens + 1)
+            k = sched._blocks_needed(s, s.n_tokens + ahead)
             if k:
                 s.block_ids.extend(self.bm.allocate(k))
-        return self.runner.decode_launch(seqs, ahead=1)
+        return self.runner.decode_launch(seqs, ahead=ahead)
 
     def _step_pipelined(self) -> List[RequestOutput]:
-        batch, handle = self._inflight
+        batch, handle = self._inflight[0]
         t0 = time.perf_counter()
-        nxt = self._speculate(batch)
+        # top the queue up to depth + 1 steps before waiting on the oldest
+        while len(self._inflight) <= self.pipeline_depth:
+            nxt = self._speculate(batch, len(self._inflight))
+            if nxt is None:
+                break
+            self._inflight.append((ScheduledBatch(list(batch.decode_seqs), [], [], []), nxt))
         tl = time.perf_counter()
         toks = self.runner.decode_collect(handle)
         t1 = time.perf_counter()
+        self._inflight.pop(0)
         outs = self._complete(batch, batch.decode_seqs, toks)
         t2 = time.perf_counter()
-        self._inflight = (ScheduledBatch(list(batch.decode_seqs), [], [], []), nxt) if nxt else None
         dt = t2 - self._last_complete if self._last_complete else t2 - t0
         self._last_complete = t2
         self.step_times.append((False, len(batch.decode_seqs), len(batch.decode_seqs), dt))
@@ -202,8 +211,8 @@ class LLMEngine:
             self._profiler.after_step()
 
     def reset_inflight(self):
-        """Forget a queued decode step (after a failed step)."""
-        self._inflight = None
+        """Forget the queued decode steps (after a failed step)."""
+        self._inflight = []
 
     def fail_unfinished(self, error: str):
         """After a failed step: every unfinished sequence ends with an error and
@@ -215,7 +224,7 @@ class LLMEngine:
             self._finalize(seq, "error", emit=True, error=error)
 
     def _step(self) -> List[RequestOutput]:
-        if self._inflight is not None:
+        if self._inflight:
             return self._step_pipelined()
         self._last_complete = 0.0
         ts = time.perf_counter()
@@ -236,7 +245,7 @@ class LLMEngine:
         if not batch.decode_seqs and not batch.prefill_seqs:
             return outs
         if not outs and self._pipeline_ok(batch):
-            self._inflight = (batch, self.runner.decode_launch(batch.decode_seqs))
+            self._inflight = [(batch, self.runner.decode_launch(batch.decode_seqs))]
             return self._step_pipelined()
         sampled_seqs = batch.sampled_seqs()
         masks = self._masks_for(sampled_seqs)
@@ -419,7 +428,9 @@ class LLMEngine:
             "decode_batch_avg": sum(x[1] for x in dec) / len(dec) if dec else 0.0,
             "prefill_step_ms_avg": 1e3 * sum(x[3] for x in pre) / len(pre) if pre else 0.0,
             **{k: v for k, v in self.stats.items()},
-            "runner": dict(getattr(self.runner, "stats", {})),
+            "runner": {**getattr(self.runner, "stats", {}),
+                       **({"gpu_gaps": self.runner.gap_summary()}
+                          if getattr(self.runner, "_gaps", None) else {})},
             "decode_host_ms": {k: round(1e3 * v / max(1, self.host_prof["steps"]), 3)
                                for k, v in self.host_prof.items() if k != "steps"},
         }

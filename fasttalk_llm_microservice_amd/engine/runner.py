@@ -202,9 +202,10 @@ class ModelRunner:
         self.d_temp = self.d_f32[0:mb]
         self.d_top_p = self.d_f32[mb:2 * mb]
         self.d_out = torch.zeros(mb, dtype=i32, device=dv)
-        # two pinned staging sets: while decode step n runs, step n+1 is filled
-        # and queued behind it from the other set (pipelined decode)
-        self.stg = [_Staging(mb, self.max_blocks_per_seq, pin, self.is_gpu) for _ in range(2)]
+        # pinned staging sets: while decode step n runs, steps n+1 .. n+depth are
+        # filled and queued behind it from the other sets (pipelined decode)
+        nstg = max(2, int(getattr(cfg, "pipeline_depth", 1)) + 1)
+        self.stg = [_Staging(mb, self.max_blocks_per_seq, pin, self.is_gpu) for _ in range(nstg)]
         self._stg_next = 0
         self._upload = _Uploader(dv, pin) if self.is_gpu else None
         self.h_out = torch.zeros(mb, dtype=i32, pin_memory=pin)  # eager-step sampler output
@@ -253,6 +254,10 @@ class ModelRunner:
             if stall else (None, 0.0)
         self._graph_msgs = 0
         self.stats = {"graph_replays": 0, "eager_decode": 0, "prefill_steps": 0, "captures": 0}
+        # FT_GPU_GAPS=1: timing events around every graph-replayed decode step, so
+        # gap_summary() can report how long the GPU sat idle BETWEEN consecutive
+        # decode steps (the host enqueued the next one late), without a profiler
+        self._gaps = [] if self.is_gpu and os.environ.get("FT_GPU_GAPS", "0") == "1" else None
         self.bcast = None  # TP rank 0: parallel.shm_broadcast.ShmBroadcast writer
 
     # ------------------------------------------------------------------ memory
@@ -334,6 +339,8 @@ class ModelRunner:
         Decode-only steps replay a hipGraph; steps that carry prefill chunks run
         eagerly as one mixed forward pass (decode rows first)."""
         if batch.has_prefill:
+            if self._gaps is not None:
+                self._gaps.append([None, None])
             return self._mixed(batch, masks)
         if not batch.decode_seqs:
             return []
@@ -548,13 +555,13 @@ class ModelRunner:
 
     def decode_launch(self, seqs, ahead: int = 0, masks: Optional[np.ndarray] = None) -> DecodeHandle:
         """Fills a staging set and queues a graph-replayed decode step (returns at
-        once).  ``ahead=1`` launches the step AFTER the one in flight: positions
-        are one further and the input ids are the in-flight step's sampled ids,
-        copied device-to-device, so the host never waits between steps."""
+        once).  ``ahead=a`` launches the step after the ``a`` in flight: positions
+        are ``a`` further and the input ids are the last in-flight step's sampled
+        ids, copied device-to-device, so the host never waits between steps."""
         n = len(seqs)
         nb = self._bucket(n)
         st = self.stg[self._stg_next]
-        self._stg_next ^= 1
+        self._stg_next = (self._stg_next + 1) % len(self.stg)
         maxblk = self._decode_fill(seqs, nb, st, ahead)
         if self.bcast is not None:
             self.bcast.send(("graph", {"nb": nb, "n": n, "small": st.hs.copy(),
@@ -627,8 +634,39 @@ class ModelRunner:
             st.hf[mb + n:mb + nb] = 1.0
         return maxblk
 
+    def _gap_mark(self, start: bool):
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        if start:
+            self._gaps.append([ev, None])
+        else:
+            self._gaps[-1][1] = ev
+
+    def gap_summary(self) -> Dict[str, float]:
+        """FT_GPU_GAPS: idle GPU time between consecutive graph-replayed decode
+        steps (ms total / per step / max) and their mean on-GPU time."""
+        if not self._gaps:
+            return {}
+        torch.cuda.synchronize(self.device)
+        gaps, busy, prev = [], [], None
+        for e0, e1 in self._gaps:
+            if e0 is None:   # an eager (mixed) step ran in between: chain broken
+                prev = None
+                continue
+            busy.append(e0.elapsed_time(e1))
+            if prev is not None:
+                gaps.append(max(0.0, prev.elapsed_time(e0)))
+            prev = e1
+        if not gaps:
+            return {}
+        return {"idle_ms_total": round(sum(gaps), 1), "idle_ms_per_step": round(sum(gaps) / len(gaps), 3),
+                "idle_ms_max": round(max(gaps), 2), "gpu_ms_per_step": round(sum(busy) / len(busy), 3),
+                "steps": len(busy)}
+
     def _decode_enqueue(self, st: "_Staging", nb: int, n: int, from_device: bool = False):
         nw = 10 * self.max_decode_batch + nb * self.max_blocks_per_seq
+        if self._gaps is not None:
+            self._gap_mark(True)
         self.d_in[:nw].copy_(st.h_in[:nw], non_blocking=True)
         if from_device:  # the previous step's sampled ids feed this step
             self.d_input_ids[:nb].copy_(self.d_out[:nb])
@@ -643,6 +681,8 @@ class ModelRunner:
         if flag is not None:  # the graph folded the ranks' error words into it
             st.h_err.copy_(flag, non_blocking=True)
         st.event.record()
+        if self._gaps is not None:
+            self._gap_mark(False)
 
     # ------------------------------------------------------------------ TP workers
     @torch.inference_mode()

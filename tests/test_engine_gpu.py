@@ -124,8 +124,10 @@ def test_pipelined_decode_matches_synchronous():
     early on a stop token, at max_tokens, or at different lengths."""
     prompts = _prompts(12, [5 + 7 * i for i in range(12)], seed=3)
     outs = []
-    for async_output in (True, False):
-        eng = _engine(max_num_seqs=32, num_kv_blocks=1024, async_output=async_output)
+    # pipeline depth 1 / 2 / 3 (ENGINE_PIPELINE_DEPTH: steps queued ahead), then synchronous
+    for async_output, depth in ((True, 1), (True, 2), (True, 3), (False, 1)):
+        eng = _engine(max_num_seqs=32, num_kv_blocks=1024, async_output=async_output,
+                      pipeline_depth=depth)
         res = {}
         for i, p in enumerate(prompts):
             sp = SamplingParams(temperature=0.8, top_p=0.95, seed=100 + i, max_tokens=8 + 3 * i,
@@ -141,8 +143,9 @@ def test_pipelined_decode_matches_synchronous():
     # engine's in-flight step still carries the finished row while the synchronous
     # one has dropped it, and the decode-attention work partition (balanced over all
     # rows of the step) rounds the other rows differently.  Lengths must agree.
-    assert [len(o) for o in outs[0]] == [len(o) for o in outs[1]]
-    assert [o[:8] for o in outs[0]] == [o[:8] for o in outs[1]]
+    for piped in outs[:-1]:
+        assert [len(o) for o in piped] == [len(o) for o in outs[-1]]
+        assert [o[:8] for o in piped] == [o[:8] for o in outs[-1]]
 
 
 def test_host_swap_roundtrip_and_engine():
