@@ -117,13 +117,76 @@ __device__ __forceinline__ void mt_load(MTile<D>& t, const uint16_t* __restrict_
     t.v[nd] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(vr, voff_b, nd * vstep_b, 2));
 }
 
-template <int D, int G, int R, bool FC, int WPC>
+// RoPE + KV write folded into the attention launch (RP = true): q and the new
+// token's K / V come straight from the QKV GEMM's fp32 split-K slabs instead of a
+// separate slab_rope_kv launch.  Each wave RoPEs its segment's q fragments in
+// registers (a lane's dims d and d + D/2 sit in fragments kc and kc + KC/2), and
+// the wave that owns a segment's LAST tile builds the new token's K row / V^T
+// column, writes them to the paged cache for later steps and patches them into
+// the tile registers it loaded (that row of the cache is not read back).
+struct DecRope {
+  const float* ws;        // [splits][rows][cols] fp32 qkv slabs
+  int splits, rows, cols;
+  const float* cos_sin;   // [pos][D]: cos in [0, D/2), sin in [D/2, D)
+  const int* positions;
+  const int* slot_mapping;
+  int nq;
+};
+
+// x[kc][j] = sum over splits of src[kc * 32 + j] (fp32 slabs, `slab` floats apart)
+template <int KC>
+__device__ __forceinline__ void rp_gather(float (&x)[KC][8], const float* __restrict__ src,
+                                          size_t slab, int splits) {
+#pragma unroll
+  for (int kc = 0; kc < KC; ++kc) {
+    const float4 a = *reinterpret_cast<const float4*>(src + kc * 32);
+    const float4 c = *reinterpret_cast<const float4*>(src + kc * 32 + 4);
+    x[kc][0] = a.x; x[kc][1] = a.y; x[kc][2] = a.z; x[kc][3] = a.w;
+    x[kc][4] = c.x; x[kc][5] = c.y; x[kc][6] = c.z; x[kc][7] = c.w;
+  }
+  for (int s = 1; s < splits; ++s) {
+    const float* p = src + (size_t)s * slab;
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc) {
+      const float4 a = *reinterpret_cast<const float4*>(p + kc * 32);
+      const float4 c = *reinterpret_cast<const float4*>(p + kc * 32 + 4);
+      x[kc][0] += a.x; x[kc][1] += a.y; x[kc][2] += a.z; x[kc][3] += a.w;
+      x[kc][4] += c.x; x[kc][5] += c.y; x[kc][6] += c.z; x[kc][7] += c.w;
+    }
+  }
+}
+
+// rotate-half RoPE of one lane's fragments (dims 32 kc + 8 g + j), packed to bf16
+template <int D>
+__device__ __forceinline__ void rp_rope(uint4 (&frag)[D / 32], float (&x)[D / 32][8],
+                                        const float* __restrict__ cs, int g) {
+  constexpr int KC = D / 32, HK = KC / 2;
+#pragma unroll
+  for (int kc = 0; kc < HK; ++kc) {
+    uint32_t lo[4], hi[4];
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) {
+      const int d = kc * 32 + 8 * g + j;
+      const float c0 = cs[d], c1 = cs[d + 1], s0 = cs[D / 2 + d], s1 = cs[D / 2 + d + 1];
+      const float a0 = x[kc][j] * c0 - x[kc + HK][j] * s0;
+      const float a1 = x[kc][j + 1] * c1 - x[kc + HK][j + 1] * s1;
+      const float b0 = x[kc + HK][j] * c0 + x[kc][j] * s0;
+      const float b1 = x[kc + HK][j + 1] * c1 + x[kc][j + 1] * s1;
+      lo[j / 2] = (uint32_t)f32_to_bf16(a0) | ((uint32_t)f32_to_bf16(a1) << 16);
+      hi[j / 2] = (uint32_t)f32_to_bf16(b0) | ((uint32_t)f32_to_bf16(b1) << 16);
+    }
+    frag[kc] = make_uint4(lo[0], lo[1], lo[2], lo[3]);
+    frag[kc + HK] = make_uint4(hi[0], hi[1], hi[2], hi[3]);
+  }
+}
+
+template <int D, int G, int R, bool FC, int WPC, bool RP>
 __global__ __launch_bounds__(256, WPC) void paged_decode_kernel(
     uint16_t* __restrict__ out, int out_stride, float* __restrict__ tmp_out,
     float* __restrict__ tmp_ml, const uint16_t* __restrict__ q, int q_stride,
-    const uint16_t* __restrict__ k_cache, const uint16_t* __restrict__ v_cache,
+    uint16_t* __restrict__ k_cache, uint16_t* __restrict__ v_cache,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ seq_lens,
-    int batch, int nkv, int bs_shift, float scale_log2, int* __restrict__ counters) {
+    int batch, int nkv, int bs_shift, float scale_log2, int* __restrict__ counters, DecRope rp) {
   static_assert(G >= 1 && G <= 16, "GQA group must fit the 16 MFMA columns");
   constexpr int KC = D / 32, ND = D / 16;
   __shared__ int s_pre[kDecMaxBatch + 1];
@@ -175,11 +238,57 @@ __global__ __launch_bounds__(256, WPC) void paged_decode_kernel(
 
     // Q^T fragments (B operand): lane (g, n) = head n of this kv head, dims 8g.. (+32 kc)
     uint4 qb[KC];
+    // RP: the new token's K row (lanes n == r) and V^T column (lanes g == r / 4)
+    uint4 knew[KC];
+    uint32_t vnew[ND];
+    const bool has_last = RP && t0 + cnt == nb;
+    const int r_new = (L - 1) & 15;
+    // RP: issued after the first chunk's tile loads so the slab / cos-sin loads'
+    // latency hides under the KV stream's
+    auto rp_prep = [&]() {
+      const size_t slab = (size_t)rp.rows * rp.cols;
+      const float* cs = rp.cos_sin + (size_t)rp.positions[b] * D;
+      const float* row = rp.ws + (size_t)b * rp.cols;
+      float x[KC][8];
+      rp_gather<KC>(x, row + (h * G + min(n, G - 1)) * D + 8 * g, slab, rp.splits);
+      rp_rope<D>(qb, x, cs, g);
 #pragma unroll
-    for (int kc = 0; kc < KC; ++kc)
-      qb[kc] = n < G ? *reinterpret_cast<const uint4*>(q + (size_t)b * q_stride +
-                                                       (h * G + n) * D + kc * 32 + 8 * g)
-                     : make_uint4(0, 0, 0, 0);
+      for (int kc = 0; kc < KC; ++kc)
+        if (n >= G) qb[kc] = make_uint4(0, 0, 0, 0);
+      if (has_last) {
+        rp_gather<KC>(x, row + (rp.nq + h) * D + 8 * g, slab, rp.splits);
+        rp_rope<D>(knew, x, cs, g);
+        const float* vs = row + (rp.nq + nkv + h) * D + n;
+#pragma unroll
+        for (int nd = 0; nd < ND; ++nd) {
+          float v = vs[nd * 16];
+          for (int s2 = 1; s2 < rp.splits; ++s2) v += vs[(size_t)s2 * slab + nd * 16];
+          vnew[nd] = f32_to_bf16(v);
+        }
+        const int slot = rp.slot_mapping[b];
+        if (slot >= 0) {   // the paged cache keeps the new token for later steps
+          const size_t blk = (size_t)(slot >> bs_shift);
+          const int off = slot & bmask;
+          if (n == r_new) {
+            uint16_t* kp = k_cache + ((blk * nkv + h) * bsz + off) * D + 8 * g;
+#pragma unroll
+            for (int kc = 0; kc < KC; ++kc) *reinterpret_cast<uint4*>(kp + kc * 32) = knew[kc];
+          }
+          if (g == 0) {   // V^T column: dims n + 16 nd
+            uint16_t* vp = v_cache + ((blk * nkv + h) * D + n) * bsz + off;
+#pragma unroll
+            for (int nd = 0; nd < ND; ++nd) vp[(size_t)nd * 16 * bsz] = (uint16_t)vnew[nd];
+          }
+        }
+      }
+    };
+    if constexpr (!RP) {
+#pragma unroll
+      for (int kc = 0; kc < KC; ++kc)
+        qb[kc] = n < G ? *reinterpret_cast<const uint4*>(q + (size_t)b * q_stride +
+                                                         (h * G + n) * D + kc * 32 + 8 * g)
+                       : make_uint4(0, 0, 0, 0);
+    }
     floatx4_t o[ND];
 #pragma unroll
     for (int nd = 0; nd < ND; ++nd) o[nd] = floatx4_t{0.f, 0.f, 0.f, 0.f};
@@ -203,8 +312,25 @@ __global__ __launch_bounds__(256, WPC) void paged_decode_kernel(
         const size_t hb = blk * blk_stride + (size_t)h * bsz * D;
         mt_load<D>(t, k_cache, v_cache, hb + (size_t)off * D, hb + off, koff_b, voff_b, vstep_b);
       };
-      auto consume = [&](const MTile<D>& t, int i) {
+      auto consume = [&](MTile<D>& t, int i) {
         const int valid = L - ((t0 + c0 + i) << 4);   // tokens of this tile inside the sequence
+        if (RP && has_last && t0 + c0 + i == nb - 1) {
+          // the new token's row of the last tile: registers, not the (unwritten) cache
+#pragma unroll
+          for (int kc = 0; kc < KC; ++kc)
+            if (n == r_new) t.k[kc] = knew[kc];
+          if (g == (r_new >> 2)) {
+            const int sh = (r_new & 1) * 16;
+            const uint32_t keep = ~(0xFFFFu << sh);
+#pragma unroll
+            for (int nd = 0; nd < ND; ++nd) {
+              if (r_new & 2)
+                t.v[nd].y = (t.v[nd].y & keep) | (vnew[nd] << sh);
+              else
+                t.v[nd].x = (t.v[nd].x & keep) | (vnew[nd] << sh);
+            }
+          }
+        }
         floatx4_t s = floatx4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int kc = 0; kc < KC; ++kc)
@@ -248,6 +374,9 @@ __global__ __launch_bounds__(256, WPC) void paged_decode_kernel(
       MTile<D> ring[R];
 #pragma unroll
       for (int r = 0; r + 1 < R; ++r) ld(ring[r], r);
+      if constexpr (RP) {
+        if (c0 == 0) rp_prep();
+      }
       for (int i = 0; i < cc; i += R) {
 #pragma unroll
         for (int r = 0; r < R; ++r) {
@@ -472,16 +601,24 @@ static int dec_wg_per_cu() {
 extern "C" int ft_decode_waves() { return ft_num_cus() * 3 * 4; }
 extern "C" int ft_decode_max_batch() { return ft::kDecMaxBatch; }
 
-extern "C" int ft_paged_decode_attention(void* out, int out_stride, float* tmp_out, float* tmp_ml,
-                                         const void* q, int q_stride, const void* k_cache,
-                                         const void* v_cache, const int* block_tables,
-                                         int bt_stride, const int* seq_lens, int batch, int nq,
-                                         int nkv, int head_dim, int block_size, float scale,
-                                         int* counters, hipStream_t stream) {
+extern "C" int ft_paged_decode_attention_rp(void* out, int out_stride, float* tmp_out, float* tmp_ml,
+                                            const void* q, int q_stride, void* k_cache,
+                                            void* v_cache, const int* block_tables,
+                                            int bt_stride, const int* seq_lens, int batch, int nq,
+                                            int nkv, int head_dim, int block_size, float scale,
+                                            int* counters, const float* rope_ws, int rope_splits,
+                                            int rope_rows, int rope_cols, const float* cos_sin,
+                                            const int* positions, const int* slot_mapping,
+                                            hipStream_t stream) {
   if (batch <= 0) return 0;
   if (nq % nkv != 0) return -1;
   if (batch > ft::kDecMaxBatch) return -5;
   if (block_size < 16 || (block_size & (block_size - 1))) return -4;
+  const bool rp_on = rope_ws != nullptr;
+  if (rp_on && (rope_splits < 1 || rope_rows < batch || rope_cols != (nq + 2 * nkv) * head_dim ||
+                cos_sin == nullptr || positions == nullptr || slot_mapping == nullptr))
+    return -6;
+  const ft::DecRope rp{rope_ws, rope_splits, rope_rows, rope_cols, cos_sin, positions, slot_mapping, nq};
   const int bs_shift = __builtin_ctz(block_size);
   const int G = nq / nkv;
   const float scale_log2 = scale * 1.4426950408889634f;
@@ -495,22 +632,26 @@ extern "C" int ft_paged_decode_attention(void* out, int out_stride, float* tmp_o
   // 1 workgroup per CU, or the register-limited maximum for the ring depth
   const int wpc = min(dec_wg_per_cu(), ring == 2 ? 3 : 2);
   int nwg = 0;
-#define FT_DEC_LAUNCH(DD, GG, RR, FCC)                                                         \
+#define FT_DEC_ARGS                                                                             \
+  (uint16_t*)out, out_stride, tmp_out, tmp_ml, (const uint16_t*)q, q_stride, (uint16_t*)k_cache, \
+      (uint16_t*)v_cache, block_tables, bt_stride, seq_lens, batch, nkv, bs_shift, scale_log2,   \
+      counters, rp
+#define FT_DEC_LAUNCH_RP(DD, GG, RR, FCC, RPP)                                                  \
   if (wpc == 1)                                                                                \
-    hipLaunchKernelGGL((ft::paged_decode_kernel<DD, GG, RR, FCC, 1>), dim3(nwg), dim3(256), 0,  \
-                       stream, (uint16_t*)out, out_stride, tmp_out, tmp_ml, (const uint16_t*)q, \
-                       q_stride, (const uint16_t*)k_cache, (const uint16_t*)v_cache,            \
-                       block_tables, bt_stride, seq_lens, batch, nkv, bs_shift, scale_log2,     \
-                       counters);                                                               \
+    hipLaunchKernelGGL((ft::paged_decode_kernel<DD, GG, RR, FCC, 1, RPP>), dim3(nwg), dim3(256), \
+                       0, stream, FT_DEC_ARGS);                                                \
   else                                                                                         \
-  hipLaunchKernelGGL((ft::paged_decode_kernel<DD, GG, RR, FCC, (RR == 2 ? 3 : 2)>), dim3(nwg),  \
-                     dim3(256), 0, stream, (uint16_t*)out, out_stride, tmp_out, tmp_ml,          \
-                     (const uint16_t*)q, q_stride, (const uint16_t*)k_cache,                     \
-                     (const uint16_t*)v_cache, block_tables, bt_stride, seq_lens, batch, nkv,    \
-                     bs_shift, scale_log2, counters)
+    hipLaunchKernelGGL((ft::paged_decode_kernel<DD, GG, RR, FCC, (RR == 2 ? 3 : 2), RPP>),     \
+                       dim3(nwg), dim3(256), 0, stream, FT_DEC_ARGS)
+#define FT_DEC_LAUNCH(DD, GG, RR, FCC)                                                         \
+  if (rp_on) {                                                                                 \
+    FT_DEC_LAUNCH_RP(DD, GG, RR, FCC, true);                                                   \
+  } else {                                                                                     \
+    FT_DEC_LAUNCH_RP(DD, GG, RR, FCC, false);                                                  \
+  }
 #define FT_DEC_CASE(DD, GG, RR)                                                                \
   if (head_dim == DD && G == GG) {                                                             \
-    nwg = ft_num_cus() * wpc;                                                    \
+    nwg = ft_num_cus() * wpc;                                                                  \
     if (counters != nullptr) {                                                                 \
       FT_DEC_LAUNCH(DD, GG, RR, true);                                                         \
     } else {                                                                                   \
@@ -536,5 +677,20 @@ extern "C" int ft_paged_decode_attention(void* out, int out_stride, float* tmp_o
   FT_DEC_CASE(64, 8, 2)
 #undef FT_DEC_CASE
 #undef FT_DEC_LAUNCH
+#undef FT_DEC_LAUNCH_RP
+#undef FT_DEC_ARGS
   return -2;
+}
+
+extern "C" int ft_paged_decode_attention(void* out, int out_stride, float* tmp_out, float* tmp_ml,
+                                         const void* q, int q_stride, const void* k_cache,
+                                         const void* v_cache, const int* block_tables,
+                                         int bt_stride, const int* seq_lens, int batch, int nq,
+                                         int nkv, int head_dim, int block_size, float scale,
+                                         int* counters, hipStream_t stream) {
+  return ft_paged_decode_attention_rp(out, out_stride, tmp_out, tmp_ml, q, q_stride,
+                                      const_cast<void*>(k_cache), const_cast<void*>(v_cache),
+                                      block_tables, bt_stride, seq_lens, batch, nq, nkv, head_dim,
+                                      block_size, scale, counters, nullptr, 0, 0, 0, nullptr,
+                                      nullptr, nullptr, stream);
 }

@@ -558,6 +558,54 @@ def test_slab_rope_kv(nq, nkv, d):
     _close(v1, v2, atol=3e-2, rtol=2e-2, msg="v")
 
 
+@pytest.mark.parametrize("nq,nkv,d,splits", [(32, 8, 128, 2), (32, 8, 128, 1), (32, 8, 64, 4),
+                                             (8, 1, 128, 2)])
+@pytest.mark.parametrize("fused", [True, False])
+def test_decode_attention_rope(nq, nkv, d, splits, fused):
+    """RoPE + the new token's K/V write inside the decode attention launch (the
+    decode graph's path) == slab_rope_kv followed by decode_attention: same output,
+    same cache contents; lengths at tile / block edges and an empty padding row."""
+    torch.manual_seed(7)
+    bs = 16
+    lens = [1, 16, 17, 255, 256, 257, 1000, 2100, 0]
+    b = len(lens)
+    cols = (nq + 2 * nkv) * d
+    nblocks = sum((l + bs - 1) // bs for l in lens) + 4
+    k1, v1 = _alloc_cache(nblocks, nkv, bs, d)
+    k2, v2 = k1.clone(), v1.clone()
+    bt = _random_tables([max(1, l) for l in lens], bs, nblocks).to(DEV)
+    sl = torch.tensor(lens, dtype=torch.int32, device=DEV)
+    pos = torch.tensor([max(0, l - 1) for l in lens], dtype=torch.int32, device=DEV)
+    btc = bt.cpu()
+    slots = torch.tensor([int(btc[i, (l - 1) // bs]) * bs + (l - 1) % bs if l > 0 else -1
+                          for i, l in enumerate(lens)], dtype=torch.int32, device=DEV)
+    ws = torch.randn(splits, b, cols, device=DEV)
+    cs = ref.rope_cos_sin(d, 8192, 500000.0, None, DEV)
+    n_out, n_ml = ops.decode_workspace(b, nq, nkv, d)
+    scale = d ** -0.5
+
+    def ws_buf():
+        return torch.full((n_out,), float("nan"), device=DEV), torch.full((n_ml,), float("nan"), device=DEV)
+
+    cnt = ops.decode_counters(b, nkv, DEV) if fused else None
+    out1 = torch.full((b, nq * d), float("nan"), device=DEV).bfloat16()
+    t_o, t_ml = ws_buf()
+    ops.decode_attention_rope(out1, ws.flatten(), splits, b, pos, cs, slots, k1, v1, bt, sl, t_o, t_ml,
+                              nq, nkv, d, scale, counters=cnt)
+    q = torch.zeros(b, nq * d, device=DEV).bfloat16()
+    ops.slab_rope_kv(ws.flatten(), splits, b, cols, q, pos, cs, slots, k2, v2, nq, nkv, d)
+    out2 = torch.full((b, nq * d), float("nan"), device=DEV).bfloat16()
+    t_o, t_ml = ws_buf()
+    ops.decode_attention(out2, q, k2, v2, bt, sl, t_o, t_ml, nq, nkv, d, scale, counters=cnt)
+    torch.cuda.synchronize()
+    _close(k1, k2, atol=2e-2, rtol=1e-2, msg="k cache")
+    _close(v1, v2, atol=2e-2, rtol=1e-2, msg="v cache")
+    assert torch.isfinite(out1[:-1].float()).all()
+    _close(out1, out2, atol=2e-2, rtol=2e-2, msg="attention output")
+    if cnt is not None:
+        assert int(cnt.abs().sum()) == 0
+
+
 @pytest.mark.parametrize("hidden", [2048, 3072, 4096, 8192])
 def test_embed_rmsnorm(hidden):
     vocab = 1000
