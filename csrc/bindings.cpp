@@ -41,7 +41,8 @@ int ft_prefill_attention(void* out, int out_stride, const void* q, int q_stride,
 int ft_sample(int* out_tokens, const void* logits, int logits_is_bf16, long logit_stride,
               int batch, int vocab, const float* temperature, const float* top_p,
               const int* top_k, const long long* seeds, const int* steps,
-              const uint32_t* allow_mask, int mask_words, hipStream_t stream);
+              const uint32_t* allow_mask, int mask_words, float* ws, hipStream_t stream);
+int ft_sample_ws_floats();
 int ft_kv_block_copy(void* k_cache, void* v_cache, const int* src_dst, int num_pairs,
                      long block_elems, hipStream_t stream);
 int ft_w4_gemm(const void* x, int x_stride, int M, const uint32_t* wq, const void* sz, int N, int K,
@@ -356,11 +357,21 @@ void sample(at::Tensor out_tokens, at::Tensor logits, at::Tensor temperature, at
     TORCH_CHECK(mask->size(0) >= batch && words * 32 >= vocab, "mask shape");
     mp = reinterpret_cast<const uint32_t*>(mask->data_ptr<int>());
   }
+  // per-row scratch of the multi-workgroup sampler (stream-ordered: safe to reuse
+  // from the caching allocator, graph-capturable); FT_SAMPLER_ONE_WG=1 keeps the
+  // single-workgroup kernel for every row
+  static const bool one_wg = [] {
+    const char* e = getenv("FT_SAMPLER_ONE_WG");
+    return e && e[0] == '1';
+  }();
+  at::Tensor ws;
+  if (!one_wg) ws = at::empty({(int64_t)batch * ft_sample_ws_floats()}, logits.options().dtype(at::kFloat));
   check_rc(ft_sample(out_tokens.data_ptr<int>(), logits.data_ptr(), is_bf16 ? 1 : 0,
                      (long)logits.stride(0), batch, vocab, temperature.data_ptr<float>(),
                      top_p.data_ptr<float>(), top_k.data_ptr<int>(),
                      reinterpret_cast<const long long*>(seeds.data_ptr<int64_t>()),
-                     steps.data_ptr<int>(), mp, words, cur_stream()),
+                     steps.data_ptr<int>(), mp, words, one_wg ? nullptr : ws.data_ptr<float>(),
+                     cur_stream()),
            "sample");
 }
 

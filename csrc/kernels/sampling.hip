@@ -164,15 +164,55 @@ __device__ __forceinline__ void load_keys8(const T* x, const uint32_t* mrow, int
 
 constexpr int kChunks = kSlots / 8;  // 16 chunks of 8 ids per lane
 
+// multi-workgroup sampler (samp_*_kernel below)
+constexpr int kSlices = 32;
+constexpr int kSlThreads = 256;
+// per-row fp32 scratch: slice stats [kSlices][4] (M_p, Z_p, key, id) | M, Z |
+// cand (key, id) x 2 | above [kSlices][2] | flag
+constexpr int kWsStats = 0, kWsMZ = 4 * kSlices, kWsCand = kWsMZ + 2, kWsAbove = kWsCand + 4,
+              kWsFlag = kWsAbove + 2 * kSlices, kWsRow = kWsFlag + 1;
+
 template <typename T>
 __global__ __launch_bounds__(kSampThreads) void sample_kernel(
     int* __restrict__ out_tokens, const T* __restrict__ logits, long logit_stride, int vocab,
     const float* __restrict__ temperature, const float* __restrict__ top_p,
     const int* __restrict__ top_k, const long long* __restrict__ seeds,
-    const int* __restrict__ steps, const uint32_t* __restrict__ allow_mask, int mask_words) {
+    const int* __restrict__ steps, const uint32_t* __restrict__ allow_mask, int mask_words,
+    const int* __restrict__ flags, int flag_stride) {
   __shared__ SampShared sh;
   __shared__ float chunk_mass[kChunks * kSampThreads];  // 64 KiB
   const int row = blockIdx.x;
+  // multi-workgroup path (flags != null): 0 = row already sampled there, 1 = both of
+  // its candidates were rejected (run here on fresh uniforms, rounds 2..), 2 = top-k row
+  int fl = flags ? flags[(long)row * flag_stride] : 2;
+  if (fl == 0) return;
+  if (fl == 3) {
+    // accept step of the multi-workgroup path: candidate r is in the nucleus iff the
+    // mass strictly above it (samp_above_kernel, per slice) is < top_p * Z
+    if (threadIdx.x == 0) {
+      const float* wr = reinterpret_cast<const float*>(flags) + (long)row * flag_stride - kWsFlag;
+      float a0 = 0.f, a1 = 0.f;
+      for (int p = 0; p < kSlices; ++p) {
+        a0 += wr[kWsAbove + 2 * p];
+        a1 += wr[kWsAbove + 2 * p + 1];
+      }
+      const float lim = top_p[row] * wr[kWsMZ + 1];
+      int res = 1;
+      if (a0 < lim) {
+        out_tokens[row] = __float_as_int(wr[kWsCand + 1]);
+        res = 0;
+      } else if (a1 < lim) {
+        out_tokens[row] = __float_as_int(wr[kWsCand + 3]);
+        res = 0;
+      }
+      sh.winner = res;
+    }
+    __syncthreads();
+    fl = sh.winner;
+    __syncthreads();
+    if (fl == 0) return;
+  }
+  const int r0 = fl == 1 ? 2 : 0;
   const int tid = threadIdx.x;
   const T* x = logits + (long)row * logit_stride;
   const uint32_t* mrow = allow_mask ? allow_mask + (long)row * mask_words : nullptr;
@@ -339,7 +379,7 @@ __global__ __launch_bounds__(kSampThreads) void sample_kernel(
     return sh.found ? sh.winner : besti;
   };
   for (int r = 0; r < rounds; ++r) {
-    const uint64_t h = splitmix64(s0 + (uint64_t)r * 0xD1B54A32D192ED03ull);
+    const uint64_t h = splitmix64(s0 + (uint64_t)(r + r0) * 0xD1B54A32D192ED03ull);
     const float u = ((float)(h >> 40) + 0.5f) * (1.0f / 16777216.0f);
     const int s = draw(thr, u);
     if (tp >= 1.f) {
@@ -399,30 +439,412 @@ __global__ __launch_bounds__(kSampThreads) void sample_kernel(
     }
     const uint32_t tstar = lo + 1u;
     masses(tstar > thr ? tstar : thr);
-    const uint64_t h = splitmix64(s0 + 8ull * 0xD1B54A32D192ED03ull);
+    const uint64_t h = splitmix64(s0 + (uint64_t)(8 + r0) * 0xD1B54A32D192ED03ull);
     chosen = draw(tstar > thr ? tstar : thr, ((float)(h >> 40) + 0.5f) * (1.0f / 16777216.0f));
   }
   if (tid == 0) out_tokens[row] = chosen;
 }
 
+// ---------------------------------------------------------------------------
+// Multi-workgroup path for the rows without top-k (the serving default: greedy,
+// or temperature + top-p).  One 1024-thread workgroup per row is VALU bound on a
+// single CU (every pass is 128k exp2 / compares): 97 us per 50-row step.  Here
+// the vocabulary is cut into kSlices slices, each streamed by its own workgroup:
+//   K1 slice stats     (rows x kSlices): argmax key / id, and the slice's mass
+//                      Z_p = sum exp2((x - M_p) c) relative to its own max M_p
+//   K2 draw            (rows): M, Z = sum Z_p 2^((M_p - M) c); greedy rows end
+//                      here; two inverse-CDF candidates (uniforms u0, u1 of the
+//                      same splitmix64 stream): slice by the prefix of the Z_p,
+//                      then the id inside that slice (one pass over 1/kSlices)
+//   K3 above-mass      (rows x kSlices): per slice, the mass of ids strictly more
+//                      likely than each candidate
+//   accept             (sample_kernel's first step, rows): candidate r is in the
+//                      nucleus iff its above-mass < top_p * Z; the first accepted
+//                      one is the sample
+// A row whose two candidates are both rejected (probability (1 - top_p)^2) is
+// finished by the one-workgroup kernel on uniforms 2.. (independent of u0, u1,
+// so the mixture is exactly the renormalised nucleus); top-k rows go there too.
+
+
+__device__ __forceinline__ int slice_len(int vocab) {
+  return ((vocab + kSlices * 8 - 1) / (kSlices * 8)) * 8;
+}
+
+__device__ __forceinline__ bool topk_row(const int* top_k, int row, int vocab) {
+  const int k = top_k[row];
+  return k > 0 && k < vocab;
+}
+
+// (key desc, id asc) argmax over a small workgroup (<= 16 waves) via LDS
+__device__ __forceinline__ void wg_argmax(uint32_t& k, int& idx, uint32_t* su, int* si) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint32_t ok = __shfl_xor(k, o, 64);
+    const int oi = __shfl_xor(idx, o, 64);
+    if (ok > k || (ok == k && oi < idx)) {
+      k = ok;
+      idx = oi;
+    }
+  }
+  __syncthreads();
+  if (lane_id() == 0) {
+    su[wave_id()] = k;
+    si[wave_id()] = idx;
+  }
+  __syncthreads();
+  const int nw = blockDim.x >> 6;
+  k = su[0];
+  idx = si[0];
+  for (int w = 1; w < nw; ++w)
+    if (su[w] > k || (su[w] == k && si[w] < idx)) {
+      k = su[w];
+      idx = si[w];
+    }
+}
+
+__device__ __forceinline__ float wg_sum(float v, float* sf) {
+  v = wave_sum(v);
+  __syncthreads();
+  if (lane_id() == 0) sf[wave_id()] = v;
+  __syncthreads();
+  float t = 0.f;
+  const int nw = blockDim.x >> 6;
+  for (int w = 0; w < nw; ++w) t += sf[w];
+  return t;
+}
+
+template <typename T>
+__global__ __launch_bounds__(kSlThreads) void samp_stats_kernel(
+    const T* __restrict__ logits, long stride, int vocab, const float* __restrict__ temperature,
+    const int* __restrict__ top_k, const uint32_t* __restrict__ allow_mask, int mask_words,
+    float* __restrict__ ws) {
+  __shared__ uint32_t su[kSlThreads / 64];
+  __shared__ int si[kSlThreads / 64];
+  __shared__ float sf[kSlThreads / 64];
+  const int row = blockIdx.y, p = blockIdx.x;
+  if (topk_row(top_k, row, vocab)) return;
+  const T* x = logits + (long)row * stride;
+  const uint32_t* mrow = allow_mask ? allow_mask + (long)row * mask_words : nullptr;
+  const int S = slice_len(vocab);
+  const int beg = p * S, end = min(vocab, beg + S);
+  // argmax: exact on fp32 input (32-bit ordered keys, masked ids excluded), bf16 keys
+  // otherwise -- the same rule as sample_kernel's pass 1
+  uint32_t best = 0u;
+  int besti = 0x7fffffff;
+  for (int base = beg + threadIdx.x * 8; base < end; base += kSlThreads * 8) {
+    if constexpr (sizeof(T) == 4) {
+      const uint32_t mb = mrow ? (mrow[base >> 5] >> (base & 31)) : 0xFFu;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t u = __float_as_uint(x[base + j]);
+        const uint32_t k32 = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+        if (((mb >> j) & 1u) && k32 > best) {
+          best = k32;
+          besti = base + j;
+        }
+      }
+    } else {
+      uint32_t key[8];
+      load_keys8<T>(x, mrow, base, vocab, key);
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (key[j] > best) {
+          best = key[j];
+          besti = base + j;
+        }
+    }
+  }
+  wg_argmax(best, besti, su, si);
+  uint32_t bestk = best;
+  if constexpr (sizeof(T) == 4) {
+    const uint32_t bits = (best & 0x80000000u) ? (best & 0x7fffffffu) : ~best;
+    bestk = best ? bf16_to_key(f32_to_bf16(__uint_as_float(bits))) : 0u;
+  }
+  float* st = ws + (long)row * kWsRow + kWsStats + 4 * p;
+  const float temp = temperature[row];
+  float Mp = -INFINITY, Zp = 0.f;
+  if (temp > 0.f && besti != 0x7fffffff && bestk > kNegInfKey) {
+    Mp = key_to_f32(bestk);
+    const float cexp = 1.4426950408889634f / temp;
+    float z = 0.f;
+    for (int base = beg + threadIdx.x * 8; base < end; base += kSlThreads * 8) {
+      uint32_t key[8];
+      load_keys8<T>(x, mrow, base, vocab, key);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) z += key[j] > kNegInfKey ? exp2f((key_to_f32(key[j]) - Mp) * cexp) : 0.f;
+    }
+    Zp = wg_sum(z, sf);
+  }
+  if (threadIdx.x == 0) {
+    st[0] = Mp;
+    st[1] = Zp;
+    st[2] = __uint_as_float(best);   // 32-bit key (fp32 input) or 16-bit key
+    st[3] = __int_as_float(besti);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kSampThreads) void samp_draw_kernel(
+    int* __restrict__ out_tokens, const T* __restrict__ logits, long stride, int vocab,
+    const float* __restrict__ temperature, const float* __restrict__ top_p,
+    const int* __restrict__ top_k, const long long* __restrict__ seeds,
+    const int* __restrict__ steps, const uint32_t* __restrict__ allow_mask, int mask_words,
+    float* __restrict__ ws) {
+  static_assert(kSlices <= 64, "one lane per slice");
+  constexpr int HALF = kSampThreads / 2;   // candidate r is searched by threads [r * HALF, ...)
+  __shared__ float s_scan[2][HALF / 64];
+  __shared__ float s_M, s_cexp, s_tgt[2];
+  __shared__ int s_ps[2], s_done, s_last[2], s_found[2];
+  const int row = blockIdx.x, tid = threadIdx.x, lane = lane_id();
+  float* wr = ws + (long)row * kWsRow;
+  int* flag = reinterpret_cast<int*>(wr + kWsFlag);
+  if (topk_row(top_k, row, vocab)) {
+    if (tid == 0) *flag = 2;
+    return;
+  }
+  const float tp = top_p[row];
+  if (wave_id() == 0) {
+    // lane p: slice p's stats; argmax (key desc, id asc), global max, masses
+    uint32_t k = 0u;
+    int i = 0x7fffffff;
+    float Mp = -INFINITY, Zp = 0.f;
+    if (lane < kSlices) {
+      const float4 st = *reinterpret_cast<const float4*>(wr + kWsStats + 4 * lane);
+      Mp = st.x;
+      Zp = st.y;
+      k = __float_as_uint(st.z);
+      i = __float_as_int(st.w);
+    }
+    uint32_t best = k;
+    int besti = i;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const uint32_t ok = __shfl_xor(best, o, 64);
+      const int oi = __shfl_xor(besti, o, 64);
+      if (ok > best || (ok == best && oi < besti)) {
+        best = ok;
+        besti = oi;
+      }
+    }
+    const float M = wave_max(Mp);
+    uint32_t bestk = best;
+    if constexpr (sizeof(T) == 4) {
+      const uint32_t bits = (best & 0x80000000u) ? (best & 0x7fffffffu) : ~best;
+      bestk = best ? bf16_to_key(f32_to_bf16(__uint_as_float(bits))) : 0u;
+    }
+    const float temp = temperature[row];
+    const bool done = temp <= 0.f || besti == 0x7fffffff || bestk <= kNegInfKey;
+    if (done) {
+      if (lane == 0) {
+        out_tokens[row] = (besti == 0x7fffffff) ? 0 : besti;
+        *flag = 0;
+        s_done = 1;
+      }
+    } else {
+      const float cexp = 1.4426950408889634f / temp;
+      const float zp = Mp == -INFINITY ? 0.f : Zp * exp2f((Mp - M) * cexp);
+      float incl = zp;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const float y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+      }
+      const float Z = __shfl(incl, 63, 64);
+      const uint64_t lastmask = __builtin_amdgcn_ballot_w64(zp > 0.f);
+      const int lastp = lastmask ? 63 - __builtin_clzll(lastmask) : 0;
+      const uint64_t s0 =
+          splitmix64((uint64_t)seeds[row] ^ (0x632BE59BD9B4E019ull * (uint64_t)(steps[row] + 1)));
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        const uint64_t h = splitmix64(s0 + (uint64_t)r * 0xD1B54A32D192ED03ull);
+        const float u = ((float)(h >> 40) + 0.5f) * (1.0f / 16777216.0f);
+        const float T0 = u * Z;
+        // first slice whose inclusive prefix passes the target; rounding tail: the
+        // last slice with mass, at its end
+        const uint64_t hit = __builtin_amdgcn_ballot_w64(zp > 0.f && incl > T0);
+        const int ps = hit ? __builtin_ctzll(hit) : lastp;
+        const float base = __shfl(incl - zp, ps, 64);
+        const float tgt = hit ? T0 - base : __shfl(zp, ps, 64);
+        if (lane == 0) {
+          s_ps[r] = ps;
+          s_tgt[r] = tgt;
+        }
+      }
+      if (lane == 0) {
+        s_M = M;
+        s_cexp = cexp;
+        s_done = 0;
+        wr[kWsMZ] = M;
+        wr[kWsMZ + 1] = Z;
+        wr[kWsCand] = __uint_as_float(bestk);   // defined even if a search finds nothing
+        wr[kWsCand + 1] = __int_as_float(besti);
+        wr[kWsCand + 2] = __uint_as_float(bestk);
+        wr[kWsCand + 3] = __int_as_float(besti);
+      }
+    }
+  }
+  if (tid < 2) {
+    s_last[tid] = -1;
+    s_found[tid] = 0;
+  }
+  __syncthreads();
+  if (s_done) return;
+  // inverse CDF inside the chosen slice, both candidates at once (one half each),
+  // in (thread, chunk, id) order; the first chunk's keys stay in registers
+  const int r = tid / HALF, lt = tid - r * HALF, w = lt >> 6;
+  const bool active = r == 0 || tp < 1.f;
+  const float M = s_M, cexp = s_cexp, tgt = s_tgt[r];
+  const int S = slice_len(vocab);
+  const int beg = s_ps[r] * S, end = min(vocab, beg + S);
+  const uint32_t* mrow = allow_mask ? allow_mask + (long)row * mask_words : nullptr;
+  const T* x = logits + (long)row * stride;
+  uint32_t k0[8];
+  float mass = 0.f;
+  {
+    load_keys8<T>(x, mrow, active && beg + lt * 8 < end ? beg + lt * 8 : vocab, vocab, k0);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) mass += k0[j] > kNegInfKey ? exp2f((key_to_f32(k0[j]) - M) * cexp) : 0.f;
+    for (int b2 = beg + (lt + HALF) * 8; active && b2 < end; b2 += HALF * 8) {
+      uint32_t key[8];
+      load_keys8<T>(x, mrow, b2, vocab, key);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) mass += key[j] > kNegInfKey ? exp2f((key_to_f32(key[j]) - M) * cexp) : 0.f;
+    }
+  }
+  float incl = mass;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const float y = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += y;
+  }
+  if (lane == 63) s_scan[r][w] = incl;
+  if (mass > 0.f) atomicMax(&s_last[r], lt);
+  __syncthreads();
+  float wbase = 0.f;
+  for (int w2 = 0; w2 < w; ++w2) wbase += s_scan[r][w2];
+  const float excl = wbase + incl - mass;
+  const bool mine = active && mass > 0.f &&
+                    ((tgt >= excl && tgt < excl + mass) || (lt == s_last[r] && tgt >= excl + mass));
+  if (mine) {
+    float a = excl;
+    int pick = -1, lastk = -1;
+    uint32_t pk = 0u, lastkey = 0u;
+    auto walk = [&](const uint32_t (&key)[8], int base) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (pick < 0 && key[j] > kNegInfKey) {
+          const float pj = exp2f((key_to_f32(key[j]) - M) * cexp);
+          lastk = base + j;
+          lastkey = key[j];
+          if (a + pj > tgt) {
+            pick = base + j;
+            pk = key[j];
+          }
+          a += pj;
+        }
+      }
+    };
+    walk(k0, beg + lt * 8);
+    for (int b2 = beg + (lt + HALF) * 8; pick < 0 && b2 < end; b2 += HALF * 8) {
+      uint32_t key[8];
+      load_keys8<T>(x, mrow, b2, vocab, key);
+      walk(key, b2);
+    }
+    if (pick < 0) {   // rounding tail: this thread's last kept id
+      pick = lastk;
+      pk = lastkey;
+    }
+    if (pick >= 0 && atomicCAS(&s_found[r], 0, 1) == 0) {
+      wr[kWsCand + 2 * r] = __uint_as_float(pk);
+      wr[kWsCand + 2 * r + 1] = __int_as_float(pick);
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    if (tp >= 1.f) {   // no nucleus: the first draw is the sample
+      out_tokens[row] = __float_as_int(wr[kWsCand + 1]);
+      *flag = 0;
+    } else {
+      *flag = 3;   // samp_above_kernel + the accept step decide
+    }
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kSlThreads) void samp_above_kernel(
+    const T* __restrict__ logits, long stride, int vocab, const float* __restrict__ temperature,
+    const uint32_t* __restrict__ allow_mask, int mask_words, float* __restrict__ ws) {
+  __shared__ float sf[kSlThreads / 64];
+  const int row = blockIdx.y, p = blockIdx.x;
+  float* wr = ws + (long)row * kWsRow;
+  if (*reinterpret_cast<const int*>(wr + kWsFlag) != 3) return;
+  const T* x = logits + (long)row * stride;
+  const uint32_t* mrow = allow_mask ? allow_mask + (long)row * mask_words : nullptr;
+  const float M = wr[kWsMZ];
+  const float cexp = 1.4426950408889634f / temperature[row];
+  const uint32_t k0 = __float_as_uint(wr[kWsCand]), k1 = __float_as_uint(wr[kWsCand + 2]);
+  const int S = slice_len(vocab);
+  const int beg = p * S, end = min(vocab, beg + S);
+  float a0 = 0.f, a1 = 0.f;
+  for (int base = beg + threadIdx.x * 8; base < end; base += kSlThreads * 8) {
+    uint32_t key[8];
+    load_keys8<T>(x, mrow, base, vocab, key);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float e = key[j] > k1 || key[j] > k0 ? exp2f((key_to_f32(key[j]) - M) * cexp) : 0.f;
+      a0 += key[j] > k0 ? e : 0.f;
+      a1 += key[j] > k1 ? e : 0.f;
+    }
+  }
+  a0 = wg_sum(a0, sf);
+  a1 = wg_sum(a1, sf);
+  if (threadIdx.x == 0) {
+    wr[kWsAbove + 2 * p] = a0;
+    wr[kWsAbove + 2 * p + 1] = a1;
+  }
+}
+
 }  // namespace ft
+
+extern "C" int ft_sample_ws_floats() { return ft::kWsRow; }
 
 extern "C" int ft_sample(int* out_tokens, const void* logits, int logits_is_bf16, long logit_stride,
                          int batch, int vocab, const float* temperature, const float* top_p,
                          const int* top_k, const long long* seeds, const int* steps,
-                         const uint32_t* allow_mask, int mask_words, hipStream_t stream) {
+                         const uint32_t* allow_mask, int mask_words, float* ws, hipStream_t stream) {
   if (batch <= 0) return 0;
   if (vocab > ft::kSlots * ft::kSampThreads) return -3;
   if (vocab % 8 != 0 || logit_stride % 8 != 0) return -4;
+  int* flags = nullptr;
+  // ws (batch * ft_sample_ws_floats() fp32): the multi-workgroup path for every row
+  // without top-k, then the one-workgroup kernel only for top-k and fallback rows
+#define FT_SAMPLE_ALL(TT)                                                                       \
+  {                                                                                             \
+    const TT* lg = (const TT*)logits;                                                           \
+    if (ws != nullptr) {                                                                        \
+      hipLaunchKernelGGL(ft::samp_stats_kernel<TT>, dim3(ft::kSlices, batch), dim3(ft::kSlThreads),\
+                         0, stream, lg, logit_stride, vocab, temperature, top_k, allow_mask,     \
+                         mask_words, ws);                                                        \
+      hipLaunchKernelGGL(ft::samp_draw_kernel<TT>, dim3(batch), dim3(ft::kSampThreads), 0, stream,\
+                         out_tokens, lg, logit_stride, vocab, temperature, top_p, top_k, seeds,  \
+                         steps, allow_mask, mask_words, ws);                                     \
+      hipLaunchKernelGGL(ft::samp_above_kernel<TT>, dim3(ft::kSlices, batch), dim3(ft::kSlThreads),\
+                         0, stream, lg, logit_stride, vocab, temperature, allow_mask, mask_words, \
+                         ws);                                                                    \
+      flags = reinterpret_cast<int*>(ws + ft::kWsFlag);                                          \
+    }                                                                                            \
+  }
+  if (logits_is_bf16) FT_SAMPLE_ALL(uint16_t) else FT_SAMPLE_ALL(float)
+#undef FT_SAMPLE_ALL
   dim3 grid(batch), block(ft::kSampThreads);
   if (logits_is_bf16) {
     hipLaunchKernelGGL(ft::sample_kernel<uint16_t>, grid, block, 0, stream, out_tokens,
                        (const uint16_t*)logits, logit_stride, vocab, temperature, top_p, top_k,
-                       seeds, steps, allow_mask, mask_words);
+                       seeds, steps, allow_mask, mask_words, (const int*)flags, ft::kWsRow);
   } else {
     hipLaunchKernelGGL(ft::sample_kernel<float>, grid, block, 0, stream, out_tokens,
                        (const float*)logits, logit_stride, vocab, temperature, top_p, top_k,
-                       seeds, steps, allow_mask, mask_words);
+                       seeds, steps, allow_mask, mask_words, (const int*)flags, ft::kWsRow);
   }
   return static_cast<int>(hipGetLastError());
 }
