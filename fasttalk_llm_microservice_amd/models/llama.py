@@ -117,6 +117,8 @@ PACKED_PLAN = {
     "qkv": {1: (1, -3, 1), 8: (2, -3, 1), 16: (2, -3, 1), 32: (2, -4, 8), 64: (1, -5, 2)},
     "o": {1: (1, -3, 2), 8: (2, -3, 2), 16: (2, -3, 2), 32: (2, -3, 2), 64: (1, -5, 4)},
     "gu": {1: (1, -3, 1), 8: (1, -3, 1), 16: (4, -3, 1), 32: (4, -3, 1), 64: (2, -6, 1)},
+    # (at M = 64 the cold-cache sweep prefers down 2/-5/7 and LM head 1/-5/1, but in the
+    # decode graph they measured 0.05 ms/step SLOWER: profiles/ab_sampler_plan_r02.log)
     "down": {1: (1, -3, 2), 8: (2, -3, 4), 16: (4, -3, 4), 32: (4, -3, 4), 64: (1, -5, 4)},
     "lm": {1: (1, -3, 1), 8: (2, -3, 1), 16: (4, -3, 1), 32: (1, -4, 1), 64: (2, -5, 1)},
 }
