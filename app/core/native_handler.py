@@ -25,7 +25,10 @@ Extras the WS server uses:
   ``ENGINE_HISTORY_KEEP`` (fraction of the cap, default 0.5) in one go, so the
   prefix stays stable for the next ~cap/4 turns.  The kept size is jittered per
   session (down by up to ``ENGINE_HISTORY_JITTER`` of the cap, default 0.3), so
-  sessions that reach the cap on the same turn cut again on different turns.
+  sessions that reach the cap on the same turn cut again on different turns, and
+  the window limit itself is lowered per session until its first cut (by up to
+  ``ENGINE_HISTORY_LEAD`` of the cap, default 0.15), so a burst of sessions that started together does not
+  reach its first cut on the same turn either.
 """
 from __future__ import annotations
 
@@ -100,7 +103,7 @@ def _fingerprint(messages: List[Dict[str, Any]]) -> List[str]:
 
 
 class _SessionTokens:
-    __slots__ = ("fps", "head", "prompt_ids", "gen_ids", "reply_fp", "tools_fp")
+    __slots__ = ("fps", "head", "prompt_ids", "gen_ids", "reply_fp", "tools_fp", "cut")
 
     def __init__(self):
         self.fps: List[str] = []          # messages of the engine window (rendered)
@@ -109,6 +112,7 @@ class _SessionTokens:
         self.gen_ids: List[int] = []
         self.reply_fp: Optional[str] = None
         self.tools_fp: str = ""
+        self.cut = False                  # the window has been cut at least once
 
 
 def _tools_fp(tools) -> str:
@@ -140,6 +144,7 @@ class NativeHandler:
         self.history_cap = int(getattr(config, "max_history_length", 0) or 0)
         self.keep_frac = float(os.environ.get("ENGINE_HISTORY_KEEP", "0.5"))
         self.jitter_frac = float(os.environ.get("ENGINE_HISTORY_JITTER", "0.3"))
+        self.lead_frac = float(os.environ.get("ENGINE_HISTORY_LEAD", "0.15"))
 
     # ------------------------------------------------------------------ health / info
     def check_connection(self) -> bool:
@@ -164,9 +169,21 @@ class NativeHandler:
     # ------------------------------------------------------------------ prompt building
     def _window_limit(self, session_id: Optional[str]) -> int:
         """Most non-system messages the engine window may hold (0: no count cap):
-        what ConversationManager keeps (cap - 1 besides the system prompt)."""
+        what ConversationManager keeps (cap - 1 besides the system prompt), less a
+        per-session lead of up to ENGINE_HISTORY_LEAD of it until the window's first
+        cut, so sessions that started together (a burst of conversations) do not all
+        reach the cap -- and re-prefill a cut window -- on the same turn (that one turn set p99 TTFT: 815 ms at 40
+        turns, profiles/bench_40_turns_r02.log)."""
         cap = self.history_cap
-        return cap - 1 if cap > 2 else 0
+        if cap <= 2:
+            return 0
+        limit = cap - 1
+        span = int(self.lead_frac * limit)
+        st = self._sessions.get(session_id) if session_id else None
+        if span > 0 and session_id and not (st is not None and st.cut):
+            h = int(hashlib.blake2b(b"lead:" + str(session_id).encode(), digest_size=4).hexdigest(), 16)
+            limit -= h % (span + 1)
+        return max(4, limit)
 
     def _keep(self, limit: int, session_id: Optional[str]) -> int:
         """Messages a cut window keeps: ENGINE_HISTORY_KEEP of the limit, minus a
@@ -218,6 +235,7 @@ class NativeHandler:
         tfp = _tools_fp(tools)
         st = self._sessions.get(session_id) if session_id else None
         ids: Optional[List[int]] = None
+        was_cut = False
         if st is not None and st.reply_fp is not None and st.tools_fp == tfp:
             prev = st.fps + [st.reply_fp]
             j = self._find_window(fps, head, prev, st.head)
@@ -233,7 +251,9 @@ class NativeHandler:
                 if len(ids) > budget:
                     ids = None
         if ids is None:
+            n_before = len(msgs)
             msgs = self._cut_window(msgs, head, session_id, at_cap=st is not None)
+            was_cut = len(msgs) < n_before
             ids = self.template.render(msgs, tools=tools)
             if len(ids) > budget:
                 # token-aware truncation: drop the oldest non-system messages, down to
@@ -249,6 +269,8 @@ class NativeHandler:
             st = self._sessions.setdefault(session_id, _SessionTokens())
             st.fps, st.head, st.prompt_ids, st.gen_ids, st.reply_fp, st.tools_fp = \
                 fps, head, ids, [], None, tfp
+            if was_cut:
+                st.cut = True
         return ids
 
     def _remember_reply(self, session_id: Optional[str], gen_ids: List[int], text: str):

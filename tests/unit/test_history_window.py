@@ -76,12 +76,13 @@ def _simulate(turns, sessions=12, seed=0):
 
 
 def test_history_window_keeps_prefix_cache_over_40_turns():
-    ratio, per_turn = _simulate(40)
+    ratio, per_turn = _simulate(40, sessions=50)
     assert ratio >= 0.95, ratio
-    # every session reaches the cap on the same turn once (all re-prefill a cut
-    # window together); after that the jittered keep sizes spread the cuts out
-    low = [t for t, r in enumerate(per_turn) if t > 0 and r < 0.6]
-    assert len(low) <= 1, per_turn
+    # sessions that start together reach their first cut on different turns (the
+    # per-session window lead) and cut again on different turns (the jittered keep
+    # sizes): no turn re-prefills most of the sessions at once (p99 TTFT)
+    low = [t for t, r in enumerate(per_turn) if t > 1 and r < 0.6]
+    assert not low, per_turn
 
 
 def test_window_is_suffix_of_api_history_and_cuts_in_chunks():
