@@ -180,6 +180,7 @@ class LLMEngine:
         dt = t2 - self._last_complete if self._last_complete else t2 - t0
         self._last_complete = t2
         self.step_times.append((False, len(batch.decode_seqs), len(batch.decode_seqs), dt))
+        self.stats["decode_ms_sum"] += 1e3 * dt
         if self._trace_path:
             self._trace.append(("decode_p", t0, t2, len(batch.decode_seqs), 0, 0))
         self.stats["decode_steps"] += 1
@@ -265,6 +266,8 @@ class LLMEngine:
             hp["process"] += t2 - t1
             hp["steps"] += 1
         self.step_times.append((batch.has_prefill, len(batch.decode_seqs), batch.total_tokens, dt))
+        if not batch.has_prefill:
+            self.stats["decode_ms_sum"] += 1e3 * dt
         if self._trace_path:
             self._trace.append(("mixed" if batch.has_prefill else "decode", ts, t2,
                                 len(batch.decode_seqs), sum(batch.prefill_tokens),
