@@ -43,6 +43,19 @@ def main():
     # pipeline restarts: a decode_p step whose predecessor was not decode_p
     starts = sum(1 for i in range(1, len(tr)) if tr[i][0] == "decode_p" and tr[i - 1][0] != "decode_p")
     print(f"  pipeline (re)starts {starts}, request arrivals {len(arrivals)}")
+    # mixed / prefill steps by total GEMM rows (decode rows + prefill tokens): the
+    # prefill GEMMs tile M by 256, so steps just past a multiple of 256 pay a tile row
+    hist = {}
+    for kind, t0, t1, nd, ptok, npre in tr:
+        if ptok:
+            h = hist.setdefault(min(2048, (nd + ptok + 255) // 256 * 256), [0, 0.0, 0])
+            h[0] += 1
+            h[1] += t1 - t0
+            h[2] += nd + ptok
+    for lim in sorted(hist):
+        n, s, rows = hist[lim]
+        print(f"  rows <= {lim:5d}{'+' if lim == 2048 else ' '} n {n:5d}  avg {1e3 * s / n:7.2f} ms  "
+              f"avg rows {rows / n:7.1f}  total {s:6.2f} s")
 
 
 if __name__ == "__main__":

@@ -58,7 +58,8 @@ class LLMEngine:
         self.scheduler = Scheduler(self.bm, cfg.block_size, cfg.max_num_seqs,
                                    cfg.max_num_batched_tokens, self.max_model_len,
                                    host_blocks=getattr(runner, "num_host_blocks", 0),
-                                   prefill_chunk=cfg.prefill_chunk)
+                                   prefill_chunk=cfg.prefill_chunk,
+                                   chunk_counts_decode=cfg.prefill_chunk_rows)
         self.stop_ids = set(self.tokenizer.stop_ids) | set(self.model_cfg.eos_token_ids)
         self._trie = None
         self.stats = collections.Counter()

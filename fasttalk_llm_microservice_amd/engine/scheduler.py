@@ -85,7 +85,7 @@ class HostSwapPool:
 class Scheduler:
     def __init__(self, block_manager, block_size: int, max_num_seqs: int,
                  max_num_batched_tokens: int, max_model_len: int, host_blocks: int = 0,
-                 prefill_chunk: int = 0):
+                 prefill_chunk: int = 0, chunk_counts_decode: bool = False):
         self.bm = block_manager
         self.bs = block_size
         self.max_num_seqs = max_num_seqs
@@ -96,8 +96,12 @@ class Scheduler:
         # (every session of a voice chat answering at once) is then served in several
         # short steps instead of one long one, so most of them see their first token
         # after a fraction of the burst: p50 TTFT 127 -> 62 ms at 50 sessions for
-        # -1% throughput (profiles/ab_prefill_chunk_r02.log).
+        # -1% throughput (profiles/ab_prefill_chunk_r02.log).  chunk_counts_decode:
+        # the budget bounds decode rows + prefill tokens, so burst steps stay inside
+        # four 256-row prefill GEMM tiles (mixed steps at 953-1050 rows 32.4/31.5 ms
+        # -> 28.6 ms at <= 1024 rows, profiles/ab_prefill_chunk_rows_r02.log).
         self.prefill_chunk = int(prefill_chunk)
+        self.chunk_counts_decode = bool(chunk_counts_decode)
         self.max_model_len = max_model_len
         self.waiting: Deque[Sequence] = collections.deque()
         self.running: List[Sequence] = []
@@ -241,6 +245,10 @@ class Scheduler:
         # session re-rendering its history window at once) the step is filled to the
         # hard budget instead, for throughput
         soft = self.prefill_chunk
+        if soft and self.chunk_counts_decode:
+            # the soft budget bounds the step's GEMM rows (decode rows + prefill
+            # tokens), so a burst step stays inside the prefill GEMMs' 256-row tiles
+            soft = max(self.bs, soft - n_decode)
         while self.waiting and budget > 0 and n_decode + len(seqs) < self.max_num_seqs:
             if seqs and soft and used >= soft:
                 break

@@ -161,6 +161,25 @@ def test_soft_prefill_chunk_splits_bursts_not_lone_prompts():
     assert sum(eng.runner.batches[0][1]) == 256
 
 
+def test_soft_prefill_chunk_counting_decode_rows():
+    """prefill_chunk_rows: while sequences decode, a burst of short prompts joins
+    only up to prefill_chunk GEMM rows per step (decode rows + prefill tokens)."""
+    eng = _fake_engine(max_num_seqs=32, max_num_batched_tokens=256, prefill_chunk=48,
+                       prefill_chunk_rows=True, num_blocks=1024)
+    sp = SamplingParams(temperature=0, max_tokens=40, ignore_eos=True)
+    for i in range(8):
+        eng.add_request(f"d{i}", list(range(10 * i + 1, 10 * i + 6)), sp)
+    for _ in range(3):
+        eng.step()
+    for i in range(6):
+        eng.add_request(f"b{i}", list(range(500 + 12 * i, 512 + 12 * i)), sp)
+    while eng.has_work():
+        eng.step()
+    mixed = [(nd, pre) for nd, pre in eng.runner.batches if nd and pre]
+    assert mixed and all(nd + sum(pre) <= 48 for nd, pre in mixed), mixed
+    assert eng.bm.num_free() == eng.bm.num_blocks
+
+
 def test_preemption_under_kv_pressure_completes_everything():
     eng = _fake_engine(num_blocks=12, max_num_seqs=8, max_num_batched_tokens=64)
     prompts = [[i + 1] * 6 for i in range(5)]
