@@ -145,6 +145,8 @@ class NativeHandler:
         self.keep_frac = float(os.environ.get("ENGINE_HISTORY_KEEP", "0.5"))
         self.jitter_frac = float(os.environ.get("ENGINE_HISTORY_JITTER", "0.3"))
         self.lead_frac = float(os.environ.get("ENGINE_HISTORY_LEAD", "0.15"))
+        self.warm_cuts = os.environ.get("ENGINE_WARM_CUT_WINDOW", "1").lower() in ("1", "true")
+        self.warmups = 0
 
     # ------------------------------------------------------------------ health / info
     def check_connection(self) -> bool:
@@ -271,7 +273,37 @@ class NativeHandler:
                 fps, head, ids, [], None, tfp
             if was_cut:
                 st.cut = True
+            if self.warm_cuts:
+                self._warm_next_cut(messages, msgs, head, session_id, budget, tools)
         return ids
+
+    def _warm_next_cut(self, api_msgs: List[Dict[str, Any]], window: List[Dict[str, Any]],
+                       head: int, session_id: str, budget: int, tools=None):
+        """When this turn's window plus the next turn's two messages (this reply,
+        the next user message) will exceed the window limit, the next turn re-renders
+        a cut window (``_cut_window``) and would prefill it on its own critical path
+        (TTFT of a ~2-3k token prefill, plus a long step every streaming session
+        waits for).  Its prefix -- everything up to this turn's user message -- is
+        known now, so it is queued as a background prefill: the engine computes it
+        in spare step room while this turn streams, and the cut turn then hits the
+        prefix cache for all but its newest two messages."""
+        limit = self._window_limit(session_id)
+        if not limit or len(window) - head + 2 <= limit:
+            return
+        keep = self._keep(limit, session_id)
+        nxt = list(api_msgs) + [{"role": "assistant", "content": ""}, {"role": "user", "content": ""}]
+        start = len(nxt) - keep
+        while start < len(nxt) - 1 and nxt[start].get("role") != "user":
+            start += 1
+        if start >= len(api_msgs):
+            return
+        ids = self.template.render(nxt[:head] + list(api_msgs[start:]), add_generation_prompt=False,
+                                   tools=tools)
+        warm = getattr(self.engine, "prefill_background", None)
+        if warm is None or len(ids) >= budget:
+            return
+        warm(ids)
+        self.warmups += 1
 
     def _remember_reply(self, session_id: Optional[str], gen_ids: List[int], text: str):
         if not session_id:

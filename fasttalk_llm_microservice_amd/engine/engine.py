@@ -83,7 +83,7 @@ class LLMEngine:
     # ------------------------------------------------------------------ requests
     def add_request(self, request_id: str, prompt_ids: Seq[int], params: SamplingParams,
                     on_output: Optional[Callable[[RequestOutput], None]] = None,
-                    meta: Any = None) -> Sequence:
+                    meta: Any = None, background: bool = False) -> Sequence:
         prompt_ids = list(prompt_ids)
         if not prompt_ids:
             prompt_ids = [self.tokenizer.bos_id]
@@ -91,6 +91,7 @@ class LLMEngine:
             raise EngineError(f"prompt of {len(prompt_ids)} tokens exceeds max_model_len "
                               f"{self.max_model_len}")
         seq = Sequence(request_id, prompt_ids, params, on_output, meta)
+        seq.background = bool(background)
         if self._trace_path:
             self._trace.append(("arrive", time.perf_counter(), len(prompt_ids)))
         seq.detok_stream = self.detok.new_stream()
@@ -148,7 +149,7 @@ class LLMEngine:
         sequence's end, which are not in the prefix cache."""
         sched = self.scheduler
         seqs = batch.decode_seqs
-        if sched.waiting or any(s.status == SeqStatus.FINISHED for s in seqs):
+        if sched.waiting or sched.background or any(s.status == SeqStatus.FINISHED for s in seqs):
             return None
         need = 0
         for s in seqs:
@@ -222,7 +223,8 @@ class LLMEngine:
         the failing step was the swap itself their host copies may be garbage)."""
         self.reset_inflight()
         sched = self.scheduler
-        for seq in list(sched.running) + list(sched.waiting) + list(sched.swapped):
+        for seq in list(sched.running) + list(sched.waiting) + list(sched.swapped) + \
+                list(sched.background):
             self._finalize(seq, "error", emit=True, error=error)
 
     def _step(self) -> List[RequestOutput]:
@@ -596,6 +598,13 @@ class AsyncEngine:
             except Exception as e:
                 self._deliver(RequestOutput(rid, "", [], finished=True, finish_reason="error",
                                             error=str(e)))
+        elif kind == "warm":
+            _, rid, prompt = cmd
+            try:
+                self.engine.add_request(rid, prompt, SamplingParams(temperature=0.0, max_tokens=1),
+                                        background=True)
+            except Exception as e:  # optional work: never fails a session
+                log.warning("prefix warm-up %s not queued: %s", rid, e)
         elif kind == "abort":
             self.engine.abort(cmd[1])
 
@@ -631,6 +640,16 @@ class AsyncEngine:
                 self._cmds.put(("abort", rid))
                 self._wake.set()
             self._loops.pop(rid, None)
+
+    def prefill_background(self, prompt_ids: Seq[int]) -> str:
+        """Queue a prompt whose only purpose is to leave its KV blocks in the
+        prefix cache (e.g. the window a conversation will be cut back to on its
+        next turn).  It is prefilled in the room steps leave after every waiting
+        prompt and produces no output."""
+        rid = f"warm-{next(self._ids)}"
+        self._cmds.put(("warm", rid, list(prompt_ids)))
+        self._wake.set()
+        return rid
 
     def abort(self, request_id: str) -> bool:
         if request_id not in self._loops:

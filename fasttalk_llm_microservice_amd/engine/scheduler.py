@@ -109,6 +109,9 @@ class Scheduler:
         self._admit_counter = 0
         self.num_preemptions = 0
         self.swapped: Deque[Sequence] = collections.deque()
+        # background (prefix-cache warm-up) prompts: prefilled only into the room a
+        # step has left after every waiting prompt, within the soft budget
+        self.background: Deque[Sequence] = collections.deque()
         self.host = HostSwapPool(host_blocks) if host_blocks > 0 else None
         self._swap_out: List[Tuple[int, int]] = []
         self.num_swap_out = 0
@@ -117,13 +120,13 @@ class Scheduler:
     # ------------------------------------------------------------------ queue ops
     def add(self, seq: Sequence):
         self.by_id[seq.request_id] = seq
-        self.waiting.append(seq)
+        (self.background if seq.background else self.waiting).append(seq)
 
     def has_work(self) -> bool:
-        return bool(self.waiting) or bool(self.running) or bool(self.swapped)
+        return bool(self.waiting) or bool(self.running) or bool(self.swapped) or bool(self.background)
 
     def num_unfinished(self) -> int:
-        return len(self.waiting) + len(self.running) + len(self.swapped)
+        return len(self.waiting) + len(self.running) + len(self.swapped) + len(self.background)
 
     def release(self, seq: Sequence):
         """Free a sequence's KV blocks (full blocks stay cached for reuse) and its
@@ -142,7 +145,7 @@ class Scheduler:
         if seq in self.running:
             self.running.remove(seq)
         else:
-            for q in (self.waiting, self.swapped):
+            for q in (self.waiting, self.swapped, self.background):
                 try:
                     q.remove(seq)
                     break
@@ -301,10 +304,51 @@ class Scheduler:
                 self.waiting.popleft()
             else:
                 break  # the partially prefilled prompt continues next step
+        if self.background and not self.waiting and budget > 0 \
+                and n_decode + len(seqs) < self.max_num_seqs:
+            room = min(budget, soft - used) if soft else budget
+            if room > 0:
+                self._schedule_background(room, seqs, ntok, samp, rejected)
         return seqs, ntok, samp, rejected
 
+    def _schedule_background(self, room: int, seqs, ntok, samp, rejected):
+        """One chunk of the oldest background prompt into ``room`` spare tokens.
+        Warm-up is optional work: under KV pressure it is dropped, not waited for."""
+        seq = self.background[0]
+        if seq.num_computed == 0 and not seq.block_ids:
+            max_blocks = (seq.n_tokens - 1) // self.bs
+            hit = self.bm.match_prefix(seq.tokens, max_blocks) if max_blocks > 0 else []
+            if hit:
+                seq.block_ids = list(hit)
+                seq.num_computed = len(hit) * self.bs
+                seq.num_committed_blocks = len(hit)
+                seq.num_cached_tokens = seq.num_computed
+        remaining = seq.n_tokens - seq.num_computed
+        chunk = min(remaining, room)
+        need = self._blocks_needed(seq, seq.num_computed + chunk)
+        if need and not self.bm.can_allocate(need):
+            self.background.popleft()
+            self.release(seq)
+            seq.status = SeqStatus.FINISHED
+            seq.finish_reason = "abort"
+            rejected.append(seq)
+            return
+        if need:
+            seq.block_ids.extend(self.bm.allocate(need))
+        seqs.append(seq)
+        ntok.append(chunk)
+        samp.append(chunk == remaining)
+        if chunk == remaining:
+            self.background.popleft()
+
     def _preempt_one(self, keep: Sequence) -> bool:
-        # a waiting sequence in the middle of a chunked prefill gives its blocks up first
+        # a background warm-up gives its blocks up first (it is optional work)
+        for w in self.background:
+            if w.block_ids:
+                self._reset_to_waiting(w)
+                self.num_preemptions += 1
+                return True
+        # a waiting sequence in the middle of a chunked prefill gives its blocks up next
         for w in self.waiting:
             if w.block_ids:
                 self._reset_to_waiting(w)

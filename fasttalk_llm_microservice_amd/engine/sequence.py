@@ -38,7 +38,7 @@ class Sequence:
                  "num_computed", "num_committed_blocks", "num_cached_tokens", "arrival",
                  "first_token_time", "finish_reason", "detok_stream", "on_output", "grammar",
                  "grammar_state", "stop_buf", "text_len", "aborted", "preemptions", "admit_order",
-                 "meta", "host_slots")
+                 "meta", "host_slots", "background")
 
     def __init__(self, request_id: str, prompt_ids: List[int], params: SamplingParams,
                  on_output: Optional[Callable[[RequestOutput], None]] = None, meta: Any = None):
@@ -64,6 +64,7 @@ class Sequence:
         self.stop_buf = ""
         self.text_len = 0
         self.aborted = False
+        self.background = False   # prefix-cache warm-up: prefilled only into spare step room
         self.preemptions = 0
         self.admit_order = 0
         self.meta = meta

@@ -180,6 +180,40 @@ def test_soft_prefill_chunk_counting_decode_rows():
     assert eng.bm.num_free() == eng.bm.num_blocks
 
 
+def test_background_prefill_fills_spare_room_and_warms_prefix_cache():
+    """A background (warm-up) prompt never displaces waiting prompts, is chunked
+    into the soft budget's spare rows, stops after one token, and leaves its full
+    blocks in the prefix cache for the request that follows it."""
+    eng = _fake_engine(max_num_seqs=32, max_num_batched_tokens=256, prefill_chunk=48,
+                       num_blocks=1024)
+    sp = SamplingParams(temperature=0, max_tokens=30, ignore_eos=True)
+    for i in range(4):
+        eng.add_request(f"d{i}", list(range(10 * i + 1, 10 * i + 6)), sp)
+    eng.step()
+    warm = list(range(2000, 2160))                      # 160 tokens = 40 blocks of 4
+    seen = []
+    eng.add_request("warm", warm, SamplingParams(temperature=0, max_tokens=1),
+                    on_output=seen.append, background=True)
+    eng.add_request("late", list(range(700, 730)), sp)   # queued after the warm-up
+    steps = []
+    while eng.scheduler.background or eng.scheduler.waiting:
+        eng.step()
+        steps.append(eng.runner.batches[-1])
+    # the waiting prompt went first; warm-up chunks only used the spare rows
+    assert steps[0][1][0] == 30
+    assert all(nd + sum(pre) <= 48 for nd, pre in steps), steps
+    assert sum(sum(pre) for _, pre in steps) == 30 + 160
+    while eng.has_work():
+        eng.step()
+    assert seen[-1].finished and seen[-1].num_output_tokens == 1
+    # the follow-up turn (warm prefix + new tokens) re-attaches the warmed blocks
+    eng.runner.batches.clear()
+    outs = eng.generate([warm + [9, 9, 9]], SamplingParams(temperature=0, max_tokens=2, ignore_eos=True))
+    assert outs == [_expected(warm + [9, 9, 9], 2)]
+    assert eng.runner.batches[0] == (0, [3])   # all 40 warmed blocks re-attached
+    assert eng.bm.num_free() == eng.bm.num_blocks
+
+
 def test_preemption_under_kv_pressure_completes_everything():
     eng = _fake_engine(num_blocks=12, max_num_seqs=8, max_num_batched_tokens=64)
     prompts = [[i + 1] * 6 for i in range(5)]

@@ -107,3 +107,50 @@ def test_window_is_suffix_of_api_history_and_cuts_in_chunks():
         h._remember_reply("a", [5, 6, 7], f"answer {t}")
         cm.add_assistant_message("a", f"answer {t}", 3)
     assert 1 <= cuts <= 4, cuts
+
+
+class _WarmEngine(_FakeEngine):
+    def __init__(self):
+        super().__init__()
+        self.warm = []
+
+    def prefill_background(self, ids):
+        self.warm.append(list(ids))
+
+
+import pytest
+
+
+@pytest.mark.parametrize("tools", [None, [{"type": "function", "function": {
+    "name": "web_search", "description": "Search the web", "parameters": {"type": "object"}}}]])
+def test_cut_window_prefix_is_warmed_one_turn_ahead(tools):
+    """The turn before a window cut queues the cut window's known prefix as a
+    background prefill; the cut turn's prompt starts with exactly those tokens, so
+    it hits the prefix cache instead of re-prefilling the window on its TTFT."""
+    eng = _WarmEngine()
+    h = NativeHandler(_Cfg(), engine=eng)
+    cm = ConversationManager(max_history_length=50)
+    rng = random.Random(1)
+    words = "the voice assistant should answer quickly about weather news music travel".split()
+    cuts = warmed = 0
+    for s in range(6):
+        sid = f"w{s}"
+        cm.create_session(sid, "You are a helpful voice assistant.")
+        last_warm = None
+        for t in range(60):
+            cm.add_user_message(sid, " ".join(rng.choice(words) for _ in range(20)) + "?")
+            n_warm = len(eng.warm)
+            ids = h.build_prompt(cm.get_messages_for_generation(sid), 128, session_id=sid, tools=tools)
+            st = h._sessions[sid]
+            if st.reply_fp is None and st.gen_ids == [] and t and len(st.fps) < prev_len:
+                cuts += 1
+                assert last_warm is not None, f"cut at turn {t} was not warmed"
+                assert ids[:len(last_warm)] == last_warm
+                assert len(last_warm) > len(ids) // 2
+                warmed += 1
+            prev_len = len(st.fps) + 2
+            last_warm = eng.warm[-1] if len(eng.warm) > n_warm else None
+            text = " ".join(rng.choice(words) for _ in range(30))
+            h._remember_reply(sid, [rng.randrange(1000, 60000) for _ in range(40)], text)
+            cm.add_assistant_message(sid, text, 40)
+    assert cuts >= 6 and warmed == cuts, (cuts, warmed)
