@@ -42,7 +42,7 @@ class EngineConfig:
     dp_size: int = 1
     max_num_seqs: int = 256
     max_num_batched_tokens: int = 8192
-    prefill_chunk: int = 1024          # soft per-step prefill budget beyond the first prompt (0 = off)
+    prefill_chunk: int = 512          # soft per-step prefill budget beyond the first prompt (0 = off)
     prefill_chunk_rows: bool = True    # the soft budget also counts the step's decode rows
     max_model_len: int = 8192
     gpu_memory_utilization: float = 0.90
@@ -95,7 +95,7 @@ class EngineConfig:
             max_num_batched_tokens=_env(["ENGINE_MAX_NUM_BATCHED_TOKENS",
                                          "VLLM_MAX_NUM_BATCHED_TOKENS"], 8192, int),
             max_model_len=_env(["ENGINE_MAX_MODEL_LEN", "VLLM_MAX_MODEL_LEN"], 8192, int),
-            prefill_chunk=_env(["ENGINE_PREFILL_CHUNK"], 1024, int),
+            prefill_chunk=_env(["ENGINE_PREFILL_CHUNK"], 512, int),
             prefill_chunk_rows=_env(["ENGINE_PREFILL_CHUNK_ROWS"], "1", str).lower() in ("1", "true"),
             gpu_memory_utilization=_env(["ENGINE_GPU_MEMORY_UTILIZATION",
                                          "VLLM_GPU_MEMORY_UTILIZATION"], 0.90, float),

@@ -99,7 +99,9 @@ class Scheduler:
         # -1% throughput (profiles/ab_prefill_chunk_r02.log).  chunk_counts_decode:
         # the budget bounds decode rows + prefill tokens, so burst steps stay inside
         # four 256-row prefill GEMM tiles (mixed steps at 953-1050 rows 32.4/31.5 ms
-        # -> 28.6 ms at <= 1024 rows, profiles/ab_prefill_chunk_rows_r02.log).
+        # -> 28.6 ms at <= 1024 rows, profiles/ab_prefill_chunk_rows_r02.log).  The
+        # default budget is 512 rows: p50 TTFT 63 -> 39-42 ms at unchanged tok/s vs
+        # 1024; 384 / 256 cost 2.5-3.5% tok/s (profiles/ab_prefill_chunk_512_r02.log).
         self.prefill_chunk = int(prefill_chunk)
         self.chunk_counts_decode = bool(chunk_counts_decode)
         self.max_model_len = max_model_len
