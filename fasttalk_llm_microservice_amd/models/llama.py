@@ -128,9 +128,10 @@ MAX_SPLITS = 4
 # split-K) per projection from bench/pg_probe.py on MI355X vs hipBLASLt on row-major
 # weights (profiles/packed_gemm_*_r02.log): split-K fills the chip at mixed-step
 # sizes (80-256 rows: 0.8-1.7x hipBLASLt), whole tiles above.
-# Up to 2047 rows (the soft prefill chunk of 1024 tokens + decode rows lands at
-# ~1.1k) the M = 1024 measurements rule: split-K keeps o / down at 512 workgroups
-# (whole tiles there: 80 workgroups on 256 CUs, 2-3x slower).
+# Soft-budgeted mixed steps land at <= 512 rows (entries re-checked at 300 / 400 /
+# 512 rows: profiles/pg_probe_300_512_r02.log).  Up to 2047 rows the M = 1024
+# measurements rule: split-K keeps o / down at 512 workgroups (whole tiles there:
+# 80 workgroups on 256 CUs, 2-3x slower).
 PG_PLAN = {
     "qkv": ((128, 1, 8), (256, 2, 4), (512, 2, 2), (2047, 0, 2), (1 << 30, 2, 1)),
     "o": ((128, 2, 8), (256, 1, 8), (512, 2, 4), (2047, 1, 2), (1 << 30, 0, 1)),
