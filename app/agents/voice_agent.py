@@ -222,7 +222,7 @@ class VoiceAgent:
             async for out in backend.stream_events(
                     messages, temperature=temp, max_tokens=round_mt, top_p=tp, top_k=top_k, stop=stop,
                     request_id=sid, session_id=sid if (rnd == 0 and guided is None) else None,
-                    tools=schemas or None, guided=guided, seed=seed,
+                    prefix_session=sid, tools=schemas or None, guided=guided, seed=seed,
                     ignore_eos=ignore_eos and guided is None, min_tokens=min_tokens):
                 if out.finished:
                     finish = out.finish_reason

@@ -229,7 +229,13 @@ class NativeHandler:
         return -1
 
     def build_prompt(self, messages: List[Dict[str, Any]], max_tokens: int,
-                     session_id: Optional[str] = None, tools=None) -> List[int]:
+                     session_id: Optional[str] = None, tools=None, remember: bool = True) -> List[int]:
+        """Prompt ids for ``messages``; with ``session_id`` a follow-up turn continues
+        the session's previous token stream (so the prefix cache matches it).
+        ``remember=False`` continues it without recording this prompt as the
+        session's new state: the agent's tool rounds (a guided tool call, the answer
+        after the tool result) extend the session's cached prefix, but their
+        messages are not part of the API history the next turn continues from."""
         budget = max(16, self.max_model_len - max(1, max_tokens) - 1)
         msgs = list(messages)
         head = 1 if msgs and msgs[0].get("role") == "system" else 0
@@ -267,7 +273,7 @@ class NativeHandler:
             fps = _fingerprint(msgs)
             if len(ids) > budget:
                 ids = ids[-budget:]
-        if session_id is not None:
+        if session_id is not None and remember:
             st = self._sessions.setdefault(session_id, _SessionTokens())
             st.fps, st.head, st.prompt_ids, st.gen_ids, st.reply_fp, st.tools_fp = \
                 fps, head, ids, [], None, tfp
@@ -332,12 +338,18 @@ class NativeHandler:
                             request_id: Optional[str] = None, session_id: Optional[str] = None,
                             prompt_ids: Optional[List[int]] = None, tools=None, guided=None,
                             seed: Optional[int] = None, ignore_eos: bool = False,
-                            min_tokens: int = 0) -> AsyncIterator[Any]:
+                            min_tokens: int = 0, prefix_session: Optional[str] = None
+                            ) -> AsyncIterator[Any]:
+        """``prefix_session`` (with ``session_id=None``): build the prompt on that
+        session's token stream without making this request the session's turn."""
         mt = int(max_tokens or self.default_max_tokens)
         params = self._params(temperature, mt, top_p, top_k, stop, seed, guided, ignore_eos,
                               min_tokens)
         if prompt_ids is None:
-            prompt_ids = self.build_prompt(messages, mt, session_id, tools)
+            if session_id is None and prefix_session is not None:
+                prompt_ids = self.build_prompt(messages, mt, prefix_session, tools, remember=False)
+            else:
+                prompt_ids = self.build_prompt(messages, mt, session_id, tools)
         key = request_id or session_id or f"native-{time.time_ns()}"
         with self._lock:
             self._seq += 1

@@ -154,3 +154,31 @@ def test_cut_window_prefix_is_warmed_one_turn_ahead(tools):
             h._remember_reply(sid, [rng.randrange(1000, 60000) for _ in range(40)], text)
             cm.add_assistant_message(sid, text, 40)
     assert cuts >= 6 and warmed == cuts, (cuts, warmed)
+
+
+def test_tool_rounds_continue_the_session_stream_without_becoming_its_state():
+    """The agent's guided tool call and its post-tool answer are built on the
+    session's token stream (previous prompt + generated ids), so they hit the
+    prefix cache, but they do not replace the state the next turn continues."""
+    h = NativeHandler(_Cfg(), engine=_FakeEngine())
+    cm = ConversationManager(max_history_length=50)
+    cm.create_session("t", "sys")
+    cm.add_user_message("t", "hello there")
+    ids0 = h.build_prompt(cm.get_messages_for_generation("t"), 64, session_id="t")
+    gen = [70001, 70002, 70003]                    # generated ids (not a re-tokenization)
+    h._remember_reply("t", gen, "hi! how can I help")
+    cm.add_assistant_message("t", "hi! how can I help", 3)
+    cm.add_user_message("t", "search the news please")
+    msgs = cm.get_messages_for_generation("t")
+    before = (list(h._sessions["t"].prompt_ids), list(h._sessions["t"].gen_ids))
+    stream = ids0 + gen
+    g = h.build_prompt(msgs, 64, session_id="t", remember=False)          # guided round
+    assert g[:len(stream)] == stream
+    call = {"role": "assistant", "content": '{"name": "web_search", "arguments": {"query": "news"}}'}
+    tool = {"role": "tool", "content": "stub results"}
+    a = h.build_prompt(msgs + [call, tool], 64, session_id="t", remember=False)   # answer round
+    assert a[:len(g) - len(h.template.generation_prompt())] == g[:len(g) - len(h.template.generation_prompt())]
+    assert (h._sessions["t"].prompt_ids, h._sessions["t"].gen_ids) == before
+    # a full re-render (what these rounds used before) diverges at the first reply
+    full = h.template.render(msgs)
+    assert full[:len(stream)] != stream
