@@ -72,6 +72,8 @@ class AgentConfig(BaseModel):
                           "complex formatting - speak naturally as if in a conversation.")
     guided_tool_calls: bool = False
     max_tool_rounds: int = 3
+    # one forced tool: write its call's fixed head into the prompt (AGENT_PREFILL_TOOL_HEAD)
+    prefill_tool_head: bool = True
 
 
 @dataclass
@@ -108,6 +110,7 @@ class VoiceAgent:
             duckduckgo_rate_limit=float(e("DUCKDUCKGO_RATE_LIMIT", "1.0")),
             system_prompt=e("SYSTEM_PROMPT", AgentConfig().system_prompt),
             guided_tool_calls=e("AGENT_GUIDED_TOOL_CALLS", "false").lower() == "true",
+            prefill_tool_head=e("AGENT_PREFILL_TOOL_HEAD", "true").lower() == "true",
         )
 
     # ------------------------------------------------------------------ backend
@@ -208,10 +211,18 @@ class VoiceAgent:
         tools_by_name = self.tools()
         for rnd in range(self.config.max_tool_rounds + 1):
             guided = None
+            head = ""
             if force and rnd == 0:
                 pick = [s for s in schemas if force == "required" or s["function"]["name"] == force]
-                guided = GuidedSpec.tool_call(pick or schemas)
+                if len(pick) == 1 and self.config.prefill_tool_head:
+                    # one possible tool: its call's fixed head goes into the prompt
+                    # (one prefill instead of a decode step per token of it)
+                    head, guided = GuidedSpec.tool_call_tail(pick[0])
+                else:
+                    guided = GuidedSpec.tool_call(pick or schemas)
             det = StreamingToolDetector() if (schemas and rnd < self.config.max_tool_rounds) else None
+            if det is not None and head:
+                det.feed(head)
             held: List[str] = []
             held_tokens = 0
             finish = None
@@ -222,7 +233,8 @@ class VoiceAgent:
             async for out in backend.stream_events(
                     messages, temperature=temp, max_tokens=round_mt, top_p=tp, top_k=top_k, stop=stop,
                     request_id=sid, session_id=sid if (rnd == 0 and guided is None) else None,
-                    prefix_session=sid, tools=schemas or None, guided=guided, seed=seed,
+                    prefix_session=sid, assistant_prefix=head, tools=schemas or None, guided=guided,
+                    seed=seed,
                     ignore_eos=ignore_eos and guided is None, min_tokens=min_tokens):
                 if out.finished:
                     finish = out.finish_reason

@@ -338,10 +338,12 @@ class NativeHandler:
                             request_id: Optional[str] = None, session_id: Optional[str] = None,
                             prompt_ids: Optional[List[int]] = None, tools=None, guided=None,
                             seed: Optional[int] = None, ignore_eos: bool = False,
-                            min_tokens: int = 0, prefix_session: Optional[str] = None
-                            ) -> AsyncIterator[Any]:
+                            min_tokens: int = 0, prefix_session: Optional[str] = None,
+                            assistant_prefix: str = "") -> AsyncIterator[Any]:
         """``prefix_session`` (with ``session_id=None``): build the prompt on that
-        session's token stream without making this request the session's turn."""
+        session's token stream without making this request the session's turn.
+        ``assistant_prefix``: text the assistant turn starts with (written into the
+        prompt; the output stream holds only what follows it)."""
         mt = int(max_tokens or self.default_max_tokens)
         params = self._params(temperature, mt, top_p, top_k, stop, seed, guided, ignore_eos,
                               min_tokens)
@@ -350,6 +352,8 @@ class NativeHandler:
                 prompt_ids = self.build_prompt(messages, mt, prefix_session, tools, remember=False)
             else:
                 prompt_ids = self.build_prompt(messages, mt, session_id, tools)
+            if assistant_prefix:
+                prompt_ids = list(prompt_ids) + self.tokenizer.encode(assistant_prefix)
         key = request_id or session_id or f"native-{time.time_ns()}"
         with self._lock:
             self._seq += 1

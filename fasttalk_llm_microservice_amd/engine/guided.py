@@ -135,3 +135,13 @@ class GuidedSpec:
     @classmethod
     def tool_call(cls, tools: Sequence[Dict[str, Any]]) -> "GuidedSpec":
         return cls(tool_call_ast(tools))
+
+    @classmethod
+    def tool_call_tail(cls, tool: Dict[str, Any]) -> "tuple[str, GuidedSpec]":
+        """One forced tool: the call's fixed head ``{"name": "<tool>", "parameters": ``
+        (the agent writes it into the prompt as the start of the assistant turn, so
+        it costs one prefill instead of a decode step per token) and the grammar of
+        the rest of the call (``tool_call_ast`` minus that head)."""
+        fn = tool.get("function", tool)
+        head = '{"name": ' + json.dumps(fn["name"]) + ', "parameters": '
+        return head, cls(seq(schema_ast(fn.get("parameters") or {"type": "object"}, 1), lit("}")))

@@ -60,9 +60,20 @@ def test_agent_guided_tool_call_round_trip(engine):
     assert events[-1].finish_reason in ("stop", "length")
 
 
-def test_agent_plain_answer_and_custom_tool(engine):
+@pytest.mark.parametrize("head", [True, False])
+def test_agent_plain_answer_and_custom_tool(engine, head):
+    """tool_choice names one tool: with prefill_tool_head its call's fixed head is
+    written into the prompt and only the arguments are decoded under the grammar."""
     handler = NativeHandler(engine=engine)
-    agent = VoiceAgent(AgentConfig(guided_tool_calls=False), backend=handler)
+    agent = VoiceAgent(AgentConfig(guided_tool_calls=False, prefill_tool_head=head), backend=handler)
+    prompts = []
+    orig = engine.generate
+
+    def spy(prompt_ids, params, request_id=None):
+        prompts.append((list(prompt_ids), params.guided is not None))
+        return orig(prompt_ids, params, request_id=request_id)
+
+    engine.generate = spy
 
     @agent.tool(description="Adds two numbers", parameters={
         "type": "object", "properties": {"a": {"type": "integer"}, "b": {"type": "integer"}}})
@@ -76,9 +87,15 @@ def test_agent_plain_answer_and_custom_tool(engine):
                                                         max_tokens=8, tool_choice="add", seed=1)]
         return evs
 
-    evs = asyncio.run(run())
+    try:
+        evs = asyncio.run(run())
+    finally:
+        engine.generate = orig
     call = [e for e in evs if e.tool_call][0]
     assert call.tool_call["name"] == "add"
+    guided_prompt = [p for p, g in prompts if g][0]
+    tail = handler.tokenizer.encode('{"name": "add", "parameters": ')
+    assert (guided_prompt[-len(tail):] == tail) == head
     a, b = call.tool_call["arguments"]["a"], call.tool_call["arguments"]["b"]
     assert call.tool_result == str(a + b)
     info = agent.get_model_info()
