@@ -37,6 +37,13 @@ logger = logging.getLogger(__name__)
 
 _TOOL_HINTS = re.compile(r"\b(search|look up|lookup|news|weather|latest|current|today|time|date|"
                          r"session|google|find)\b", re.I)
+# hint words that name one tool: a message whose hints all point at one tool forces
+# that tool (its call's fixed head is then prefilled); mixed or ambiguous hints
+# ("current", "today") leave the choice among all tools to the model
+_HINT_TOOLS = ((re.compile(r"\b(search|look up|lookup|news|weather|latest|google|find)\b", re.I),
+                "duckduckgo_search"),
+               (re.compile(r"\b(time|date)\b", re.I), "get_current_time"),
+               (re.compile(r"\bsession\b", re.I), "get_session_info"))
 
 
 @dataclass
@@ -178,6 +185,11 @@ class VoiceAgent:
             return tool_choice
         if tool_choice in (None, "auto") and self.config.guided_tool_calls and \
                 _TOOL_HINTS.search(user_message or ""):
+            msg = user_message or ""
+            named = {name for rx, name in _HINT_TOOLS if rx.search(msg)}
+            ambiguous = re.search(r"\b(current|today)\b", msg, re.I) is not None
+            if len(named) == 1 and not ambiguous and next(iter(named)) in self.tools():
+                return next(iter(named))
             return "required"
         return None
 

@@ -307,3 +307,13 @@ def test_manual_client_scripted(monkeypatch, engine, capsys):
     assert asyncio.run(main()) == 0
     out = capsys.readouterr().out
     assert out.count("[4 tokens") == 2 and "session ended" in out
+
+
+def test_tool_hints_force_one_tool_when_unambiguous(engine):
+    agent = VoiceAgent(AgentConfig(guided_tool_calls=True), backend=NativeHandler(engine=engine))
+    assert agent._wants_tool("Search the web for the latest news about tea", None) == "duckduckgo_search"
+    assert agent._wants_tool("what time is it", None) == "get_current_time"
+    assert agent._wants_tool("search for the date of the match", None) == "required"
+    assert agent._wants_tool("what is the current weather", None) == "required"
+    assert agent._wants_tool("tell me a story", None) is None
+    assert agent._wants_tool("search news", "get_session_info") == "get_session_info"
