@@ -108,6 +108,24 @@ def tool_call_ast(tools: Sequence[Dict[str, Any]]) -> Dict[str, Any]:
     return seq(lit('{"name": '), alt(*branches), lit("}"))
 
 
+def _peel_literal(ast: Dict[str, Any]):
+    """(fixed leading bytes, the rest of the grammar or None when nothing is left):
+    the literal run a grammar must start with, e.g. ``{"query": "`` of an object
+    whose first property is a string."""
+    if ast["t"] == "lit":
+        return ast["s"], None
+    if ast["t"] == "seq":
+        acc = b""
+        kids = ast["c"]
+        for i, k in enumerate(kids):
+            p, r = _peel_literal(k)
+            acc += p
+            if r is not None:
+                return acc, seq(r, *kids[i + 1:])
+        return acc, None
+    return b"", ast
+
+
 class GuidedSpec:
     """Attach to ``SamplingParams.guided``; the engine compiles it lazily."""
 
@@ -144,4 +162,8 @@ class GuidedSpec:
         the rest of the call (``tool_call_ast`` minus that head)."""
         fn = tool.get("function", tool)
         head = '{"name": ' + json.dumps(fn["name"]) + ', "parameters": '
-        return head, cls(seq(schema_ast(fn.get("parameters") or {"type": "object"}, 1), lit("}")))
+        rest = seq(schema_ast(fn.get("parameters") or {"type": "object"}, 1), lit("}"))
+        more, tail = _peel_literal(rest)
+        if tail is None:  # an all-literal call: keep a grammar to end it with
+            return head, cls(rest)
+        return head + more.decode("utf-8"), cls(tail)

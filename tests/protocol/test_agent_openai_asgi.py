@@ -94,7 +94,11 @@ def test_agent_plain_answer_and_custom_tool(engine, head):
     call = [e for e in evs if e.tool_call][0]
     assert call.tool_call["name"] == "add"
     guided_prompt = [p for p, g in prompts if g][0]
-    tail = handler.tokenizer.encode('{"name": "add", "parameters": ')
+    from fasttalk_llm_microservice_amd.engine.guided import GuidedSpec
+
+    head_text = GuidedSpec.tool_call_tail(agent.tools()["add"].schema())[0]
+    assert head_text == '{"name": "add", "parameters": {"a": '
+    tail = handler.tokenizer.encode(head_text)
     assert (guided_prompt[-len(tail):] == tail) == head
     a, b = call.tool_call["arguments"]["a"], call.tool_call["arguments"]["b"]
     assert call.tool_result == str(a + b)
