@@ -149,7 +149,10 @@ class LLMEngine:
         sequence's end, which are not in the prefix cache."""
         sched = self.scheduler
         seqs = batch.decode_seqs
-        if sched.waiting or sched.background or any(s.status == SeqStatus.FINISHED for s in seqs):
+        # new prompts end the pipeline; so does a background warm-up, unless the batch
+        # is full (it could not join a step anyway)
+        warm = bool(sched.background) and len(sched.running) < sched.max_num_seqs
+        if sched.waiting or warm or any(s.status == SeqStatus.FINISHED for s in seqs):
             return None
         need = 0
         for s in seqs:
@@ -244,6 +247,9 @@ class LLMEngine:
         # sequences the scheduler had to reject (cannot fit in the KV pool)
         for s in batch.rejected:
             self.scheduler.by_id.pop(s.request_id, None)
+            if s.background:  # a dropped warm-up is not a failed request
+                self._finalize(s, "abort", emit=False)
+                continue
             outs.append(self._finalize(s, "error", emit=True,
                                        error="prompt does not fit in the KV cache"))
         if not batch.decode_seqs and not batch.prefill_seqs:

@@ -214,6 +214,24 @@ def test_background_prefill_fills_spare_room_and_warms_prefix_cache():
     assert eng.bm.num_free() == eng.bm.num_blocks
 
 
+def test_background_prefill_is_dropped_under_kv_pressure():
+    """A warm-up that does not fit is dropped (finished as an abort, not an error)
+    and never displaces the sessions that are decoding."""
+    eng = _fake_engine(max_num_seqs=8, max_num_batched_tokens=64, prefill_chunk=32,
+                       num_blocks=12)
+    sp = SamplingParams(temperature=0, max_tokens=8, ignore_eos=True)
+    for i in range(2):
+        eng.add_request(f"d{i}", list(range(10 * i + 1, 10 * i + 9)), sp)
+    eng.step()
+    eng.add_request("warm", list(range(500, 600)), SamplingParams(temperature=0, max_tokens=1),
+                    background=True)                 # 25 blocks: can never fit in 12
+    while eng.has_work():
+        eng.step()
+    assert eng.stats["finished_abort"] == 1 and eng.stats["finished_error"] == 0
+    assert eng.stats["finished_length"] == 2
+    assert eng.bm.num_free() == eng.bm.num_blocks
+
+
 def test_preemption_under_kv_pressure_completes_everything():
     eng = _fake_engine(num_blocks=12, max_num_seqs=8, max_num_batched_tokens=64)
     prompts = [[i + 1] * 6 for i in range(5)]
