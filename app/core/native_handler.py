@@ -308,7 +308,7 @@ class NativeHandler:
         warm = getattr(self.engine, "prefill_background", None)
         if warm is None or len(ids) >= budget:
             return
-        warm(ids)
+        warm(ids, session_id=session_id)   # DP: routed to the replica owning the session
         self.warmups += 1
 
     def _remember_reply(self, session_id: Optional[str], gen_ids: List[int], text: str):

@@ -75,8 +75,10 @@ def register_openai_routes(app, handler) -> None:
                 yield chunk({"role": "assistant", "content": ""})
                 finish = "stop"
                 det = StreamingToolDetector() if tools else None
-                tcp = StreamingToolCallParser() if tools else None
+                names = [(t.get("function") or t).get("name") for t in tools or []]
+                tcp = StreamingToolCallParser(names) if tools else None
                 any_call = False
+                tool_text = []   # what the parser consumed, re-sent as content if no call
                 async for out in handler.stream_events(messages, request_id=rid, **kw):
                     if out.finished:
                         finish = out.finish_reason
@@ -91,12 +93,17 @@ def register_openai_routes(app, handler) -> None:
                             yield chunk({"content": emit})
                     elif mode == "tool":
                         held, det.buf = det.buf, ""   # the parser owns the tool text now
+                        tool_text.append(held)
                         deltas = tcp.feed(held)
                         if deltas:
                             any_call = True
                             yield chunk({"tool_calls": deltas})
                 if det is not None and det.mode is None and det.buf:
                     yield chunk({"content": det.buf})   # never became a tool call
+                elif det is not None and det.mode == "tool" and not any_call and tool_text:
+                    # looked like a call ('{', a tag) but no call of a requested tool
+                    # came out of it: it was text (e.g. a JSON answer)
+                    yield chunk({"content": "".join(tool_text)})
                 if any_call:
                     finish = "tool_calls"
                 yield chunk({}, finish if finish in ("stop", "length", "tool_calls") else "stop")
@@ -117,7 +124,8 @@ def register_openai_routes(app, handler) -> None:
         msg: Dict[str, Any] = {"role": "assistant", "content": text}
         if tools:
             calls, rest = parse_tool_calls(text)
-            if calls:
+            names = {(t.get("function") or t).get("name") for t in tools}
+            if calls and all(c.name in names for c in calls):
                 msg = {"role": "assistant", "content": rest or None,
                        "tool_calls": [c.to_openai() for c in calls]}
                 finish = "tool_calls"

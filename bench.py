@@ -14,6 +14,15 @@ Weights are random-init (no checkpoints offline) with the exact Llama-3-8B
 architecture; prompts are synthetic English.
 
 python bench.py [--gpus N] [--steps K] [--warmup W] [--sessions 50] [--gen 128]
+
+``--gpus N`` with N > 1 and no ``WORLD_SIZE`` in the environment: this process
+becomes a launcher that starts N rank processes itself (``RANK`` / ``LOCAL_RANK``
+/ ``WORLD_SIZE`` / ``MASTER_*`` on 127.0.0.1) before anything touches a GPU, waits
+for them and exits with the worst rank's code; rank 0 prints the JSON line.
+Under ``torch.distributed.run`` the ranks exist already and ``--gpus`` must equal
+``WORLD_SIZE``.  Each rank needs its own GPU unless ``FT_BENCH_SHARED_GPU=1``
+(rehearsal: all ranks on the visible GPU(s); the JSON then reports the distinct
+devices as ``n_gpus`` and the rank count as ``ranks``).
 """
 from __future__ import annotations
 
@@ -21,7 +30,9 @@ import argparse
 import json
 import multiprocessing as mp
 import os
+import signal
 import socket
+import subprocess
 import sys
 import threading
 import time
@@ -47,9 +58,78 @@ def _free_port(base: int) -> int:
     raise RuntimeError("no free port")
 
 
+def _launch_ranks(n: int, argv) -> int:
+    """Start ``n`` bench ranks (this file, same arguments) with the torch.distributed
+    env contract and wait for them.  Runs before this process imports torch, so it
+    never touches a GPU; if one rank fails the others are stopped."""
+    env = dict(os.environ)
+    shared = env.get("FT_BENCH_SHARED_GPU", "0") == "1"
+    if shared and not env.get("ENGINE_GPU_MEMORY_UTILIZATION"):
+        # every rank's engine sizes its KV cache from the same device
+        env["ENGINE_GPU_MEMORY_UTILIZATION"] = f"{0.85 / n:.3f}"
+    port = _free_port(29500 + (os.getpid() % 400))
+    procs = []
+    for r in range(n):
+        e = dict(env, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                 GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=e))
+
+    def stop_all(*_):
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        t_end = time.time() + 20
+        for p in procs:
+            try:
+                p.wait(timeout=max(0.1, t_end - time.time()))
+            except subprocess.TimeoutExpired:
+                p.kill()
+
+    signal.signal(signal.SIGTERM, lambda *_: (stop_all(), sys.exit(143)))
+    rc = 0
+    try:
+        live = list(procs)
+        while live:
+            for p in list(live):
+                r = p.poll()
+                if r is None:
+                    continue
+                live.remove(p)
+                if r != 0:
+                    rc = rc or r
+                    print(f"bench launcher: rank {procs.index(p)} exited with {r}; stopping the others",
+                          file=sys.stderr, flush=True)
+                    stop_all()
+                    live = []
+                    break
+            time.sleep(0.2)
+    finally:
+        stop_all()
+    return rc
+
+
+def _device_plan(world: int, local_rank: int, device: str):
+    """(device index, distinct devices used) for this rank; fails loudly when the
+    node has fewer GPUs than ranks, unless FT_BENCH_SHARED_GPU=1."""
+    if device != "cuda":
+        return None, 0
+    import torch
+
+    ndev = torch.cuda.device_count()  # does not initialise the GPU
+    if ndev < 1:
+        raise SystemExit("bench: no GPU visible")
+    if os.environ.get("FT_BENCH_SHARED_GPU", "0") == "1":
+        return local_rank % ndev, min(world, ndev)
+    if ndev < world:
+        raise SystemExit(f"bench: {world} ranks need {world} GPUs, {ndev} visible "
+                         "(FT_BENCH_SHARED_GPU=1 rehearses several ranks on one GPU)")
+    return local_rank, world
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one GPU each); default: WORLD_SIZE, else 1")
     ap.add_argument("--steps", type=int, default=4)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--sessions", type=int, default=50)
@@ -64,13 +144,18 @@ def main():
                     help="tensor parallel: the N ranks form ONE engine (e.g. --model llama3-70b --tp 8); "
                          "default: data parallel, one engine per rank")
     ap.add_argument("--custom-allreduce", action="store_true", help="TP: one-shot xGMI all-reduce")
-    ap.add_argument("--device", default="cuda", help="TP mode only: cpu runs the same path over gloo")
+    ap.add_argument("--device", default="cuda", help="cpu runs the same path over gloo (tests)")
     ap.add_argument("--quant", default="", choices=["", "w4", "awq"],
                     help="W4A16 layer weights (the reference's AWQ-INT4 model); default bf16")
     ap.add_argument("--agent-tools", type=float, default=-1.0, metavar="FRAC",
                     help="BASELINE config 5: agent with JSON-guided tool calls, FRAC of the turns "
                          "ask for a web search (stub backend); e.g. 0.2")
     a = ap.parse_args()
+    if "WORLD_SIZE" not in os.environ:
+        if (a.gpus or 1) > 1:
+            sys.exit(_launch_ranks(a.gpus, sys.argv[1:]))
+    elif a.gpus is not None and a.gpus != int(os.environ["WORLD_SIZE"]):
+        raise SystemExit(f"bench: --gpus {a.gpus} but WORLD_SIZE={os.environ['WORLD_SIZE']}")
     if a.quant:
         os.environ["ENGINE_QUANTIZATION"] = a.quant
     if a.agent_tools >= 0:
@@ -104,18 +189,24 @@ def main():
     os.environ["ENGINE_MODEL"] = a.model
     os.environ["ENABLE_PYDANTIC_AI"] = "false" if a.no_agent else "true"
     os.environ.setdefault("LLM_MAX_CONNECTIONS", str(max(64, a.sessions + 8)))
+    cpu = a.device == "cpu"
+    if cpu:
+        os.environ["COMPUTE_DEVICE"] = "cpu"
+        os.environ.setdefault("ENGINE_NUM_KV_BLOCKS", "512")
+        os.environ.setdefault("ENGINE_MAX_MODEL_LEN", "2048")
+    # FT_BENCH_SHARED_GPU=1: rehearse the N-rank DP path with every rank on one
+    # GPU (ranks map round-robin onto the visible devices, gloo instead of RCCL,
+    # which refuses two ranks on one device); the launcher sizes
+    # ENGINE_GPU_MEMORY_UTILIZATION to 1/N.  The driver's multi-GPU runs leave it unset.
+    shared = os.environ.get("FT_BENCH_SHARED_GPU", "0") == "1"
+    dev_idx, n_dev = _device_plan(world, local_rank, a.device)
     import torch
     import torch.distributed as dist
 
-    # FT_BENCH_SHARED_GPU=1: rehearse the N-rank DP path with every rank on one
-    # GPU (ranks map round-robin onto the visible devices, gloo instead of RCCL,
-    # which refuses two ranks on one device); size ENGINE_GPU_MEMORY_UTILIZATION
-    # to 1/N then.  The driver's multi-GPU runs leave it unset.
-    shared = os.environ.get("FT_BENCH_SHARED_GPU", "0") == "1"
-    dev_idx = local_rank % max(1, torch.cuda.device_count()) if shared else local_rank
-    torch.cuda.set_device(dev_idx)
+    if not cpu:
+        torch.cuda.set_device(dev_idx)
     if world > 1:
-        if shared:
+        if shared or cpu:
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=torch.device(f"cuda:{dev_idx}"))
@@ -130,7 +221,7 @@ def main():
     engine = server.native_handler.engine
     # capture the decode graphs the run will use before serving (a process-isolated
     # engine warms itself up before it reports ready)
-    if hasattr(engine.engine, "runner"):
+    if hasattr(engine.engine, "runner") and not cpu:
         engine.engine.runner.warmup([b for b in engine.engine.runner.graph_sizes if b <= 2 * a.sessions])
     import asyncio
 
@@ -164,7 +255,8 @@ def main():
     def barrier():
         if world > 1:
             dist.barrier()
-        torch.cuda.synchronize()
+        if not cpu:
+            torch.cuda.synchronize()
 
     barrier()
     m_before = engine.engine.metrics()
@@ -200,14 +292,16 @@ def main():
                          if a.agent_tools >= 0 else ""),
             "value": round(value, 2),
             "unit": "tokens/s",
-            "n_gpus": world,
+            "n_gpus": n_dev,
+            "ranks": world,
+            "device": a.device,
             "steps": a.steps,
             "warmup": a.warmup,
             "ms_per_step": round(1e3 * t_max / a.steps, 2),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "w4a16 (bf16 compute)" if a.quant else "bf16",
+            "dtype": ("w4a16 (bf16 compute)" if a.quant else "bf16") if not cpu else "fp32",
             "data": f"synthetic (random-init {mlabel} weights, synthetic English prompts, "
                     "synthetic Llama-3 tokenizer)",
             "config": {"model": mlabel, "global_batch": a.sessions * world,
@@ -290,6 +384,7 @@ def bench_tp(a, rank: int, world: int, local_rank: int):
     os.environ.setdefault("LLM_MAX_CONNECTIONS", str(max(64, a.sessions + 8)))
     if a.device == "cpu":
         os.environ["COMPUTE_DEVICE"] = "cpu"
+    _, n_dev = _device_plan(world, local_rank, a.device)
     import torch
 
     from fasttalk_llm_microservice_amd.engine.config import EngineConfig
@@ -298,7 +393,8 @@ def bench_tp(a, rank: int, world: int, local_rank: int):
 
     t_init = time.time()
     cfg = EngineConfig.from_env(model=a.model, device=a.device, tp_size=world,
-                                custom_allreduce=a.custom_allreduce)
+                                custom_allreduce=a.custom_allreduce,
+                                tp_share_device=os.environ.get("FT_BENCH_SHARED_GPU", "0") == "1")
     if a.device == "cpu":
         cfg.num_kv_blocks = cfg.num_kv_blocks or 512
         cfg.max_model_len = min(cfg.max_model_len, 2048)
@@ -354,7 +450,8 @@ def bench_tp(a, rank: int, world: int, local_rank: int):
     out = {
         "metric": "output tokens/sec (node) + p50 TTFT over WebSocket, "
                   f"{a.model} TP={world} at {a.sessions} sessions",
-        "value": round(value, 2), "unit": "tokens/s", "n_gpus": world, "steps": a.steps,
+        "value": round(value, 2), "unit": "tokens/s", "n_gpus": n_dev, "ranks": world,
+        "device": a.device, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": round(1e3 * elapsed / a.steps, 2),
         "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
         "dtype": ("w4a16 (bf16 compute)" if a.quant else "bf16") if a.device == "cuda" else "fp32",

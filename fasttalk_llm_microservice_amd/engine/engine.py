@@ -220,15 +220,19 @@ class LLMEngine:
         """Forget the queued decode steps (after a failed step)."""
         self._inflight = []
 
-    def fail_unfinished(self, error: str):
+    def fail_unfinished(self, error: str, reset_cache: bool = False):
         """After a failed step: every unfinished sequence ends with an error and
         gives back its KV blocks and host swap slots -- swapped-out ones too (if
-        the failing step was the swap itself their host copies may be garbage)."""
+        the failing step was the swap itself their host copies may be garbage).
+        ``reset_cache`` (a collective fault: KV written from un-reduced partial sums
+        may sit in committed blocks) also empties the prefix cache."""
         self.reset_inflight()
         sched = self.scheduler
         for seq in list(sched.running) + list(sched.waiting) + list(sched.swapped) + \
                 list(sched.background):
             self._finalize(seq, "error", emit=True, error=error)
+        if reset_cache and hasattr(self.bm, "reset_prefix_cache"):
+            self.bm.reset_prefix_cache()
 
     def _step(self) -> List[RequestOutput]:
         if self._inflight:
@@ -561,7 +565,9 @@ class AsyncEngine:
                 fatal = not self._recoverable(e) or self._fail_streak >= self.max_fail_streak
                 if fatal:  # set before the error outputs go out: no new request slips in
                     self.error = e
-                eng.fail_unfinished(str(e))
+                from .runner import CommFault
+
+                eng.fail_unfinished(str(e), reset_cache=isinstance(e, CommFault))
                 self._flush()
                 continue
             self._fail_streak = 0
@@ -647,12 +653,13 @@ class AsyncEngine:
                 self._wake.set()
             self._loops.pop(rid, None)
 
-    def prefill_background(self, prompt_ids: Seq[int]) -> str:
+    def prefill_background(self, prompt_ids: Seq[int], session_id: Optional[str] = None) -> str:
         """Queue a prompt whose only purpose is to leave its KV blocks in the
         prefix cache (e.g. the window a conversation will be cut back to on its
         next turn).  It is prefilled in the room steps leave after every waiting
-        prompt and produces no output."""
-        rid = f"warm-{next(self._ids)}"
+        prompt and produces no output.  ``session_id`` keys the request id like the
+        session's turns (``<session>#...``), which is what DP routing is affine to."""
+        rid = f"{session_id}#warm-{next(self._ids)}" if session_id else f"warm-{next(self._ids)}"
         self._cmds.put(("warm", rid, list(prompt_ids)))
         self._wake.set()
         return rid

@@ -249,10 +249,14 @@ class ModelRunner:
         # decode graph message, stall until rank 0's custom all-reduce has run out of
         # spin budget (its error word is set; at most <seconds>) -- the fault test
         # of the collective timeout contract
+        # "m<n>:<seconds>" stalls before the n-th eager (mixed / prefill) message instead
         stall = os.environ.get("FT_FAULT_TP_STALL", "") if comm.rank > 0 else ""
+        self._stall_mixed = stall.startswith("m")
+        stall = stall.lstrip("m")
         self._stall_at, self._stall_s = (int(stall.split(":")[0]), float(stall.split(":")[1])) \
             if stall else (None, 0.0)
         self._graph_msgs = 0
+        self._mixed_msgs = 0
         self.stats = {"graph_replays": 0, "eager_decode": 0, "prefill_steps": 0, "captures": 0}
         # FT_GPU_GAPS=1: timing events around every graph-replayed decode step, so
         # gap_summary() can report how long the GPU sat idle BETWEEN consecutive
@@ -463,6 +467,15 @@ class ModelRunner:
             meta.dec_counters = self.dec_counters
         h = self.model.forward(d["ids"], meta, self.kv)
         if not has_logits:
+            # a middle chunk of a chunked prefill samples nothing, but its all-reduces
+            # wrote KV blocks that post_step commits to the prefix cache: check the
+            # custom collectives' error word before anything is committed
+            flag = self._arm_comm_check() if self.is_gpu else None
+            if flag is not None:
+                self.h_err.copy_(flag, non_blocking=True)
+                self._wait()
+                if int(self.h_err[0]):
+                    self._comm_fault()
             return []
         k = len(names)
         samp = dev[k:k + 5]
@@ -693,15 +706,14 @@ class ModelRunner:
         if kind == "stop":
             return False
         if kind == "mixed":
+            self._mixed_msgs += 1
+            if self._stall_mixed and self._mixed_msgs == self._stall_at:
+                self._fault_stall()
             self._mixed_run(host, masks)
         elif kind == "graph":
             self._graph_msgs += 1
-            if self._stall_at is not None and self._graph_msgs == self._stall_at:
-                log.warning("FT_FAULT_TP_STALL: rank %d stalls", self.comm.rank)
-                t_end = time.time() + self._stall_s
-                while time.time() < t_end and not (self.comm.custom is not None
-                                                   and self.comm.custom.peer_error(0)):
-                    time.sleep(0.01)
+            if not self._stall_mixed and self._graph_msgs == self._stall_at:
+                self._fault_stall()
             nb, n = host["nb"], host["n"]
             self._set_masks(masks, n)
             st = self.stg[0]
@@ -721,6 +733,13 @@ class ModelRunner:
         else:
             raise ValueError(f"unknown TP message {kind!r}")
         return True
+
+    def _fault_stall(self):
+        log.warning("FT_FAULT_TP_STALL: rank %d stalls", self.comm.rank)
+        t_end = time.time() + self._stall_s
+        while time.time() < t_end and not (self.comm.custom is not None
+                                           and self.comm.custom.peer_error(0)):
+            time.sleep(0.01)
 
     def _decode_meta(self, nb: int) -> AttnMeta:
         assert nb <= self.max_decode_rows

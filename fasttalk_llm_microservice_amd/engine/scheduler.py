@@ -273,6 +273,8 @@ class Scheduler:
             limit = budget if not seqs or not soft else min(budget, soft - used)
             chunk = min(remaining, limit)
             need = self._blocks_needed(seq, seq.num_computed + chunk)
+            if need and not self.bm.can_allocate(need) and self._release_background():
+                pass  # a warm-up's blocks went back to the pool first (optional work)
             if need and not self.bm.can_allocate(need):
                 # A waiting sequence must not sit on blocks (matched prefix or an
                 # unfinished chunked prefill): they would starve the running
@@ -312,6 +314,18 @@ class Scheduler:
             if room > 0:
                 self._schedule_background(room, seqs, ntok, samp, rejected)
         return seqs, ntok, samp, rejected
+
+    def _release_background(self) -> bool:
+        """Background warm-ups give up the blocks of their unfinished prefill (full
+        blocks stay in the prefix cache) so a real prompt can be admitted; they
+        only run when nothing is waiting, so otherwise they would hold the blocks
+        without progressing.  True if anything was released."""
+        freed = False
+        for w in self.background:
+            if w.block_ids:
+                self._reset_to_waiting(w)
+                freed = True
+        return freed
 
     def _schedule_background(self, room: int, seqs, ntok, samp, rejected):
         """One chunk of the oldest background prompt into ``room`` spare tokens.

@@ -144,9 +144,15 @@ class StreamingToolCallParser:
     first ``{index, id, type, function: {name, arguments: ""}}``, then argument
     fragments ``{index, function: {arguments}}`` as the JSON of the arguments
     object streams in.  The concatenated fragments of a call are exactly the
-    arguments' JSON text as the model wrote it."""
+    arguments' JSON text as the model wrote it.
 
-    def __init__(self):
+    ``names``: the request's tool names; an object whose ``"name"`` is not one of
+    them is not a call (``self.rejected``, nothing more is emitted) -- e.g. a JSON
+    text answer that happens to carry a "name" key."""
+
+    def __init__(self, names=None):
+        self.names = set(names) if names is not None else None
+        self.rejected = False
         self.buf = ""
         self.obj_start: Optional[int] = None   # offset of the current call's '{'
         self.header_sent = False
@@ -205,7 +211,7 @@ class StreamingToolCallParser:
     def feed(self, delta: str) -> List[Dict[str, Any]]:
         self.buf += delta
         out: List[Dict[str, Any]] = []
-        while True:
+        while not self.rejected:
             if self.obj_start is None:
                 i = self.buf.find("{", self.scan)
                 if i < 0:
@@ -217,11 +223,15 @@ class StreamingToolCallParser:
                 m = _NAME_RE.search(seg)
                 if m is None:
                     return out
+                name = json.loads('"' + m.group(1) + '"')
+                if self.names is not None and name not in self.names:
+                    self.rejected = True
+                    return out
                 self.index = self.ncalls
                 self.ncalls += 1
                 self.call_id = f"call_{uuid.uuid4().hex[:12]}"
                 out.append({"index": self.index, "id": self.call_id, "type": "function",
-                            "function": {"name": json.loads('"' + m.group(1) + '"'), "arguments": ""}})
+                            "function": {"name": name, "arguments": ""}})
                 self.header_sent = True
             if self.args_start is None:
                 m = _ARGS_RE.search(seg)
@@ -266,3 +276,4 @@ class StreamingToolCallParser:
                     out.append({"index": self.index, "function": {"arguments": frag}})
                     self.args_sent = len(avail)
             return out
+        return out

@@ -121,6 +121,15 @@ def _replica_main(index: int, cfg, conn, device_base: int = 0):
                     except Exception as e:
                         outs.append(RequestOutput(rid, "", [], finished=True, finish_reason="error",
                                                   error=str(e)))
+                elif cmd[0] == "warm":  # background prefix warm-up: optional work
+                    _, rid, prompt = cmd
+                    try:
+                        from ..engine.sampling_params import SamplingParams
+
+                        eng.add_request(rid, prompt, SamplingParams(temperature=0.0, max_tokens=1),
+                                        background=True)
+                    except Exception as e:
+                        log.warning("prefix warm-up %s not queued: %s", rid, e)
                 elif cmd[0] == "abort":
                     eng.abort(cmd[1])
                 elif cmd[0] == "stop":
@@ -131,7 +140,11 @@ def _replica_main(index: int, cfg, conn, device_base: int = 0):
                     streak = 0
                 except Exception as e:  # same contract as AsyncEngine._run
                     log.exception("replica step failed")
-                    eng.fail_unfinished(str(e))  # error outputs land in `outs`
+                    from ..engine.runner import CommFault
+
+                    # error outputs land in `outs`; a collective fault may have left
+                    # KV from partial sums in committed blocks: drop the prefix cache
+                    eng.fail_unfinished(str(e), reset_cache=isinstance(e, CommFault))
                     streak += 1
                     if not AsyncEngine._recoverable(e) or streak >= int(
                             os.environ.get("ENGINE_MAX_FAIL_STREAK", "3")):
@@ -405,6 +418,19 @@ class MultiGPUEngine:
                     rep.send(("abort", rid))
                 except Exception:
                     pass
+
+    def prefill_background(self, prompt_ids: Seq[int], session_id: Optional[str] = None) -> str:
+        """AsyncEngine.prefill_background across replicas: the warm-up goes to the
+        replica the session's turns are affine to (its prefix cache is the one the
+        next turn will hit).  Fire and forget: a warm-up produces no output."""
+        rid = f"{session_id}#warm-{next(self._ids)}" if session_id else self.new_request_id()
+        rep = self._pick(rid)
+        if rep.error is None:
+            try:
+                rep.send(("warm", rid, list(prompt_ids)))
+            except Exception:  # optional work: never fails a session
+                pass
+        return rid
 
     def abort(self, request_id: str) -> bool:
         rep = self._owner.get(request_id)

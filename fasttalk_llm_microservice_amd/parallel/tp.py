@@ -205,10 +205,12 @@ def torchrun_tp(cfg) -> Optional[object]:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     device = cfg.resolved_device()
-    _set_device(device, local)
+    dev_index = 0 if cfg.tp_share_device else local
+    _set_device(device, dev_index)
     if not dist.is_initialized():
-        kw = {"device_id": torch.device(f"cuda:{local}")} if device == "cuda" else {}
-        dist.init_process_group(_backend(device), **kw)
+        kw = {"device_id": torch.device(f"cuda:{dev_index}")} \
+            if device == "cuda" and not cfg.tp_share_device else {}
+        dist.init_process_group(_backend(device, cfg), **kw)
     comm = TPComm(dist.group.WORLD, rank, world)
     _maybe_custom_ar(cfg, comm, device)
     name = [None]

@@ -103,6 +103,18 @@ def test_dp2_router_session_affinity_and_outputs():
         time.sleep(0.6)
         asyncio.run(one(9, prompts[0], "sess0"))
         assert eng.engine.metrics()["replicas"] == 2
+        # a background warm-up reaches the replica that owns the session,
+        # so that session's next turn re-attaches the warmed prefix
+        warm = rng.integers(0, 120000, 96).tolist()
+        eng.prefill_background(warm, session_id="sess1")
+        time.sleep(1.5)
+
+        async def cached(sid):
+            n = 0
+            async for o in eng.generate(warm + [5, 6, 7], sp, request_id=f"{sid}#w"):
+                n = max(n, o.num_cached_tokens)
+            return n
+        assert asyncio.run(cached("sess1")) >= 64
     finally:
         eng.shutdown()
 

@@ -138,3 +138,39 @@ def test_tp2_on_one_gpu_graph_decode_matches_tp1(tp1_tokens, monkeypatch):
     print("TP2 vs TP1 token agreement", _agree(out, tp1_tokens), "common prefix",
           _common_prefix(out, tp1_tokens))
     assert _common_prefix(out, tp1_tokens) >= 4, (out, tp1_tokens)
+
+
+def test_tp2_allreduce_timeout_in_a_no_logits_prefill_chunk(monkeypatch):
+    """a middle chunk of a chunked prefill samples nothing; a custom
+    all-reduce timeout there must fail THAT step (before post_step commits its
+    KV blocks to the prefix cache), and a CommFault empties the prefix cache."""
+    from fasttalk_llm_microservice_amd.engine.runner import CommFault
+    from fasttalk_llm_microservice_amd.engine.sampling_params import SamplingParams
+    from fasttalk_llm_microservice_amd.parallel.tp import spawn_tp_engine
+
+    monkeypatch.setenv("FT_CONSISTENT_INIT", "1")
+    monkeypatch.setenv("FT_FAULT_TP_STALL", "m1:60")   # the worker's first eager step
+    monkeypatch.setenv("ENGINE_CUSTOM_AR_SPIN", str(1 << 20))
+    eng = spawn_tp_engine(_cfg(tp_size=2, tp_share_device=True, custom_allreduce=True,
+                               enable_prefix_caching=True, max_num_batched_tokens=64))
+    try:
+        rng = np.random.default_rng(5)
+        prompt = rng.integers(0, 120000, 200).tolist()       # 4 chunks of 64 tokens
+        sp = SamplingParams(temperature=0, max_tokens=4, ignore_eos=True)
+        eng.add_request("p0", prompt, sp)
+        fault = None
+        for _ in range(20):
+            try:
+                eng.step()
+            except CommFault as e:
+                fault = e
+                break
+        assert fault is not None, "the stalled chunk must fail its own step"
+        # the failing step was the first (no-logits) chunk: nothing was committed
+        assert eng.runner.stats["prefill_steps"] == 1
+        eng.fail_unfinished(str(fault), reset_cache=True)
+        assert eng.bm.num_cached() == 0 and eng.bm.num_free() == eng.bm.num_blocks
+        out = eng.generate([prompt], sp)                    # fallback collectives
+        assert len(out[0]) == 4 and eng.tp_group.alive()
+    finally:
+        eng.shutdown()

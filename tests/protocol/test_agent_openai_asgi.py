@@ -217,6 +217,37 @@ def test_openai_streams_with_tools(monkeypatch, engine):
     assert all(i < fin[0] for i in content + calls)
 
 
+def test_openai_stream_json_text_with_tools_is_content(monkeypatch, engine):
+    """with ``tools`` present, a reply that starts with '{' but is not a
+    call of one of the request's tools (a JSON answer) is streamed as content."""
+    from app.core.websocket_server_vllm import WebSocketLLMServer
+    from app.utils.config import Config
+    from fasttalk_llm_microservice_amd.engine.tool_parser import StreamingToolCallParser
+
+    monkeypatch.setenv("LLM_PROVIDER", "native")
+    monkeypatch.setenv("ENABLE_PYDANTIC_AI", "false")
+    c = TestClient(WebSocketLLMServer(Config(), engine=engine).app)
+    tools = [{"type": "function", "function": {"name": "get_weather", "parameters": {
+        "type": "object", "properties": {"city": {"type": "string"}}}}}]
+    rf = {"type": "json_schema", "json_schema": {"schema": {
+        "type": "object", "properties": {"ok": {"type": "boolean"}}, "required": ["ok"]}}}
+    s = c.post("/v1/chat/completions", json={
+        "messages": [{"role": "user", "content": "json please"}], "tools": tools,
+        "response_format": rf, "max_tokens": 20, "seed": 2, "stream": True})
+    chunks = _sse(s.text)
+    deltas = [ch["choices"][0]["delta"] for ch in chunks]
+    assert not any(d.get("tool_calls") for d in deltas)
+    text = "".join(d.get("content") or "" for d in deltas)
+    assert isinstance(json.loads(text)["ok"], bool)
+    assert chunks[-1]["choices"][0]["finish_reason"] in ("stop", "length")
+    # a "name" that is not a requested tool never becomes a call header
+    p = StreamingToolCallParser(["get_weather"])
+    assert p.feed('{"name": "Alice", "parameters": {"a": 1}}') == [] and p.rejected
+    p = StreamingToolCallParser(["get_weather"])
+    out = p.feed('{"name": "get_weather", "parameters": {"city": "Oslo"}}')
+    assert out[0]["function"]["name"] == "get_weather"
+
+
 # ----------------------------------------------------------------------------- ASGI over aiohttp
 def test_aiohttp_asgi_transport_serves_ws_and_http(monkeypatch, engine):
     import aiohttp

@@ -232,6 +232,46 @@ def test_background_prefill_is_dropped_under_kv_pressure():
     assert eng.bm.num_free() == eng.bm.num_blocks
 
 
+def test_partial_warmup_gives_blocks_to_a_waiting_prompt():
+    """a warm-up part-way through its chunked prefill must not keep
+    its blocks while a real prompt waits for them (nothing running: the prompt
+    was rejected; sequences running: the warm-up never progressed)."""
+    eng = _fake_engine(max_num_seqs=8, max_num_batched_tokens=64, prefill_chunk=32,
+                       num_blocks=16)
+    eng.add_request("warm", list(range(500, 560)), SamplingParams(temperature=0, max_tokens=1),
+                    background=True)                  # 15 blocks of 4
+    eng.step()                                        # one 32-token chunk: 8 blocks held
+    assert eng.scheduler.background and eng.scheduler.background[0].block_ids
+    outs = eng.generate([list(range(1, 41))], SamplingParams(temperature=0, max_tokens=3,
+                                                             ignore_eos=True))  # 10 blocks
+    assert outs == [_expected(list(range(1, 41)), 3)]
+    assert eng.stats["finished_error"] == 0
+    while eng.has_work():
+        eng.step()
+    assert eng.bm.num_free() == eng.bm.num_blocks
+
+
+def test_partial_warmup_yields_while_sessions_decode():
+    eng = _fake_engine(max_num_seqs=8, max_num_batched_tokens=64, prefill_chunk=32,
+                       num_blocks=20)
+    sp = SamplingParams(temperature=0, max_tokens=12, ignore_eos=True)
+    eng.add_request("d0", list(range(1, 9)), sp)      # 2 blocks, grows to 5
+    eng.step()
+    eng.add_request("warm", list(range(500, 560)), SamplingParams(temperature=0, max_tokens=1),
+                    background=True)
+    eng.step()                                        # warm-up takes a chunk
+    assert eng.scheduler.background[0].block_ids
+    seen = []
+    eng.add_request("late", list(range(100, 140)), sp, on_output=seen.append)  # 10 blocks + growth
+    for _ in range(3):
+        eng.step()
+    assert any(o.num_output_tokens > 0 for o in seen), "the waiting prompt never got admitted"
+    while eng.has_work():
+        eng.step()
+    assert eng.stats["finished_error"] == 0
+    assert eng.bm.num_free() == eng.bm.num_blocks
+
+
 def test_preemption_under_kv_pressure_completes_everything():
     eng = _fake_engine(num_blocks=12, max_num_seqs=8, max_num_batched_tokens=64)
     prompts = [[i + 1] * 6 for i in range(5)]
