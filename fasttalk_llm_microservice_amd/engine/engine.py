@@ -62,6 +62,9 @@ class LLMEngine:
                                    chunk_counts_decode=cfg.prefill_chunk_rows)
         self.stop_ids = set(self.tokenizer.stop_ids) | set(self.model_cfg.eos_token_ids)
         self._trie = None
+        # jump-forward over grammar-forced runs (ENGINE_JUMP_FORWARD=0 disables)
+        self.jump_forward = os.environ.get("ENGINE_JUMP_FORWARD", "1") != "0"
+        self._jf_cache: Dict[bytes, List[int]] = {}
         self.stats = collections.Counter()
         self.step_times = collections.deque(maxlen=512)
         # FT_STEP_TRACE=<path>: per-step timeline (kind, rows, tokens, start/end) and
@@ -98,6 +101,9 @@ class LLMEngine:
         if params.guided is not None:
             seq.grammar = params.guided.grammar(self)
             seq.grammar_state = seq.grammar.initial()
+            # the grammar's fixed head (e.g. '{"name": "' of a tool call) is output the
+            # model cannot choose: appended now, prefilled with the prompt
+            seq.jf_text, seq.jf_ids = self._jump_forward(seq, room=params.max_tokens - 1)
         self.scheduler.add(seq)
         self.stats["requests"] += 1
         return seq
@@ -291,6 +297,46 @@ class LLMEngine:
         self.last_step_end = time.time()
         return outs
 
+    def _forced_ids(self, fb: bytes) -> List[int]:
+        """Token ids whose bytes are exactly ``fb`` (cut at the last complete UTF-8
+        character), or [] when the tokenizer does not round-trip them."""
+        cache = self._jf_cache
+        ids = cache.get(fb)
+        if ids is None:
+            text = fb.decode("utf-8", errors="ignore")
+            while text and text.encode("utf-8") != fb[:len(text.encode("utf-8"))]:
+                text = text[:-1]
+            ids = self.tokenizer.encode(text) if text else []
+            tb = self.tokenizer.id_to_bytes
+            if b"".join(tb[i] for i in ids) != text.encode("utf-8"):
+                ids = []
+            if len(cache) < 4096:
+                cache[fb] = ids
+        return ids
+
+    def _jump_forward(self, seq: Sequence, room: int):
+        """Appends the bytes the grammar forces from the sequence's current state (the
+        rest of a key, '": "', closing braces, a tool name once its prefix is unique)
+        as tokens, advancing the grammar and the detokenizer; returns (text, ids).
+        They are prefilled in the next step instead of decoded one step each."""
+        if not self.jump_forward or room <= 0 or seq.grammar_state < 0:
+            return "", []
+        fb = seq.grammar.forced(seq.grammar_state)
+        if not fb:
+            return "", []
+        text, used = "", []
+        for t in self._forced_ids(fb)[:room]:
+            st = seq.grammar.advance_token(seq.grammar_state, t)
+            if st < 0:
+                break
+            seq.grammar_state = st
+            seq.append(t)
+            text += self.detok.push(seq.detok_stream, t)
+            used.append(t)
+        if used:
+            self.stats["jump_forward_tokens"] += len(used)
+        return text, used
+
     def _process_token(self, seq: Sequence, tok: int) -> Optional[RequestOutput]:
         if seq.status == SeqStatus.FINISHED:
             return None
@@ -311,11 +357,20 @@ class LLMEngine:
                 seq.grammar_state = seq.grammar.advance_token(seq.grammar_state, tok)
                 if seq.grammar_state < 0:
                     reason = "stop"
+        pre_text, pre_ids, post_ids = "", [], []
+        if first and seq.jf_ids:   # the head forced at admission goes out with the first token
+            pre_text, pre_ids = seq.jf_text, seq.jf_ids
+            seq.jf_text, seq.jf_ids = "", []
         if is_stop_tok and n_out > p.min_tokens:
             reason = "stop"
-            delta = ""
+            delta = pre_text
         else:
-            delta = self.detok.push(seq.detok_stream, tok)
+            delta = pre_text + self.detok.push(seq.detok_stream, tok)
+            if seq.grammar is not None and reason is None:
+                room = min(p.max_tokens - n_out, self.max_model_len - 1 - seq.n_tokens)
+                jtext, post_ids = self._jump_forward(seq, room)
+                delta += jtext
+                n_out = seq.num_output
         if reason is None:
             if n_out >= p.max_tokens or seq.n_tokens >= self.max_model_len:
                 reason = "length"
@@ -325,7 +380,7 @@ class LLMEngine:
                 reason = "stop"
         elif p.stop and reason is not None:
             pass
-        ids = [] if (is_stop_tok and reason == "stop") else [tok]
+        ids = pre_ids + ([] if (is_stop_tok and reason == "stop") else [tok]) + post_ids
         if reason is not None:
             return self._finalize(seq, reason, emit=True, delta=delta, ids=ids)
         if not delta and not first:

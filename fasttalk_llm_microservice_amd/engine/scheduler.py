@@ -174,11 +174,21 @@ class Scheduler:
         if self.swapped and not self._swap_out:
             resumed, swap_in = self._schedule_swap_in(len(decode))
             decode += resumed
-        budget = self.max_tokens - len(decode)
+        # jump-forward (guided decoding): a running sequence whose grammar forced a run
+        # of tokens has them pending past the sampled one; they are prefilled as one
+        # chunk (sampled at its last row) instead of one decode step each
+        jumps = [s for s in decode if s.n_tokens - s.num_computed > 1]
+        if jumps:
+            decode = [s for s in decode if s.n_tokens - s.num_computed <= 1]
+        jtok = [s.n_tokens - s.num_computed for s in jumps]
+        budget = self.max_tokens - len(decode) - sum(jtok)
+        n_rows = len(decode) + len(jumps)
         if self.swapped:  # swapped sequences go first; only unfinished chunks continue
             pseqs, ptok, psamp, rejected = [], [], [], []
         else:
-            pseqs, ptok, psamp, rejected = self._schedule_prefill(budget, len(decode))
+            pseqs, ptok, psamp, rejected = self._schedule_prefill(budget, n_rows)
+        if jumps:
+            pseqs, ptok, psamp = jumps + pseqs, jtok + ptok, [True] * len(jumps) + psamp
         swap_out, self._swap_out = self._swap_out, []
         if not decode and not pseqs and not rejected and not swap_out and not swap_in:
             return None
@@ -412,7 +422,7 @@ class Scheduler:
             if seq.status == SeqStatus.FINISHED:
                 continue
             seq.num_computed += n
-            if smp:
+            if smp and seq.status != SeqStatus.RUNNING:   # (a jump-forward chunk already runs)
                 seq.status = SeqStatus.RUNNING
                 self._admit_counter += 1
                 seq.admit_order = self._admit_counter

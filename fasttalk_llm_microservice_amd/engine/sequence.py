@@ -38,7 +38,7 @@ class Sequence:
                  "num_computed", "num_committed_blocks", "num_cached_tokens", "arrival",
                  "first_token_time", "finish_reason", "detok_stream", "on_output", "grammar",
                  "grammar_state", "stop_buf", "text_len", "aborted", "preemptions", "admit_order",
-                 "meta", "host_slots", "background")
+                 "meta", "host_slots", "background", "jf_text", "jf_ids")
 
     def __init__(self, request_id: str, prompt_ids: List[int], params: SamplingParams,
                  on_output: Optional[Callable[[RequestOutput], None]] = None, meta: Any = None):
@@ -69,6 +69,10 @@ class Sequence:
         self.admit_order = 0
         self.meta = meta
         self.host_slots: List[int] = []
+        # jump-forward tokens appended at admission (guided decoding), reported with
+        # the first sampled token's output
+        self.jf_text = ""
+        self.jf_ids: List[int] = []
 
     # ---------------------------------------------------------------- tokens
     @property

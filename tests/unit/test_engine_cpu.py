@@ -416,3 +416,48 @@ def test_tiny_cpu_guided_json(tiny_engine):
     ids = tiny_engine.generate([[1, 2, 3]], sp)[0]
     obj = json.loads(tiny_engine.tokenizer.decode(ids))
     assert set(obj) == {"city", "n"} and isinstance(obj["n"], int)
+
+
+def test_jump_forward_prefills_forced_grammar_runs(tiny_engine, monkeypatch):
+    """bytes the grammar forces (a tool call's '{"name": "', the rest
+    of a tool name once its prefix is unique, '", "parameters": {"query": "', the
+    closing braces) are appended as tokens and prefilled in ONE step instead of
+    one decode step per token; the call stays valid JSON."""
+    from fasttalk_llm_microservice_amd.engine.guided import tool_call_ast
+
+    tools = [{"type": "function", "function": {"name": "duckduckgo_search", "parameters": {
+        "type": "object", "properties": {"query": {"type": "string", "maxLength": 12}},
+        "required": ["query"]}}},
+        {"type": "function", "function": {"name": "get_current_time",
+                                          "parameters": {"type": "object", "properties": {}}}}]
+    spec = GuidedSpec(tool_call_ast(tools))
+    eng = tiny_engine
+    steps = []
+    orig = eng.runner.execute
+
+    def spy(batch, masks):
+        steps.append([(s.num_computed, n, s.status.name) for s, n in
+                      zip(batch.prefill_seqs, batch.prefill_tokens)] + [("d", len(batch.decode_seqs))])
+        return orig(batch, masks)
+
+    monkeypatch.setattr(eng.runner, "execute", spy)
+    before = eng.stats["jump_forward_tokens"]
+    outs = []
+    for seed in range(4):
+        sp = SamplingParams(temperature=1.0, max_tokens=80, seed=seed, guided=spec)
+        ids = eng.generate([[1, 2, 3]], sp)[0]
+        call = json.loads(eng.tokenizer.decode(ids))
+        assert call["name"] in ("duckduckgo_search", "get_current_time")
+        outs.append((call, len(ids)))
+    assert eng.stats["jump_forward_tokens"] > before
+    # the call head was prefilled with the prompt (3 prompt tokens + forced head)
+    assert any(n > 3 for row in steps for (a, n, st) in row[:-1] if a == 0)
+    # forced runs of a running sequence went in as multi-token prefill chunks
+    assert any(n > 1 and st == "RUNNING" for row in steps for (a, n, st) in row[:-1])
+    # fewer forward passes than output tokens
+    assert len(steps) < sum(n for _, n in outs)
+    monkeypatch.setenv("ENGINE_JUMP_FORWARD", "0")
+    off = LLMEngine(EngineConfig(model="tiny", device="cpu", num_kv_blocks=256, max_model_len=1024))
+    assert not off.jump_forward
+    ids = off.generate([[1, 2, 3]], SamplingParams(temperature=1.0, max_tokens=80, seed=0, guided=spec))[0]
+    assert json.loads(off.tokenizer.decode(ids))["name"] in ("duckduckgo_search", "get_current_time")

@@ -114,8 +114,9 @@ class _WarmEngine(_FakeEngine):
         super().__init__()
         self.warm = []
 
-    def prefill_background(self, ids):
+    def prefill_background(self, ids, session_id=None):
         self.warm.append(list(ids))
+        self.warm_sessions = getattr(self, "warm_sessions", []) + [session_id]
 
 
 import pytest
