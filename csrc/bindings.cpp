@@ -24,13 +24,6 @@ int ft_paged_decode_attention(void* out, int out_stride, float* tmp_out, float* 
                               const void* v_cache, const int* block_tables, int bt_stride,
                               const int* seq_lens, int batch, int nq, int nkv, int head_dim,
                               int block_size, float scale, int* counters, hipStream_t stream);
-int ft_paged_decode_attention_rp(void* out, int out_stride, float* tmp_out, float* tmp_ml,
-                                 const void* q, int q_stride, void* k_cache, void* v_cache,
-                                 const int* block_tables, int bt_stride, const int* seq_lens,
-                                 int batch, int nq, int nkv, int head_dim, int block_size,
-                                 float scale, int* counters, const float* rope_ws, int rope_splits,
-                                 int rope_rows, int rope_cols, const float* cos_sin,
-                                 const int* positions, const int* slot_mapping, hipStream_t stream);
 int ft_prefill_tile_tokens(int nq, int nkv);
 int ft_prefill_attention(void* out, int out_stride, const void* q, int q_stride,
                          const void* k_cache, const void* v_cache, const int* block_tables,
@@ -232,56 +225,6 @@ void paged_decode_attention(at::Tensor out, at::Tensor q, at::Tensor k_cache, at
                                      (int)head_dim, (int)k_cache.size(2), (float)scale, cnt,
                                      cur_stream()),
            "paged_decode_attention");
-}
-
-// Decode attention with RoPE + the new token's KV write folded in: q / k / v of
-// the `batch` decode rows come from the QKV GEMM's fp32 split-K slabs
-// ws[splits][batch][(nq + 2 nkv) * D] (csrc/kernels/attn_decode.hip, DecRope).
-void paged_decode_attention_rope(at::Tensor out, at::Tensor ws, int64_t splits, int64_t batch,
-                                 at::Tensor positions, at::Tensor cos_sin, at::Tensor slot_mapping,
-                                 at::Tensor k_cache, at::Tensor v_cache, at::Tensor block_tables,
-                                 at::Tensor seq_lens, at::Tensor tmp_out, at::Tensor tmp_ml,
-                                 int64_t nq, int64_t nkv, int64_t head_dim, double scale,
-                                 c10::optional<at::Tensor> counters) {
-  check_bf16(out, "out");
-  check_rows(out, "out");
-  check_kv_caches(k_cache, v_cache, nkv, head_dim);
-  check_i32(block_tables, "block_tables");
-  check_i32(seq_lens, "seq_lens");
-  check_i32(positions, "positions");
-  check_i32(slot_mapping, "slot_mapping");
-  TORCH_CHECK(ws.is_cuda() && ws.scalar_type() == at::kFloat && ws.is_contiguous(), "ws: fp32 slabs");
-  TORCH_CHECK(cos_sin.is_cuda() && cos_sin.scalar_type() == at::kFloat && cos_sin.is_contiguous() &&
-                  cos_sin.size(-1) == head_dim, "cos_sin [positions, head_dim] fp32");
-  const int64_t cols = (nq + 2 * nkv) * head_dim;
-  TORCH_CHECK(splits >= 1 && ws.numel() >= splits * batch * cols, "qkv slabs too small");
-  TORCH_CHECK(out.size(0) >= batch && out.size(1) >= nq * head_dim && seq_lens.numel() >= batch &&
-                  block_tables.size(0) >= batch && positions.numel() >= batch &&
-                  slot_mapping.numel() >= batch, "batch sizes");
-  TORCH_CHECK(batch <= ft_decode_max_batch(), "decode batch above ", ft_decode_max_batch());
-  TORCH_CHECK(nq % nkv == 0 && nq / nkv <= 16, "GQA group must be <= 16");
-  TORCH_CHECK(head_dim % 64 == 0, "head_dim");
-  const int64_t slots = batch * nkv + ft_decode_waves();
-  TORCH_CHECK(tmp_out.scalar_type() == at::kFloat && tmp_ml.scalar_type() == at::kFloat &&
-                  tmp_out.numel() >= slots * (nq / nkv) * head_dim &&
-                  tmp_ml.numel() >= slots * (nq / nkv) * 2,
-              "decode workspace too small (ops.decode_workspace)");
-  int* cnt = nullptr;
-  if (counters.has_value()) {
-    check_i32(*counters, "counters");
-    TORCH_CHECK(counters->numel() >= batch * nkv, "decode counters too small");
-    cnt = counters->data_ptr<int>();
-  }
-  check_rc(ft_paged_decode_attention_rp(out.data_ptr(), (int)out.stride(0), tmp_out.data_ptr<float>(),
-                                        tmp_ml.data_ptr<float>(), nullptr, 0, k_cache.data_ptr(),
-                                        v_cache.data_ptr(), block_tables.data_ptr<int>(),
-                                        (int)block_tables.stride(0), seq_lens.data_ptr<int>(),
-                                        (int)batch, (int)nq, (int)nkv, (int)head_dim,
-                                        (int)k_cache.size(2), (float)scale, cnt,
-                                        ws.data_ptr<float>(), (int)splits, (int)batch, (int)cols,
-                                        cos_sin.data_ptr<float>(), positions.data_ptr<int>(),
-                                        slot_mapping.data_ptr<int>(), cur_stream()),
-           "paged_decode_attention_rope");
 }
 
 void prefill_attention(at::Tensor out, at::Tensor q, at::Tensor k_cache, at::Tensor v_cache,
@@ -824,7 +767,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("silu_mul", &silu_mul);
   m.def("rope_kv_write", &rope_kv_write);
   m.def("paged_decode_attention", &paged_decode_attention);
-  m.def("paged_decode_attention_rope", &paged_decode_attention_rope);
   m.def("decode_waves", []() { return ft_decode_waves(); });
   m.def("decode_max_batch", []() { return ft_decode_max_batch(); });
   m.def("prefill_attention", &prefill_attention);

@@ -117,76 +117,139 @@ __device__ __forceinline__ void mt_load(MTile<D>& t, const uint16_t* __restrict_
     t.v[nd] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(vr, voff_b, nd * vstep_b, 2));
 }
 
-// RoPE + KV write folded into the attention launch (RP = true): q and the new
-// token's K / V come straight from the QKV GEMM's fp32 split-K slabs instead of a
-// separate slab_rope_kv launch.  Each wave RoPEs its segment's q fragments in
-// registers (a lane's dims d and d + D/2 sit in fragments kc and kc + KC/2), and
-// the wave that owns a segment's LAST tile builds the new token's K row / V^T
-// column, writes them to the paged cache for later steps and patches them into
-// the tile registers it loaded (that row of the cache is not read back).
-struct DecRope {
-  const float* ws;        // [splits][rows][cols] fp32 qkv slabs
-  int splits, rows, cols;
-  const float* cos_sin;   // [pos][D]: cos in [0, D/2), sin in [D/2, D)
-  const int* positions;
-  const int* slot_mapping;
-  int nq;
-};
-
-// x[kc][j] = sum over splits of src[kc * 32 + j] (fp32 slabs, `slab` floats apart)
-template <int KC>
-__device__ __forceinline__ void rp_gather(float (&x)[KC][8], const float* __restrict__ src,
-                                          size_t slab, int splits) {
+// End of a wave's piece of segment (b, h): the whole segment -> bf16 output;
+// otherwise an fp32 (acc, m, l) partial at slot segment + wave, and with FC the
+// in-launch combine by the last arriving wave (see the header comment).
+template <int D, int G, int ND, bool FC>
+__device__ __forceinline__ void dec_finish(floatx4_t (&o)[ND], float l_run, float m_run, int b, int h,
+                                           int t0, int cnt, int nb, int w, int nw, int total, int nkv,
+                                           const int* s_pre, uint16_t* __restrict__ out, int out_stride,
+                                           float* __restrict__ tmp_out, float* __restrict__ tmp_ml,
+                                           int* __restrict__ counters, int lane, int g, int n) {
+  // head n's sum over the 4 token groups
+  float l_tot = l_run + __shfl_xor(l_run, 16, 64);
+  l_tot += __shfl_xor(l_tot, 32, 64);
+  // C-layout rows of O: lane (g, n) holds heads 4g+i, dim n (+16 nd)
+  const int seg = b * nkv + h;
+  if (t0 == 0 && cnt == nb) {   // the whole segment: final bf16 output
 #pragma unroll
-  for (int kc = 0; kc < KC; ++kc) {
-    const float4 a = *reinterpret_cast<const float4*>(src + kc * 32);
-    const float4 c = *reinterpret_cast<const float4*>(src + kc * 32 + 4);
-    x[kc][0] = a.x; x[kc][1] = a.y; x[kc][2] = a.z; x[kc][3] = a.w;
-    x[kc][4] = c.x; x[kc][5] = c.y; x[kc][6] = c.z; x[kc][7] = c.w;
-  }
-  for (int s = 1; s < splits; ++s) {
-    const float* p = src + (size_t)s * slab;
+    for (int i4 = 0; i4 < 4; ++i4) {
+      const int r = 4 * g + i4;
+      const float lr = __shfl(l_tot, r & 15, 64);
+      if (r < G) {
+        const float inv = 1.f / lr;
+        uint16_t* op = out + (size_t)b * out_stride + (h * G + r) * D + n;
 #pragma unroll
-    for (int kc = 0; kc < KC; ++kc) {
-      const float4 a = *reinterpret_cast<const float4*>(p + kc * 32);
-      const float4 c = *reinterpret_cast<const float4*>(p + kc * 32 + 4);
-      x[kc][0] += a.x; x[kc][1] += a.y; x[kc][2] += a.z; x[kc][3] += a.w;
-      x[kc][4] += c.x; x[kc][5] += c.y; x[kc][6] += c.z; x[kc][7] += c.w;
+        for (int nd = 0; nd < ND; ++nd) op[nd * 16] = f32_to_bf16(o[nd][i4] * inv);
+      }
+    }
+  } else {
+    const size_t slot = (size_t)(seg + w);
+#pragma unroll
+    for (int i4 = 0; i4 < 4; ++i4) {
+      const int r = 4 * g + i4;
+      const float lr = __shfl(l_tot, r & 15, 64);
+      const float mr = __shfl(m_run, r & 15, 64);
+      if (r < G) {
+        float* dst = tmp_out + (slot * G + r) * D + n;
+        if (FC) {
+          // write-through (read by another wave in this launch), dims permuted to
+          // [n][nd] so each lane's ND values are contiguous: 8-B sc1 stores, and
+          // (m, l) as one 8-B store
+          uint64_t* dp = reinterpret_cast<uint64_t*>(tmp_out + (slot * G + r) * D + n * ND);
+#pragma unroll
+          for (int p2 = 0; p2 < ND / 2; ++p2) {
+            const uint64_t v = (uint64_t)__float_as_uint(o[2 * p2][i4]) |
+                               ((uint64_t)__float_as_uint(o[2 * p2 + 1][i4]) << 32);
+            __hip_atomic_store(dp + p2, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+          if (n == 0) {
+            const uint64_t ml = (uint64_t)__float_as_uint(mr) | ((uint64_t)__float_as_uint(lr) << 32);
+            __hip_atomic_store(reinterpret_cast<uint64_t*>(tmp_ml + (slot * G + r) * 2), ml,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+        } else {
+#pragma unroll
+          for (int nd = 0; nd < ND; ++nd) dst[nd * 16] = o[nd][i4];
+          if (n == 0) {
+            tmp_ml[(slot * G + r) * 2] = mr;
+            tmp_ml[(slot * G + r) * 2 + 1] = lr;
+          }
+        }
+      }
+    }
+    if (FC) {
+      // publish (every partial store of this wave retired), then take a ticket
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      int prev = 0;
+      if (lane == 0)
+        prev = __hip_atomic_fetch_add(counters + seg, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      prev = __shfl(prev, 0, 64);
+      // waves sharing the segment: the first and last whose tile range meets it
+      const int S = nkv * s_pre[b] + h * nb, E = S + nb;
+      const int wf = (int)(((long long)(S + 1) * nw - 1) / total);
+      const int wl = (int)(((long long)E * nw - 1) / total);
+      const int np = wl - wf + 1;
+      if (prev == np - 1) {   // last arriver: merge the np partials of this segment
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keep the loads below the ticket
+        const size_t base = (size_t)(seg + wf);
+        uint16_t* op = out + (size_t)b * out_stride + h * G * D;
+        // lane (r, c): head r, dims c + 16 nd of the permuted partials; the
+        // partial slots are read in batches of 8 with every load of a batch in
+        // flight at once (8-B sc1 loads; slots past np re-read the last one and
+        // are masked), online-max merge
+        for (int q4 = lane; q4 < G * 16; q4 += 64) {
+          const int r = q4 >> 4, c = q4 & 15;
+          float M = -INFINITY, den = 0.f, acc[ND];
+#pragma unroll
+          for (int nd = 0; nd < ND; ++nd) acc[nd] = 0.f;
+          for (int k0 = 0; k0 < np; k0 += 8) {
+            uint64_t mlv[8], ov[8][ND / 2];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+              const size_t sl = (base + min(k0 + k, np - 1)) * G + r;
+              mlv[k] = __hip_atomic_load(reinterpret_cast<const uint64_t*>(tmp_ml + sl * 2),
+                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              const uint64_t* sp = reinterpret_cast<const uint64_t*>(tmp_out + sl * D + c * ND);
+#pragma unroll
+              for (int p2 = 0; p2 < ND / 2; ++p2)
+                ov[k][p2] = __hip_atomic_load(sp + p2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+              if (k0 + k < np) {
+                const float m = __uint_as_float((uint32_t)mlv[k]);
+                const float l = __uint_as_float((uint32_t)(mlv[k] >> 32));
+                const float mn = fmaxf(M, m);
+                const float a = exp2f(M - mn), e = exp2f(m - mn);
+                den = den * a + e * l;
+#pragma unroll
+                for (int p2 = 0; p2 < ND / 2; ++p2) {
+                  acc[2 * p2] = acc[2 * p2] * a + e * __uint_as_float((uint32_t)ov[k][p2]);
+                  acc[2 * p2 + 1] = acc[2 * p2 + 1] * a + e * __uint_as_float((uint32_t)(ov[k][p2] >> 32));
+                }
+                M = mn;
+              }
+            }
+          }
+          const float inv = 1.f / den;
+#pragma unroll
+          for (int nd = 0; nd < ND; ++nd) op[r * D + 16 * nd + c] = f32_to_bf16(acc[nd] * inv);
+        }
+        if (lane == 0)
+          __hip_atomic_store(counters + seg, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
   }
 }
 
-// rotate-half RoPE of one lane's fragments (dims 32 kc + 8 g + j), packed to bf16
-template <int D>
-__device__ __forceinline__ void rp_rope(uint4 (&frag)[D / 32], float (&x)[D / 32][8],
-                                        const float* __restrict__ cs, int g) {
-  constexpr int KC = D / 32, HK = KC / 2;
-#pragma unroll
-  for (int kc = 0; kc < HK; ++kc) {
-    uint32_t lo[4], hi[4];
-#pragma unroll
-    for (int j = 0; j < 8; j += 2) {
-      const int d = kc * 32 + 8 * g + j;
-      const float c0 = cs[d], c1 = cs[d + 1], s0 = cs[D / 2 + d], s1 = cs[D / 2 + d + 1];
-      const float a0 = x[kc][j] * c0 - x[kc + HK][j] * s0;
-      const float a1 = x[kc][j + 1] * c1 - x[kc + HK][j + 1] * s1;
-      const float b0 = x[kc + HK][j] * c0 + x[kc][j] * s0;
-      const float b1 = x[kc + HK][j + 1] * c1 + x[kc][j + 1] * s1;
-      lo[j / 2] = (uint32_t)f32_to_bf16(a0) | ((uint32_t)f32_to_bf16(a1) << 16);
-      hi[j / 2] = (uint32_t)f32_to_bf16(b0) | ((uint32_t)f32_to_bf16(b1) << 16);
-    }
-    frag[kc] = make_uint4(lo[0], lo[1], lo[2], lo[3]);
-    frag[kc + HK] = make_uint4(hi[0], hi[1], hi[2], hi[3]);
-  }
-}
-
-template <int D, int G, int R, bool FC, int WPC, bool RP>
+template <int D, int G, int R, bool FC, int WPC>
 __global__ __launch_bounds__(256, WPC) void paged_decode_kernel(
     uint16_t* __restrict__ out, int out_stride, float* __restrict__ tmp_out,
     float* __restrict__ tmp_ml, const uint16_t* __restrict__ q, int q_stride,
     uint16_t* __restrict__ k_cache, uint16_t* __restrict__ v_cache,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ seq_lens,
-    int batch, int nkv, int bs_shift, float scale_log2, int* __restrict__ counters, DecRope rp) {
+    int batch, int nkv, int bs_shift, float scale_log2, int* __restrict__ counters) {
   static_assert(G >= 1 && G <= 16, "GQA group must fit the 16 MFMA columns");
   constexpr int KC = D / 32, ND = D / 16;
   __shared__ int s_pre[kDecMaxBatch + 1];
@@ -238,57 +301,11 @@ __global__ __launch_bounds__(256, WPC) void paged_decode_kernel(
 
     // Q^T fragments (B operand): lane (g, n) = head n of this kv head, dims 8g.. (+32 kc)
     uint4 qb[KC];
-    // RP: the new token's K row (lanes n == r) and V^T column (lanes g == r / 4)
-    uint4 knew[KC];
-    uint32_t vnew[ND];
-    const bool has_last = RP && t0 + cnt == nb;
-    const int r_new = (L - 1) & 15;
-    // RP: issued after the first chunk's tile loads so the slab / cos-sin loads'
-    // latency hides under the KV stream's
-    auto rp_prep = [&]() {
-      const size_t slab = (size_t)rp.rows * rp.cols;
-      const float* cs = rp.cos_sin + (size_t)rp.positions[b] * D;
-      const float* row = rp.ws + (size_t)b * rp.cols;
-      float x[KC][8];
-      rp_gather<KC>(x, row + (h * G + min(n, G - 1)) * D + 8 * g, slab, rp.splits);
-      rp_rope<D>(qb, x, cs, g);
 #pragma unroll
-      for (int kc = 0; kc < KC; ++kc)
-        if (n >= G) qb[kc] = make_uint4(0, 0, 0, 0);
-      if (has_last) {
-        rp_gather<KC>(x, row + (rp.nq + h) * D + 8 * g, slab, rp.splits);
-        rp_rope<D>(knew, x, cs, g);
-        const float* vs = row + (rp.nq + nkv + h) * D + n;
-#pragma unroll
-        for (int nd = 0; nd < ND; ++nd) {
-          float v = vs[nd * 16];
-          for (int s2 = 1; s2 < rp.splits; ++s2) v += vs[(size_t)s2 * slab + nd * 16];
-          vnew[nd] = f32_to_bf16(v);
-        }
-        const int slot = rp.slot_mapping[b];
-        if (slot >= 0) {   // the paged cache keeps the new token for later steps
-          const size_t blk = (size_t)(slot >> bs_shift);
-          const int off = slot & bmask;
-          if (n == r_new) {
-            uint16_t* kp = k_cache + ((blk * nkv + h) * bsz + off) * D + 8 * g;
-#pragma unroll
-            for (int kc = 0; kc < KC; ++kc) *reinterpret_cast<uint4*>(kp + kc * 32) = knew[kc];
-          }
-          if (g == 0) {   // V^T column: dims n + 16 nd
-            uint16_t* vp = v_cache + ((blk * nkv + h) * D + n) * bsz + off;
-#pragma unroll
-            for (int nd = 0; nd < ND; ++nd) vp[(size_t)nd * 16 * bsz] = (uint16_t)vnew[nd];
-          }
-        }
-      }
-    };
-    if constexpr (!RP) {
-#pragma unroll
-      for (int kc = 0; kc < KC; ++kc)
-        qb[kc] = n < G ? *reinterpret_cast<const uint4*>(q + (size_t)b * q_stride +
-                                                         (h * G + n) * D + kc * 32 + 8 * g)
-                       : make_uint4(0, 0, 0, 0);
-    }
+    for (int kc = 0; kc < KC; ++kc)
+      qb[kc] = n < G ? *reinterpret_cast<const uint4*>(q + (size_t)b * q_stride +
+                                                       (h * G + n) * D + kc * 32 + 8 * g)
+                     : make_uint4(0, 0, 0, 0);
     floatx4_t o[ND];
 #pragma unroll
     for (int nd = 0; nd < ND; ++nd) o[nd] = floatx4_t{0.f, 0.f, 0.f, 0.f};
@@ -314,23 +331,6 @@ __global__ __launch_bounds__(256, WPC) void paged_decode_kernel(
       };
       auto consume = [&](MTile<D>& t, int i) {
         const int valid = L - ((t0 + c0 + i) << 4);   // tokens of this tile inside the sequence
-        if (RP && has_last && t0 + c0 + i == nb - 1) {
-          // the new token's row of the last tile: registers, not the (unwritten) cache
-#pragma unroll
-          for (int kc = 0; kc < KC; ++kc)
-            if (n == r_new) t.k[kc] = knew[kc];
-          if (g == (r_new >> 2)) {
-            const int sh = (r_new & 1) * 16;
-            const uint32_t keep = ~(0xFFFFu << sh);
-#pragma unroll
-            for (int nd = 0; nd < ND; ++nd) {
-              if (r_new & 2)
-                t.v[nd].y = (t.v[nd].y & keep) | (vnew[nd] << sh);
-              else
-                t.v[nd].x = (t.v[nd].x & keep) | (vnew[nd] << sh);
-            }
-          }
-        }
         floatx4_t s = floatx4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int kc = 0; kc < KC; ++kc)
@@ -374,9 +374,6 @@ __global__ __launch_bounds__(256, WPC) void paged_decode_kernel(
       MTile<D> ring[R];
 #pragma unroll
       for (int r = 0; r + 1 < R; ++r) ld(ring[r], r);
-      if constexpr (RP) {
-        if (c0 == 0) rp_prep();
-      }
       for (int i = 0; i < cc; i += R) {
 #pragma unroll
         for (int r = 0; r < R; ++r) {
@@ -388,121 +385,8 @@ __global__ __launch_bounds__(256, WPC) void paged_decode_kernel(
       }
     }
 
-    // head n's sum over the 4 token groups
-    float l_tot = l_run + __shfl_xor(l_run, 16, 64);
-    l_tot += __shfl_xor(l_tot, 32, 64);
-    // C-layout rows of O: lane (g, n) holds heads 4g+i, dim n (+16 nd)
-    const int seg = b * nkv + h;
-    if (t0 == 0 && cnt == nb) {   // the whole segment: final bf16 output
-#pragma unroll
-      for (int i4 = 0; i4 < 4; ++i4) {
-        const int r = 4 * g + i4;
-        const float lr = __shfl(l_tot, r & 15, 64);
-        if (r < G) {
-          const float inv = 1.f / lr;
-          uint16_t* op = out + (size_t)b * out_stride + (h * G + r) * D + n;
-#pragma unroll
-          for (int nd = 0; nd < ND; ++nd) op[nd * 16] = f32_to_bf16(o[nd][i4] * inv);
-        }
-      }
-    } else {
-      const size_t slot = (size_t)(seg + w);
-#pragma unroll
-      for (int i4 = 0; i4 < 4; ++i4) {
-        const int r = 4 * g + i4;
-        const float lr = __shfl(l_tot, r & 15, 64);
-        const float mr = __shfl(m_run, r & 15, 64);
-        if (r < G) {
-          float* dst = tmp_out + (slot * G + r) * D + n;
-          if (FC) {
-            // write-through (read by another wave in this launch), dims permuted to
-            // [n][nd] so each lane's ND values are contiguous: 8-B sc1 stores, and
-            // (m, l) as one 8-B store
-            uint64_t* dp = reinterpret_cast<uint64_t*>(tmp_out + (slot * G + r) * D + n * ND);
-#pragma unroll
-            for (int p2 = 0; p2 < ND / 2; ++p2) {
-              const uint64_t v = (uint64_t)__float_as_uint(o[2 * p2][i4]) |
-                                 ((uint64_t)__float_as_uint(o[2 * p2 + 1][i4]) << 32);
-              __hip_atomic_store(dp + p2, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            if (n == 0) {
-              const uint64_t ml = (uint64_t)__float_as_uint(mr) | ((uint64_t)__float_as_uint(lr) << 32);
-              __hip_atomic_store(reinterpret_cast<uint64_t*>(tmp_ml + (slot * G + r) * 2), ml,
-                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-          } else {
-#pragma unroll
-            for (int nd = 0; nd < ND; ++nd) dst[nd * 16] = o[nd][i4];
-            if (n == 0) {
-              tmp_ml[(slot * G + r) * 2] = mr;
-              tmp_ml[(slot * G + r) * 2 + 1] = lr;
-            }
-          }
-        }
-      }
-      if (FC) {
-        // publish (every partial store of this wave retired), then take a ticket
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        int prev = 0;
-        if (lane == 0)
-          prev = __hip_atomic_fetch_add(counters + seg, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        prev = __shfl(prev, 0, 64);
-        // waves sharing the segment: the first and last whose tile range meets it
-        const int S = nkv * s_pre[b] + h * nb, E = S + nb;
-        const int wf = (int)(((long long)(S + 1) * nw - 1) / total);
-        const int wl = (int)(((long long)E * nw - 1) / total);
-        const int np = wl - wf + 1;
-        if (prev == np - 1) {   // last arriver: merge the np partials of this segment
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keep the loads below the ticket
-          const size_t base = (size_t)(seg + wf);
-          uint16_t* op = out + (size_t)b * out_stride + h * G * D;
-          // lane (r, c): head r, dims c + 16 nd of the permuted partials; the
-          // partial slots are read in batches of 8 with every load of a batch in
-          // flight at once (8-B sc1 loads; slots past np re-read the last one and
-          // are masked), online-max merge
-          for (int q4 = lane; q4 < G * 16; q4 += 64) {
-            const int r = q4 >> 4, c = q4 & 15;
-            float M = -INFINITY, den = 0.f, acc[ND];
-#pragma unroll
-            for (int nd = 0; nd < ND; ++nd) acc[nd] = 0.f;
-            for (int k0 = 0; k0 < np; k0 += 8) {
-              uint64_t mlv[8], ov[8][ND / 2];
-#pragma unroll
-              for (int k = 0; k < 8; ++k) {
-                const size_t sl = (base + min(k0 + k, np - 1)) * G + r;
-                mlv[k] = __hip_atomic_load(reinterpret_cast<const uint64_t*>(tmp_ml + sl * 2),
-                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const uint64_t* sp = reinterpret_cast<const uint64_t*>(tmp_out + sl * D + c * ND);
-#pragma unroll
-                for (int p2 = 0; p2 < ND / 2; ++p2)
-                  ov[k][p2] = __hip_atomic_load(sp + p2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              }
-#pragma unroll
-              for (int k = 0; k < 8; ++k) {
-                if (k0 + k < np) {
-                  const float m = __uint_as_float((uint32_t)mlv[k]);
-                  const float l = __uint_as_float((uint32_t)(mlv[k] >> 32));
-                  const float mn = fmaxf(M, m);
-                  const float a = exp2f(M - mn), e = exp2f(m - mn);
-                  den = den * a + e * l;
-#pragma unroll
-                  for (int p2 = 0; p2 < ND / 2; ++p2) {
-                    acc[2 * p2] = acc[2 * p2] * a + e * __uint_as_float((uint32_t)ov[k][p2]);
-                    acc[2 * p2 + 1] = acc[2 * p2 + 1] * a + e * __uint_as_float((uint32_t)(ov[k][p2] >> 32));
-                  }
-                  M = mn;
-                }
-              }
-            }
-            const float inv = 1.f / den;
-#pragma unroll
-            for (int nd = 0; nd < ND; ++nd) op[r * D + 16 * nd + c] = f32_to_bf16(acc[nd] * inv);
-          }
-          if (lane == 0)
-            __hip_atomic_store(counters + seg, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-      }
-    }
+    dec_finish<D, G, ND, FC>(o, l_run, m_run, b, h, t0, cnt, nb, w, nw, total, nkv, s_pre, out,
+                             out_stride, tmp_out, tmp_ml, counters, lane, g, n);
     f += cnt;
   }
 }
@@ -601,24 +485,16 @@ static int dec_wg_per_cu() {
 extern "C" int ft_decode_waves() { return ft_num_cus() * 3 * 4; }
 extern "C" int ft_decode_max_batch() { return ft::kDecMaxBatch; }
 
-extern "C" int ft_paged_decode_attention_rp(void* out, int out_stride, float* tmp_out, float* tmp_ml,
-                                            const void* q, int q_stride, void* k_cache,
-                                            void* v_cache, const int* block_tables,
-                                            int bt_stride, const int* seq_lens, int batch, int nq,
-                                            int nkv, int head_dim, int block_size, float scale,
-                                            int* counters, const float* rope_ws, int rope_splits,
-                                            int rope_rows, int rope_cols, const float* cos_sin,
-                                            const int* positions, const int* slot_mapping,
-                                            hipStream_t stream) {
+extern "C" int ft_paged_decode_attention(void* out, int out_stride, float* tmp_out, float* tmp_ml,
+                                         const void* q, int q_stride, const void* k_cache,
+                                         const void* v_cache, const int* block_tables,
+                                         int bt_stride, const int* seq_lens, int batch, int nq,
+                                         int nkv, int head_dim, int block_size, float scale,
+                                         int* counters, hipStream_t stream) {
   if (batch <= 0) return 0;
   if (nq % nkv != 0) return -1;
   if (batch > ft::kDecMaxBatch) return -5;
   if (block_size < 16 || (block_size & (block_size - 1))) return -4;
-  const bool rp_on = rope_ws != nullptr;
-  if (rp_on && (rope_splits < 1 || rope_rows < batch || rope_cols != (nq + 2 * nkv) * head_dim ||
-                cos_sin == nullptr || positions == nullptr || slot_mapping == nullptr))
-    return -6;
-  const ft::DecRope rp{rope_ws, rope_splits, rope_rows, rope_cols, cos_sin, positions, slot_mapping, nq};
   const int bs_shift = __builtin_ctz(block_size);
   const int G = nq / nkv;
   const float scale_log2 = scale * 1.4426950408889634f;
@@ -635,20 +511,14 @@ extern "C" int ft_paged_decode_attention_rp(void* out, int out_stride, float* tm
 #define FT_DEC_ARGS                                                                             \
   (uint16_t*)out, out_stride, tmp_out, tmp_ml, (const uint16_t*)q, q_stride, (uint16_t*)k_cache, \
       (uint16_t*)v_cache, block_tables, bt_stride, seq_lens, batch, nkv, bs_shift, scale_log2,   \
-      counters, rp
-#define FT_DEC_LAUNCH_RP(DD, GG, RR, FCC, RPP)                                                  \
+      counters
+#define FT_DEC_LAUNCH(DD, GG, RR, FCC)                                                  \
   if (wpc == 1)                                                                                \
-    hipLaunchKernelGGL((ft::paged_decode_kernel<DD, GG, RR, FCC, 1, RPP>), dim3(nwg), dim3(256), \
+    hipLaunchKernelGGL((ft::paged_decode_kernel<DD, GG, RR, FCC, 1>), dim3(nwg), dim3(256),      \
                        0, stream, FT_DEC_ARGS);                                                \
   else                                                                                         \
-    hipLaunchKernelGGL((ft::paged_decode_kernel<DD, GG, RR, FCC, (RR == 2 ? 3 : 2), RPP>),     \
+    hipLaunchKernelGGL((ft::paged_decode_kernel<DD, GG, RR, FCC, (RR == 2 ? 3 : 2)>),          \
                        dim3(nwg), dim3(256), 0, stream, FT_DEC_ARGS)
-#define FT_DEC_LAUNCH(DD, GG, RR, FCC)                                                         \
-  if (rp_on) {                                                                                 \
-    FT_DEC_LAUNCH_RP(DD, GG, RR, FCC, true);                                                   \
-  } else {                                                                                     \
-    FT_DEC_LAUNCH_RP(DD, GG, RR, FCC, false);                                                  \
-  }
 #define FT_DEC_CASE(DD, GG, RR)                                                                \
   if (head_dim == DD && G == GG) {                                                             \
     nwg = ft_num_cus() * wpc;                                                                  \
@@ -677,20 +547,6 @@ extern "C" int ft_paged_decode_attention_rp(void* out, int out_stride, float* tm
   FT_DEC_CASE(64, 8, 2)
 #undef FT_DEC_CASE
 #undef FT_DEC_LAUNCH
-#undef FT_DEC_LAUNCH_RP
 #undef FT_DEC_ARGS
   return -2;
-}
-
-extern "C" int ft_paged_decode_attention(void* out, int out_stride, float* tmp_out, float* tmp_ml,
-                                         const void* q, int q_stride, const void* k_cache,
-                                         const void* v_cache, const int* block_tables,
-                                         int bt_stride, const int* seq_lens, int batch, int nq,
-                                         int nkv, int head_dim, int block_size, float scale,
-                                         int* counters, hipStream_t stream) {
-  return ft_paged_decode_attention_rp(out, out_stride, tmp_out, tmp_ml, q, q_stride,
-                                      const_cast<void*>(k_cache), const_cast<void*>(v_cache),
-                                      block_tables, bt_stride, seq_lens, batch, nq, nkv, head_dim,
-                                      block_size, scale, counters, nullptr, 0, 0, 0, nullptr,
-                                      nullptr, nullptr, stream);
 }

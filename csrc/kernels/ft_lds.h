@@ -42,6 +42,20 @@ __device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_dst) {
       : "memory");
 }
 
+// the same with the non-temporal policy (streamed-once data: decode K/V)
+__device__ __forceinline__ void glds16nt(const void* gsrc, uint32_t lds_dst) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off nt\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(lds_dst))
+      : "memory");
+}
+
 template <int N>
 __device__ __forceinline__ void lgkm_wait() {
   asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory");

@@ -172,10 +172,16 @@ constexpr int kChunks = kSlots / 8;  // 16 chunks of 8 ids per lane
 // multi-workgroup sampler (samp_*_kernel below)
 constexpr int kSlices = 32;
 constexpr int kSlThreads = 256;
+// top-k rows with k <= kTopkMax take the multi-workgroup top-k path: each slice
+// keeps its own top-k candidates (the global top-k is a subset of their union)
+constexpr int kTopkMax = 64;
+constexpr int kTopkKept = 256;   // kept set (top-k + ties) the merge kernel holds
 // per-row fp32 scratch: slice stats [kSlices][4] (M_p, Z_p, key, id) | M, Z |
-// cand (key, id) x 2 | above [kSlices][2] | flag
+// cand (key, id) x 2 | above [kSlices][2] | flag | top-k candidate counts
+// [kSlices] | top-k candidates [kSlices][kTopkMax] (key, id)
 constexpr int kWsStats = 0, kWsMZ = 4 * kSlices, kWsCand = kWsMZ + 2, kWsAbove = kWsCand + 4,
-              kWsFlag = kWsAbove + 2 * kSlices, kWsRow = kWsFlag + 1;
+              kWsFlag = kWsAbove + 2 * kSlices, kWsTkCnt = kWsFlag + 1,
+              kWsTk = kWsTkCnt + kSlices, kWsRow = kWsTk + 2 * kSlices * kTopkMax;
 
 template <typename T>
 __global__ __launch_bounds__(kSampThreads) void sample_kernel(
@@ -480,6 +486,62 @@ __device__ __forceinline__ bool topk_row(const int* top_k, int row, int vocab) {
   return k > 0 && k < vocab;
 }
 
+__device__ __forceinline__ int wave_sum_int(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// max over the workgroup (<= 16 waves), s: >= waves ints of LDS
+__device__ __forceinline__ uint32_t wave_max_u32_wg(uint32_t v, int* s) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o, 64));
+  __syncthreads();
+  if (lane_id() == 0) s[wave_id()] = (int)v;
+  __syncthreads();
+  uint32_t m = 0u;
+  for (int w = 0; w < (int)(blockDim.x >> 6); ++w) m = max(m, (uint32_t)s[w]);
+  return m;
+}
+
+// top-k rows the multi-workgroup path samples (greedy rows stay on the argmax path)
+__device__ __forceinline__ bool mw_topk_row(const int* top_k, const float* temperature, int row,
+                                            int vocab) {
+  return topk_row(top_k, row, vocab) && top_k[row] <= kTopkMax && temperature[row] > 0.f;
+}
+
+// largest t with count(key >= t) >= kk over NK register keys per thread of the
+// workgroup (4-ary search on the 16-bit key, 3 counts per pass); kk >= 1
+template <int NK>
+__device__ __forceinline__ uint32_t wg_kth_key(const uint32_t (&key)[NK], int kk, int* s3) {
+  uint32_t t = 0u;
+#pragma unroll 1
+  for (int shift = 14; shift >= 0; shift -= 2) {
+    int c[3] = {0, 0, 0};
+#pragma unroll
+    for (int j = 0; j < NK; ++j)
+#pragma unroll
+      for (int q = 0; q < 3; ++q) c[q] += key[j] >= t + ((uint32_t)(q + 1) << shift) ? 1 : 0;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) c[q] = wave_sum_int(c[q]);
+    __syncthreads();
+    if (lane_id() == 0)
+#pragma unroll
+      for (int q = 0; q < 3; ++q) s3[3 * wave_id() + q] = c[q];
+    __syncthreads();
+    const int nw = blockDim.x >> 6;
+    uint32_t nt = t;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      int tot = 0;
+      for (int w = 0; w < nw; ++w) tot += s3[3 * w + q];
+      if (tot >= kk) nt = t + ((uint32_t)(q + 1) << shift);
+    }
+    t = nt;
+  }
+  return t;
+}
+
 // (key desc, id asc) argmax over a small workgroup (<= 16 waves) via LDS
 __device__ __forceinline__ void wg_argmax(uint32_t& k, int& idx, uint32_t* su, int* si) {
 #pragma unroll
@@ -526,12 +588,67 @@ __global__ __launch_bounds__(kSlThreads) void samp_stats_kernel(
   __shared__ uint32_t su[kSlThreads / 64];
   __shared__ int si[kSlThreads / 64];
   __shared__ float sf[kSlThreads / 64];
+  __shared__ int s3[3 * (kSlThreads / 64)];
+  __shared__ int s_n;
+  __shared__ uint32_t s_ck[kTopkMax];
+  __shared__ int s_ci[kTopkMax];
   const int row = blockIdx.y, p = blockIdx.x;
-  if (topk_row(top_k, row, vocab)) return;
   const T* x = logits + (long)row * stride;
   const uint32_t* mrow = allow_mask ? allow_mask + (long)row * mask_words : nullptr;
   const int S = slice_len(vocab);
   const int beg = p * S, end = min(vocab, beg + S);
+  if (mw_topk_row(top_k, temperature, row, vocab)) {
+    // this slice's top-k candidates: every id whose key is >= the slice's own k-th
+    // largest key (ties included); the global k-th largest key is never below it
+    static_assert(kSlThreads * 16 >= 4096, "two 8-id chunks per thread cover a slice");
+    uint32_t key[16];
+    {
+      uint32_t a[8], b[8];
+      const int b0 = beg + threadIdx.x * 8, b1 = b0 + kSlThreads * 8;
+      load_keys8<T>(x, mrow, b0 < end ? b0 : vocab, vocab, a);
+      load_keys8<T>(x, mrow, b1 < end ? b1 : vocab, vocab, b);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        key[j] = a[j];
+        key[8 + j] = b[j];
+      }
+    }
+    int nv = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) nv += key[j] > kNegInfKey ? 1 : 0;
+    nv = wave_sum_int(nv);
+    if (lane_id() == 0) s3[wave_id()] = nv;
+    if (threadIdx.x == 0) s_n = 0;
+    __syncthreads();
+    int valid = 0;
+    for (int w = 0; w < kSlThreads / 64; ++w) valid += s3[w];
+    const int kk = min(top_k[row], valid);
+    int* cnt = reinterpret_cast<int*>(ws + (long)row * kWsRow + kWsTkCnt);
+    if (kk == 0) {
+      if (threadIdx.x == 0) cnt[p] = 0;
+      return;
+    }
+    const uint32_t th = max(wg_kth_key<16>(key, kk, s3), kNegInfKey + 1u);
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      if (key[j] >= th) {
+        const int slot = atomicAdd(&s_n, 1);
+        if (slot < kTopkMax) {
+          s_ck[slot] = key[j];
+          s_ci[slot] = beg + threadIdx.x * 8 + (j & 7) + (j >> 3) * kSlThreads * 8;
+        }
+      }
+    __syncthreads();
+    const int n = s_n;
+    float* cand = ws + (long)row * kWsRow + kWsTk + 2 * kTopkMax * p;
+    if (threadIdx.x < min(n, kTopkMax)) {
+      cand[2 * threadIdx.x] = __uint_as_float(s_ck[threadIdx.x]);
+      cand[2 * threadIdx.x + 1] = __int_as_float(s_ci[threadIdx.x]);
+    }
+    if (threadIdx.x == 0) cnt[p] = n <= kTopkMax ? n : -1;   // -1: ties overflow, one-WG path
+    return;
+  }
+  if (topk_row(top_k, row, vocab)) return;
   // argmax: exact on fp32 input (32-bit ordered keys, masked ids excluded), bf16 keys
   // otherwise -- the same rule as sample_kernel's pass 1
   uint32_t best = 0u;
@@ -604,7 +721,8 @@ __global__ __launch_bounds__(kSampThreads) void samp_draw_kernel(
   float* wr = ws + (long)row * kWsRow;
   int* flag = reinterpret_cast<int*>(wr + kWsFlag);
   if (topk_row(top_k, row, vocab)) {
-    if (tid == 0) *flag = 2;
+    // multi-workgroup top-k rows: samp_topk_kernel sets the flag; others: one-WG path
+    if (tid == 0 && !mw_topk_row(top_k, temperature, row, vocab)) *flag = 2;
     return;
   }
   const float tp = top_p[row];
@@ -809,6 +927,131 @@ __global__ __launch_bounds__(kSlThreads) void samp_above_kernel(
   }
 }
 
+// Top-k rows (k <= kTopkMax, temperature > 0), one workgroup per row: merge the
+// slices' candidates, keep key >= t* (t* = largest key with count(key >= t*) >= k,
+// the single-workgroup kernel's rule: ties at the threshold stay), then top-p over
+// the kept ids (an id is in the nucleus iff the mass of strictly more likely kept
+// ids is < top_p * Z) and one inverse-CDF draw in (key desc, id asc) order --
+// deterministic whatever order the candidates were appended in.  Rows whose
+// candidates or kept set overflow go to the one-workgroup kernel (flag 2).
+__global__ __launch_bounds__(kSlThreads) void samp_topk_kernel(
+    int* __restrict__ out_tokens, int vocab, const float* __restrict__ temperature,
+    const float* __restrict__ top_p, const int* __restrict__ top_k,
+    const long long* __restrict__ seeds, const int* __restrict__ steps, float* __restrict__ ws) {
+  constexpr int NC = kSlices * kTopkMax / kSlThreads;   // candidates per thread
+  __shared__ int s_off[kSlices + 1];
+  __shared__ int s3[3 * (kSlThreads / 64)];
+  __shared__ float sf[kSlThreads / 64];
+  __shared__ int s_nk, s_bad, s_pick, s_last;
+  __shared__ uint32_t s_k[kTopkKept];
+  __shared__ int s_i[kTopkKept];
+  __shared__ float s_e[kTopkKept];
+  const int row = blockIdx.x, tid = threadIdx.x;
+  if (!mw_topk_row(top_k, temperature, row, vocab)) return;
+  float* wr = ws + (long)row * kWsRow;
+  int* flag = reinterpret_cast<int*>(wr + kWsFlag);
+  const int* cnt = reinterpret_cast<const int*>(wr + kWsTkCnt);
+  if (tid == 0) {
+    int o = 0, bad = 0;
+    for (int p = 0; p < kSlices; ++p) {
+      s_off[p] = o;
+      bad |= cnt[p] < 0;
+      o += max(cnt[p], 0);
+    }
+    s_off[kSlices] = o;
+    s_bad = bad;
+    s_nk = 0;
+    s_pick = -1;
+    s_last = -1;
+  }
+  __syncthreads();
+  if (s_bad) {
+    if (tid == 0) *flag = 2;
+    return;
+  }
+  const int C = s_off[kSlices];
+  uint32_t key[NC];
+  int id[NC];
+#pragma unroll
+  for (int j = 0; j < NC; ++j) {
+    const int c = tid + kSlThreads * j;
+    key[j] = 0u;
+    id[j] = 0;
+    if (c < C) {
+      int p = 0;
+      while (s_off[p + 1] <= c) ++p;
+      const float* e = wr + kWsTk + 2 * kTopkMax * p + 2 * (c - s_off[p]);
+      key[j] = __float_as_uint(e[0]);
+      id[j] = __float_as_int(e[1]);
+    }
+  }
+  const int kk = min(top_k[row], C);
+  if (kk == 0) {   // everything masked
+    if (tid == 0) {
+      out_tokens[row] = 0;
+      *flag = 0;
+    }
+    return;
+  }
+  const uint32_t th = wg_kth_key<NC>(key, kk, s3);
+#pragma unroll
+  for (int j = 0; j < NC; ++j)
+    if (key[j] >= th && key[j] > kNegInfKey) {
+      const int slot = atomicAdd(&s_nk, 1);
+      if (slot < kTopkKept) {
+        s_k[slot] = key[j];
+        s_i[slot] = id[j];
+      }
+    }
+  __syncthreads();
+  const int nk = s_nk;
+  if (nk > kTopkKept) {
+    if (tid == 0) *flag = 2;
+    return;
+  }
+  const float cexp = 1.4426950408889634f / temperature[row];
+  const uint32_t kmax = wave_max_u32_wg(tid < nk ? s_k[tid] : 0u, s3);
+  const float M = key_to_f32(kmax);
+  const float e = tid < nk ? exp2f((key_to_f32(s_k[tid]) - M) * cexp) : 0.f;
+  if (tid < nk) s_e[tid] = e;
+  const float Z = wg_sum(e, sf);   // (its barriers also publish s_e)
+  const float tp = top_p[row];
+  // strictly-more-likely mass and (key desc, id asc) rank of this thread's kept id
+  float above = 0.f;
+  int rank = 0;
+  const uint32_t mk = tid < nk ? s_k[tid] : 0u;
+  const int mi = tid < nk ? s_i[tid] : 0;
+  for (int j = 0; j < nk; ++j) {
+    const uint32_t kj = s_k[j];
+    if (kj > mk) above += s_e[j];
+    rank += (kj > mk || (kj == mk && s_i[j] < mi)) ? 1 : 0;
+  }
+  const bool member = tid < nk && (tp >= 1.f || above < tp * Z);
+  __syncthreads();
+  if (tid < nk) s_e[tid] = member ? e : 0.f;   // nucleus masses
+  const float Zn = wg_sum(member ? e : 0.f, sf);
+  // mass of the members ranked before this one
+  float cum = 0.f;
+  if (member)
+    for (int j = 0; j < nk; ++j) {
+      const uint32_t kj = s_k[j];
+      if (kj > mk || (kj == mk && s_i[j] < mi)) cum += s_e[j];
+    }
+  const uint64_t s0 =
+      splitmix64((uint64_t)seeds[row] ^ (0x632BE59BD9B4E019ull * (uint64_t)(steps[row] + 1)));
+  const uint64_t h = splitmix64(s0);
+  const float T = ((float)(h >> 40) + 0.5f) * (1.0f / 16777216.0f) * Zn;
+  if (member && T >= cum && T < cum + e) s_pick = mi;
+  if (member) atomicMax(&s_last, rank);   // rounding tail: the last-ranked member
+  __syncthreads();
+  if (s_pick < 0 && member && rank == s_last) s_pick = mi;
+  __syncthreads();
+  if (tid == 0) {
+    out_tokens[row] = s_pick;
+    *flag = 0;
+  }
+}
+
 }  // namespace ft
 
 extern "C" int ft_sample_ws_floats() { return ft::kWsRow; }
@@ -836,6 +1079,8 @@ extern "C" int ft_sample(int* out_tokens, const void* logits, int logits_is_bf16
       hipLaunchKernelGGL(ft::samp_above_kernel<TT>, dim3(ft::kSlices, batch), dim3(ft::kSlThreads),\
                          0, stream, lg, logit_stride, vocab, temperature, allow_mask, mask_words, \
                          ws);                                                                    \
+      hipLaunchKernelGGL(ft::samp_topk_kernel, dim3(batch), dim3(ft::kSlThreads), 0, stream,     \
+                         out_tokens, vocab, temperature, top_p, top_k, seeds, steps, ws);        \
       flags = reinterpret_cast<int*>(ws + ft::kWsFlag);                                          \
     }                                                                                            \
   }

@@ -330,13 +330,6 @@ class LlamaModel:
         self._unpack_need = 0
         self.tickets: Optional[torch.Tensor] = None
         self.resid_layer = False     # 33-64 row decode steps on the residual stream (_forward_resid)
-        # FT_ROPE_IN_ATTN=1: decode-only steps whose QKV GEMM leaves split-K slabs run
-        # RoPE + the paged K/V write inside the decode attention launch (no
-        # slab_rope_kv launch).  Opt-in: measured SLOWER at the driver config (7.84
-        # vs 7.64 ms of GPU per decode step, profiles/ab_rope_in_attn_r02.log) -- the
-        # per-segment slab gathers and 255 VGPRs cost the attention more than the
-        # 6 us launch it saves
-        self.rope_in_attn = os.environ.get("FT_ROPE_IN_ATTN", "0") == "1"
 
     # ------------------------------------------------------------------ weights
     def _set_layers(self, shards):
@@ -797,22 +790,14 @@ class LlamaModel:
                 ops.fused_add_rmsnorm(x, residual, L.ln1, eps)
             kc, vc = kv_caches[li]
             sq, qkv = self._lin(x, L, "qkv")
-            if sq and self.rope_in_attn and meta.num_decode == t and x.is_cuda:
-                # decode-only step: RoPE + the K/V write ride in the attention launch
-                attn = torch.empty(t, nq * d, dtype=self.dtype, device=self.device)
-                ops.decode_attention_rope(attn, self.ws, sq, t, meta.positions, self.cos_sin,
-                                          meta.slot_mapping, kc, vc, meta.dec_block_tables,
-                                          meta.dec_seq_lens, meta.tmp_out, meta.tmp_ml, nq, nkv, d,
-                                          self.scale, counters=meta.dec_counters)
-            elif sq:  # split-K slabs -> RoPE'd q and the paged K/V write in one kernel
+            if sq:  # split-K slabs -> RoPE'd q and the paged K/V write in one kernel
                 qkv = torch.empty(t, (nq + 2 * nkv) * d, dtype=self.dtype, device=self.device)
                 ops.slab_rope_kv(self.ws, sq, t, qkv.shape[1], qkv, meta.positions, self.cos_sin,
                                  meta.slot_mapping, kc, vc, nq, nkv, d)
             else:
                 ops.rope_kv_write(qkv, meta.positions, self.cos_sin, meta.slot_mapping, kc, vc,
                                   nq, nkv, d)
-            if not (sq and self.rope_in_attn and meta.num_decode == t and x.is_cuda):
-                attn = self._attention(qkv, meta, kc, vc)
+            attn = self._attention(qkv, meta, kc, vc)
             so, y = self._lin(attn, L, "o")
             if so:
                 x = torch.empty(t, H, dtype=self.dtype, device=self.device)

@@ -159,26 +159,6 @@ def decode_attention(out, q, k_cache, v_cache, block_tables, seq_lens, tmp_out, 
     return out
 
 
-def decode_attention_rope(out, ws, splits, batch, positions, cos_sin, slot_mapping, k_cache, v_cache,
-                          block_tables, seq_lens, tmp_out, tmp_ml, nq, nkv, head_dim, scale,
-                          counters: Optional[torch.Tensor] = None):
-    """decode_attention with RoPE and the new token's paged K/V write folded in:
-    q / k / v of the ``batch`` decode rows are the sums of the QKV GEMM's fp32
-    split-K slabs ws[splits][batch][(nq + 2 nkv) * D] (replaces slab_rope_kv +
-    decode_attention on the decode-graph path)."""
-    cols = (nq + 2 * nkv) * head_dim
-    if out.is_cuda:
-        native().paged_decode_attention_rope(out, ws, splits, batch, positions, cos_sin,
-                                             slot_mapping, k_cache, v_cache, block_tables,
-                                             seq_lens, tmp_out, tmp_ml, nq, nkv, head_dim, scale,
-                                             counters)
-        return out
-    qkv = ws[: splits * batch * cols].view(splits, batch, cols).sum(0).to(k_cache.dtype)
-    rope_kv_write(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, nq, nkv, head_dim)
-    return decode_attention(out, qkv, k_cache, v_cache, block_tables, seq_lens, tmp_out, tmp_ml,
-                            nq, nkv, head_dim, scale)
-
-
 def prefill_attention(out, q, k_cache, v_cache, block_tables, seq_lens, q_start_loc, tile_info,
                       num_tiles, nq, nkv, head_dim, scale, part_o=None, part_ml=None, combine=None,
                       num_combine: int = 0, num_partials: int = 0):
