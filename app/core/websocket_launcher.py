@@ -52,7 +52,31 @@ class WebSocketLauncher:
             logger.error(f"Backend for provider '{self.config.llm_provider}' is not reachable")
         return ok
 
+    def _dp_workers(self) -> int:
+        c = self.config
+        if c.llm_provider == "native" and int(getattr(c, "engine_dp_size", 1) or 1) > 1 and \
+                getattr(c, "engine_dp_mode", "workers") == "workers":
+            return int(c.engine_dp_size)
+        return 0
+
     def start(self):
+        n = self._dp_workers()
+        if n:
+            # N service processes on one port, one engine (GPU / TP group) each
+            from app.server.workers import WorkerPool
+
+            logger.info(f"Starting {n} DP service workers on {self.config.host}:{self.config.port}")
+            import os
+
+            self._pool = WorkerPool(n, self.config.host, self.config.port,
+                                    tp=int(getattr(self.config, "engine_tp_size", 1) or 1),
+                                    max_restarts=int(os.environ.get("ENGINE_MAX_RESTARTS", "3")))
+            self._pool.start()
+            try:
+                self._pool.run()
+            except (KeyboardInterrupt, SystemExit):
+                pass
+            return
         logger.info(f"Starting LLM WebSocket server (provider: {self.config.llm_provider})")
         self.server = self._create_server()
         if self.monitor is not None and hasattr(self.monitor, "attach_server"):
@@ -71,6 +95,9 @@ class WebSocketLauncher:
 
     def stop(self):
         logger.info("Stopping LLM WebSocket server")
+        pool = getattr(self, "_pool", None)
+        if pool is not None:
+            pool.stop()
         if self.server is not None and getattr(self.server, "ollama_handler", None) is not None:
             self.server.ollama_handler.close()
         if self.server is not None and getattr(self.server, "native_handler", None) is not None:

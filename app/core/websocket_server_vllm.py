@@ -58,6 +58,8 @@ class _Turn:
         self.finish_reason: Optional[str] = None
         self.prompt_tokens = 0
         self.cached_tokens = 0
+        self.frames = 0            # token frames not yet folded into the connection stats
+        self.tokens_recorded = 0
 
 
 class WebSocketLLMServer:
@@ -222,10 +224,21 @@ class WebSocketLLMServer:
         session_id = str(uuid.uuid4())
         await websocket.accept()
         send_lock = asyncio.Lock()
+        # the aiohttp transport hands out its socket (app/server/asgi_aiohttp.py): text
+        # frames go out directly instead of through starlette + the ASGI bridge, the
+        # per-token cost that bounds one process's stream rate (bench/dp_ceiling.py)
+        raw = (websocket.scope.get("extensions") or {}).get("fasttalk.aiohttp_ws")
 
-        async def send(obj: Dict[str, Any]):
+        async def send(obj: Any):
+            txt = obj if isinstance(obj, str) else json.dumps(obj)
             async with send_lock:
-                await websocket.send_text(json.dumps(obj))
+                ws = raw.get("ws") if raw is not None else None
+                if ws is None:
+                    await websocket.send_text(txt)
+                elif ws.closed:
+                    raise WebSocketDisconnect(1006)
+                else:
+                    await ws.send_str(txt)
 
         if self.connection_manager.add_connection(session_id, websocket) is None:
             await send({"type": "error", "error": {"code": "max_connections",
@@ -383,6 +396,7 @@ class WebSocketLLMServer:
             if turn.prompt_tokens:
                 stats["prompt_tokens"] = turn.prompt_tokens
                 stats["cached_prompt_tokens"] = turn.cached_tokens
+            self._flush_turn_stats(session_id, turn)
             await send({"type": "response_complete", "stats": stats})
             self.connection_manager.record_message_sent(session_id)
         except LLMServiceError as e:
@@ -399,6 +413,7 @@ class WebSocketLLMServer:
             await send({"type": "error", "error": {"code": info.category.value, "message": info.message,
                                                    "severity": info.severity.value}})
         finally:
+            self._flush_turn_stats(session_id, turn)
             self.connection_manager.update_connection_state(session_id, ConnectionState.ACTIVE)
 
     async def _emit(self, session_id: str, send, turn: _Turn, text: str, ntok: int, t_start: float):
@@ -412,9 +427,19 @@ class WebSocketLLMServer:
         turn.tokens += ntok
         if text:
             turn.text.append(text)
-            await send({"type": "token", "data": text})
-            self.connection_manager.record_message_sent(session_id)
-        self.connection_manager.record_tokens_generated(session_id, ntok)
+            # the frame {"type": "token", "data": ...} json.dumps would write
+            await send('{"type": "token", "data": ' + json.dumps(text) + "}")
+            turn.frames += 1
+        # connection counters are folded in once per turn (_flush_turn_stats)
+
+    def _flush_turn_stats(self, session_id: str, turn: _Turn):
+        if turn.frames:
+            self.connection_manager.record_message_sent(session_id, turn.frames)
+        n = turn.tokens - turn.tokens_recorded
+        if n:
+            self.connection_manager.record_tokens_generated(session_id, n)
+        turn.frames = 0
+        turn.tokens_recorded = turn.tokens
 
     async def _generate_with_native(self, session_id: str, send, turn: _Turn):
         messages = self.conversation_manager.get_messages_for_generation(session_id) or []

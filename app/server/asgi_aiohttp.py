@@ -51,10 +51,11 @@ def _base_scope(request: web.Request, kind: str) -> Dict[str, Any]:
 
 class AiohttpASGIServer:
     def __init__(self, app: ASGIApp, host: str = "0.0.0.0", port: int = 8000,
-                 max_msg_size: int = 16 << 20):
+                 max_msg_size: int = 16 << 20, reuse_port: bool = False):
         self.app = app
         self.host = host
         self.port = port
+        self.reuse_port = reuse_port   # several worker processes on one port (app/server/workers.py)
         self.max_msg_size = max_msg_size
         self._runner: Optional[web.AppRunner] = None
         self._lifespan_q: Optional[asyncio.Queue] = None
@@ -118,6 +119,10 @@ class AiohttpASGIServer:
         inbox: asyncio.Queue = asyncio.Queue()
         inbox.put_nowait({"type": "websocket.connect"})
         state: Dict[str, Any] = {"ws": None, "reader": None, "closed": False}
+        # the app may send text frames straight on the aiohttp socket once accepted
+        # (state["ws"]): the token stream skips the per-frame ASGI dict / starlette
+        # layers (app/core/websocket_server_vllm.py, send)
+        scope["extensions"] = {"fasttalk.aiohttp_ws": state}
 
         async def reader(ws: web.WebSocketResponse):
             code = 1000
@@ -228,7 +233,8 @@ class AiohttpASGIServer:
         web_app.router.add_route("*", "/{tail:.*}", self._dispatch)
         self._runner = web.AppRunner(web_app, access_log=None, handle_signals=False)
         await self._runner.setup()
-        site = web.TCPSite(self._runner, self.host, self.port, reuse_address=True)
+        site = web.TCPSite(self._runner, self.host, self.port, reuse_address=True,
+                           reuse_port=self.reuse_port or None)
         await site.start()
         if self.port == 0:
             for s in self._runner.sites:

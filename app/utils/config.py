@@ -117,6 +117,9 @@ class Config:
     engine_tp_size: int = field(default_factory=lambda: int(_e(
         "ENGINE_TP_SIZE", _e("VLLM_TENSOR_PARALLEL_SIZE", "1"))))
     engine_dp_size: int = field(default_factory=lambda: int(_e("ENGINE_DP_SIZE", "1")))
+    # DP>1: "workers" = N service processes on one port (SO_REUSEPORT, app/server/workers.py);
+    # "router" = one service process in front of N engine replica processes
+    engine_dp_mode: str = field(default_factory=lambda: _e("ENGINE_DP_MODE", "workers").lower())
     engine_max_num_seqs: int = field(default_factory=lambda: int(_e(
         "ENGINE_MAX_NUM_SEQS", _e("VLLM_MAX_NUM_SEQS", "256"))))
     engine_max_model_len: int = field(default_factory=lambda: int(_e(

@@ -120,7 +120,8 @@ class LoadClient:
     async def open(self):
         import aiohttp
 
-        self.http = aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=None))
+        self.http = aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=None),
+                                          connector=aiohttp.TCPConnector(limit=0))  # WS: no pool cap
         self.sessions = [Session(i, self.url, self.cfg, self.words, self.seed, self.tool_frac)
                          for i in range(self.n)]
         await asyncio.gather(*[s.open(self.http) for s in self.sessions])

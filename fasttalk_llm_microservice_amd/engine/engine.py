@@ -26,7 +26,7 @@ from .chat_template import ChatTemplate
 from .config import EngineConfig
 from .sampling_params import SamplingParams
 from .scheduler import ScheduledBatch, Scheduler
-from .sequence import RequestOutput, SeqStatus, Sequence
+from .sequence import coalesce, RequestOutput, SeqStatus, Sequence
 from .tokenizer import get_tokenizer
 
 log = logging.getLogger("fasttalk.engine")
@@ -47,9 +47,14 @@ class LLMEngine:
         self.tokenizer = get_tokenizer(tok_path)
         self.template = ChatTemplate(self.tokenizer)
         if runner is None:
-            from .runner import ModelRunner
+            from .synthetic import make_synthetic_runner, synthetic_step_ms
 
-            runner = ModelRunner(cfg, self.model_cfg, comm)
+            if synthetic_step_ms() > 0:   # service load tests (ENGINE_SYNTHETIC_STEP_MS)
+                runner = make_synthetic_runner(cfg, self.model_cfg)
+            else:
+                from .runner import ModelRunner
+
+                runner = ModelRunner(cfg, self.model_cfg, comm)
         self.runner = runner
         self.max_model_len = runner.max_model_len
         R = rt()
@@ -694,7 +699,7 @@ class AsyncEngine:
         finished = False
         try:
             while True:
-                o = await q.get()
+                o = coalesce(await q.get(), q)
                 if o.finished:
                     finished = True
                 yield o

@@ -100,3 +100,26 @@ class Sequence:
     @property
     def is_finished(self) -> bool:
         return self.status == SeqStatus.FINISHED
+
+
+def coalesce(first: RequestOutput, q) -> RequestOutput:
+    """``first`` merged with the outputs already waiting in asyncio queue ``q``
+    (text deltas concatenated, token ids appended, the last one's finish state).
+    A consumer that fell behind the engine (e.g. one service process streaming
+    many replicas' tokens) then sends one WS frame per wake-up instead of one per
+    token, so it catches up instead of queueing without bound."""
+    if q.empty() or first.finished:
+        return first
+    text = [first.text]
+    ids = list(first.token_ids)
+    o = first
+    while not q.empty() and not o.finished:
+        o = q.get_nowait()
+        text.append(o.text)
+        ids.extend(o.token_ids)
+    return RequestOutput(first.request_id, "".join(text), ids, finished=o.finished,
+                         finish_reason=o.finish_reason,
+                         num_prompt_tokens=first.num_prompt_tokens or o.num_prompt_tokens,
+                         num_cached_tokens=first.num_cached_tokens or o.num_cached_tokens,
+                         num_output_tokens=o.num_output_tokens,
+                         ttft_s=first.ttft_s if first.ttft_s is not None else o.ttft_s, error=o.error)

@@ -36,7 +36,7 @@ from typing import Any, AsyncIterator, Dict, List, Optional, Sequence as Seq
 
 from ..engine.chat_template import ChatTemplate
 from ..engine.engine import EngineError
-from ..engine.sequence import RequestOutput
+from ..engine.sequence import RequestOutput, coalesce
 from ..engine.tokenizer import get_tokenizer
 from ..models.config import resolve_model
 
@@ -90,7 +90,7 @@ def _replica_main(index: int, cfg, conn, device_base: int = 0):
             from ..engine.engine import LLMEngine
 
             eng = LLMEngine(cfg)
-        if cfg.resolved_device() == "cuda" and not cfg.enforce_eager:
+        if cfg.resolved_device() == "cuda" and not cfg.enforce_eager and hasattr(eng.runner, "warmup"):
             eng.runner.warmup()
     except BaseException as e:  # pragma: no cover - reported to the router
         conn.send(("dead", repr(e)))
@@ -225,6 +225,8 @@ class MultiGPUEngine:
 
     def __init__(self, cfg, device_base: Optional[int] = None):
         self.cfg = cfg
+        if device_base is None and os.environ.get("ENGINE_DEVICE_BASE"):
+            device_base = int(os.environ["ENGINE_DEVICE_BASE"])   # a DP service worker's GPUs
         if device_base is None:
             device_base = int(os.environ.get("LOCAL_RANK", "0")) * max(1, cfg.dp_size) * \
                 max(1, cfg.tp_size) if cfg.resolved_device() == "cuda" else 0
@@ -403,7 +405,7 @@ class MultiGPUEngine:
         try:
             rep.send(("add", rid, list(prompt_ids), params))
             while True:
-                o = await q.get()
+                o = coalesce(await q.get(), q)
                 finished = o.finished
                 yield o
                 if finished:
