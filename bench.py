@@ -143,7 +143,8 @@ def main():
     ap.add_argument("--tp", type=int, default=1,
                     help="tensor parallel: the N ranks form ONE engine (e.g. --model llama3-70b --tp 8); "
                          "default: data parallel, one engine per rank")
-    ap.add_argument("--custom-allreduce", action="store_true", help="TP: one-shot xGMI all-reduce")
+    ap.add_argument("--no-custom-allreduce", dest="custom_allreduce", action="store_false",
+                    help="TP: RCCL only (default: the xGMI custom collectives for decode sizes)")
     ap.add_argument("--device", default="cuda", help="cpu runs the same path over gloo (tests)")
     ap.add_argument("--quant", default="", choices=["", "w4", "awq"],
                     help="W4A16 layer weights (the reference's AWQ-INT4 model); default bf16")

@@ -54,6 +54,10 @@ int ft_ar_ipc_handle(void* ptr, char* out64);
 int ft_ar_ipc_open(const char* in64, void** ptr);
 int ft_ar_ipc_close(void* ptr);
 int ft_ar_read_error(void* mine, int* err);
+int ft_ar_add_rmsnorm(void* out, int out_stride, void* residual, const void* weight, float eps,
+                      const float* ws, int splits, const void* x, int x_stride, long rows, long hidden,
+                      const uint64_t* peers_dev, int rank, int world, size_t max_bytes,
+                      unsigned spin_budget, hipStream_t stream);
 int ft_ar_allreduce(void* out, const void* x, long n, const uint64_t* peers_dev, int rank, int world,
                     size_t max_bytes, unsigned spin_budget, int two_shot, hipStream_t stream);
 int ft_ar_allgather(void* out, const void* x, long rows, long row_elems, const uint64_t* peers_dev,
@@ -62,8 +66,7 @@ int ft_ar_export_error(int* dst, const uint64_t* peers_dev, int world, hipStream
 int ft_skinny_gemm_pk(const void* x, int x_stride, int M, const void* wpk, int N, int K, float* ws,
                       void* out, int out_stride, int splits, int nt, hipStream_t stream);
 int ft_skinny_gemm_xr(const void* x, int x_stride, int M, const void* w, int N, int K, float* ws,
-                      void* out, int out_stride, int splits, int nt, int epi, int norm,
-                      void* residual, int res_stride, int* tickets, float eps, hipStream_t stream);
+                      void* out, int out_stride, int splits, int nt, int epi, hipStream_t stream);
 int ft_packed_gemm(const void* x, int x_stride, int M, const void* wpk, int N, int K, int splits,
                    int epi, int cfg, void* out, int out_stride, float* ws, hipStream_t stream);
 int ft_unpack_weight(void* out, const void* wpk, int N, int K, hipStream_t stream);
@@ -438,8 +441,7 @@ void skinny_gemm(at::Tensor x, at::Tensor w, c10::optional<at::Tensor> out,
   }
   if (u <= -5)
     check_rc(ft_skinny_gemm_xr(x.data_ptr(), (int)x.stride(0), M, w.data_ptr(), N, K, wsp, op,
-                               ostride, (int)splits, (int)nt, silu ? 1 : 0, 0, nullptr, 0, nullptr,
-                               0.f, cur_stream()),
+                               ostride, (int)splits, (int)nt, silu ? 1 : 0, cur_stream()),
              "skinny_gemm_xr");
   else if (u == -3)  // w is the packed [N/16][K/64][2][64][8] image (ops.pack_weight)
     check_rc(ft_skinny_gemm_pk(x.data_ptr(), (int)x.stride(0), M, w.data_ptr(), N, K, wsp, op,
@@ -451,13 +453,10 @@ void skinny_gemm(at::Tensor x, at::Tensor w, c10::optional<at::Tensor> out,
              "skinny_gemm_xc");
 }
 
-// "xr" decode GEMM with the fused epilogues (csrc/kernels/skinny_gemm.hip):
-// epi 1 SiLU (norm: x is the raw residual, rows RMS-scaled), epi 2 residual +=
-// x w^T with split-K reduced in the launch (ws + zeroed tickets).
+// "xr" decode GEMM (csrc/kernels/skinny_gemm.hip): epi 0 bf16 out / fp32 slabs,
+// epi 1 SiLU of the interleaved gate/up image.
 void skinny_gemm_xr(at::Tensor x, at::Tensor w, c10::optional<at::Tensor> out,
-                    c10::optional<at::Tensor> ws, int64_t splits, int64_t nt, int64_t epi,
-                    bool norm, c10::optional<at::Tensor> residual,
-                    c10::optional<at::Tensor> tickets, double eps) {
+                    c10::optional<at::Tensor> ws, int64_t splits, int64_t nt, int64_t epi) {
   check_bf16(x, "x");
   check_bf16(w, "w");
   check_rows(x, "x");
@@ -477,29 +476,11 @@ void skinny_gemm_xr(at::Tensor x, at::Tensor w, c10::optional<at::Tensor> out,
   float* wsp = nullptr;
   if (splits > 1) {
     TORCH_CHECK(ws.has_value(), "xr: splits > 1 needs a workspace");
-    check_ws(*ws, (int64_t)splits * N * 16 * ((M + 15) / 16));
     check_ws(*ws, (int64_t)splits * M * N);
     wsp = ws->data_ptr<float>();
   }
-  void* rp = nullptr;
-  int rstride = 0;
-  if (epi == 2) {
-    TORCH_CHECK(residual.has_value(), "xr resid: residual required");
-    check_bf16(*residual, "residual");
-    TORCH_CHECK(residual->dim() == 2 && residual->stride(1) == 1 && residual->size(0) >= M &&
-                    residual->size(1) >= N, "xr resid: residual shape");
-    rp = residual->data_ptr();
-    rstride = (int)residual->stride(0);
-  }
-  int* tp = nullptr;
-  if (epi == 2 && splits > 1) {
-    TORCH_CHECK(tickets.has_value() && tickets->scalar_type() == at::kInt && tickets->is_cuda() &&
-                    tickets->numel() >= N / (16 * nt), "xr resid: int32 tickets >= N / (16 nt)");
-    tp = tickets->data_ptr<int>();
-  }
   check_rc(ft_skinny_gemm_xr(x.data_ptr(), (int)x.stride(0), M, w.data_ptr(), N, K, wsp, op, ostride,
-                             (int)splits, (int)nt, (int)epi, norm ? 1 : 0, rp, rstride, tp, (float)eps,
-                             cur_stream()),
+                             (int)splits, (int)nt, (int)epi, cur_stream()),
            "skinny_gemm_xr");
 }
 
@@ -635,6 +616,39 @@ void custom_ar_allreduce(at::Tensor out, at::Tensor x, at::Tensor peers, int64_t
                            (int)world, (size_t)max_bytes, (unsigned)spin_budget, two_shot ? 1 : 0,
                            cur_stream()),
            "custom_ar_allreduce");
+}
+// residual += all-reduce(partial); out = rmsnorm(residual) * weight.  partial: fp32
+// split-K slabs ws[splits][rows][hidden] (ws given) or bf16 x [rows, hidden].
+void custom_ar_add_rmsnorm(at::Tensor out, at::Tensor residual, at::Tensor weight, double eps,
+                           c10::optional<at::Tensor> ws, int64_t splits, c10::optional<at::Tensor> x,
+                           int64_t rows, at::Tensor peers, int64_t rank, int64_t world,
+                           int64_t max_bytes, int64_t spin_budget) {
+  check_bf16(out, "out");
+  check_bf16(residual, "residual");
+  check_bf16(weight, "weight");
+  const int64_t hidden = residual.size(1);
+  TORCH_CHECK(residual.is_contiguous() && residual.size(0) >= rows, "residual");
+  TORCH_CHECK(out.size(0) >= rows && out.size(1) == hidden && out.stride(1) == 1, "out");
+  TORCH_CHECK(weight.numel() == hidden, "weight");
+  TORCH_CHECK(peers.scalar_type() == at::kLong && peers.is_cuda() && peers.numel() == world, "peers");
+  const float* wsp = nullptr;
+  const void* xp = nullptr;
+  int x_stride = 0;
+  if (ws.has_value()) {
+    TORCH_CHECK(ws->scalar_type() == at::kFloat && ws->numel() >= splits * rows * hidden, "ws");
+    wsp = ws->data_ptr<float>();
+  } else {
+    TORCH_CHECK(x.has_value(), "ws or x");
+    check_bf16(*x, "x");
+    TORCH_CHECK(x->size(1) == hidden && x->stride(1) == 1 && x->size(0) >= rows, "x");
+    xp = x->data_ptr();
+    x_stride = (int)x->stride(0);
+  }
+  check_rc(ft_ar_add_rmsnorm(out.data_ptr(), (int)out.stride(0), residual.data_ptr(), weight.data_ptr(),
+                             (float)eps, wsp, (int)splits, xp, x_stride, (long)rows, (long)hidden,
+                             reinterpret_cast<const uint64_t*>(peers.data_ptr<int64_t>()), (int)rank,
+                             (int)world, (size_t)max_bytes, (unsigned)spin_budget, cur_stream()),
+           "custom_ar_add_rmsnorm");
 }
 // x: [rows, shard] bf16 -> out: [rows, world * shard]
 void custom_ar_allgather(at::Tensor out, at::Tensor x, at::Tensor peers, int64_t rank, int64_t world,
@@ -781,9 +795,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("nt") = 1);
   m.def("w4_dequant", &w4_dequant);
   m.def("skinny_gemm_xr", &skinny_gemm_xr, py::arg("x"), py::arg("w"), py::arg("out") = py::none(),
-        py::arg("ws") = py::none(), py::arg("splits") = 1, py::arg("nt") = 2, py::arg("epi") = 0,
-        py::arg("norm") = false, py::arg("residual") = py::none(), py::arg("tickets") = py::none(),
-        py::arg("eps") = 1e-5);
+        py::arg("ws") = py::none(), py::arg("splits") = 1, py::arg("nt") = 2, py::arg("epi") = 0);
   m.def("skinny_gemm", &skinny_gemm, py::arg("x"), py::arg("w"), py::arg("out") = py::none(),
         py::arg("ws") = py::none(), py::arg("splits") = 1, py::arg("nt") = 1, py::arg("u") = -3);
   m.def("pkr_gemm", &pkr_gemm, py::arg("x"), py::arg("w"), py::arg("out") = py::none(),
@@ -803,6 +815,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("custom_ar_close", &custom_ar_close);
   m.def("custom_ar_error", &custom_ar_error);
   m.def("custom_ar_allreduce", &custom_ar_allreduce);
+  m.def("custom_ar_add_rmsnorm", &custom_ar_add_rmsnorm);
   m.def("packed_gemm", &packed_gemm);
   m.def("unpack_weight", &unpack_weight);
   m.def("custom_ar_allgather", &custom_ar_allgather);

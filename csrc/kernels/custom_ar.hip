@@ -225,6 +225,107 @@ __global__ __launch_bounds__(256) void ar_allgather_kernel(uint16_t* __restrict_
   }
 }
 
+// X1/X2 fused with the residual add + RMSNorm that follows every row-parallel
+// projection (o, down) -- one launch instead of slab_store -> all-reduce ->
+// add+RMSNorm:
+//   publish  this rank's partial rows as bf16: its split-K fp32 slabs summed
+//            (ws != null, the projection's own epilogue format) or a bf16 block x;
+//   barrier  (one, as the one-shot all-reduce);
+//   rows     strided over the blocks: the W partials summed in rank order (fp32,
+//            identical on every rank) + residual -> residual (bf16) and
+//            out = rmsnorm(residual) * w, both rounded like row_add_rmsnorm_kernel.
+// A timed-out barrier leaves residual / out untouched and the error word set
+// (the step is discarded by the runner, as for every custom collective).
+template <int W, int VPT>
+__global__ __launch_bounds__(256) void ar_add_rmsnorm_kernel(
+    uint16_t* __restrict__ out, int out_stride, uint16_t* __restrict__ residual,
+    const uint16_t* __restrict__ weight, float eps, const float* __restrict__ ws, int splits,
+    const uint16_t* __restrict__ x, int x_stride, int rows, int hidden,
+    const uint64_t* __restrict__ peers, int rank, size_t max_bytes, uint32_t spin_budget) {
+  uint8_t* mine = reinterpret_cast<uint8_t*>(peers[rank]);
+  __shared__ uint32_t s_epoch;
+  __shared__ int s_ok;
+  __shared__ float red[4];
+  const uint32_t epoch = ar_begin(mine, &s_epoch);
+  if (epoch == 0) return;
+  const size_t slot = ArLayout::kStaging + (epoch & 1) * max_bytes;
+  const int h8 = hidden / 8;
+  const int n8 = rows * h8;
+  uint4* stage = reinterpret_cast<uint4*>(mine + slot);
+  const size_t slab = (size_t)rows * hidden;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += gridDim.x * blockDim.x) {
+    const int row = i / h8, c = (i - row * h8) * 8;
+    float v[8];
+    if (ws != nullptr) {
+      const float* p = ws + (size_t)row * hidden + c;
+      float4 a = reinterpret_cast<const float4*>(p)[0], b = reinterpret_cast<const float4*>(p)[1];
+      for (int sp = 1; sp < splits; ++sp) {
+        const float4 a2 = reinterpret_cast<const float4*>(p + sp * slab)[0];
+        const float4 b2 = reinterpret_cast<const float4*>(p + sp * slab)[1];
+        a.x += a2.x; a.y += a2.y; a.z += a2.z; a.w += a2.w;
+        b.x += b2.x; b.y += b2.y; b.z += b2.z; b.w += b2.w;
+      }
+      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+    } else {
+      load8(*reinterpret_cast<const uint4*>(x + (size_t)row * x_stride + c), v);
+    }
+    stage[i] = store8(v);
+  }
+  if (!ar_barrier<W>(mine, peers, rank, epoch, 0, spin_budget, &s_ok)) return;
+  const uint4* in[W];
+#pragma unroll
+  for (int r = 0; r < W; ++r)
+    in[r] = reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(peers[r]) + slot);
+  for (int row = blockIdx.x; row < rows; row += gridDim.x) {
+    float v[VPT][8];
+    uint4 wv[VPT];
+#pragma unroll
+    for (int c = 0; c < VPT; ++c) {
+      const int e = row * h8 + c * 256 + threadIdx.x;
+      uint4 raw[W];
+#pragma unroll
+      for (int r = 0; r < W; ++r) raw[r] = in[r][e];   // W peer loads in flight
+      load8(raw[0], v[c]);
+#pragma unroll
+      for (int r = 1; r < W; ++r) {
+        float t[8];
+        load8(raw[r], t);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[c][j] += t[j];
+      }
+      wv[c] = *reinterpret_cast<const uint4*>(weight + (c * 256 + threadIdx.x) * 8);
+    }
+    uint4* rr = reinterpret_cast<uint4*>(residual + (size_t)row * hidden);
+    float ss = 0.f;
+#pragma unroll
+    for (int c = 0; c < VPT; ++c) {
+      float rv[8];
+      load8(rr[c * 256 + threadIdx.x], rv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[c][j] += rv[j];
+      const uint4 rb = store8(v[c]);
+      rr[c * 256 + threadIdx.x] = rb;
+      load8(rb, v[c]);   // continue from the bf16-rounded residual
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ss += v[c][j] * v[c][j];
+    }
+    ss = wave_sum(ss);
+    __syncthreads();
+    if (lane_id() == 0) red[wave_id()] = ss;
+    __syncthreads();
+    const float inv = rsqrtf((red[0] + red[1] + red[2] + red[3]) / (float)hidden + eps);
+    uint4* orow = reinterpret_cast<uint4*>(out + (size_t)row * out_stride);
+#pragma unroll
+    for (int c = 0; c < VPT; ++c) {
+      float wf[8];
+      load8(wv[c], wf);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[c][j] = bf16_to_f32(f32_to_bf16(v[c][j] * inv)) * wf[j];
+      orow[c * 256 + threadIdx.x] = store8(v[c]);
+    }
+  }
+}
+
 // dst[0] = OR of the W ranks' error words (one lane; captured in the decode graph).
 __global__ void ar_export_error_kernel(int* __restrict__ dst, const uint64_t* __restrict__ peers,
                                        int world) {
@@ -331,6 +432,37 @@ extern "C" int ft_ar_allgather(void* out, const void* x, long rows, long row_ele
   }
 #undef FT_AG_CASE
   return static_cast<int>(hipGetLastError());
+}
+
+// residual [rows, hidden] += sum over ranks of this rank's partial (fp32 split-K slabs
+// ws[splits][rows][hidden], or bf16 x [rows, x_stride]); out = rmsnorm(residual) * w.
+// hidden % 2048 == 0 (<= 8192), rows * hidden * 2 <= max_bytes.
+extern "C" int ft_ar_add_rmsnorm(void* out, int out_stride, void* residual, const void* weight,
+                                 float eps, const float* ws, int splits, const void* x,
+                                 int x_stride, long rows, long hidden, const uint64_t* peers_dev,
+                                 int rank, int world, size_t max_bytes, unsigned spin_budget,
+                                 hipStream_t stream) {
+  if (rows <= 0) return 0;
+  if (hidden % 2048 != 0 || hidden > 8192) return -3;
+  if ((size_t)(rows * hidden) * 2 > max_bytes) return -1;
+  if ((ws == nullptr) == (x == nullptr) || (ws != nullptr && splits < 1)) return -4;
+  const int blocks = (int)std::min<long>(rows, 128);
+  const int vpt = (int)(hidden / 2048);
+#define FT_ARN(WW, VV)                                                                         \
+  if (world == WW && vpt == VV) {                                                              \
+    hipLaunchKernelGGL((ft::ar_add_rmsnorm_kernel<WW, VV>), dim3(blocks), dim3(256), 0, stream,\
+                       (uint16_t*)out, out_stride, (uint16_t*)residual, (const uint16_t*)weight,\
+                       eps, ws, splits, (const uint16_t*)x, x_stride, (int)rows, (int)hidden,   \
+                       peers_dev, rank, max_bytes, spin_budget);                               \
+    return static_cast<int>(hipGetLastError());                                                \
+  }
+#define FT_ARN_W(WW) FT_ARN(WW, 1) FT_ARN(WW, 2) FT_ARN(WW, 3) FT_ARN(WW, 4)
+  FT_ARN_W(2)
+  FT_ARN_W(4)
+  FT_ARN_W(8)
+#undef FT_ARN_W
+#undef FT_ARN
+  return -2;
 }
 
 extern "C" int ft_ar_export_error(int* dst, const uint64_t* peers_dev, int world,

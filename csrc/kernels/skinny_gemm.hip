@@ -195,20 +195,13 @@ __global__ __launch_bounds__(256) void skinny_xc_kernel(
 // a wave holds a gate tile and its up tile and writes h = silu(g) * u (bf16,
 // N/2 columns) itself -- no slabs, no slab_silu launch.
 // Epilogues: EPI 0 bf16 out (one split) / fp32 slabs ws[s][m][n]; EPI 1 SiLU
-// (above); EPI 2 residual[m][n] += y in place, split-K reduced inside the launch:
-// every split wave stores its tile write-through (8-B sc1 stores, column-major
-// [s][n][rows] so a lane's 4 rows are contiguous), drains, takes a ticket; the
-// last arriver of the tile loads the splits' tiles (sc1, all in flight at once),
-// sums them in split order (deterministic) and updates the residual -- the
-// guide's sc1 hand-off, no fences -- replacing the separate add+RMSNorm launch.
-// NORM (EPI 1, one split): x is the raw residual stream; every thread sums the
-// squares of the x elements it stages, so the workgroup knows each row's RMS by
-// the last chunk and the epilogue scales by it (the norm weight is folded into W).
-template <int MT, int NT, int KC, int EPI, bool NORM>
+// (above).  (An in-launch split-K residual epilogue and an RMS-scaled SiLU variant
+// were measured slower than the separate add+RMSNorm launches they replaced --
+// profiles/ab_resid_layer_r02.log -- and removed.)
+template <int MT, int NT, int KC, int EPI>
 __global__ __launch_bounds__(256, 1) void skinny_xr_kernel(
     const uint16_t* __restrict__ x, int x_stride, int M, const uint16_t* __restrict__ w, int K,
-    float* __restrict__ ws, uint16_t* __restrict__ out, int out_stride, int N, int k_slice,
-    uint16_t* __restrict__ residual, int res_stride, int* __restrict__ tickets, float eps) {
+    float* __restrict__ ws, uint16_t* __restrict__ out, int out_stride, int N, int k_slice) {
   constexpr bool SILU = EPI == 1;
   constexpr int KS = KC / 64;
   constexpr int ROWS = 16 * MT;
@@ -216,12 +209,7 @@ __global__ __launch_bounds__(256, 1) void skinny_xr_kernel(
   constexpr int XL = ROWS * CPR / 256;
   static_assert(XL >= 1 && (ROWS * CPR) % 256 == 0, "x chunk must tile the workgroup");
   static_assert(!SILU || NT == 2, "the SiLU epilogue pairs a gate tile with its up tile");
-  static_assert(!NORM || (SILU && CPR == 64), "NORM: SiLU epilogue, 512-wide chunks (a wave per x row)");
   __shared__ __attribute__((aligned(16))) uint16_t s_x[2][ROWS * KC];
-  __shared__ float s_rms[NORM ? ROWS : 1];
-  float ssq[NORM ? XL : 1];
-#pragma unroll
-  for (int p = 0; p < (NORM ? XL : 1); ++p) ssq[p] = 0.f;
   const int tid = threadIdx.x;
   const int lane = lane_id(), wave = wave_id();
   const int l15 = lane & 15, g = lane >> 4;
@@ -277,14 +265,6 @@ __global__ __launch_bounds__(256, 1) void skinny_xr_kernel(
       const int row = e / CPR, ch = e % CPR;
       const int slot = (ch & ~7) | ((ch & 7) ^ (row & 7));
       *reinterpret_cast<sk_u32x4*>(&sx[row * KC + slot * 8]) = xr[p];
-      if constexpr (NORM) {
-#pragma unroll
-        for (int e2 = 0; e2 < 4; ++e2) {
-          float lo, hi;
-          unpack2(xr[p][e2], lo, hi);
-          ssq[p] = fmaf(lo, lo, fmaf(hi, hi, ssq[p]));
-        }
-      }
     }
     if constexpr (MORE) {
 #pragma unroll
@@ -325,15 +305,6 @@ __global__ __launch_bounds__(256, 1) void skinny_xr_kernel(
   };
   for (int c = 0; c + 1 < nch; ++c) chunk(c, std::true_type{});
   chunk(nch - 1, std::false_type{});
-  if constexpr (NORM) {
-    // rows wave + 4p of the workgroup: each row's 64 chunks sit in one wave
-#pragma unroll
-    for (int p = 0; p < XL; ++p) {
-      const float t = wave_sum(ssq[p]);
-      if (lane == 0) s_rms[(tid + 256 * p) / CPR] = rsqrtf(t / (float)K + eps);
-    }
-    __syncthreads();
-  }
   if (!active) return;
   if constexpr (SILU) {
     const int col = (n0 >> 1) + l15;   // 16-column gate group n0/32 -> h columns
@@ -343,96 +314,8 @@ __global__ __launch_bounds__(256, 1) void skinny_xr_kernel(
       for (int r = 0; r < 4; ++r) {
         const int m = 16 * i + g * 4 + r;
         if (m < M) {
-          float gt = acc[i][0][r], up = acc[i][1][r];
-          if constexpr (NORM) {
-            const float rs = s_rms[m];
-            gt *= rs;
-            up *= rs;
-          }
+          const float gt = acc[i][0][r], up = acc[i][1][r];
           out[(size_t)m * out_stride + col] = f32_to_bf16(gt / (1.f + __expf(-gt)) * up);
-        }
-      }
-    return;
-  }
-  if constexpr (EPI == 2) {
-    // this lane's residual elements, read before the hand-off so the latency overlaps it
-    float res_pre[MT][NT][4];
-#pragma unroll
-    for (int i = 0; i < MT; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = min(16 * i + 4 * g + r, M - 1);
-#pragma unroll
-        for (int j = 0; j < NT; ++j)
-          res_pre[i][j][r] = bf16_to_f32(residual[(size_t)m * res_stride + n0 + 16 * j + l15]);
-      }
-    if (gridDim.y > 1) {
-      const int S = (int)gridDim.y;
-      auto slot = [&](int sp, int i, int j) {
-        return reinterpret_cast<uint64_t*>(ws + ((size_t)sp * N + n0 + 16 * j + l15) * ROWS + 16 * i + 4 * g);
-      };
-#pragma unroll
-      for (int i = 0; i < MT; ++i)
-#pragma unroll
-        for (int j = 0; j < NT; ++j) {
-          uint64_t* d = slot(s, i, j);
-          __hip_atomic_store(d, (uint64_t)__float_as_uint(acc[i][j][0]) |
-                                    ((uint64_t)__float_as_uint(acc[i][j][1]) << 32),
-                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_store(d + 1, (uint64_t)__float_as_uint(acc[i][j][2]) |
-                                        ((uint64_t)__float_as_uint(acc[i][j][3]) << 32),
-                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every store of this wave retired
-      const int tile = blockIdx.x * 4 + wave;
-      int prev = 0;
-      if (lane == 0)
-        prev = __hip_atomic_fetch_add(tickets + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      prev = __shfl(prev, 0, 64);
-      if (prev != S - 1) return;
-      // last arriver: every split's tile (own included) in split order
-#pragma unroll
-      for (int i = 0; i < MT; ++i)
-#pragma unroll
-        for (int j = 0; j < NT; ++j) acc[i][j] = sk_floatx4{0.f, 0.f, 0.f, 0.f};
-      for (int s0 = 0; s0 < S; s0 += 4) {
-        uint64_t v[4][MT][NT][2];
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-#pragma unroll
-          for (int i = 0; i < MT; ++i)
-#pragma unroll
-            for (int j = 0; j < NT; ++j) {
-              const uint64_t* src = slot(min(s0 + q, S - 1), i, j);
-              v[q][i][j][0] = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              v[q][i][j][1] = __hip_atomic_load(src + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          if (s0 + q < S) {
-#pragma unroll
-            for (int i = 0; i < MT; ++i)
-#pragma unroll
-              for (int j = 0; j < NT; ++j) {
-                acc[i][j][0] += __uint_as_float((uint32_t)v[q][i][j][0]);
-                acc[i][j][1] += __uint_as_float((uint32_t)(v[q][i][j][0] >> 32));
-                acc[i][j][2] += __uint_as_float((uint32_t)v[q][i][j][1]);
-                acc[i][j][3] += __uint_as_float((uint32_t)(v[q][i][j][1] >> 32));
-              }
-          }
-      }
-      if (lane == 0)   // re-arm for the next launch
-        __hip_atomic_store(tickets + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-#pragma unroll
-    for (int i = 0; i < MT; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = 16 * i + 4 * g + r;
-        if (m < M) {
-#pragma unroll
-          for (int j = 0; j < NT; ++j)
-            residual[(size_t)m * res_stride + n0 + 16 * j + l15] = f32_to_bf16(res_pre[i][j][r] + acc[i][j][r]);
         }
       }
     return;
@@ -596,13 +479,9 @@ extern "C" int ft_skinny_gemm_xc(const void* x, int x_stride, int M, const void*
 // Ring-pipelined x-chunk variant.  Requirements (checked): M <= 64,
 // N % (16*nt) == 0, K % (kc*splits) == 0 with kc = 512 (nt 2) / 256 (nt 1; two
 // 64-column workgroups per CU).  epi 0: out (one split) or ws [splits, M, N];
-// epi 1 (SiLU): nt 2, one split, out = [M, N/2]; norm: x is the raw residual and
-// rows are RMS-scaled (eps); epi 2 (resid): residual [M, N] += y, splits > 1 needs
-// ws (splits * N * 16 * ceil(M/16) floats) and N / (16 nt) zeroed tickets (left
-// zeroed on return).
+// epi 1 (SiLU): nt 2, one split, out = [M, N/2].
 extern "C" int ft_skinny_gemm_xr(const void* x, int x_stride, int M, const void* w, int N, int K,
                                  float* ws, void* out, int out_stride, int splits, int nt, int epi,
-                                 int norm, void* residual, int res_stride, int* tickets, float eps,
                                  hipStream_t stream) {
   if (M <= 0) return 0;
   if (M > 64 || splits < 1) return -1;
@@ -610,26 +489,21 @@ extern "C" int ft_skinny_gemm_xr(const void* x, int x_stride, int M, const void*
   if (N % (16 * nt) != 0) return -2;
   const int kc = nt == 2 ? 512 : 256;
   if (K % (kc * splits) != 0) return -3;
-  if (epi < 0 || epi > 2) return -6;
+  if (epi < 0 || epi > 1) return -6;
   if (epi == 1 && (nt != 2 || splits != 1)) return -6;
-  if (norm && epi != 1) return -6;
-  if (epi == 2 && (residual == nullptr || (splits > 1 && (ws == nullptr || tickets == nullptr)))) return -4;
   if (epi == 0 && splits > 1 && ws == nullptr) return -4;
   const int mt = (M + 15) / 16;
   const int cols = 4 * 16 * nt;
   dim3 grid((N + cols - 1) / cols, splits), block(256);
   const int k_slice = K / splits;
-#define FT_XR(MT_, NT_, KC_, E_, N_)                                                          \
-  if (mt == MT_ && nt == NT_ && epi == E_ && (norm != 0) == N_) {                             \
-    hipLaunchKernelGGL((ft::skinny_xr_kernel<MT_, NT_, KC_, E_, N_>), grid, block, 0, stream, \
+#define FT_XR(MT_, NT_, KC_, E_)                                                              \
+  if (mt == MT_ && nt == NT_ && epi == E_) {                                                  \
+    hipLaunchKernelGGL((ft::skinny_xr_kernel<MT_, NT_, KC_, E_>), grid, block, 0, stream,     \
                        (const uint16_t*)x, x_stride, M, (const uint16_t*)w, K, ws,            \
-                       (uint16_t*)out, out_stride, N, k_slice, (uint16_t*)residual,           \
-                       res_stride, tickets, eps);                                             \
+                       (uint16_t*)out, out_stride, N, k_slice);                               \
     return static_cast<int>(hipGetLastError());                                               \
   }
-#define FT_XR_MT(MT_)                                                                         \
-  FT_XR(MT_, 1, 256, 0, false) FT_XR(MT_, 2, 512, 0, false) FT_XR(MT_, 2, 512, 1, false)     \
-  FT_XR(MT_, 2, 512, 1, true) FT_XR(MT_, 1, 256, 2, false) FT_XR(MT_, 2, 512, 2, false)
+#define FT_XR_MT(MT_) FT_XR(MT_, 1, 256, 0) FT_XR(MT_, 2, 512, 0) FT_XR(MT_, 2, 512, 1)
   FT_XR_MT(1)
   FT_XR_MT(2)
   FT_XR_MT(3)

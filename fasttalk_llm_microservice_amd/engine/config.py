@@ -55,7 +55,10 @@ class EngineConfig:
     async_output: bool = True          # overlap detokenize/streaming with the next GPU step
     pipeline_depth: int = 1            # decode steps queued on the GPU ahead of the one collected
     separate_process: bool = False     # run the step loop in its own process (no GIL sharing)
-    custom_allreduce: bool = False     # TP: xGMI one/two-shot all-reduce for decode-size messages
+    # TP: xGMI one/two-shot all-reduce (and the fused all-reduce + add + RMSNorm) for
+    # decode-size messages, RCCL above; on by default, falls back to RCCL when the IPC
+    # mapping fails or a peer times out
+    custom_allreduce: bool = True
     tp_share_device: bool = False      # TP ranks all on device_base (tests: gloo control + IPC data)
     max_restarts: int = 3              # separate-process engines: respawns after a replica dies
     quantization: Optional[str] = None  # None | "awq" | "w4" (W4A16, group 128; --quantization awq)
@@ -106,7 +109,7 @@ class EngineConfig:
             enforce_eager=_env(["ENGINE_ENFORCE_EAGER", "VLLM_ENFORCE_EAGER"], False, _bool),
             separate_process=_env(["ENGINE_SEPARATE_PROCESS"], None, _bool),
             pipeline_depth=max(1, min(3, _env(["ENGINE_PIPELINE_DEPTH"], 1, int))),
-            custom_allreduce=_env(["ENGINE_CUSTOM_ALLREDUCE"], False, _bool),
+            custom_allreduce=_env(["ENGINE_CUSTOM_ALLREDUCE"], True, _bool),
             tp_share_device=_env(["ENGINE_TP_SHARE_DEVICE"], False, _bool),
             max_restarts=_env(["ENGINE_MAX_RESTARTS"], 3, int),
             quantization=_env(["ENGINE_QUANTIZATION", "VLLM_QUANTIZATION"], None) or None,

@@ -329,7 +329,6 @@ class LlamaModel:
         self._unpack_buf: Optional[torch.Tensor] = None  # transient row-major weight (prefill)
         self._unpack_need = 0
         self.tickets: Optional[torch.Tensor] = None
-        self.resid_layer = False     # 33-64 row decode steps on the residual stream (_forward_resid)
 
     # ------------------------------------------------------------------ weights
     def _set_layers(self, shards):
@@ -506,12 +505,9 @@ class LlamaModel:
             if self.w4_slab[proj]:
                 need = max(need, max(sp * b * q.n for b, (_, sp) in W4_PLAN[proj].items()))
         self.ws = torch.empty(need, dtype=torch.float32, device=self.device)
-        # in-launch split-K tickets (xr "resid" epilogue, fused ring layer): zeroed,
+        # in-launch split-K tickets (fused ring layer): zeroed,
         # every launch leaves them zeroed
         self.tickets = torch.zeros(max(4096, H // 16), dtype=torch.int32, device=self.device)
-        self.resid_layer = (fold and self.tp == 1 and L0.wqkv_pk is not None and L0.wo_pk is not None
-                            and L0.wgu_pk is not None and L0.wd_pk is not None
-                            and os.environ.get("FT_RESID_LAYER", "0") == "1")
         torch.cuda.empty_cache()
         self._prepare_fused()
 
@@ -560,14 +556,20 @@ class LlamaModel:
         return total
 
     # ------------------------------------------------------------------ projections
-    def _slab_ok(self, proj: str) -> bool:
+    def _tp_fused(self, rows: int) -> bool:
+        """TP decode-size steps: the row-parallel o / down outputs go through ONE
+        launch -- custom all-reduce + residual add + RMSNorm (custom_ar.hip
+        ar_add_rmsnorm_kernel) -- straight from their split-K slabs."""
+        return self.tp > 1 and self.comm.fused_norm_ok(rows, self.cfg.hidden_size, self.device.type)
+
+    def _slab_ok(self, proj: str, rows: int = 0) -> bool:
         """May this projection leave split-K fp32 slabs for its consumer?  qkv ->
         slab_rope_kv, gate_up -> slab_silu (both rank-local); o / down -> the
-        residual add + RMSNorm, which is TP=1 only (under TP the row-parallel
-        outputs are all-reduced first) and needs hidden % 2048."""
+        residual add + RMSNorm (TP=1), or the fused all-reduce + add + RMSNorm
+        (TP, custom collectives on); both need hidden % 2048."""
         if proj in ("qkv", "gu"):
             return True
-        return self.tp == 1 and self.cfg.hidden_size % 2048 == 0
+        return self.cfg.hidden_size % 2048 == 0 and (self.tp == 1 or self._tp_fused(rows))
 
     def _lin(self, x: torch.Tensor, L: LayerWeights, proj: str) -> Tuple[int, Optional[torch.Tensor]]:
         """One layer projection y = x W^T.  Returns (splits, None) when the result
@@ -598,7 +600,7 @@ class LlamaModel:
         rows = x.shape[0]
         n, k = wp.shape
         gu = proj == "gu"
-        slab_ok = self._slab_ok(proj) and self.ws is not None
+        slab_ok = self._slab_ok(proj, rows) and self.ws is not None
         c = packed_cfg(proj, rows) if proj in PACKED_PLAN else None
         if c is not None and _cfg_fits(c, n, k):
             nt, u, sp = c
@@ -704,74 +706,10 @@ class LlamaModel:
             return rows
         return ops.rmsnorm(rows, self.norm, eps)
 
-    def _resid_cfgs(self, t: int):
-        """Opt-in (FT_RESID_LAYER=1).  Measured on MI355X at the 50-session bench it
-        LOSES to the add+RMSNorm launches it replaces (7.80 vs 7.62 ms per decode
-        step, profiles/ab_resid_layer_r02.log): each in-launch split-K seam (sc1
-        partial stores, ticket, the last arriver's sc1 loads) costs ~3 us more than
-        the separate row kernel -- the guide's "splitk-seam" price.
-        The residual-stream decode layer (33-64 rows): the plan's qkv / o / gu /
-        down configs when they are the xr kernels this path needs (qkv split-K for
-        slab_rope_kv's RMS scaling, o / down any split with the in-launch residual
-        update, gate_up one split with the SiLU + RMS epilogue), else None."""
-        if (not self.resid_layer or t > PACKED_ROWS or t <= 0 or self.ws is None
-                or self.tickets is None):
-            return None
-        cfgs = {p: packed_cfg(p, t) for p in ("qkv", "o", "gu", "down")}
-        cq, co, cg, cd = cfgs["qkv"], cfgs["o"], cfgs["gu"], cfgs["down"]
-        if cq is None or co is None or cg is None or cd is None:
-            return None
-        if not (cq[2] > 1 and co[1] == -5 and cd[1] == -5 and cg[1] == -6):
-            return None
-        nqkv = (self.nq + 2 * self.nkv) * self.d
-        H, I = self.cfg.hidden_size, self.cfg.intermediate_size
-        if not (_cfg_fits(cq, nqkv, H) and _cfg_fits(co, H, self.nq * self.d) and _cfg_fits(cg, 2 * I, H)
-                and _cfg_fits(cd, H, I)):
-            return None
-        if any(sp * 64 * n > self.ws.numel() for (_, _, sp), n in ((cq, nqkv), (co, H), (cd, H))):
-            return None
-        return cq, co, cg, cd
-
-    def _forward_resid(self, input_ids: torch.Tensor, meta: AttnMeta, kv_caches, cfgs) -> torch.Tensor:
-        """33-64 decode rows: the residual stream is the GEMM input and output, no
-        separate add + RMSNorm launches.  o / down update the residual in place
-        (split-K reduced inside the xr launch), gate_up reads the raw residual and
-        scales its rows by their RMS in the SiLU epilogue, qkv's split-K slabs are
-        RMS-scaled by slab_rope_kv (ln1 / ln2 are folded into the packed images)."""
-        cfg = self.cfg
-        eps = cfg.rms_norm_eps
-        nq, nkv, d = self.nq, self.nkv, self.d
-        t = input_ids.shape[0]
-        nqkv = (nq + 2 * nkv) * d
-        (qnt, qu, qsp), (ont, _, osp), (gnt, _, _), (dnt, _, dsp) = cfgs
-        ws, tk = self.ws, self.tickets
-        x, residual = ops.embed_rmsnorm(input_ids, self.embed, self.layers[0].ln1, eps)
-        for li, L in enumerate(self.layers):
-            kc, vc = kv_caches[li]
-            src = x if li == 0 else residual   # layer 0: the embedding gather's normed rows
-            ops.skinny_gemm(src, L.wqkv_pk, ws=ws, splits=qsp, nt=qnt, u=qu)
-            qkv = torch.empty(t, nqkv, dtype=self.dtype, device=self.device)
-            ops.slab_rope_kv(ws, qsp, t, nqkv, qkv, meta.positions, self.cos_sin, meta.slot_mapping,
-                             kc, vc, nq, nkv, d, residual=None if li == 0 else residual, eps=eps)
-            attn = self._attention(qkv, meta, kc, vc)
-            ops.skinny_gemm_xr(attn, L.wo_pk, ws=ws, splits=osp, nt=ont, epi="resid",
-                               residual=residual, tickets=tk)
-            h = ops.skinny_gemm_xr(residual, L.wgu_pk, nt=gnt, epi="silu", norm=True, eps=eps)
-            ops.skinny_gemm_xr(h, L.wd_pk, ws=ws, splits=dsp, nt=dnt, epi="resid",
-                               residual=residual, tickets=tk)
-        idx = meta.logits_indices
-        rows = residual.index_select(0, idx) if idx.numel() != t else residual
-        if rows.shape[0] == 0:
-            return rows
-        return ops.rmsnorm(rows, self.norm, eps)
-
     def forward(self, input_ids: torch.Tensor, meta: AttnMeta, kv_caches) -> torch.Tensor:
         """Returns the final-normed hidden rows at ``meta.logits_indices``."""
         if self.fused and input_ids.shape[0] <= FUSED_ROWS:
             return self._forward_fused(input_ids, meta, kv_caches)
-        rc = self._resid_cfgs(input_ids.shape[0])
-        if rc is not None:
-            return self._forward_resid(input_ids, meta, kv_caches, rc)
         cfg = self.cfg
         eps = cfg.rms_norm_eps
         nq, nkv, d = self.nq, self.nkv, self.d
@@ -780,9 +718,19 @@ class LlamaModel:
         residual = None
         x = None
         slab = 0  # >0: the previous down projection left that many fp32 slabs in self.ws
+        # TP at decode sizes: o / down partials (slabs or bf16) are all-reduced inside
+        # the next norm's launch; `pend` holds the last down's (splits, bf16 partial)
+        tpf = self._tp_fused(t)
+        pend = None
         for li, L in enumerate(self.layers):
             if residual is None:
                 x, residual = ops.embed_rmsnorm(input_ids, self.embed, L.ln1, eps)  # K1 + K2
+            elif pend is not None:   # residual += all-reduce(down partial); x = rmsnorm * ln1
+                x = torch.empty(t, H, dtype=self.dtype, device=self.device)
+                self.comm.all_reduce_add_rmsnorm(x, residual, L.ln1, eps, t,
+                                                 ws=self.ws if pend[0] else None, splits=pend[0],
+                                                 x=pend[1])
+                pend = None
             elif slab:  # residual += sum(slabs); x = rmsnorm(residual) * ln1
                 x = torch.empty(t, H, dtype=self.dtype, device=self.device)
                 ops.row_rmsnorm(x, L.ln1, eps, t, ws=self.ws, splits=slab, residual=residual)
@@ -799,7 +747,12 @@ class LlamaModel:
                                   nq, nkv, d)
             attn = self._attention(qkv, meta, kc, vc)
             so, y = self._lin(attn, L, "o")
-            if so:
+            if tpf:
+                x = torch.empty(t, H, dtype=self.dtype, device=self.device)
+                self.comm.all_reduce_add_rmsnorm(x, residual, L.ln2, eps, t,
+                                                 ws=self.ws if so else None, splits=so,
+                                                 x=None if so else y)
+            elif so:
                 x = torch.empty(t, H, dtype=self.dtype, device=self.device)
                 ops.row_rmsnorm(x, L.ln2, eps, t, ws=self.ws, splits=so, residual=residual)
             else:
@@ -812,10 +765,19 @@ class LlamaModel:
                                 device=self.device)
                 ops.slab_silu(self.ws, sg, t, h.shape[1], h, interleaved=self.gu_il)
             slab, y = self._lin(h, L, "down")
-            if not slab:
+            if tpf:
+                pend, slab = (slab, y), 0
+            elif not slab:
                 x = y
                 self.comm.all_reduce(x)
-        if slab:
+        if pend is not None:   # the last layer's down partial: all-reduce, then the final norm
+            if pend[0]:
+                x = torch.empty(t, H, dtype=self.dtype, device=self.device)
+                ops.slab_store(self.ws, pend[0], t, H, x)
+            else:
+                x = pend[1]
+            self.comm.all_reduce(x)
+        elif slab:
             x = torch.empty(t, H, dtype=self.dtype, device=self.device)
             ops.slab_store(self.ws, slab, t, H, x)
         idx = meta.logits_indices

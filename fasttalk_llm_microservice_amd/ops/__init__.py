@@ -315,21 +315,16 @@ def skinny_gemm(x, w, out=None, ws=None, splits: int = 1, nt: int = 1, u: int = 
     return out if splits == 1 else ws
 
 
-def skinny_gemm_xr(x, w, out=None, ws=None, splits: int = 1, nt: int = 2, epi: str = "store",
-                   norm: bool = False, residual=None, tickets=None, eps: float = 1e-5):
-    """The "xr" decode GEMM (M <= 64) with its fused epilogues:
-    epi "store": bf16 out (one split) or fp32 slabs [splits, M, N] in ``ws``;
-    "silu": h = silu(gate) * up of an interleave_gate_up(w, 1) image, [M, N / 2]
-    (norm=True: x is the raw residual stream and each row is scaled by its RMS --
-    the norm weight folded into w);
-    "resid": residual += x w^T in place, split-K reduced inside the launch (needs
-    ``ws`` and zeroed int32 ``tickets``, N / (16 nt) of them, left zeroed)."""
-    code = {"store": 0, "silu": 1, "resid": 2}[epi]
-    if out is None and (code == 1 or (code == 0 and splits == 1)):
+def skinny_gemm_xr(x, w, out=None, ws=None, splits: int = 1, nt: int = 2, epi: str = "store"):
+    """The "xr" decode GEMM (M <= 64): epi "store": bf16 out (one split) or fp32 slabs
+    [splits, M, N] in ``ws``; "silu": h = silu(gate) * up of an interleave_gate_up(w, 1)
+    image, [M, N / 2]."""
+    code = {"store": 0, "silu": 1}[epi]
+    if out is None and (code == 1 or splits == 1):
         cols = w.shape[0] // 2 if code == 1 else w.shape[0]
         out = torch.empty(x.shape[0], cols, dtype=x.dtype, device=x.device)
-    native().skinny_gemm_xr(x, w, out, ws, splits, nt, code, norm, residual, tickets, eps)
-    return residual if code == 2 else (out if code == 1 or splits == 1 else ws)
+    native().skinny_gemm_xr(x, w, out, ws, splits, nt, code)
+    return out if code == 1 or splits == 1 else ws
 
 
 def packed_gemm(x, w, out=None, ws=None, splits: int = 1, epi: str = "store", cfg: int = 0):

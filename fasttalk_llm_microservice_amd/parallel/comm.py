@@ -55,6 +55,15 @@ class TPComm:
         dist.all_reduce(x, group=self.group)
         return x
 
+    def fused_norm_ok(self, rows: int, hidden: int, device_type: str = "cuda") -> bool:
+        """Can residual-add + RMSNorm ride in the all-reduce (custom collectives on)?"""
+        return (self.world_size > 1 and device_type == "cuda" and self._custom_on()
+                and self.custom.can_fuse_norm(rows, hidden))
+
+    def all_reduce_add_rmsnorm(self, out, residual, weight, eps, rows, ws=None, splits=0, x=None):
+        return self.custom.all_reduce_add_rmsnorm(out, residual, weight, eps, rows, ws=ws,
+                                                  splits=splits, x=x)
+
     def all_gather_last(self, x: torch.Tensor) -> torch.Tensor:
         """Concatenate rank shards along the last dim."""
         if self.world_size == 1:

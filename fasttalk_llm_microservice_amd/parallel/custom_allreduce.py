@@ -91,6 +91,21 @@ class CustomAllReduce:
                                     self.spin_budget, two)
         return x
 
+    def can_fuse_norm(self, rows: int, hidden: int) -> bool:
+        return (not self.failed and hidden % 2048 == 0 and hidden <= 8192
+                and rows * hidden * 2 <= self.max_bytes)
+
+    def all_reduce_add_rmsnorm(self, out: torch.Tensor, residual: torch.Tensor, weight: torch.Tensor,
+                               eps: float, rows: int, ws: Optional[torch.Tensor] = None,
+                               splits: int = 0, x: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """residual[:rows] += all-reduce(partial); out = rmsnorm(residual) * weight, in
+        ONE launch (the o / down epilogue of tensor parallelism).  The partial is this
+        rank's split-K fp32 slabs (``ws``, ``splits``) or a bf16 block ``x``."""
+        self._C.custom_ar_add_rmsnorm(out, residual, weight, float(eps), ws, int(splits), x,
+                                      int(rows), self.peers, self.rank, self.world, self.max_bytes,
+                                      self.spin_budget)
+        return out
+
     def can_gather(self, x: torch.Tensor) -> bool:
         return (not self.failed and x.dtype == torch.bfloat16 and x.dim() == 2
                 and x.is_contiguous() and x.shape[1] % 8 == 0

@@ -80,9 +80,19 @@ def _maybe_custom_ar(cfg, comm: TPComm, device: str):
         return
     from .custom_allreduce import CustomAllReduce
 
-    if comm.world_size in CustomAllReduce.SUPPORTED_WORLD:
-        comm.custom = CustomAllReduce(comm.group, comm.rank, comm.world_size,
-                                      torch.device("cuda", torch.cuda.current_device()))
+    if comm.world_size not in CustomAllReduce.SUPPORTED_WORLD:
+        return
+    ar, ok = None, 1
+    try:
+        ar = CustomAllReduce(comm.group, comm.rank, comm.world_size,
+                             torch.device("cuda", torch.cuda.current_device()))
+    except Exception as e:  # e.g. IPC mapping refused: the group stays on RCCL
+        log.warning("custom all-reduce unavailable on rank %d: %s", comm.rank, e)
+        ok = 0
+    if comm.min_int(ok):    # every rank mapped every peer
+        comm.custom = ar
+    elif ar is not None:
+        ar.close()
 
 
 def _make_runner(cfg, comm: TPComm):

@@ -506,46 +506,6 @@ def test_skinny_gemm_xr_silu(m, n, k):
     _close(h.float(), ref_h, atol=3e-2, rtol=2e-2, msg="xr silu")
 
 
-@pytest.mark.parametrize("m", [1, 37, 64])
-@pytest.mark.parametrize("n,k,splits,nt", [(4096, 4096, 4, 1), (4096, 14336, 4, 1), (4096, 4096, 1, 1),
-                                            (2048, 4096, 2, 2), (4096, 14336, 7, 2)])
-def test_skinny_gemm_xr_resid(m, n, k, splits, nt):
-    """xr "resid" epilogue: residual += x W^T in place with the split-K partials
-    reduced inside the launch (last arriver per tile); tickets come back zeroed and
-    a second launch on the re-armed tickets is right too."""
-    w = (torch.randn(n, k, device=DEV) * 0.02).bfloat16()
-    x = torch.randn(m, k, device=DEV).bfloat16()
-    res0 = torch.randn(m, n, device=DEV).bfloat16()
-    wp = ops.pack_weight(w)
-    ws = torch.full((splits * n * 64,), float("nan"), device=DEV)
-    tk = torch.zeros(n // 16, dtype=torch.int32, device=DEV)
-    res = res0.clone()
-    ops.skinny_gemm_xr(x, wp, ws=ws, splits=splits, nt=nt, epi="resid", residual=res, tickets=tk)
-    ref_r = res0.float() + x.float() @ w.float().t()
-    _close(res.float(), ref_r, atol=5e-2, rtol=2e-2, msg="xr resid")
-    assert int(tk.abs().sum().item()) == 0
-    ops.skinny_gemm_xr(x, wp, ws=ws, splits=splits, nt=nt, epi="resid", residual=res, tickets=tk)
-    _close(res.float(), ref_r + x.float() @ w.float().t(), atol=8e-2, rtol=2e-2, msg="xr resid 2")
-    assert int(tk.abs().sum().item()) == 0
-
-
-@pytest.mark.parametrize("m", [1, 50, 64])
-def test_skinny_gemm_xr_silu_norm(m):
-    """xr SiLU epilogue on the raw residual stream (norm=True): h = silu(r Wg) * (r Wu)
-    of the RMS-normalised rows, the norm weight folded into the image."""
-    n, k = 2 * 2048, 4096
-    wg = (torch.randn(n // 2, k, device=DEV) * 0.02).bfloat16()
-    wu = (torch.randn(n // 2, k, device=DEV) * 0.02).bfloat16()
-    ln = (1 + 0.1 * torch.randn(k, device=DEV)).bfloat16()
-    x = (torch.randn(m, k, device=DEV) * 3).bfloat16()
-    xn = x.float() * torch.rsqrt(x.float().pow(2).mean(-1, keepdim=True) + 1e-5) * ln.float()
-    ref_h = torch.nn.functional.silu(xn @ wg.float().t()) * (xn @ wu.float().t())
-    wf = torch.cat([wg, wu]).float() * ln.float()[None, :]
-    wp = ops.pack_weight(ops.interleave_gate_up(wf.bfloat16(), 1))
-    h = ops.skinny_gemm_xr(x, wp, nt=2, epi="silu", norm=True, eps=1e-5)
-    _close(h.float(), ref_h, atol=4e-2, rtol=3e-2, msg="xr silu norm")
-
-
 def test_skinny_gemm_strided_x():
     n, k, m = 512, 2048, 20
     w = (torch.randn(n, k, device=DEV) * 0.05).bfloat16()
