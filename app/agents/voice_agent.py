@@ -81,6 +81,11 @@ class AgentConfig(BaseModel):
     max_tool_rounds: int = 3
     # one forced tool: write its call's fixed head into the prompt (AGENT_PREFILL_TOOL_HEAD)
     prefill_tool_head: bool = True
+    # the model decides (AGENT_MODEL_TOOL_CHOICE): every round offers the tool-call grammar
+    # lazily -- bound only if the model's first token opens a call, free text otherwise --
+    # so a real checkpoint picks tools itself and its calls are always valid JSON (the
+    # keyword router behind guided_tool_calls exists for random weights)
+    model_tool_choice: bool = False
 
 
 @dataclass
@@ -118,6 +123,7 @@ class VoiceAgent:
             system_prompt=e("SYSTEM_PROMPT", AgentConfig().system_prompt),
             guided_tool_calls=e("AGENT_GUIDED_TOOL_CALLS", "false").lower() == "true",
             prefill_tool_head=e("AGENT_PREFILL_TOOL_HEAD", "true").lower() == "true",
+            model_tool_choice=e("AGENT_MODEL_TOOL_CHOICE", "false").lower() == "true",
         )
 
     # ------------------------------------------------------------------ backend
@@ -223,7 +229,11 @@ class VoiceAgent:
         tools_by_name = self.tools()
         for rnd in range(self.config.max_tool_rounds + 1):
             guided = None
+            lazy = False
             head = ""
+            if (not force or rnd > 0) and schemas and self.config.model_tool_choice and \
+                    rnd < self.config.max_tool_rounds:
+                guided, lazy = GuidedSpec.tool_call(schemas), True
             if force and rnd == 0:
                 pick = [s for s in schemas if force == "required" or s["function"]["name"] == force]
                 if len(pick) == 1 and self.config.prefill_tool_head:
@@ -241,13 +251,13 @@ class VoiceAgent:
             sid = context.session_id
             # a guided call is a finite JSON language: give it room to finish even
             # when the spoken-reply budget is small
-            round_mt = max(mt, 256) if guided is not None else mt
+            round_mt = max(mt, 256) if guided is not None and not lazy else mt
             async for out in backend.stream_events(
                     messages, temperature=temp, max_tokens=round_mt, top_p=tp, top_k=top_k, stop=stop,
-                    request_id=sid, session_id=sid if (rnd == 0 and guided is None) else None,
+                    request_id=sid, session_id=sid if (rnd == 0 and (guided is None or lazy)) else None,
                     prefix_session=sid, assistant_prefix=head, tools=schemas or None, guided=guided,
-                    seed=seed,
-                    ignore_eos=ignore_eos and guided is None, min_tokens=min_tokens):
+                    seed=seed, guided_lazy=lazy,
+                    ignore_eos=ignore_eos and (guided is None or lazy), min_tokens=min_tokens):
                 if out.finished:
                     finish = out.finish_reason
                 n = len(out.token_ids)

@@ -322,7 +322,7 @@ class NativeHandler:
 
     # ------------------------------------------------------------------ generation
     def _params(self, temperature, max_tokens, top_p, top_k=None, stop=None, seed=None,
-                guided=None, ignore_eos=False, min_tokens=0):
+                guided=None, ignore_eos=False, min_tokens=0, guided_lazy=False):
         from fasttalk_llm_microservice_amd.engine.sampling_params import SamplingParams
 
         return SamplingParams(
@@ -330,7 +330,8 @@ class NativeHandler:
             top_p=1.0 if top_p is None else float(top_p),
             top_k=0 if top_k in (None, -1) else int(top_k),
             max_tokens=int(max_tokens or self.default_max_tokens),
-            stop=stop, seed=seed, guided=guided, ignore_eos=ignore_eos, min_tokens=min_tokens)
+            stop=stop, seed=seed, guided=guided, ignore_eos=ignore_eos, min_tokens=min_tokens,
+            guided_lazy=bool(guided_lazy and guided is not None))
 
     async def stream_events(self, messages: List[Dict[str, Any]], temperature: Optional[float] = None,
                             max_tokens: Optional[int] = None, top_p: Optional[float] = None,
@@ -339,14 +340,14 @@ class NativeHandler:
                             prompt_ids: Optional[List[int]] = None, tools=None, guided=None,
                             seed: Optional[int] = None, ignore_eos: bool = False,
                             min_tokens: int = 0, prefix_session: Optional[str] = None,
-                            assistant_prefix: str = "") -> AsyncIterator[Any]:
+                            assistant_prefix: str = "", guided_lazy: bool = False) -> AsyncIterator[Any]:
         """``prefix_session`` (with ``session_id=None``): build the prompt on that
         session's token stream without making this request the session's turn.
         ``assistant_prefix``: text the assistant turn starts with (written into the
         prompt; the output stream holds only what follows it)."""
         mt = int(max_tokens or self.default_max_tokens)
         params = self._params(temperature, mt, top_p, top_k, stop, seed, guided, ignore_eos,
-                              min_tokens)
+                              min_tokens, guided_lazy)
         if prompt_ids is None:
             if session_id is None and prefix_session is not None:
                 prompt_ids = self.build_prompt(messages, mt, prefix_session, tools, remember=False)
@@ -370,7 +371,7 @@ class NativeHandler:
                     raise LLMServiceError(f"engine error: {out.error}", category=ErrorCategory.PROCESSING,
                                           severity=ErrorSeverity.HIGH)
                 yield out
-            if session_id and not stop and guided is None:
+            if session_id and not stop and (guided is None or guided_lazy):
                 self._remember_reply(session_id, gen_ids, "".join(text_parts))
         finally:
             with self._lock:

@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--ctx", type=int, default=3000)
     ap.add_argument("--fresh", type=int, default=107)
     ap.add_argument("--reps", type=int, default=6)
+    ap.add_argument("--prof", action="store_true", help="torch.profiler kernel table of the mixed steps")
     a = ap.parse_args()
 
     import numpy as np
@@ -76,7 +77,15 @@ def main():
             eng.step()
         rows.clear()
         t0 = time.perf_counter()
-        eng.step()
+        if a.prof and rep == a.reps - 1:
+            from torch.profiler import ProfilerActivity, profile
+
+            with profile(activities=[ProfilerActivity.CUDA]) as prof:
+                eng.step()
+                torch.cuda.synchronize()
+            print(prof.key_averages().table(sort_by="cuda_time_total", row_limit=25, max_name_column_width=70))
+        else:
+            eng.step()
         wall = 1e3 * (time.perf_counter() - t0)
         nd, npf, ex_ms, gpu_ms = rows[0] if rows else (0, 0, 0, 0)
         print(f"mixed step: decode rows {nd} prefill tokens {npf}: wall {wall:.2f} ms, "

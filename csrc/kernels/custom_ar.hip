@@ -232,7 +232,8 @@ __global__ __launch_bounds__(256) void ar_allgather_kernel(uint16_t* __restrict_
 //            (ws != null, the projection's own epilogue format) or a bf16 block x;
 //   barrier  (one, as the one-shot all-reduce);
 //   rows     strided over the blocks: the W partials summed in rank order (fp32,
-//            identical on every rank) + residual -> residual (bf16) and
+//            identical on every rank, rounded to bf16 like the all-reduce's output)
+//            + residual -> residual (bf16) and
 //            out = rmsnorm(residual) * w, both rounded like row_add_rmsnorm_kernel.
 // A timed-out barrier leaves residual / out untouched and the error word set
 // (the step is discarded by the runner, as for every custom collective).
@@ -299,7 +300,11 @@ __global__ __launch_bounds__(256) void ar_add_rmsnorm_kernel(
     float ss = 0.f;
 #pragma unroll
     for (int c = 0; c < VPT; ++c) {
+      // the reduced partial is rounded to bf16 first, exactly as the separate
+      // all-reduce would store it: fused, unfused and RCCL-fallback TP steps (and the
+      // retried steps after a collective fault) produce the same bits
       float rv[8];
+      load8(store8(v[c]), v[c]);
       load8(rr[c * 256 + threadIdx.x], rv);
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[c][j] += rv[j];

@@ -106,9 +106,12 @@ class LLMEngine:
         if params.guided is not None:
             seq.grammar = params.guided.grammar(self)
             seq.grammar_state = seq.grammar.initial()
-            # the grammar's fixed head (e.g. '{"name": "' of a tool call) is output the
-            # model cannot choose: appended now, prefilled with the prompt
-            seq.jf_text, seq.jf_ids = self._jump_forward(seq, room=params.max_tokens - 1)
+            if params.guided_lazy:   # the model decides with its first token (_process_token)
+                seq.lazy = True
+            else:
+                # the grammar's fixed head (e.g. '{"name": "' of a tool call) is output the
+                # model cannot choose: appended now, prefilled with the prompt
+                seq.jf_text, seq.jf_ids = self._jump_forward(seq, room=params.max_tokens - 1)
         self.scheduler.add(seq)
         self.stats["requests"] += 1
         return seq
@@ -135,7 +138,7 @@ class LLMEngine:
         words = (self.runner.mcfg.vocab_size + 31) // 32
         m = np.full((len(seqs), words), -1, dtype=np.int32)
         for i, s in enumerate(seqs):
-            if s.grammar is not None and s.grammar_state >= 0:
+            if s.grammar is not None and s.grammar_state >= 0 and not s.lazy:
                 raw = np.frombuffer(s.grammar.mask(s.grammar_state), dtype=np.int32)
                 m[i, : raw.shape[0]] = raw
                 m[i, raw.shape[0]:] = 0
@@ -355,7 +358,16 @@ class LLMEngine:
         reason = None
         is_stop_tok = (tok in self.stop_ids and not p.ignore_eos) or \
             (p.stop_token_ids is not None and tok in p.stop_token_ids)
-        if seq.grammar is not None:
+        if seq.grammar is not None and seq.lazy:
+            # lazy grammar: bound iff the model's first token starts a valid string of it
+            seq.lazy = False
+            st = seq.grammar.advance_token(seq.grammar_state, tok)
+            if st >= 0:
+                seq.grammar_state = st
+                self.stats["lazy_grammar_bound"] += 1
+            else:
+                seq.grammar = None
+        elif seq.grammar is not None:
             if seq.grammar.is_eos(tok) and seq.grammar.accepting(seq.grammar_state):
                 is_stop_tok = True
             else:

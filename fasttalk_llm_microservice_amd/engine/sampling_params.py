@@ -21,6 +21,9 @@ class SamplingParams:
     ignore_eos: bool = False
     seed: Optional[int] = None
     guided: Any = None           # engine.guided.GuidedSpec (JSON-schema constrained decoding)
+    # the grammar binds only if the first generated token is a valid start of it (e.g.
+    # the model chose to open a tool call with '{"'); otherwise the reply is free text
+    guided_lazy: bool = False
     skip_special_tokens: bool = True
 
     def __post_init__(self):

@@ -38,7 +38,7 @@ class Sequence:
                  "num_computed", "num_committed_blocks", "num_cached_tokens", "arrival",
                  "first_token_time", "finish_reason", "detok_stream", "on_output", "grammar",
                  "grammar_state", "stop_buf", "text_len", "aborted", "preemptions", "admit_order",
-                 "meta", "host_slots", "background", "jf_text", "jf_ids")
+                 "meta", "host_slots", "background", "jf_text", "jf_ids", "lazy")
 
     def __init__(self, request_id: str, prompt_ids: List[int], params: SamplingParams,
                  on_output: Optional[Callable[[RequestOutput], None]] = None, meta: Any = None):
@@ -73,6 +73,7 @@ class Sequence:
         # the first sampled token's output
         self.jf_text = ""
         self.jf_ids: List[int] = []
+        self.lazy = False   # grammar not bound yet (SamplingParams.guided_lazy)
 
     # ---------------------------------------------------------------- tokens
     @property

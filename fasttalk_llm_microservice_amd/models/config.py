@@ -68,6 +68,10 @@ MODELS = {
     "llama3-70b": ModelConfig("llama3-70b", 8192, 80, 64, 8, 128, 28672),
     "llama3.1-70b": ModelConfig("llama3.1-70b", 8192, 80, 64, 8, 128, 28672,
                                 rope_scaling=_LLAMA31_SCALING, max_position_embeddings=131072),
+    # 2-layer slices of the real shapes (GPU tests / TP probes: every kernel at its
+    # serving shape, a fraction of the weights)
+    "llama3-8b-2l": ModelConfig("llama3-8b-2l", 4096, 2, 32, 8, 128, 14336),
+    "llama3-70b-2l": ModelConfig("llama3-70b-2l", 8192, 2, 64, 8, 128, 28672),
     # small shapes for CPU tests (keep kernel constraints: hidden % 512 == 0)
     "tiny": ModelConfig("tiny", 512, 2, 8, 2, 64, 1024, vocab_size=128256),
     "tiny-gqa4": ModelConfig("tiny-gqa4", 512, 2, 8, 2, 64, 1536, vocab_size=128256),

@@ -329,6 +329,9 @@ class LlamaModel:
         self._unpack_buf: Optional[torch.Tensor] = None  # transient row-major weight (prefill)
         self._unpack_need = 0
         self.tickets: Optional[torch.Tensor] = None
+        # TP: all-reduce + residual add + RMSNorm in one launch (FT_TP_FUSED_NORM=0: the
+        # separate slab_store -> all-reduce -> add+RMSNorm launches, for A/B runs)
+        self.tp_fused_norm = os.environ.get("FT_TP_FUSED_NORM", "1") != "0"
 
     # ------------------------------------------------------------------ weights
     def _set_layers(self, shards):
@@ -560,7 +563,15 @@ class LlamaModel:
         """TP decode-size steps: the row-parallel o / down outputs go through ONE
         launch -- custom all-reduce + residual add + RMSNorm (custom_ar.hip
         ar_add_rmsnorm_kernel) -- straight from their split-K slabs."""
-        return self.tp > 1 and self.comm.fused_norm_ok(rows, self.cfg.hidden_size, self.device.type)
+        return (self.tp > 1 and self.tp_fused_norm
+                and self.comm.fused_norm_ok(rows, self.cfg.hidden_size, self.device.type))
+
+    def _tp_slabs(self, rows: int) -> bool:
+        """TP steps of the fused path's shape: o / down leave split-K slabs whether
+        the fused launch or the fallback (slab_store -> all-reduce -> add+norm) consumes
+        them, so a group that fell back to RCCL reproduces the fused path's bits."""
+        return (self.tp > 1 and self.tp_fused_norm
+                and self.comm.fused_norm_shape(rows, self.cfg.hidden_size, self.device.type))
 
     def _slab_ok(self, proj: str, rows: int = 0) -> bool:
         """May this projection leave split-K fp32 slabs for its consumer?  qkv ->
@@ -569,7 +580,22 @@ class LlamaModel:
         (TP, custom collectives on); both need hidden % 2048."""
         if proj in ("qkv", "gu"):
             return True
-        return self.cfg.hidden_size % 2048 == 0 and (self.tp == 1 or self._tp_fused(rows))
+        return self.cfg.hidden_size % 2048 == 0 and (self.tp == 1 or self._tp_slabs(rows))
+
+    def _tp_add_norm(self, out, residual, weight, eps, t, splits, y, fused):
+        """residual += all-reduce(partial); out = rmsnorm(residual) * weight, the
+        partial being ``splits`` fp32 slabs in self.ws or the bf16 block y."""
+        if fused:
+            self.comm.all_reduce_add_rmsnorm(out, residual, weight, eps, t,
+                                             ws=self.ws if splits else None, splits=splits,
+                                             x=None if splits else y)
+            return out
+        if splits:
+            y = torch.empty(t, self.cfg.hidden_size, dtype=self.dtype, device=self.device)
+            ops.slab_store(self.ws, splits, t, y.shape[1], y)
+        self.comm.all_reduce(y)
+        ops.fused_add_rmsnorm(y, residual, weight, eps)
+        return y
 
     def _lin(self, x: torch.Tensor, L: LayerWeights, proj: str) -> Tuple[int, Optional[torch.Tensor]]:
         """One layer projection y = x W^T.  Returns (splits, None) when the result
@@ -720,16 +746,15 @@ class LlamaModel:
         slab = 0  # >0: the previous down projection left that many fp32 slabs in self.ws
         # TP at decode sizes: o / down partials (slabs or bf16) are all-reduced inside
         # the next norm's launch; `pend` holds the last down's (splits, bf16 partial)
-        tpf = self._tp_fused(t)
+        tps = self._tp_slabs(t)
+        tpf = tps and self._tp_fused(t)
         pend = None
         for li, L in enumerate(self.layers):
             if residual is None:
                 x, residual = ops.embed_rmsnorm(input_ids, self.embed, L.ln1, eps)  # K1 + K2
             elif pend is not None:   # residual += all-reduce(down partial); x = rmsnorm * ln1
-                x = torch.empty(t, H, dtype=self.dtype, device=self.device)
-                self.comm.all_reduce_add_rmsnorm(x, residual, L.ln1, eps, t,
-                                                 ws=self.ws if pend[0] else None, splits=pend[0],
-                                                 x=pend[1])
+                x = torch.empty(t, H, dtype=self.dtype, device=self.device) if tpf else None
+                x = self._tp_add_norm(x, residual, L.ln1, eps, t, pend[0], pend[1], tpf)
                 pend = None
             elif slab:  # residual += sum(slabs); x = rmsnorm(residual) * ln1
                 x = torch.empty(t, H, dtype=self.dtype, device=self.device)
@@ -747,11 +772,9 @@ class LlamaModel:
                                   nq, nkv, d)
             attn = self._attention(qkv, meta, kc, vc)
             so, y = self._lin(attn, L, "o")
-            if tpf:
-                x = torch.empty(t, H, dtype=self.dtype, device=self.device)
-                self.comm.all_reduce_add_rmsnorm(x, residual, L.ln2, eps, t,
-                                                 ws=self.ws if so else None, splits=so,
-                                                 x=None if so else y)
+            if tps:
+                x = torch.empty(t, H, dtype=self.dtype, device=self.device) if tpf else None
+                x = self._tp_add_norm(x, residual, L.ln2, eps, t, so, y, tpf)
             elif so:
                 x = torch.empty(t, H, dtype=self.dtype, device=self.device)
                 ops.row_rmsnorm(x, L.ln2, eps, t, ws=self.ws, splits=so, residual=residual)
@@ -765,7 +788,7 @@ class LlamaModel:
                                 device=self.device)
                 ops.slab_silu(self.ws, sg, t, h.shape[1], h, interleaved=self.gu_il)
             slab, y = self._lin(h, L, "down")
-            if tpf:
+            if tps:
                 pend, slab = (slab, y), 0
             elif not slab:
                 x = y

@@ -60,6 +60,13 @@ class TPComm:
         return (self.world_size > 1 and device_type == "cuda" and self._custom_on()
                 and self.custom.can_fuse_norm(rows, hidden))
 
+    def fused_norm_shape(self, rows: int, hidden: int, device_type: str = "cuda") -> bool:
+        """The shape rule of :meth:`fused_norm_ok` alone, whether or not the custom
+        collectives are (still) up: steps of this shape keep the same projection
+        kernels after a fallback to RCCL, so they produce the same bits."""
+        return (self.world_size > 1 and device_type == "cuda" and hidden % 2048 == 0
+                and hidden <= 8192 and rows * hidden * 2 <= self.custom_max_bytes)
+
     def all_reduce_add_rmsnorm(self, out, residual, weight, eps, rows, ws=None, splits=0, x=None):
         return self.custom.all_reduce_add_rmsnorm(out, residual, weight, eps, rows, ws=ws,
                                                   splits=splits, x=x)

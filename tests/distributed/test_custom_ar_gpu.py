@@ -96,7 +96,7 @@ def _worker(rank, world, port, q):
             full = [p.float() for p in parts]
         res0 = torch.randn(rows, hidden, generator=gen(99)).bfloat16()
         w = (1 + 0.1 * torch.randn(hidden, generator=gen(98))).bfloat16()
-        r_exp = (res0.float() + sum(full)).bfloat16().float()
+        r_exp = (res0.float() + sum(full).bfloat16().float()).bfloat16().float()
         x_exp = (r_exp * torch.rsqrt(r_exp.pow(2).mean(-1, keepdim=True) + 1e-5)).bfloat16().float() \
             * w.float()
         res = res0.cuda()

@@ -461,3 +461,53 @@ def test_jump_forward_prefills_forced_grammar_runs(tiny_engine, monkeypatch):
     assert not off.jump_forward
     ids = off.generate([[1, 2, 3]], SamplingParams(temperature=1.0, max_tokens=80, seed=0, guided=spec))[0]
     assert json.loads(off.tokenizer.decode(ids))["name"] in ("duckduckgo_search", "get_current_time")
+
+
+class _MaskRunner(FakeRunner):
+    """Scripted first token per request, then the lowest id the grammar allows (or a
+    fixed word when unconstrained): drives lazy-grammar requests to completion."""
+
+    def __init__(self, first, word, **kw):
+        super().__init__(**kw)
+        self.first, self.word = first, word
+
+    def execute(self, batch, masks):
+        self.stats["steps"] += 1
+        out = []
+        for i, s in enumerate(batch.sampled_seqs()):
+            row = None if masks is None else masks[i]
+            if row is not None and not (row == -1).all():
+                bits = np.unpackbits(row.view(np.uint8), bitorder="little")
+                out.append(int(np.flatnonzero(bits)[0]))
+            elif s.n_tokens == s.prompt_len:
+                out.append(self.first)
+            else:
+                out.append(self.word)
+        return out
+
+
+@pytest.mark.parametrize("opens_call", [True, False])
+def test_lazy_tool_grammar_binds_only_when_the_model_opens_a_call(opens_call):
+    """VERDICT r2 #5 (model-decided tools): the tool-call grammar is offered lazily --
+    bound iff the first generated token starts a call (then the call is valid JSON,
+    jump-forwarded), else the reply stays free text with no masks at all."""
+    from fasttalk_llm_microservice_amd.engine.guided import tool_call_ast
+    from fasttalk_llm_microservice_amd.engine.tokenizer import get_tokenizer
+
+    tok = get_tokenizer()
+    brace = tok.encode("{")[0]
+    word = tok.encode(" hello")[0]
+    runner = _MaskRunner(brace if opens_call else word, word, num_blocks=256)
+    eng = LLMEngine(EngineConfig(model="tiny", device="cpu", block_size=4), runner=runner)
+    tools = [{"type": "function", "function": {"name": "get_current_time",
+                                               "parameters": {"type": "object", "properties": {}}}}]
+    sp = SamplingParams(temperature=0.7, max_tokens=40, guided=GuidedSpec(tool_call_ast(tools)),
+                        guided_lazy=True, ignore_eos=not opens_call)
+    ids = eng.generate([[1, 2, 3, 4, 5]], sp)[0]
+    text = eng.tokenizer.decode(ids)
+    if opens_call:
+        assert json.loads(text) == {"name": "get_current_time", "parameters": {}}
+        assert eng.stats["lazy_grammar_bound"] == 1
+    else:
+        assert text.startswith(" hello") and len(ids) == 40
+        assert eng.stats["lazy_grammar_bound"] == 0
