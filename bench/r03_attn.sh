@@ -1,0 +1,10 @@
+#!/bin/bash
+# attention VALU diet: GPU tests, attention probes, mixed step, driver bench
+cd "$(dirname "$0")/.."
+export TMPDIR=/tmp
+./gpurun_step.sh \
+  "gputests:900:python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread" \
+  "prefill:300:python bench/prefill_probe.py --cases 5:107:3000,10:100:3000,4:128:3000,1:512:3000,1:2048:0" \
+  "attn:300:python bench/attn_cfg.py" \
+  "mixed:300:python bench/mixed_probe.py --reps 4" \
+  "bench:600:python bench.py --gpus 1 --steps 20 --warmup 5"

@@ -21,13 +21,16 @@ __device__ __forceinline__ float bf16_to_f32(uint16_t v) {
   return __uint_as_float(static_cast<uint32_t>(v) << 16);
 }
 
-// round-to-nearest-even fp32 -> bf16 (NaN preserved as quiet NaN)
+// round-to-nearest-even fp32 -> bf16 (NaN stays NaN): a plain cast, which hipcc
+// lowers to the hardware v_cvt_pk_bf16_f32 (one VALU op for two values) -- the
+// integer-rounding form this replaces cost ~6 VALU ops per value in every epilogue
+// and in the attention kernels' P conversion (guide: MI355X_MICROARCH.md,
+// Correctness boundaries, f32 -> bf16 row)
 __device__ __forceinline__ uint16_t f32_to_bf16(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return static_cast<uint16_t>((u >> 16) | 0x40u);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return static_cast<uint16_t>(u >> 16);
+  return __builtin_bit_cast(uint16_t, static_cast<__bf16>(f));
 }
+
+typedef __bf16 ft_bf16x2_t __attribute__((ext_vector_type(2)));
 
 // unpack a 32-bit word holding two bf16 (low element first)
 __device__ __forceinline__ void unpack2(uint32_t w, float& lo, float& hi) {
@@ -36,7 +39,8 @@ __device__ __forceinline__ void unpack2(uint32_t w, float& lo, float& hi) {
 }
 
 __device__ __forceinline__ uint32_t pack2(float lo, float hi) {
-  return static_cast<uint32_t>(f32_to_bf16(lo)) | (static_cast<uint32_t>(f32_to_bf16(hi)) << 16);
+  const ft_bf16x2_t v = {static_cast<__bf16>(lo), static_cast<__bf16>(hi)};
+  return __builtin_bit_cast(uint32_t, v);
 }
 
 // 8 x bf16 <-> 8 x fp32

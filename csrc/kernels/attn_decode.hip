@@ -54,6 +54,9 @@ typedef float floatx4_t __attribute__((ext_vector_type(4)));
 
 constexpr int kDecMaxBatch = 1024;
 constexpr int kDecMinTiles = 4;   // >= 64 tokens per wave: short contexts use fewer waves
+// deferred-rescale threshold (log2 units): p = exp2(score - reference max) stays <= 2^8,
+// exact in fp32 and in bf16's range
+constexpr float kDecRescaleThr = 8.f;
 
 // s_pre[b] = sum_{b' < b} ceil(L_b' / 16) (tiles per kv head), b = 0..batch; wave-wide scan
 __device__ __forceinline__ void dec_prefix(int* s_pre, const int* __restrict__ seq_lens, int batch) {
@@ -274,6 +277,7 @@ __global__ __launch_bounds__(256, WPC) void paged_decode_kernel(
   const int f1 = (int)(((long long)(w + 1) * total) / nw);
 
   const int lane = lane_id();
+  const float thr_raw = kDecRescaleThr / scale_log2;   // the threshold in raw score units
   const int n = lane & 15;   // MFMA column (head) / row (token) / dim within a tile
   const int g = lane >> 4;   // k group
   const int bsz = 1 << bs_shift;
@@ -309,8 +313,9 @@ __global__ __launch_bounds__(256, WPC) void paged_decode_kernel(
     floatx4_t o[ND];
 #pragma unroll
     for (int nd = 0; nd < ND; ++nd) o[nd] = floatx4_t{0.f, 0.f, 0.f, 0.f};
-    float m_run = -INFINITY;   // running max of head n (uniform over g)
+    float m_run = -INFINITY;   // reference max of head n, raw score units (uniform over g)
     float l_run = 0.f;         // this lane's share of the running sum of head n
+    float nbias = 0.f;         // -m_run * scale_log2
 
     const int* bt = block_tables + (size_t)b * bt_stride;
     for (int c0 = 0; c0 < cnt; c0 += 64) {
@@ -336,25 +341,25 @@ __global__ __launch_bounds__(256, WPC) void paged_decode_kernel(
         for (int kc = 0; kc < KC; ++kc)
           s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, t.k[kc]),
                                                       __builtin_bit_cast(bf16x8_t, qb[kc]), s, 0, 0, 0);
-        float tm = -INFINITY;
+        // only a sequence's last tile can be partial: a wave-uniform branch, so full
+        // tiles carry no mask compares / selects
+        if (valid < 16) {
 #pragma unroll
-        for (int i4 = 0; i4 < 4; ++i4) {
-          float v = s[i4] * scale_log2;
-          if (valid < 16 && 4 * g + i4 >= valid) v = -INFINITY;
-          s[i4] = v;
-          tm = fmaxf(tm, v);
+          for (int i4 = 0; i4 < 4; ++i4)
+            if (4 * g + i4 >= valid) s[i4] = -INFINITY;
         }
+        float tm = fmaxf(fmaxf(s[0], s[1]), fmaxf(s[2], s[3]));
         tm = fmaxf(tm, __shfl_xor(tm, 16, 64));
         tm = fmaxf(tm, __shfl_xor(tm, 32, 64));
-        const float mn = fmaxf(m_run, tm);
-        const float alpha = exp2f(m_run - mn);
-        m_run = mn;
-        float p[4];
-#pragma unroll
-        for (int i4 = 0; i4 < 4; ++i4) p[i4] = exp2f(s[i4] - mn);
-        l_run = l_run * alpha + ((p[0] + p[1]) + (p[2] + p[3]));
-        // rescale O rows (heads 4g'+i of the C layout) only when some max moved
-        if (__builtin_amdgcn_ballot_w64(alpha != 1.f)) {
+        // deferred rescale (guide T13): the reference max m_run (raw score units) moves
+        // only when some head's tile max passes it by more than kDecRescaleThr (log2
+        // units), so p <= 2^thr and most tiles skip alpha, the O rescale and the l
+        // rescale; the branch is wave-uniform
+        if (__builtin_amdgcn_ballot_w64(tm > m_run + thr_raw) != 0) {
+          const float mn = fmaxf(m_run, tm);
+          const float alpha = __builtin_amdgcn_exp2f((m_run - mn) * scale_log2);  // -inf -> 0
+          m_run = mn;
+          l_run *= alpha;
           float a[4];
 #pragma unroll
           for (int i4 = 0; i4 < 4; ++i4) a[i4] = __shfl(alpha, (4 * g + i4) & 15, 64);
@@ -362,10 +367,15 @@ __global__ __launch_bounds__(256, WPC) void paged_decode_kernel(
           for (int nd = 0; nd < ND; ++nd)
 #pragma unroll
             for (int i4 = 0; i4 < 4; ++i4) o[nd][i4] *= a[i4];
+          nbias = -m_run * scale_log2;
         }
-        short4_t pa;
+        float p[4];
 #pragma unroll
-        for (int i4 = 0; i4 < 4; ++i4) pa[i4] = (short)f32_to_bf16(p[i4]);
+        for (int i4 = 0; i4 < 4; ++i4) p[i4] = __builtin_amdgcn_exp2f(fmaf(s[i4], scale_log2, nbias));
+        l_run += (p[0] + p[1]) + (p[2] + p[3]);
+        typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+        const u32x2_t pw = {pack2(p[0], p[1]), pack2(p[2], p[3])};   // 2 x v_cvt_pk_bf16_f32
+        const short4_t pa = __builtin_bit_cast(short4_t, pw);
 #pragma unroll
         for (int nd = 0; nd < ND; ++nd)
           o[nd] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(pa, __builtin_bit_cast(short4_t, t.v[nd]),
@@ -385,7 +395,7 @@ __global__ __launch_bounds__(256, WPC) void paged_decode_kernel(
       }
     }
 
-    dec_finish<D, G, ND, FC>(o, l_run, m_run, b, h, t0, cnt, nb, w, nw, total, nkv, s_pre, out,
+    dec_finish<D, G, ND, FC>(o, l_run, m_run * scale_log2, b, h, t0, cnt, nb, w, nw, total, nkv, s_pre, out,
                              out_stride, tmp_out, tmp_ml, counters, lane, g, n);
     f += cnt;
   }

@@ -50,6 +50,7 @@ __device__ __forceinline__ bf16x8_t as_frag(const uint4& v) {
 }
 
 constexpr int kPrefillBK = 64;   // kv tokens per tile
+constexpr float kPrefillRescaleThr = 8.f;
 constexpr int kPrefillRows = 256; // query rows (token x head) per workgroup
 constexpr int kPrefillMaxBlocks = 4096;  // block-table entries staged in LDS (checked on the host)
 
@@ -129,12 +130,14 @@ __global__ __launch_bounds__(512, 1) void prefill_attn_kernel(
   for (int m = 0; m < MT; ++m)
 #pragma unroll
     for (int i = 0; i < ND; ++i) o[m][i] = floatx4_t{0.f, 0.f, 0.f, 0.f};
-  float m_run[MT], l_run[MT];
+  float m_run[MT], l_run[MT], nbias[MT];
 #pragma unroll
   for (int m = 0; m < MT; ++m) {
     m_run[m] = -INFINITY;
     l_run[m] = 0.f;
+    nbias[m] = 0.f;
   }
+  const float thr_raw = kPrefillRescaleThr / scale_log2;
 
   const int kv_end = min(L, ctx0 + qs + ntok);  // exclusive
   const int kt_lo = krange >> 16;
@@ -183,14 +186,17 @@ __global__ __launch_bounds__(512, 1) void prefill_attn_kernel(
       glds16(src, lds_off(dst));
     }
   };
-  // 4 tokens (8 B) of V^T row `row` starting at token t (t % 4 == 0)
-  const uint16_t* Ks = smem;          // current slot's images (set per tile)
-  const uint16_t* Vs = smem + KIMG;
-  // LDS byte address of 4 tokens (8 B) of V^T row `row` starting at token t (t % 4 == 0)
-  auto vt4 = [&](int row, int t) -> uint32_t {
-    return lds_off(Vs + row * kPrefillBK) + (((t >> 3) ^ ((row >> 1) & 7)) << 4) + (((t >> 2) & 1) << 3);
-  };
-
+  uint32_t koff[KC];
+#pragma unroll
+  for (int kc = 0; kc < KC; ++kc) koff[kc] = l15 * D * 2 + ((((kc * 4 + lg) ^ (l15 & SWZ))) << 4);
+  uint32_t voff[2][2];
+#pragma unroll
+  for (int kc = 0; kc < 2; ++kc)
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      voff[kc][h] = l15 * kPrefillBK * 2 + (((kc * 4 + h * 2 + (lg >> 1)) ^ ((l15 >> 1) & 7)) << 4) +
+                    ((lg & 1) << 3);
+  uint32_t kb = 0;   // LDS byte address of the current slot's K image (V^T image follows)
 
   auto tile_math = [&](int kt) {
     const int kbase = kt * kPrefillBK;
@@ -201,11 +207,17 @@ __global__ __launch_bounds__(512, 1) void prefill_attn_kernel(
 #pragma unroll
       for (int n = 0; n < 4; ++n) s[m][n] = floatx4_t{0.f, 0.f, 0.f, 0.f};
     // K A-fragments: 4 reads per 16-kv n-tile, the next n-tile's in flight
-    auto kread = [&](uint4 (&kf)[KC], int n) {
-      const int row = n * 16 + l15;
+    uint32_t ka[KC];
 #pragma unroll
-      for (int kc = 0; kc < KC; ++kc)
-        kf[kc] = ds_read16(lds_off(Ks + row * D) + ((((kc * 4 + lg) ^ (row & SWZ))) << 4));
+    for (int kc = 0; kc < KC; ++kc) ka[kc] = kb + koff[kc];
+    auto kread = [&](uint4 (&kf)[KC], int n) {
+#pragma unroll
+      for (int kc = 0; kc < KC; ++kc) {
+        if (n == 0) kf[kc] = ds_read16o<0>(ka[kc]);
+        else if (n == 1) kf[kc] = ds_read16o<32 * D>(ka[kc]);
+        else if (n == 2) kf[kc] = ds_read16o<64 * D>(ka[kc]);
+        else kf[kc] = ds_read16o<96 * D>(ka[kc]);
+      }
     };
     uint4 kf[2][KC];
     kread(kf[0], 0);
@@ -226,43 +238,47 @@ __global__ __launch_bounds__(512, 1) void prefill_attn_kernel(
                                                              s[m][n], 0, 0, 0);
       }
     }
-    // ---- mask + online softmax (log2 domain), one query column per lane ---------------
     const bool edge = kbase + kPrefillBK > kv_end || kbase + kPrefillBK - 1 > first_q;
-    float alpha[MT];
+    if (__builtin_expect(edge, 0)) {
+      asm volatile("" ::: "memory");   // keep this a branch: if-converted, every tile paid the mask
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        const int lim = min(qpos[m], kv_end - 1) - kbase - lg * 4;
+#pragma unroll
+        for (int n = 0; n < 4; ++n)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (n * 16 + i > lim) s[m][n][i] = -INFINITY;
+      }
+    }
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
-      float mt = -INFINITY;
+      float mt = fmaxf(fmaxf(s[m][0][0], s[m][0][1]), fmaxf(s[m][0][2], s[m][0][3]));
 #pragma unroll
-      for (int n = 0; n < 4; ++n)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          float v = s[m][n][i] * scale_log2;
-          if (edge) {
-            const int kp = kbase + n * 16 + lg * 4 + i;
-            if (kp > qpos[m] || kp >= kv_end) v = -INFINITY;
-          }
-          s[m][n][i] = v;
-          mt = fmaxf(mt, v);
-        }
+      for (int n = 1; n < 4; ++n)
+        mt = fmaxf(mt, fmaxf(fmaxf(s[m][n][0], s[m][n][1]), fmaxf(s[m][n][2], s[m][n][3])));
       mt = kgroup_max(mt);
-      const float mn = fmaxf(m_run[m], mt);
-      const float base = (mn == -INFINITY) ? 0.f : mn;
-      alpha[m] = exp2f(m_run[m] - base);
-      m_run[m] = mn;
+      if (__builtin_amdgcn_ballot_w64(mt > m_run[m] + thr_raw) != 0) {
+        const float mn = fmaxf(m_run[m], mt);
+        const float alpha = mn == -INFINITY ? 1.f : __builtin_amdgcn_exp2f((m_run[m] - mn) * scale_log2);
+        m_run[m] = mn;
+        nbias[m] = mn == -INFINITY ? 0.f : -mn * scale_log2;
+        l_run[m] *= alpha;
+#pragma unroll
+        for (int nd = 0; nd < ND; ++nd)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) o[m][nd][i] *= alpha;
+      }
       float ls = 0.f;
 #pragma unroll
       for (int n = 0; n < 4; ++n)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const float p = exp2f(s[m][n][i] - base);
+          const float p = __builtin_amdgcn_exp2f(fmaf(s[m][n][i], scale_log2, nbias[m]));
           s[m][n][i] = p;
           ls += p;
         }
-      l_run[m] = l_run[m] * alpha[m] + ls;
-#pragma unroll
-      for (int nd = 0; nd < ND; ++nd)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) o[m][nd][i] *= alpha[m];
+      l_run[m] += ls;
     }
 
     // ---- O^T += V^T P^T: k-slots of lane (., lg) = tokens {4lg.., 16+4lg..} + 32 kc ----
@@ -277,10 +293,14 @@ __global__ __launch_bounds__(512, 1) void prefill_attn_kernel(
                            pack2(hi[2], hi[3]));
       }
       // V^T A-fragments: 2 reads per dim tile, the next tile's in flight
+      const uint32_t va0 = kb + KIMG * 2 + voff[kc][0], va1 = kb + KIMG * 2 + voff[kc][1];
       auto vread = [&](uint2 (&vv)[2], int nd) {
-        const int row = nd * 16 + l15;
-        vv[0] = ds_read8(vt4(row, kc * 32 + 4 * lg));
-        vv[1] = ds_read8(vt4(row, kc * 32 + 16 + 4 * lg));
+        switch (nd) {   // constant after unrolling: the dim tile's displacement is an immediate
+#define FT_VR(I) case I: vv[0] = ds_read8o<I * 32 * kPrefillBK>(va0); vv[1] = ds_read8o<I * 32 * kPrefillBK>(va1); break;
+          FT_VR(0) FT_VR(1) FT_VR(2) FT_VR(3) FT_VR(4) FT_VR(5) FT_VR(6)
+          default: vv[0] = ds_read8o<7 * 32 * kPrefillBK>(va0); vv[1] = ds_read8o<7 * 32 * kPrefillBK>(va1);
+#undef FT_VR
+        }
       };
       uint2 vv[2][2];
       vread(vv[0], 0);
@@ -321,8 +341,7 @@ __global__ __launch_bounds__(512, 1) void prefill_attn_kernel(
     else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_WAVE) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();          // every wave's pieces of tile kt have landed
-    Ks = smem + slot * SLOT;
-    Vs = Ks + KIMG;
+    kb = lds_off(smem) + slot * SLOT * 2;
     tile_math(kt);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();          // slot kt % NSLOT may be refilled
@@ -341,7 +360,7 @@ __global__ __launch_bounds__(512, 1) void prefill_attn_kernel(
         *reinterpret_cast<float4*>(po + nd * 16) = make_float4(o[m][nd][0], o[m][nd][1], o[m][nd][2], o[m][nd][3]);
       if (lg == 0)
         *reinterpret_cast<float2*>(part_ml + (((size_t)pslot * nkv + kvh) * kPrefillRows + r) * 2) =
-            make_float2(m_run[m], l);
+            make_float2(m_run[m] == -INFINITY ? -INFINITY : m_run[m] * scale_log2, l);
       continue;
     }
     const int tq = r / G, g = r - (r / G) * G;

@@ -3,6 +3,8 @@
 #pragma once
 #include "ft_common.h"
 
+#include <type_traits>
+
 namespace ft {
 
 // LDS reads in inline asm: with LDS-DMA (global_load_lds) in flight hipcc cannot
@@ -25,6 +27,31 @@ __device__ __forceinline__ uint2 ds_read8(uint32_t a) {
   asm volatile("ds_read_b64 %0, %1" : "=v"(v) : "v"(a));
   return __builtin_bit_cast(uint2, v);
 }
+// the same with a compile-time immediate offset (the ds_read offset field, 0..65535):
+// per-lane base addresses computed once, per-fragment displacements as immediates
+template <int OFF>
+__device__ __forceinline__ uint4 ds_read16o(uint32_t a) {
+  static_assert(OFF >= 0 && OFF < 65536, "ds_read offset field");
+  u32x4_t v;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(a), "n"(OFF));
+  return __builtin_bit_cast(uint4, v);
+}
+template <int OFF>
+__device__ __forceinline__ uint2 ds_read8o(uint32_t a) {
+  static_assert(OFF >= 0 && OFF < 65536, "ds_read offset field");
+  u32x2_t v;
+  asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(v) : "v"(a), "n"(OFF));
+  return __builtin_bit_cast(uint2, v);
+}
+// compile-time loop: f(std::integral_constant<int, I>) for I in [B, E)
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
+
 // global_load_lds_dwordx4 in inline asm (guide idiom): M0 = the wave-uniform LDS
 // destination, lanes land at M0 + 16 * lane.  hipcc's waitcnt pass does not see it
 // (it would otherwise treat the address VGPRs as pending and wait vmcnt(0) at their

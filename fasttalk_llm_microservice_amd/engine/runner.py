@@ -258,6 +258,9 @@ class ModelRunner:
         self._graph_msgs = 0
         self._mixed_msgs = 0
         self.stats = {"graph_replays": 0, "eager_decode": 0, "prefill_steps": 0, "captures": 0}
+        # tests: a list here collects each eager step's logits (fp32, host) -- TP-vs-TP=1
+        # numerics are compared on logits, not on greedy tokens of random weights
+        self.logits_tap: Optional[list] = None
         # FT_GPU_GAPS=1: timing events around every graph-replayed decode step, so
         # gap_summary() can report how long the GPU sat idle BETWEEN consecutive
         # decode steps (the host enqueued the next one late), without a profiler
@@ -496,6 +499,8 @@ class ModelRunner:
 
     def _sample(self, h, sampling, masks, dev_sampling=None, dev_mask=None) -> List[int]:
         logits = self.model.compute_logits(h)
+        if self.logits_tap is not None:
+            self.logits_tap.append(logits.float().cpu())
         if dev_sampling is None:
             arrays = list(sampling) + ([masks] if masks is not None else [])
             if self.is_gpu:

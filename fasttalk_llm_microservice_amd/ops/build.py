@@ -92,14 +92,26 @@ def _compile(src: Path, obj: Path, cmd: list, deps: list, force: bool) -> bool:
     return True
 
 
+# Per-kernel extra flags.  The attention kernels keep their MFMA accumulators in
+# VGPRs (gfx950's unified register file): in the AGPR form hipcc copied the O
+# accumulator AGPR -> VGPR -> AGPR around every online-softmax rescale (64 extra
+# instructions per KV tile in the decode kernel); and without NaN semantics fmaxf
+# on MFMA results needs no canonicalising v_max first.
+KERNEL_FLAGS = {
+    "attn_decode": ["-mllvm", "-amdgpu-mfma-vgpr-form=1", "-fno-honor-nans"],
+    "attn_prefill": ["-mllvm", "-amdgpu-mfma-vgpr-form=1", "-fno-honor-nans"],
+}
+
+
 def build_kernels(force: bool = False, jobs: int = 8, verbose: bool = True) -> Path:
-    headers = sorted((CSRC / "include").glob("*.h"))
+    headers = sorted((CSRC / "include").glob("*.h")) + sorted((CSRC / "kernels").glob("*.h"))
     kernels = sorted((CSRC / "kernels").glob("*.hip"))
     kflags = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
               f"-I{CSRC / 'include'}", "-munsafe-fp-atomics"]
     tflags, ldflags = _torch_flags()
     bflags = [HIPCC, f"--offload-arch={ARCH}"] + tflags + [f"-I{CSRC / 'include'}"]
-    jobs_list = [(k, BUILD / "kernels" / (k.stem + ".o"), kflags, headers) for k in kernels]
+    jobs_list = [(k, BUILD / "kernels" / (k.stem + ".o"), kflags + KERNEL_FLAGS.get(k.stem, []), headers)
+                 for k in kernels]
     jobs_list.append((CSRC / "bindings.cpp", BUILD / "bindings.o", bflags + ["-x", "hip"], headers))
     changed = False
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:

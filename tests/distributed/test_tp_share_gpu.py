@@ -117,7 +117,10 @@ def test_tp2_on_one_gpu_matches_tp1_and_survives_an_allreduce_timeout(tp1_tokens
         eng.shutdown()
     print("post-fallback vs healthy TP2:", _agree(out, ref2), " TP2 vs TP1:", _agree(ref2, tp1_tokens))
     assert out == ref2          # same kernels, the fallback sums the same two fp32 values
-    assert _common_prefix(ref2, tp1_tokens) >= 4
+    # greedy tokens of random weights: the first (prefill) token must agree; later ones
+    # drift at near-ties (TP=2 sums two fp32 partials); the numerics check is on logits
+    # (test_tp2_on_one_gpu_teacher_forced_logits_match_tp1)
+    assert _common_prefix(ref2, tp1_tokens) >= 1
 
 
 def test_tp2_on_one_gpu_graph_decode_matches_tp1(tp1_tokens, monkeypatch):
@@ -137,7 +140,58 @@ def test_tp2_on_one_gpu_graph_decode_matches_tp1(tp1_tokens, monkeypatch):
     assert healthy and st["graph_replays"] > 0, st
     print("TP2 vs TP1 token agreement", _agree(out, tp1_tokens), "common prefix",
           _common_prefix(out, tp1_tokens))
-    assert _common_prefix(out, tp1_tokens) >= 4, (out, tp1_tokens)
+    assert _common_prefix(out, tp1_tokens) >= 1, (out, tp1_tokens)
+
+
+def _teacher_forced_logits(eng, seqs):
+    """Logits of one prefill step per sequence (max_tokens=1): row i predicts the token
+    after seqs[i].  Eager steps only (the runner's logits tap)."""
+    from fasttalk_llm_microservice_amd.engine.sampling_params import SamplingParams
+
+    sp = SamplingParams(temperature=0, max_tokens=1, ignore_eos=True)
+    rows = []
+    for q in seqs:
+        eng.runner.logits_tap = []
+        eng.generate([q], sp)
+        rows.append(eng.runner.logits_tap[-1][-1])
+        eng.runner.logits_tap = None
+    import torch
+
+    return torch.stack(rows)
+
+
+def test_tp2_on_one_gpu_teacher_forced_logits_match_tp1(tp1_tokens, monkeypatch):
+    """TP=2 (custom all-reduce + all-gather, both ranks on one MI355X) against TP=1 on
+    the same weights, compared where it is well defined: the logits of the same
+    inputs.  Each prompt is extended by the first k tokens of TP=1's greedy
+    continuation (teacher forcing, k = 0..5), so the prefill GEMMs, the varlen
+    attention over the paged cache and both collectives are all exercised; greedy
+    tokens alone flip at random-weight near-ties."""
+    import torch
+
+    from fasttalk_llm_microservice_amd.engine.engine import LLMEngine
+    from fasttalk_llm_microservice_amd.parallel.tp import spawn_tp_engine
+
+    monkeypatch.setenv("FT_CONSISTENT_INIT", "1")
+    monkeypatch.delenv("FT_FAULT_TP_STALL", raising=False)
+    seqs = [p + c[:k] for p, c in zip(_prompts(), tp1_tokens) for k in range(6)]
+    eng1 = LLMEngine(_cfg())
+    ref = _teacher_forced_logits(eng1, seqs)
+    del eng1
+    torch.cuda.empty_cache()
+    eng = spawn_tp_engine(_cfg(tp_size=2, tp_share_device=True, custom_allreduce=True))
+    try:
+        assert eng.runner.comm.custom is not None
+        got = _teacher_forced_logits(eng, seqs)
+        healthy = eng.runner.comm.custom.healthy()
+    finally:
+        eng.shutdown()
+    assert healthy and got.shape == ref.shape
+    cos = torch.nn.functional.cosine_similarity(got, ref, dim=-1)
+    agree = (got.argmax(-1) == ref.argmax(-1)).float().mean().item()
+    print(f"TP2 vs TP1 teacher-forced logits: min cos {cos.min().item():.6f}, argmax agree {agree:.3f}")
+    assert cos.min().item() > 0.999, cos
+    assert agree >= 0.75
 
 
 def test_tp2_allreduce_timeout_in_a_no_logits_prefill_chunk(monkeypatch):
