@@ -41,6 +41,9 @@ int ft_kv_block_copy(void* k_cache, void* v_cache, const int* src_dst, int num_p
 int ft_w4_gemm(const void* x, int x_stride, int M, const uint32_t* wq, const void* sz, int N, int K,
                float* ws, void* out, int out_stride, int splits, int nt, hipStream_t stream);
 int ft_w4_dequant(const uint32_t* wq, const void* sz, void* out, int N, int K, hipStream_t stream);
+int ft_w4_gemm_xr(const void* x, int x_stride, int M, const uint32_t* wq, const void* sz, int N, int K,
+                  float* ws, void* out, int out_stride, int splits, int nt, int silu,
+                  hipStream_t stream);
 int ft_kv_swap(const uint64_t* ptrs_dev, int ncache, const int* ids_dev, int n, void* staging,
                long block_elems, int to_staging, hipStream_t stream);
 int ft_skinny_gemm_xc(const void* x, int x_stride, int M, const void* w, int N, int K, float* ws,
@@ -371,7 +374,7 @@ void check_w4(const at::Tensor& wq, const at::Tensor& sz, int64_t N, int64_t K) 
 }
 
 void w4_gemm(at::Tensor x, at::Tensor wq, at::Tensor sz, int64_t N, c10::optional<at::Tensor> out,
-             c10::optional<at::Tensor> ws, int64_t splits, int64_t nt) {
+             c10::optional<at::Tensor> ws, int64_t splits, int64_t nt, bool xr, bool silu) {
   check_bf16(x, "x");
   check_rows(x, "x");
   const int M = (int)x.size(0), K = (int)x.size(1);
@@ -387,10 +390,20 @@ void w4_gemm(at::Tensor x, at::Tensor wq, at::Tensor sz, int64_t N, c10::optiona
     TORCH_CHECK(splits == 1, "splits > 1 needs a workspace");
     TORCH_CHECK(out.has_value(), "no workspace: needs out");
     check_bf16(*out, "out");
-    TORCH_CHECK(out->dim() == 2 && out->stride(1) == 1 && out->size(0) >= M && out->size(1) >= N,
+    TORCH_CHECK(out->dim() == 2 && out->stride(1) == 1 && out->size(0) >= M &&
+                    out->size(1) >= (silu ? N / 2 : N),
                 "out shape");
     op = out->data_ptr();
     ostride = (int)out->stride(0);
+  }
+  TORCH_CHECK(!silu || (xr && !ws.has_value()), "the SiLU epilogue is an xr bf16-output variant");
+  if (xr) {
+    check_rc(ft_w4_gemm_xr(x.data_ptr(), (int)x.stride(0), M,
+                           reinterpret_cast<const uint32_t*>(wq.data_ptr<int>()), sz.data_ptr(),
+                           (int)N, K, wsp, op, ostride, (int)splits, (int)nt, silu ? 1 : 0,
+                           cur_stream()),
+             "w4_gemm_xr");
+    return;
   }
   check_rc(ft_w4_gemm(x.data_ptr(), (int)x.stride(0), M,
                       reinterpret_cast<const uint32_t*>(wq.data_ptr<int>()), sz.data_ptr(), (int)N,
@@ -792,7 +805,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("kv_swap", &kv_swap);
   m.def("w4_gemm", &w4_gemm, py::arg("x"), py::arg("wq"), py::arg("sz"), py::arg("N"),
         py::arg("out") = py::none(), py::arg("ws") = py::none(), py::arg("splits") = 1,
-        py::arg("nt") = 1);
+        py::arg("nt") = 1, py::arg("xr") = false, py::arg("silu") = false);
   m.def("w4_dequant", &w4_dequant);
   m.def("skinny_gemm_xr", &skinny_gemm_xr, py::arg("x"), py::arg("w"), py::arg("out") = py::none(),
         py::arg("ws") = py::none(), py::arg("splits") = 1, py::arg("nt") = 2, py::arg("epi") = 0);

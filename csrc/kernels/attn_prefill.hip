@@ -149,41 +149,54 @@ __global__ __launch_bounds__(512, 1) void prefill_attn_kernel(
   const int bs_shift = __builtin_ctz(block_size);
   const int bmask = block_size - 1;
   const int nblk = (kv_end + block_size - 1) >> bs_shift;
-  // V^T staging: item = (block j of the tile, dim d, 8-token chunk cc), cc fastest,
-  // so consecutive lanes read consecutive 16 B of one transposed block
-  const int tb_shift = min(bs_shift, 6);          // log2 tokens of one block inside a tile
-  const int cpr_shift = tb_shift - 3;             // log2 16-B chunks per block row
+  const uint32_t lds0 = lds_off(smem);
   // LDS-DMA of one tile into ring slot `slot`: 16 KiB K image + 16 KiB V^T image (D
   // = 128) = 32 wave-instructions of 1 KiB, 4 per wave.  Lanes past kv_end re-read
   // a valid chunk (finite data; those keys are masked, their P is 0).
   constexpr int KI = KIMG * 2 / 1024, VI = VIMG * 2 / 1024;   // 1-KiB pieces per image
   constexpr int PER_WAVE = (KI + VI) / NW;
+  // Per-lane constants of this wave's DMA pieces, computed once (the per-tile issue
+  // used to recompute every lane's row / chunk / block lookup: ~140 VALU per tile).
+  //   K piece (TPP rows of one block: the block index is wave-uniform): lane -> row t
+  //   of the piece, LDS slot sl; source chunk = sl ^ swizzle(t)
+  //   V^T piece: lane -> dim d, LDS slot sl; source token chunk c = sl ^ swizzle(d)
+  constexpr int KR = KI / NW, VR = VI / NW;    // K / V^T pieces per wave per tile
+  static_assert(KR * NW == KI && VR * NW == VI, "pieces must split evenly over the waves");
+  constexpr int TPP = 64 / NCH;                // K rows per 1-KiB piece (4 at D = 128)
+  int k_lane[KR], v_lane[VR], v_tok[VR];
+#pragma unroll
+  for (int r = 0; r < KR; ++r) {
+    const int e = (wave + r * NW) * 64 + lane;   // 16-B element of the K image
+    const int t = e / NCH, sl = e - t * NCH;
+    k_lane[r] = (t & bmask) * D + (sl ^ (t & SWZ)) * 8;
+  }
+#pragma unroll
+  for (int r = 0; r < VR; ++r) {
+    const int e = (wave + r * NW) * 64 + lane;   // 16-B element of the V^T image
+    const int d = e >> 3, sl = e & 7;
+    v_lane[r] = d * block_size;
+    v_tok[r] = (sl ^ ((d >> 1) & 7)) << 3;
+  }
   auto issue_tile = [&](int kt, int slot) {
     const int kbase = kt * kPrefillBK;
-    uint16_t* kimg = smem + slot * SLOT;
-    uint16_t* vimg = kimg + KIMG;
-    auto blk_of = [&](int p) { return s_bt[p >> bs_shift]; };
+    const uint32_t kimg = lds0 + slot * SLOT * 2, vimg = kimg + KIMG * 2;
 #pragma unroll
-    for (int r = 0; r < PER_WAVE; ++r) {
+    for (int r = 0; r < KR; ++r) {
       const int piece = wave + r * NW;
-      const uint16_t* src;
-      uint16_t* dst;
-      if (piece < KI) {           // K rows: lane -> (row t, LDS slot) ; source chunk = slot ^ swz
-        const int e = piece * 64 + lane;             // 16-B element of the K image
-        const int t = e / NCH, sl = e - (e / NCH) * NCH;
-        const int p = min(kbase + t, kv_end - 1);
-        src = k_cache + (size_t)blk_of(p) * blk_stride + head_off +
-              (size_t)(p & bmask) * D + (sl ^ (t & SWZ)) * 8;
-        dst = kimg + piece * 512;
-      } else {                    // V^T rows: lane -> (dim d, LDS slot); source chunk = slot ^ swz
-        const int e = (piece - KI) * 64 + lane;      // 16-B element of the V^T image
-        const int d = e >> 3, sl = e & 7;
-        const int p = min(kbase + ((sl ^ ((d >> 1) & 7)) << 3), (kv_end - 1) & ~7);
-        src = v_cache + (size_t)blk_of(p) * blk_stride + head_off +
-              (size_t)d * block_size + (p & bmask);
-        dst = vimg + (piece - KI) * 512;
-      }
-      glds16(src, lds_off(dst));
+      // the piece's rows share one block; past kv_end the piece re-reads rows of the
+      // last block (finite data; those keys are masked, their P is 0)
+      const int tp = min(kbase + piece * TPP, kv_end - 1);
+      const int blk = __builtin_amdgcn_readfirstlane(s_bt[tp >> bs_shift]);
+      const uint16_t* src = k_cache + (size_t)blk * blk_stride + head_off +
+                            (size_t)(kbase & bmask) * D + k_lane[r];
+      glds16(src, kimg + piece * 1024);
+    }
+#pragma unroll
+    for (int r = 0; r < VR; ++r) {
+      const int p = min(kbase + v_tok[r], (kv_end - 1) & ~7);
+      const uint16_t* src = v_cache + (size_t)s_bt[p >> bs_shift] * blk_stride + head_off +
+                            v_lane[r] + (p & bmask);
+      glds16(src, vimg + (wave + r * NW) * 1024);
     }
   };
   uint32_t koff[KC];
@@ -341,7 +354,7 @@ __global__ __launch_bounds__(512, 1) void prefill_attn_kernel(
     else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_WAVE) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();          // every wave's pieces of tile kt have landed
-    kb = lds_off(smem) + slot * SLOT * 2;
+    kb = lds0 + slot * SLOT * 2;
     tile_math(kt);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();          // slot kt % NSLOT may be refilled

@@ -26,6 +26,8 @@
 // w4_dequant_kernel and runs the library GEMM.
 #include "ft_common.h"
 
+#include <type_traits>
+
 namespace ft {
 
 typedef __bf16 w4_bf16x8 __attribute__((ext_vector_type(8)));
@@ -178,6 +180,173 @@ __global__ __launch_bounds__(256) void w4_skinny_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// "xr" W4 variant for 17..64 rows (the batched decode steps): at 64 rows the
+// kernel above re-reads every x fragment per wave and column tile -- 16 B of x
+// per lane and k-group against 16 B of int4 weights for 16 columns, so its x
+// traffic is 16x the weight stream and the 64-row bucket ran no faster than the
+// bf16 image (gate_up 47.5 vs 44.7 us).  Here, as in skinny_gemm.hip's "xr":
+//   * the workgroup stages x for a 512-wide K chunk (4 groups) in LDS once
+//     (double-buffered, one barrier per chunk); each staging thread loads one
+//     (row, group) run of 128 k (256 B contiguous) and also writes that run's sum
+//     xs = x . 1 to LDS, so the zero-point correction needs no MFMAs with ones;
+//   * each wave streams NT column tiles; every group's weight registers are
+//     refilled with the next chunk's fragment right after use (a register ring
+//     across chunks: KS x NT x 16 B per lane in flight, no drain between chunks);
+//   * per (group, tile) the 4 MFMAs give a = x . (128 + q) and
+//     y += s * (a - (128 + z) * xs): 2 FMAs per accumulator register.
+// EPI 1: SiLU epilogue on a gate/up image interleaved in 16-row groups
+// (ops.quant.pack_w4 of interleave_gate_up(w, 1)): with NT = 2 a wave holds a gate
+// tile and its up tile and writes h = silu(g) * u (N/2 columns, bf16).
+template <int MT, int NT, int EPI>
+__global__ __launch_bounds__(256, 1) void w4_xr_kernel(
+    const uint16_t* __restrict__ x, int x_stride, int M, const uint32_t* __restrict__ wq,
+    const float2* __restrict__ sz, int K, float* __restrict__ ws, uint16_t* __restrict__ out,
+    int out_stride, int N, int k_slice) {
+  constexpr bool SILU = EPI == 1;
+  static_assert(!SILU || NT % 2 == 0, "SiLU pairs a gate tile with its up tile");
+  constexpr int KC = 512, NG = KC / 128;     // k per chunk, groups per chunk
+  constexpr int ROWS = 16 * MT;
+  constexpr int XR = 16;                      // 16-B loads per staging thread (one group)
+  __shared__ __attribute__((aligned(16))) uint16_t s_x[2][ROWS * KC];
+  __shared__ __attribute__((aligned(16))) float s_xs[2][NG][ROWS];
+  const int tid = threadIdx.x;
+  const int lane = lane_id(), wave = wave_id();
+  const int l15 = lane & 15, g = lane >> 4;
+  const int n0 = (blockIdx.x * 4 + wave) * (16 * NT);
+  const int s = blockIdx.y;
+  const int kbeg = s * k_slice;
+  const int nch = k_slice / KC;
+  const int groups_total = K >> 7;
+  const int grp0 = kbeg >> 7;
+
+  // staging thread -> (row, group) run of this chunk; threads past ROWS * NG idle
+  const bool stager = tid < ROWS * NG;
+  const int srow = tid / NG, sgrp = tid % NG;
+  const uint16_t* xsrc = x + (size_t)min(srow, M - 1) * x_stride + kbeg + sgrp * 128;
+
+  const uint32_t* wp[NT];
+  const float2* sp[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const size_t tile = (size_t)(min(n0 + 16 * j, N - 16) / 16) * groups_total + grp0;
+    wp[j] = wq + tile * 256 + lane * 4;
+    sp[j] = sz + tile * 16 + l15;
+  }
+
+  w4_floatx4 acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = w4_floatx4{0.f, 0.f, 0.f, 0.f};
+
+  w4_u32x4 xr[XR];
+  w4_u32x4 wr[NG][NT];
+  float2 szr[NG][NT];
+  auto load_x = [&](int c) {
+    if (stager) {
+#pragma unroll
+      for (int p = 0; p < XR; ++p) xr[p] = *reinterpret_cast<const w4_u32x4*>(xsrc + (size_t)c * KC + p * 8);
+    }
+  };
+  auto load_w = [&](int c, int gq) {
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      wr[gq][j] = __builtin_nontemporal_load(reinterpret_cast<const w4_u32x4*>(wp[j] + (size_t)(c * NG + gq) * 256));
+      szr[gq][j] = sp[j][(size_t)(c * NG + gq) * 16];
+    }
+  };
+  load_x(0);
+#pragma unroll
+  for (int gq = 0; gq < NG; ++gq) load_w(0, gq);
+
+  auto chunk = [&](int c, auto more_tag) {
+    constexpr bool MORE = decltype(more_tag)::value;
+    uint16_t* sx = s_x[c & 1];
+    if (stager) {
+      // the run's 16 chunks -> LDS (16-B chunk swizzle as in skinny_gemm.hip), and its sum
+      float sum = 0.f;
+#pragma unroll
+      for (int p = 0; p < XR; ++p) {
+        const int ch = sgrp * 16 + p;
+        const int slot = (ch & ~7) | ((ch & 7) ^ (srow & 7));
+        *reinterpret_cast<w4_u32x4*>(&sx[srow * KC + slot * 8]) = xr[p];
+        float f[8];
+        load8(__builtin_bit_cast(uint4, xr[p]), f);
+        sum += ((f[0] + f[1]) + (f[2] + f[3])) + ((f[4] + f[5]) + (f[6] + f[7]));
+      }
+      s_xs[c & 1][sgrp][srow] = sum;
+    }
+    if constexpr (MORE) load_x(c + 1);
+    __syncthreads();   // chunk c visible; every wave is past chunk c-1's reads of the other buffer
+#pragma unroll
+    for (int gq = 0; gq < NG; ++gq) {
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        const int row = 16 * i + l15;
+        w4_u32x4 xf[4];
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+          const int ch = gq * 16 + 8 * (h >> 1) + 2 * g + (h & 1);
+          const int slot = (ch & ~7) | ((ch & 7) ^ (row & 7));
+          xf[h] = *reinterpret_cast<const w4_u32x4*>(&sx[row * KC + slot * 8]);
+        }
+        const float4 xs4 = *reinterpret_cast<const float4*>(&s_xs[c & 1][gq][16 * i + 4 * g]);
+        const float xs[4] = {xs4.x, xs4.y, xs4.z, xs4.w};
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          w4_floatx4 a = w4_floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int h = 0; h < 4; ++h)
+            a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(w4_bf16x8, xf[h]),
+                                                        w4_frag(wr[gq][j][h]), a, 0, 0, 0);
+          const float sc = szr[gq][j].x, zz = szr[gq][j].y;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[i][j][r] = fmaf(sc, fmaf(-zz, xs[r], a[r]), acc[i][j][r]);
+        }
+      }
+      if constexpr (MORE) load_w(c + 1, gq);   // refill this group's registers
+    }
+  };
+  for (int c = 0; c + 1 < nch; ++c) chunk(c, std::true_type{});
+  chunk(nch - 1, std::false_type{});
+  if (n0 >= N) return;
+  if constexpr (SILU) {
+#pragma unroll
+    for (int j = 0; j < NT; j += 2) {
+      const int col = ((n0 + 16 * j) >> 1) + l15;   // (gate tile, up tile) -> 16 h columns
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = 16 * i + g * 4 + r;
+          if (m < M) {
+            const float gt = acc[i][j][r], up = acc[i][j + 1][r];
+            out[(size_t)m * out_stride + col] = f32_to_bf16(gt / (1.f + __expf(-gt)) * up);
+          }
+        }
+    }
+    return;
+  }
+  float* slab = ws + (size_t)s * M * N;
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = 16 * i + g * 4 + r;
+      if (m < M) {
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          const int n = n0 + 16 * j + l15;
+          if (ws == nullptr)
+            out[(size_t)m * out_stride + n] = f32_to_bf16(acc[i][j][r]);
+          else
+            slab[(size_t)m * N + n] = acc[i][j][r];
+        }
+      }
+    }
+}
+
 // packed image -> bf16 [N, K] row-major (prefill path and tests).  One thread
 // per (tile, group, lane): 32 weights = 4 runs of 8 consecutive k.
 __global__ __launch_bounds__(256) void w4_dequant_kernel(const uint32_t* __restrict__ wq,
@@ -237,6 +406,38 @@ extern "C" int ft_w4_gemm(const void* x, int x_stride, int M, const uint32_t* wq
   FT_W4_NT(4)
 #undef FT_W4_NT
 #undef FT_W4
+  return -5;
+}
+
+// "xr" variant (17..64 rows): N % (64 * nt) == 0, K % (512 * splits) == 0; silu: nt even,
+// out [M, N/2]; splits > 1 needs ws (slab output), silu needs splits == 1.
+extern "C" int ft_w4_gemm_xr(const void* x, int x_stride, int M, const uint32_t* wq, const void* sz,
+                             int N, int K, float* ws, void* out, int out_stride, int splits, int nt,
+                             int silu, hipStream_t stream) {
+  if (M <= 0) return 0;
+  if (M > 64 || splits < 1) return -1;
+  if (N % (64 * nt) != 0) return -2;
+  if (K % (512 * splits) != 0) return -3;
+  if (splits > 1 && (ws == nullptr || silu)) return -4;
+  if (ws == nullptr && out == nullptr) return -6;
+  if (silu && nt % 2) return -7;
+  const int mt = (M + 15) / 16;
+  dim3 grid(N / (64 * nt), splits), block(256);
+  const int k_slice = K / splits;
+#define FT_W4X(MT_, NT_, E_)                                                                 \
+  if (mt == MT_ && nt == NT_ && silu == E_) {                                                \
+    hipLaunchKernelGGL((ft::w4_xr_kernel<MT_, NT_, E_>), grid, block, 0, stream,             \
+                       (const uint16_t*)x, x_stride, M, wq, (const float2*)sz, K, ws,        \
+                       (uint16_t*)out, out_stride, N, k_slice);                              \
+    return static_cast<int>(hipGetLastError());                                              \
+  }
+#define FT_W4X_M(NT_, E_) FT_W4X(2, NT_, E_) FT_W4X(3, NT_, E_) FT_W4X(4, NT_, E_)
+  FT_W4X_M(1, 0)
+  FT_W4X_M(2, 0)
+  FT_W4X_M(4, 0)
+  FT_W4X_M(2, 1)
+#undef FT_W4X_M
+#undef FT_W4X
   return -5;
 }
 

@@ -252,21 +252,27 @@ def _fold_norm(w: torch.Tensor, ln: torch.Tensor) -> torch.Tensor:
     """W diag(ln): the RMSNorm weight moved onto the GEMM's K axis."""
     return (w.float() * ln.float()[None, :]).to(w.dtype)
 
-# W4A16 decode GEMMs (csrc/kernels/w4a16.hip): (nt, splits) per projection and
-# row bucket, from cold-cache sweeps on MI355X (bench/w4_sweep.py, us at M = 1 /
-# 8 / 16 / 32 / 64; bf16 packed plan in brackets):
-#   qkv   5.7 / 6.0 / 6.5 / 9.2 / 16.3   [9.8 / 10.3 / 11.1 / hipBLASLt]
-#   o     4.4 / 4.7 / 5.1 / 7.2 / 12.1   [7.3 / 7.5 / 7.7 / 9.0 / 13.1]
-#   gu    15.2 / 14.9 / 16.7 / 26.8 / 47.5  [35 / 38 / 41 / 45 / hipBLASLt 55-66]
-#   down  9.2 / 8.5 / 9.1 / 12.9 / 22.7  [18.6 / 19.3 / 20 / 22 / 28]
+# W4A16 decode GEMMs (csrc/kernels/w4a16.hip): (nt, splits, xr) per projection and
+# row bucket.  <= 16 rows: the register kernel, from cold-cache sweeps on MI355X
+# (bench/w4_sweep.py, us at M = 1 / 8 / 16; bf16 packed plan in brackets):
+#   qkv   5.7 / 6.0 / 6.5   [9.8 / 10.3 / 11.1]
+#   o     4.4 / 4.7 / 5.1   [7.3 / 7.5 / 7.7]
+#   gu    15.2 / 14.9 / 16.7  [35 / 38 / 41]
+#   down  9.2 / 8.5 / 9.1   [18.6 / 19.3 / 20]
+# 17..64 rows: the x-in-LDS "xr" variant where it wins (bench/w4xr_sweep.py, us at
+# M = 50 / 64, profiles/w4xr_sweep_r03.log): qkv 13.9 / 15.0 (register kernel 14.2 /
+# 15.6), o 9.3 / 9.8 (10.8 / 11.7), gate_up with the SiLU epilogue on its interleaved
+# image 40.1 / 41.2 (41.0 / 45.6 + silu_mul); down stays on the register kernel (20.1
+# / 21.8 vs 23.4 / 24.3).  At 64 rows W4 is MFMA + dequant bound (the same MFMA work
+# as bf16 on a quarter of the bytes): 83 vs 95 us per layer for the bf16 image.
 # qkv, o and down leave split-K slabs: qkv's are reduced by the RoPE + KV-write
 # kernel (slab_rope_kv), o's and down's by the fused add+RMSNorm.
 W4_ROWS = 64
 W4_PLAN = {
-    "qkv": {1: (2, 8), 8: (4, 2), 16: (4, 2), 32: (4, 2), 64: (4, 2)},
-    "o": {1: (2, 8), 8: (2, 8), 16: (4, 8), 32: (4, 4), 64: (4, 4)},
-    "gu": {1: (4, 1), 8: (4, 1), 16: (4, 1), 32: (4, 1), 64: (4, 1)},
-    "down": {1: (4, 4), 8: (4, 4), 16: (4, 4), 32: (4, 4), 64: (4, 4)},
+    "qkv": {1: (2, 8, 0), 8: (4, 2, 0), 16: (4, 2, 0), 32: (2, 4, 1), 64: (2, 4, 1)},
+    "o": {1: (2, 8, 0), 8: (2, 8, 0), 16: (4, 8, 0), 32: (2, 8, 1), 64: (2, 8, 1)},
+    "gu": {1: (4, 1, 0), 8: (4, 1, 0), 16: (4, 1, 0), 32: (2, 1, 1), 64: (2, 1, 1)},
+    "down": {1: (4, 4, 0), 8: (4, 4, 0), 16: (4, 4, 0), 32: (4, 4, 0), 64: (4, 4, 0)},
 }
 
 
@@ -322,6 +328,7 @@ class LlamaModel:
         if self.quant not in (None, "awq", "w4"):
             raise ValueError(f"unsupported quantization {quantization!r} (awq | w4)")
         self._w4_scratch: Optional[torch.Tensor] = None
+        self.w4_gu_il = False     # W4 gate_up image interleaved in 16-row groups
         self.fused = False
         self.gu_nt = 2
         self.gu_il = False        # gate_up image interleaved in groups of 16 (packed bf16)
@@ -413,6 +420,13 @@ class LlamaModel:
         if self.device.type == "cuda":
             if L.q4 is None:
                 L.q4 = {}
+            if proj == "gu" and q.shape[0] % 32 == 0:
+                # gate/up rows interleaved in 16-row groups (quantization is per row, so
+                # the permutation commutes with it): the W4 xr kernel's SiLU epilogue
+                # pairs a gate tile with its up tile; every other path un-interleaves
+                # through silu_mul(interleaved=True)
+                q, z, s = (ops.interleave_gate_up(t, 1) for t in (q, z, s))
+                self.w4_gu_il = True
             L.q4[proj] = Q.pack_w4(q.to(self.device), z.to(self.device), s.to(self.device))
             setattr(L, _ATTR[proj], None)
         else:  # CPU reference backend: the dequantized weight
@@ -502,11 +516,11 @@ class LlamaModel:
             q = L0.q4.get(proj) if L0.q4 else None
             if q is None:
                 continue
-            sp_max = max(sp for _, sp in W4_PLAN[proj].values())
-            self.w4_slab[proj] = slab_w4 and q.k % (128 * sp_max) == 0 and \
-                all(q.n % (16 * nt) == 0 for nt, _ in W4_PLAN[proj].values())
+            self.w4_slab[proj] = slab_w4 and all(
+                q.k % ((512 if xr else 128) * sp) == 0 and q.n % ((64 if xr else 16) * nt) == 0
+                for nt, sp, xr in W4_PLAN[proj].values())
             if self.w4_slab[proj]:
-                need = max(need, max(sp * b * q.n for b, (_, sp) in W4_PLAN[proj].items()))
+                need = max(need, max(sp * b * q.n for b, (_, sp, _) in W4_PLAN[proj].items()))
         self.ws = torch.empty(need, dtype=torch.float32, device=self.device)
         # in-launch split-K tickets (fused ring layer): zeroed,
         # every launch leaves them zeroed
@@ -604,15 +618,20 @@ class LlamaModel:
         rows = x.shape[0]
         q = L.q4.get(proj) if L.q4 else None
         if q is not None:  # W4A16
-            if self.ws is not None and rows <= W4_ROWS and self.w4_slab.get(proj):
-                nt, sp = w4_cfg(proj, rows)
-                Q.w4_gemm(x, q, ws=self.ws, splits=sp, nt=nt)
-                return sp, None
+            il = proj == "gu" and self.w4_gu_il
             if rows <= W4_ROWS:
-                y = Q.w4_gemm(x, q, nt=w4_cfg(proj, rows)[0])
+                nt, sp, xr = w4_cfg(proj, rows)
+                if xr and (q.n % (64 * nt) or q.k % (512 * sp)):
+                    nt, sp, xr = 1, 1, 0          # shape the xr tiles do not cover (TP shards)
+                if il and xr and nt == 2 and sp == 1 and q.n % 128 == 0:
+                    return 0, Q.w4_gemm(x, q, nt=2, xr=True, silu=True)
+                if self.ws is not None and self.w4_slab.get(proj):
+                    Q.w4_gemm(x, q, ws=self.ws, splits=sp, nt=nt, xr=bool(xr))
+                    return sp, None
+                y = Q.w4_gemm(x, q, nt=nt, xr=bool(xr))
             else:
                 y = F.linear(x, self._w4_dense(q))
-            return 0, (ops.silu_mul(y) if proj == "gu" else y)
+            return 0, (ops.silu_mul(y, interleaved=il) if proj == "gu" else y)
         attr = _ATTR[proj]
         wp = getattr(L, attr + "_pk")
         if wp is None:  # row-major weights: CPU backend, or FT_PACKED_GEMM=0

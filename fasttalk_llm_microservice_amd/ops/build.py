@@ -100,6 +100,8 @@ def _compile(src: Path, obj: Path, cmd: list, deps: list, force: bool) -> bool:
 KERNEL_FLAGS = {
     "attn_decode": ["-mllvm", "-amdgpu-mfma-vgpr-form=1", "-fno-honor-nans"],
     "attn_prefill": ["-mllvm", "-amdgpu-mfma-vgpr-form=1", "-fno-honor-nans"],
+    # W4: the per-group scale / zero correction reads every MFMA result on the VALU
+    "w4a16": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"],
 }
 
 

@@ -150,14 +150,21 @@ def w4_dequant(w: W4Weight, out: Optional[torch.Tensor] = None,
     return r
 
 
-def w4_gemm(x: torch.Tensor, w: W4Weight, out=None, ws=None, splits: int = 1, nt: int = 1):
+def w4_gemm(x: torch.Tensor, w: W4Weight, out=None, ws=None, splits: int = 1, nt: int = 1,
+            xr: bool = False, silu: bool = False):
     """y = x dequant(w)^T for M <= 64 rows.  With ``ws`` the kernel leaves fp32
-    slabs ([splits, M, N]) for a fused epilogue; otherwise returns bf16 ``out``."""
+    slabs ([splits, M, N]) for a fused epilogue; otherwise returns bf16 ``out``.
+    ``xr``: the x-in-LDS variant (17..64 rows); ``silu``: its SiLU epilogue on a
+    gate/up image interleaved in 16-row groups (returns h = silu(gate) * up)."""
     if not x.is_cuda:
-        return x @ w4_dequant(w, dtype=x.dtype).t()
+        y = x @ w4_dequant(w, dtype=x.dtype).t()
+        if silu:
+            g, u = y.view(y.shape[0], -1, 2, 16).unbind(2)
+            y = (torch.nn.functional.silu(g.float()) * u.float()).to(x.dtype).reshape(y.shape[0], -1)
+        return y
     from . import native
 
     if ws is None and out is None:
-        out = torch.empty(x.shape[0], w.n, dtype=x.dtype, device=x.device)
-    native().w4_gemm(x, w.wq, w.sz, w.n, out, ws, splits, nt)
+        out = torch.empty(x.shape[0], w.n // 2 if silu else w.n, dtype=x.dtype, device=x.device)
+    native().w4_gemm(x, w.wq, w.sz, w.n, out, ws, splits, nt, xr, silu)
     return out if ws is None else ws

@@ -466,6 +466,47 @@ def test_w4_gemm_matches_fp32(m, n, k, nt, splits):
     assert (y - ref_y).abs().max().item() < 1e-3 * ref_y.abs().max().item() + 1e-3
 
 
+@pytest.mark.parametrize("m", [17, 33, 50, 64])
+@pytest.mark.parametrize("n,k,nt,splits", [(1024, 4096, 1, 1), (2048, 4096, 2, 2), (2048, 4096, 4, 1),
+                                           (1024, 14336, 1, 4), (2048, 14336, 2, 7)])
+def test_w4_xr_gemm_matches_fp32(m, n, k, nt, splits):
+    """The x-in-LDS W4A16 variant (17..64 rows): bf16 out and split-K fp32 slabs."""
+    Q, W, ref_w = _w4(n, k, seed=m + 1)
+    x = torch.randn(m, k, generator=torch.Generator().manual_seed(9)).bfloat16()
+    ref_y = x.float() @ ref_w.t()
+    xd = x.to(DEV)
+    if splits == 1:
+        y = Q.w4_gemm(xd, W, nt=nt, xr=True).float().cpu()
+        assert (y - ref_y).abs().max().item() < 2e-2 * ref_y.abs().max().item() + 1e-2
+    ws = torch.full((splits * m * n,), float("nan"), device=DEV)
+    Q.w4_gemm(xd, W, ws=ws, splits=splits, nt=nt, xr=True)
+    y = ws.view(splits, m, n).sum(0).cpu()
+    assert (y - ref_y).abs().max().item() < 1e-3 * ref_y.abs().max().item() + 1e-3
+
+
+@pytest.mark.parametrize("m", [20, 64])
+def test_w4_xr_silu_epilogue(m):
+    """gate_up quantized with its rows interleaved in 16-row groups: the W4 xr
+    kernel's SiLU epilogue returns h = silu(gate) * up."""
+    from fasttalk_llm_microservice_amd import ops as O
+    from fasttalk_llm_microservice_amd.ops import quant as Q
+
+    inter, k = 1024, 4096
+    g = torch.Generator().manual_seed(m)
+    w = torch.randn(2 * inter, k, generator=g) * 0.05
+    wi = O.interleave_gate_up(w, 1)
+    q, z, s = Q.quantize_w4(wi)
+    W = Q.pack_w4(q.to(DEV), z.to(DEV), s.to(DEV))
+    wdq = Q.dequantize_w4(q, z, s)
+    x = torch.randn(m, k, generator=torch.Generator().manual_seed(3)).bfloat16()
+    y = x.float() @ wdq.t()
+    gt, up = y.view(m, -1, 2, 16).unbind(2)
+    ref = (torch.nn.functional.silu(gt) * up).reshape(m, inter)
+    h = Q.w4_gemm(x.to(DEV), W, nt=2, xr=True, silu=True).float().cpu()
+    assert h.shape == (m, inter)
+    assert (h - ref).abs().max().item() < 2e-2 * ref.abs().max().item() + 1e-2
+
+
 # ----------------------------------------------------------------------------------
 # decode-shape skinny GEMM + fused row epilogues
 # ----------------------------------------------------------------------------------
