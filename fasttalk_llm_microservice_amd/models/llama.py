@@ -124,6 +124,7 @@ PACKED_PLAN = {
 }
 MAX_SPLITS = 4
 
+
 # Above PACKED_ROWS rows: packed_gemm.hip on the same image, (row limit, tile cfg,
 # split-K) per projection from bench/pg_probe.py on MI355X vs hipBLASLt on row-major
 # weights (profiles/packed_gemm_*_r02.log): split-K fills the chip at mixed-step
