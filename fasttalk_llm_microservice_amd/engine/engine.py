@@ -36,6 +36,18 @@ class EngineError(RuntimeError):
     pass
 
 
+class _Inflight:
+    """A queued (launched, not yet collected) step: its batch, the runner's handle,
+    whether it is a mixed (prefill) step, and when the host launched it."""
+    __slots__ = ("batch", "handle", "mixed", "t_launch")
+
+    def __init__(self, batch: ScheduledBatch, handle, mixed: bool):
+        self.batch = batch
+        self.handle = handle
+        self.mixed = mixed
+        self.t_launch = 0.0
+
+
 class LLMEngine:
     def __init__(self, cfg: EngineConfig, comm: TPComm = SINGLE, runner=None):
         self.cfg = cfg
@@ -79,8 +91,26 @@ class LLMEngine:
         self.host_prof = collections.Counter()
         # queued decode steps, oldest first: [(batch, DecodeHandle)], at most
         # cfg.pipeline_depth + 1 of them (ENGINE_PIPELINE_DEPTH)
-        self._inflight: List = []
+        self._inflight: List[_Inflight] = []
         self.pipeline_depth = max(1, int(getattr(cfg, "pipeline_depth", 1)))
+        # ENGINE_MIXED_AHEAD (default on): waiting prompts are scheduled into a mixed
+        # step queued behind the running decode step instead of draining the queue.
+        # ENGINE_JIT_TOPUP (default on): the queue is topped up only when the running
+        # step is about to finish (ENGINE_JIT_MARGIN_MS before its expected end), with
+        # new requests handled meanwhile (``poll_hook``, set by AsyncEngine)
+        self.mixed_ahead = os.environ.get("ENGINE_MIXED_AHEAD", "1") != "0"
+        self.jit_topup = os.environ.get("ENGINE_JIT_TOPUP", "1") != "0"
+        self.jit_margin = float(os.environ.get("ENGINE_JIT_MARGIN_MS", "1.5")) / 1e3
+        self.poll_hook = None
+        self._ema_step = 0.0
+        self._t_prev_done = 0.0
+        # ENGINE_PIPELINE_SHRINK=1: a stop shrinks the queued steps instead of draining
+        # them.  Off by default: in the voice-agent loop the session's next prompt
+        # follows its stop within a step, and a drained queue lets it start one step
+        # sooner (driver config, same box: p50 TTFT 36-41 ms drained vs 50-51 ms shrunk
+        # at equal tok/s, profiles/ab_pipeline_shrink_r03.log).  Workloads with think
+        # time between turns keep the GPU busy with it on.
+        self.pipeline_shrink = os.environ.get("ENGINE_PIPELINE_SHRINK", "1" if self.jit_topup else "0") == "1"
         self._last_complete = 0.0
         from .debug import FaultInjector, StepProfiler
 
@@ -156,52 +186,164 @@ class LLMEngine:
                 and self.runner.can_pipeline(len(batch.decode_seqs))
                 and all(s.grammar is None for s in batch.decode_seqs))
 
+    def _launch_decode(self, seqs, from_device: bool, rowmap=None):
+        """Queues a graph-replayed decode step.  Positions come from each sequence's
+        ``inflight`` count (steps queued ahead of it); with ``from_device`` the
+        input ids are the previous queued step's sampled rows (``rowmap``: the row
+        of that step each sequence sat in; None = the same rows)."""
+        if rowmap is None:
+            h = self.runner.decode_launch(seqs, ahead=int(from_device))
+        else:
+            h = self.runner.decode_launch(seqs, ahead=1, rowmap=rowmap)
+        for q in seqs:
+            q.inflight += 1
+        return _Inflight(ScheduledBatch(list(seqs), [], [], []), h, False)
+
     def _speculate(self, batch: ScheduledBatch, ahead: int):
-        """Queue a step ``ahead`` steps after the collected state for the same
-        sequences (same rows), assuming none of them stops.  Rows of sequences that
-        do stop are discarded; their extra KV writes land in blocks beyond the
-        sequence's end, which are not in the prefix cache."""
+        """Queue the step after the queued ones, assuming none of their sequences
+        stops.  Rows of sequences that do stop are discarded; their extra KV writes
+        land in blocks beyond the sequence's end, which are not in the prefix cache
+        (a freed block that is re-allocated meanwhile is written by its new owner
+        later in stream order).
+
+        * New prompts waiting: a MIXED step (ahead-of-time prefill injection,
+          :meth:`_speculate_mixed`) is queued behind the running decode step, its
+          decode rows' ids gathered on the device, instead of draining the queue
+          and leaving the GPU idle while the host schedules and builds the step.
+        * A sequence known to have finished: with ``pipeline_shrink`` the queued
+          step drops its row and gathers the survivors' ids by row map; otherwise
+          the queue drains (the session's next prompt usually follows within a
+          step and then starts sooner)."""
         sched = self.scheduler
-        seqs = batch.decode_seqs
-        # new prompts end the pipeline; so does a background warm-up, unless the batch
-        # is full (it could not join a step anyway)
+        last = self._inflight[-1].batch.sampled_seqs()
+        # a background warm-up ends the pipeline unless the batch is full (it could
+        # not join a step anyway)
         warm = bool(sched.background) and len(sched.running) < sched.max_num_seqs
-        if sched.waiting or warm or any(s.status == SeqStatus.FINISHED for s in seqs):
-            return None
-        need = 0
-        for s in seqs:
-            if s.n_tokens + ahead >= self.max_model_len:
+        if sched.waiting or warm:
+            return self._speculate_mixed(last) if self.mixed_ahead else None
+        seqs = [q for q in last if q.status != SeqStatus.FINISHED]
+        rowmap = None
+        if len(seqs) != len(last):
+            if not self.pipeline_shrink or not seqs or not self.runner.can_pipeline(len(seqs)):
                 return None
-            need += sched._blocks_needed(s, s.n_tokens + ahead)
-        if need and not self.bm.can_allocate(need):
+            rowmap = [i for i, q in enumerate(last) if q.status != SeqStatus.FINISHED]
+        if not self.runner.can_pipeline(len(seqs)) or any(q.grammar is not None for q in seqs):
             return None
-        for s in seqs:
-            k = sched._blocks_needed(s, s.n_tokens + ahead)
+        if not self._grow_for_next(seqs):
+            return None
+        if rowmap is not None:
+            self.stats["pipeline_shrinks"] += 1
+        return self._launch_decode(seqs, True, rowmap)
+
+    def _grow_for_next(self, seqs) -> bool:
+        """KV blocks for one more token past everything queued (no preemption: a
+        sequence that cannot grow ends the pipeline and the scheduler decides)."""
+        sched = self.scheduler
+        need = 0
+        for q in seqs:
+            if q.n_tokens + q.inflight >= self.max_model_len:
+                return False
+            need += sched._blocks_needed(q, q.n_tokens + q.inflight)
+        if need and not self.bm.can_allocate(need):
+            return False
+        for q in seqs:
+            k = sched._blocks_needed(q, q.n_tokens + q.inflight)
             if k:
-                s.block_ids.extend(self.bm.allocate(k))
-        return self.runner.decode_launch(seqs, ahead=ahead)
+                q.block_ids.extend(self.bm.allocate(k))
+        return True
+
+    def _speculate_mixed(self, last):
+        """Schedules the waiting prompts into a mixed step queued behind the running
+        decode step: decode rows = the running sequences (each a row of the last
+        queued step, ids gathered from its sampled rows on the device), prefill
+        rows as the scheduler picks them.  At most one mixed step is in flight
+        (a prompt's next chunk needs the previous chunk's post-step state), and
+        only for grammar-free, single-process (no TP broadcast) engines."""
+        sched = self.scheduler
+        if any(e.mixed for e in self._inflight) or sched.swapped:
+            return None
+        if not hasattr(self.runner, "mixed_launch") or getattr(self.runner, "bcast", None) is not None:
+            return None
+        if any(q.grammar is not None or q.lazy or q.jf_ids for q in sched.waiting) or \
+                any(q.grammar is not None for q in sched.background):
+            return None
+        running = list(sched.running)
+        if not running:   # nothing to overlap: the drained path schedules it
+            return None
+        pos = {id(q): i for i, q in enumerate(last)}
+        if any(id(q) not in pos or q.grammar is not None for q in running):
+            return None
+        if not self._grow_for_next(running):
+            return None
+        pseqs, ptok, psamp, rejected = sched._schedule_prefill(sched.max_tokens - len(running),
+                                                               len(running))
+        for q in rejected:   # only background warm-ups are dropped while sequences run
+            sched.by_id.pop(q.request_id, None)
+            self._finalize(q, "abort", emit=False)
+        if not pseqs:
+            return None
+        mb = ScheduledBatch(running, pseqs, ptok, psamp)
+        h = self.runner.mixed_launch(mb, [pos[id(q)] for q in running])
+        for q in mb.sampled_seqs():
+            q.inflight += 1
+        self.stats["mixed_ahead"] += 1
+        return _Inflight(mb, h, True)
+
+    def _jit_wait(self, e: "_Inflight"):
+        """Delays the queue top-up until the running step is about to finish (its
+        start + the mean step time - ``jit_margin``), handling new requests
+        meanwhile: a prompt that arrives during the step is then scheduled into
+        the very next step instead of behind one more queued decode step."""
+        est = max(e.t_launch, self._t_prev_done) + self._ema_step - self.jit_margin
+        poll = self.poll_hook
+        while time.perf_counter() < est:
+            if poll is not None:
+                poll()
+            # no early return on a new prompt: the mixed step could not start before
+            # the running step ends anyway, and the prompts arriving meanwhile join it
+            # (returning at the first prompt gave mixed steps of fewer prompts and
+            # p50 TTFT 43-44 vs 35-39 ms, profiles/ab_mixed_ahead_r03.log)
+            if self.runner.step_done(e.handle):
+                return
+            time.sleep(0.0002)
 
     def _step_pipelined(self) -> List[RequestOutput]:
-        batch, handle = self._inflight[0]
+        e = self._inflight[0]
+        batch, handle = e.batch, e.handle
         t0 = time.perf_counter()
+        if self.jit_topup and not e.mixed and len(self._inflight) == 1 and self._ema_step > 0:
+            self._jit_wait(e)
         # top the queue up to depth + 1 steps before waiting on the oldest
         while len(self._inflight) <= self.pipeline_depth:
             nxt = self._speculate(batch, len(self._inflight))
             if nxt is None:
                 break
-            self._inflight.append((ScheduledBatch(list(batch.decode_seqs), [], [], []), nxt))
+            nxt.t_launch = time.perf_counter()
+            self._inflight.append(nxt)
         tl = time.perf_counter()
-        toks = self.runner.decode_collect(handle)
+        toks = self.runner.mixed_collect(handle) if e.mixed else self.runner.decode_collect(handle)
         t1 = time.perf_counter()
+        if not e.mixed:   # GPU time of a decode step ~ completion - max(launch, previous completion)
+            d = t1 - max(e.t_launch, self._t_prev_done)
+            self._ema_step = d if self._ema_step <= 0 else 0.8 * self._ema_step + 0.2 * d
+        self._t_prev_done = t1
         self._inflight.pop(0)
-        outs = self._complete(batch, batch.decode_seqs, toks)
+        sampled = batch.sampled_seqs()
+        for q in sampled:
+            q.inflight -= 1
+        outs = self._complete(batch, sampled, toks)
         t2 = time.perf_counter()
         dt = t2 - self._last_complete if self._last_complete else t2 - t0
         self._last_complete = t2
-        self.step_times.append((False, len(batch.decode_seqs), len(batch.decode_seqs), dt))
-        self.stats["decode_ms_sum"] += 1e3 * dt
+        self.step_times.append((batch.has_prefill, len(batch.decode_seqs), batch.total_tokens, dt))
         if self._trace_path:
-            self._trace.append(("decode_p", t0, t2, len(batch.decode_seqs), 0, 0))
+            self._trace.append(("mixed_p" if e.mixed else "decode_p", t0, t2, len(batch.decode_seqs),
+                                sum(batch.prefill_tokens), len(batch.prefill_seqs)))
+        if e.mixed:
+            self.stats["mixed_steps"] += 1
+            self.stats["prefill_tokens"] += sum(batch.prefill_tokens)
+            return outs
+        self.stats["decode_ms_sum"] += 1e3 * dt
         self.stats["decode_steps"] += 1
         self.stats["pipelined_steps"] += 1
         hp = self.host_prof
@@ -231,7 +373,10 @@ class LLMEngine:
             self._profiler.after_step()
 
     def reset_inflight(self):
-        """Forget the queued decode steps (after a failed step)."""
+        """Forget the queued steps (after a failed step)."""
+        for e in self._inflight:
+            for q in e.batch.sampled_seqs():
+                q.inflight = 0
         self._inflight = []
 
     def fail_unfinished(self, error: str, reset_cache: bool = False):
@@ -273,7 +418,9 @@ class LLMEngine:
         if not batch.decode_seqs and not batch.prefill_seqs:
             return outs
         if not outs and self._pipeline_ok(batch):
-            self._inflight = [(batch, self.runner.decode_launch(batch.decode_seqs))]
+            e = self._launch_decode(batch.decode_seqs, False)
+            e.t_launch = time.perf_counter()
+            self._inflight = [e]
             return self._step_pipelined()
         sampled_seqs = batch.sampled_seqs()
         masks = self._masks_for(sampled_seqs)
@@ -614,16 +761,23 @@ class AsyncEngine:
             if q is not None:
                 q.put_nowait(o)
 
+    def _poll_cmds(self):
+        while True:
+            try:
+                cmd = self._cmds.get_nowait()
+            except queue.Empty:
+                return
+            self._handle(cmd)
+
     def _run(self):
         eng = self.engine
+        if hasattr(eng, "poll_hook"):
+            # requests that arrive while a queued step runs are admitted before the
+            # queue is topped up (LLMEngine._jit_wait)
+            eng.poll_hook = self._poll_cmds
         while not self._stop:
             self.heartbeat = time.time()
-            while True:
-                try:
-                    cmd = self._cmds.get_nowait()
-                except queue.Empty:
-                    break
-                self._handle(cmd)
+            self._poll_cmds()
             if not eng.has_work():
                 self._flush()
                 self._wake.wait(0.05)

@@ -118,12 +118,24 @@ class _Staging:
         self.h_small, self.h_f32, self.h_seeds, self.h_bt = _input_views(self.h_in, mb, max_blocks)
         self.h_out = torch.zeros(mb, dtype=i32, pin_memory=pin)
         self.h_err = torch.zeros(1, dtype=i32, pin_memory=pin)  # TP collective error flag
+        self.h_map = torch.zeros(mb, dtype=torch.int64, pin_memory=pin)  # pipelined row gather
         self.err_armed = False
         self.hs = self.h_small.numpy()
         self.hbt = self.h_bt.numpy()
         self.hf = self.h_f32.numpy()
         self.hseed = self.h_seeds.numpy()
         self.event = torch.cuda.Event() if gpu else None
+
+
+class MixedHandle:
+    """A queued mixed step's sampled ids (pinned host copy) and completion event;
+    two alternate (at most one mixed step is queued at a time)."""
+    __slots__ = ("host", "event", "n")
+
+    def __init__(self, rows: int, pin: bool, gpu: bool):
+        self.host = torch.zeros(rows, dtype=torch.int32, pin_memory=pin)
+        self.event = torch.cuda.Event() if gpu else None
+        self.n = 0
 
 
 class DecodeHandle:
@@ -202,10 +214,13 @@ class ModelRunner:
         self.d_temp = self.d_f32[0:mb]
         self.d_top_p = self.d_f32[mb:2 * mb]
         self.d_out = torch.zeros(mb, dtype=i32, device=dv)
+        self.d_map = torch.zeros(mb, dtype=torch.int64, device=dv)
         # pinned staging sets: while decode step n runs, steps n+1 .. n+depth are
         # filled and queued behind it from the other sets (pipelined decode)
         nstg = max(2, int(getattr(cfg, "pipeline_depth", 1)) + 1)
         self.stg = [_Staging(mb, self.max_blocks_per_seq, pin, self.is_gpu) for _ in range(nstg)]
+        self._mx_handles = [MixedHandle(mb, pin, self.is_gpu) for _ in range(2)]
+        self._mx_next = 0
         self._stg_next = 0
         self._upload = _Uploader(dv, pin) if self.is_gpu else None
         self.h_out = torch.zeros(mb, dtype=i32, pin_memory=pin)  # eager-step sampler output
@@ -353,7 +368,7 @@ class ModelRunner:
             return []
         return self._decode(batch, masks)
 
-    def _sampling_arrays(self, seqs, ahead: int = 0):
+    def _sampling_arrays(self, seqs):
         n = len(seqs)
         temp = np.empty(n, np.float32)
         topp = np.empty(n, np.float32)
@@ -366,7 +381,7 @@ class ModelRunner:
             topp[i] = p.top_p
             topk[i] = p.top_k
             seeds[i] = p.seed
-            steps[i] = s.num_output + ahead + 131 * s.preemptions
+            steps[i] = s.num_output + s.inflight + 131 * s.preemptions
         return temp, topp, topk, seeds, steps
 
     def _mixed(self, batch: ScheduledBatch, masks) -> List[int]:
@@ -393,7 +408,7 @@ class ModelRunner:
             d_slot = np.empty(nd, np.int32)
             d_bt = np.zeros((nd, max(len(s.block_ids) for s in dseqs)), np.int32)
             for i, s in enumerate(dseqs):
-                p = s.n_tokens - 1
+                p = s.n_tokens - 1 + s.inflight   # queued ahead: ids come from the device
                 d_ids[i] = s.last_token
                 d_pos[i] = p
                 d_slot[i] = s.block_ids[p // bs] * bs + p % bs
@@ -571,22 +586,30 @@ class ModelRunner:
     def can_pipeline(self, n: int) -> bool:
         return self.use_graphs and self._bucket(n) is not None
 
-    def decode_launch(self, seqs, ahead: int = 0, masks: Optional[np.ndarray] = None) -> DecodeHandle:
+    def decode_launch(self, seqs, ahead: int = 0, masks: Optional[np.ndarray] = None,
+                      rowmap: Optional[List[int]] = None) -> DecodeHandle:
         """Fills a staging set and queues a graph-replayed decode step (returns at
-        once).  ``ahead=a`` launches the step after the ``a`` in flight: positions
-        are ``a`` further and the input ids are the last in-flight step's sampled
-        ids, copied device-to-device, so the host never waits between steps."""
+        once).  Positions are ``inflight`` tokens past each sequence's collected
+        state (steps queued ahead of it); with ``ahead`` the input ids are the last
+        queued step's sampled ids, copied device-to-device, so the host never waits
+        between steps.  ``rowmap[i]`` (with ``ahead``): the row of that step that
+        sequence i sat in (None: the same row)."""
         n = len(seqs)
         nb = self._bucket(n)
         st = self.stg[self._stg_next]
         self._stg_next = (self._stg_next + 1) % len(self.stg)
-        maxblk = self._decode_fill(seqs, nb, st, ahead)
+        maxblk = self._decode_fill(seqs, nb, st)
+        gather = None
+        if ahead and rowmap is not None:
+            gather = np.zeros(nb, dtype=np.int64)   # padding rows read row 0 (ignored)
+            gather[:n] = rowmap
         if self.bcast is not None:
             self.bcast.send(("graph", {"nb": nb, "n": n, "small": st.hs.copy(),
                                        "bt": st.hbt[:nb, :maxblk].copy(), "f32": st.hf.copy(),
-                                       "seeds": st.hseed.copy(), "from_device": bool(ahead)}, masks))
+                                       "seeds": st.hseed.copy(), "from_device": bool(ahead),
+                                       "rowmap": gather}, masks))
         self._set_masks(masks, n)
-        self._decode_enqueue(st, nb, n, from_device=bool(ahead))
+        self._decode_enqueue(st, nb, n, from_device=bool(ahead), gather=gather)
         return DecodeHandle(st, n, nb)
 
     def _set_masks(self, masks: Optional[np.ndarray], n: int):
@@ -613,7 +636,73 @@ class ModelRunner:
             self._comm_fault()
         return st.h_out[:h.n].tolist()
 
-    def _decode_fill(self, seqs, nb: int, st: "_Staging", ahead: int = 0) -> int:
+    def step_done(self, h) -> bool:
+        """Non-blocking: has the queued step behind handle ``h`` finished on the GPU?"""
+        ev = h.stage.event if isinstance(h, DecodeHandle) else h.event
+        return ev is None or ev.query()
+
+    @torch.inference_mode()
+    def mixed_launch(self, batch: ScheduledBatch, rowmap: List[int]) -> "MixedHandle":
+        """Queues a mixed (decode + prefill) step behind the queued decode step(s)
+        without waiting (engine ``_speculate_mixed``): decode row i's input id is
+        row ``rowmap[i]`` of the last queued step's sampled ids (``d_out``),
+        gathered on the device; its position is ``inflight`` tokens ahead.  The
+        sampled ids land in ``d_out`` (rows = ``batch.sampled_seqs()``) for the
+        decode step queued next, and in a pinned host buffer for the collect.
+        Single process only (no TP broadcast), no allow-masks."""
+        host = self._mixed_host(batch)
+        nd = host["nd"]
+        self.stats["prefill_steps"] += 1
+        self.stats["mixed_ahead"] = self.stats.get("mixed_ahead", 0) + 1
+        names = ["pos", "slots", "lrows", "bt", "seq_lens", "qsl", "tiles", "ids", "combine"]
+        if nd:
+            names += ["d_bt", "d_sl"]
+        arrays = [host[k] for k in names] + list(host["sampling"])
+        gather = np.asarray(rowmap, dtype=np.int64)
+        arrays.append(gather if nd else np.zeros(1, np.int64))
+        if self.is_gpu:
+            dev = self._upload(arrays)
+        else:
+            dev = [torch.from_numpy(np.ascontiguousarray(a)) for a in arrays]
+        d = dict(zip(names, dev))
+        if nd:
+            idx = dev[len(names) + 5]
+            torch.index_select(self.d_out, 0, idx, out=d["ids"][:nd])
+        meta = AttnMeta(
+            positions=d["pos"], slot_mapping=d["slots"], logits_indices=d["lrows"], num_decode=nd,
+            block_tables=d["bt"], seq_lens=d["seq_lens"],
+            q_start_loc=d["qsl"] if self.is_gpu else torch.from_numpy(host["qsl"]),
+            tile_info=d["tiles"], num_tiles=host["num_tiles"])
+        if host.get("num_combine", 0):
+            meta.pf_part_o, meta.pf_part_ml = self.pf_part_o, self.pf_part_ml
+            meta.pf_combine, meta.pf_num_combine = d["combine"], host["num_combine"]
+            meta.pf_num_partials = host["num_partials"]
+        if nd:
+            meta.dec_block_tables = d["d_bt"]
+            meta.dec_seq_lens = d["d_sl"]
+            meta.tmp_out, meta.tmp_ml = self.tmp_out, self.tmp_ml
+            meta.dec_counters = self.dec_counters
+        h = self.model.forward(d["ids"], meta, self.kv)
+        logits = self.model.compute_logits(h)
+        n = logits.shape[0]
+        temp, topp, topk, seeds, steps = dev[len(names):len(names) + 5]
+        ops.sample(logits, temp, topp, topk, seeds, steps, out=self.d_out[:n])
+        mh = self._mx_handles[self._mx_next]
+        self._mx_next ^= 1
+        if mh.host.shape[0] < n:
+            mh.host = torch.zeros(2 * n, dtype=torch.int32, pin_memory=self.is_gpu)
+        mh.n = n
+        mh.host[:n].copy_(self.d_out[:n], non_blocking=self.is_gpu)
+        if mh.event is not None:
+            mh.event.record()
+        return mh
+
+    def mixed_collect(self, h: "MixedHandle") -> List[int]:
+        if h.event is not None:
+            self._wait(h.event)
+        return h.host[:h.n].tolist()
+
+    def _decode_fill(self, seqs, nb: int, st: "_Staging") -> int:
         """Writes a decode step's inputs into a pinned staging set."""
         n = len(seqs)
         mb = self.max_decode_batch
@@ -626,15 +715,15 @@ class ModelRunner:
         bs = self.bs
         maxblk = 1
         for i, s in enumerate(seqs):
-            p = s.n_tokens - 1 + ahead
-            ids[i] = s.last_token  # replaced on the device when ahead
+            p = s.n_tokens - 1 + s.inflight   # steps queued ahead of this one
+            ids[i] = s.last_token  # replaced on the device when queued ahead
             pos[i] = p
             slots[i] = s.block_ids[p // bs] * bs + p % bs
             sl[i] = p + 1
             nbk = len(s.block_ids)
             bt[i, :nbk] = s.block_ids
             maxblk = max(maxblk, nbk)
-        temp, topp, topk, seeds, steps = self._sampling_arrays(seqs, ahead)
+        temp, topp, topk, seeds, steps = self._sampling_arrays(seqs)
         hs[4 * mb:4 * mb + n] = topk
         hs[5 * mb:5 * mb + n] = steps
         st.hf[:n] = temp
@@ -681,13 +770,19 @@ class ModelRunner:
                 "idle_ms_max": round(max(gaps), 2), "gpu_ms_per_step": round(sum(busy) / len(busy), 3),
                 "steps": len(busy)}
 
-    def _decode_enqueue(self, st: "_Staging", nb: int, n: int, from_device: bool = False):
+    def _decode_enqueue(self, st: "_Staging", nb: int, n: int, from_device: bool = False,
+                        gather: Optional[np.ndarray] = None):
         nw = 10 * self.max_decode_batch + nb * self.max_blocks_per_seq
         if self._gaps is not None:
             self._gap_mark(True)
         self.d_in[:nw].copy_(st.h_in[:nw], non_blocking=True)
         if from_device:  # the previous step's sampled ids feed this step
-            self.d_input_ids[:nb].copy_(self.d_out[:nb])
+            if gather is None:
+                self.d_input_ids[:nb].copy_(self.d_out[:nb])
+            else:   # rows of the previous step, survivors only (pinned per staging set)
+                st.h_map[:nb].numpy()[:] = gather
+                self.d_map[:nb].copy_(st.h_map[:nb], non_blocking=True)
+                torch.index_select(self.d_out, 0, self.d_map[:nb], out=self.d_input_ids[:nb])
         g = self.graphs.get(nb)
         if g is None:
             g = self._capture(nb)
@@ -727,7 +822,8 @@ class ModelRunner:
             st.hbt[:nb, :bt.shape[1]] = bt
             st.hf[:] = host["f32"]
             st.hseed[:] = host["seeds"]
-            self._decode_enqueue(st, nb, n, from_device=host.get("from_device", False))
+            self._decode_enqueue(st, nb, n, from_device=host.get("from_device", False),
+                                 gather=host.get("rowmap"))
             self._wait(st.event)
         elif kind == "warmup":
             self.warmup(host)

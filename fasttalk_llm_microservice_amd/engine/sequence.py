@@ -38,7 +38,7 @@ class Sequence:
                  "num_computed", "num_committed_blocks", "num_cached_tokens", "arrival",
                  "first_token_time", "finish_reason", "detok_stream", "on_output", "grammar",
                  "grammar_state", "stop_buf", "text_len", "aborted", "preemptions", "admit_order",
-                 "meta", "host_slots", "background", "jf_text", "jf_ids", "lazy")
+                 "meta", "host_slots", "background", "jf_text", "jf_ids", "lazy", "inflight")
 
     def __init__(self, request_id: str, prompt_ids: List[int], params: SamplingParams,
                  on_output: Optional[Callable[[RequestOutput], None]] = None, meta: Any = None):
@@ -74,6 +74,9 @@ class Sequence:
         self.jf_text = ""
         self.jf_ids: List[int] = []
         self.lazy = False   # grammar not bound yet (SamplingParams.guided_lazy)
+        # queued (launched, not yet collected) steps that sample this sequence: its
+        # next step's position / sampling step run this many tokens ahead of n_tokens
+        self.inflight = 0
 
     # ---------------------------------------------------------------- tokens
     @property

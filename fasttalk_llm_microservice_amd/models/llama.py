@@ -13,8 +13,9 @@ from __future__ import annotations
 
 import dataclasses
 import json
+import logging
 import os
-from typing import List, Optional, Tuple
+from typing import Dict, List, Optional, Tuple
 
 import torch
 import torch.nn.functional as F
@@ -25,6 +26,8 @@ from ..ops import reference as ref
 from ..parallel.comm import SINGLE, TPComm
 from .config import ModelConfig
 from . import weights as W
+
+log = logging.getLogger(__name__)
 
 
 @dataclasses.dataclass
@@ -75,6 +78,9 @@ class LayerWeights:
     wo_pk: Optional[torch.Tensor] = None
     wgu_pk: Optional[torch.Tensor] = None
     wd_pk: Optional[torch.Tensor] = None
+    # resident row-major copies of some packed projections for hipBLASLt at mixed /
+    # prefill step sizes (LlamaModel._prepare_rowmajor): proj -> [N, K]
+    rm: Optional[Dict[str, torch.Tensor]] = None
     # fused decode layer (skinny_pkr.hip): QKV / gate_up packed with the input norms
     # folded in (W diag(ln)), gate_up rows interleaved for the SiLU epilogue; o / down
     # share the packed images above when present
@@ -147,6 +153,14 @@ PG_MAX_SLAB_ROWS = 2048
 # weight, ~0.17 ms per 8B layer): from this many rows up the projection unpacks and
 # calls the library.  The resident weights stay single-image.  0 disables.
 PG_BLAS_ROWS = int(os.environ.get("FT_PG_BLAS_ROWS", "2048"))
+# With memory to spare (an 8B model is 16 GB of a 288 GB MI355X) qkv / o / gate_up
+# also stay resident row-major and run hipBLASLt from this many rows up: at the
+# soft-budgeted mixed-step sizes (300-512 rows) the library beats packed_gemm on
+# them (qkv 32.8 vs 43.4 us, o 26.5 vs 33.0, gate_up 91.7 vs 113 at 512 rows,
+# profiles/pg_probe_300_512_r02.log) while down stays packed (71.9 vs 78.7).
+# FT_ROWMAJOR_COPIES: auto (copies <= 15% of device memory) / 1 / 0.
+PG_RM_ROWS = int(os.environ.get("FT_PG_RM_ROWS", "257"))
+RM_PROJS = ("qkv", "o", "gu")
 
 
 def pg_cfg(proj: str, rows: int, k: int) -> Tuple[int, int]:
@@ -468,6 +482,25 @@ class LlamaModel:
             self._w4_scratch = torch.empty(max(need, big), dtype=self.dtype, device=self.device)
         return Q.w4_dequant(w, out=self._w4_scratch[:need].view(w.n, w.k))
 
+    def _prepare_rowmajor(self):
+        """Resident row-major copies of the RM_PROJS images (hipBLASLt from PG_RM_ROWS
+        rows, see there) when they fit the memory policy."""
+        mode = os.environ.get("FT_ROWMAJOR_COPIES", "auto")
+        if mode == "0" or not self.device.type == "cuda" or not self.layers:
+            return
+        pk = [getattr(L, _ATTR[p] + "_pk") for L in self.layers for p in RM_PROJS]
+        if any(w is None for w in pk):
+            return
+        nbytes = sum(w.numel() * w.element_size() for w in pk)
+        if mode != "1":
+            _, total = torch.cuda.mem_get_info(self.device)
+            if nbytes > 0.15 * total:
+                return
+        for L in self.layers:
+            L.rm = {p: ops.unpack_weight(getattr(L, _ATTR[p] + "_pk")) for p in RM_PROJS}
+        log.info("row-major copies of %s for hipBLASLt at >= %d rows: %.1f GB", "/".join(RM_PROJS),
+                 PG_RM_ROWS, nbytes / 1e9)
+
     def _prepare_packed(self):
         """ONE weight image on the GPU (bf16): every layer projection and the LM head
         are re-laid out into the MFMA-fragment image the decode kernels stream
@@ -500,6 +533,7 @@ class LlamaModel:
         self._unpack_need = max((w.numel() for w in (self.layers[0].wqkv_pk, self.layers[0].wo_pk,
                                                       self.layers[0].wgu_pk, self.layers[0].wd_pk)
                                  if w is not None), default=0)
+        self._prepare_rowmajor()
         if self.lm_head is not None:
             self.lm_head_pk = ops.pack_weight(self.lm_head)
             self.lm_head = None
@@ -638,14 +672,19 @@ class LlamaModel:
         if wp is None:  # row-major weights: CPU backend, or FT_PACKED_GEMM=0
             y = F.linear(x, getattr(L, attr))
             return 0, (ops.silu_mul(y) if proj == "gu" else y)
-        return self._packed(x, wp, proj)
+        return self._packed(x, wp, proj, L.rm.get(proj) if L.rm else None)
 
-    def _packed(self, x: torch.Tensor, wp: torch.Tensor, proj: str) -> Tuple[int, Optional[torch.Tensor]]:
+    def _packed(self, x: torch.Tensor, wp: torch.Tensor, proj: str,
+                rm: Optional[torch.Tensor] = None) -> Tuple[int, Optional[torch.Tensor]]:
         """y = x W^T on the packed image: the decode kernels up to PACKED_ROWS rows
-        (skinny_gemm.hip), the tiled MFMA GEMM above (packed_gemm.hip)."""
+        (skinny_gemm.hip), the tiled MFMA GEMM above (packed_gemm.hip); hipBLASLt on
+        the resident row-major copy ``rm`` from PG_RM_ROWS rows."""
         rows = x.shape[0]
         n, k = wp.shape
         gu = proj == "gu"
+        if rm is not None and rows >= PG_RM_ROWS:
+            y = F.linear(x, rm)
+            return 0, (ops.silu_mul(y, interleaved=True) if gu else y)
         slab_ok = self._slab_ok(proj, rows) and self.ws is not None
         c = packed_cfg(proj, rows) if proj in PACKED_PLAN else None
         if c is not None and _cfg_fits(c, n, k):

@@ -11,6 +11,7 @@ import os
 import threading
 from typing import Optional
 
+import numpy as np
 import torch
 
 from . import reference as ref
@@ -188,6 +189,13 @@ def prefill_partials(nkv: int, head_dim: int, max_partials: int = PREFILL_MAX_PA
     return max_partials * nkv * PREFILL_ROWS * head_dim, max_partials * nkv * PREFILL_ROWS * 2
 
 
+# per-work-item overhead of the prefill kernel in 64-token KV tiles (Q load, DMA ramp,
+# partial store + its combine), for the round-aware split plan below
+PREFILL_ITEM_TILES = float(os.environ.get("FT_PREFILL_ITEM_TILES", "1.0"))
+PREFILL_MAX_ROUNDS = 4
+PREFILL_ROUND_BLIND = os.environ.get("FT_PREFILL_ROUND_BLIND", "0") == "1"
+
+
 def build_prefill_tiles(q_lens, tile_tokens: int, seq_lens=None, nkv: int = 8, num_cus: int = 256,
                         max_partials: int = PREFILL_MAX_PARTIALS, min_split_tiles: int = 4):
     """Host plan of the prefill kernel grid: (items, combine).
@@ -195,11 +203,17 @@ def build_prefill_tiles(q_lens, tile_tokens: int, seq_lens=None, nkv: int = 8, n
     items: [(seq, first query token, kv_lo_tile << 16 | kv_hi_tile, partial slot)],
     one per (query block, KV range); combine: [(seq, first query token, first slot,
     splits)] for query blocks whose KV range is split over several workgroups.
-    Without ``seq_lens`` (or when every block is its own workgroup anyway) no
-    range is split.  A chat turn prefills ~100 tokens over thousands of cached
-    ones: ~2 query blocks per prompt, so a 10-prompt step would be 160 workgroups
-    each streaming a whole history alone -- the ranges are cut so the grid has
-    about 2 workgroups per CU (at least ``min_split_tiles`` 64-token tiles each)."""
+    Without ``seq_lens`` no range is split.  A chat turn prefills ~100 tokens over
+    thousands of cached ones: ~2 query blocks per prompt, so a 10-prompt step would
+    be 160 workgroups each streaming a whole history alone -- the ranges are cut.
+
+    The kernel runs ONE workgroup per CU (``attn_prefill.hip``: 8 waves, 144 KiB of
+    LDS), so the grid executes in rounds of ``num_cus`` workgroups (= num_cus / nkv
+    items): for 1..PREFILL_MAX_ROUNDS rounds the smallest chunk (>= min_split_tiles
+    tiles) whose items fit is found and the plan with the least estimated makespan
+    (rounds x (longest item + PREFILL_ITEM_TILES)) wins.  The earlier plan aimed at
+    ~2 workgroups per CU and rounded every block's split up, e.g. 520 workgroups for
+    5 prompts x 107 tokens over 3k: a third round for 8 workgroups."""
     blocks = []
     for b, ql in enumerate(q_lens):
         ql = int(ql)
@@ -212,11 +226,36 @@ def build_prefill_tiles(q_lens, tile_tokens: int, seq_lens=None, nkv: int = 8, n
                 nkt = (kv_end + PREFILL_BK - 1) // PREFILL_BK
             blocks.append((b, s, nkt))
     items, combine = [], []
-    target = max(1, 2 * num_cus // max(1, nkv))
-    total = sum(n for _, _, n in blocks)
+    per_round = max(1, num_cus // max(1, nkv))
     chunk = 0
-    if seq_lens is not None and len(blocks) < target and total > 0:
-        chunk = max(min_split_tiles, -(-total // target))
+    nk_lo = min(n for _, _, n in blocks) if blocks else 0
+    nk_hi = max(n for _, _, n in blocks) if blocks else 0
+    # the round model assumes near-equal items: a causal prompt's early blocks (a few
+    # tiles each) make the greedy dispatch far from it (1 x 2048 fresh tokens ran 103
+    # vs 91 us on the round-aware plan), so ranges that differ by more than 2x keep
+    # the round-blind split (profiles/prefill_round_plan_r03.log)
+    blind = PREFILL_ROUND_BLIND or nk_lo * 2 < nk_hi
+    if seq_lens is not None and blocks and blind:
+        # the round-2 plan (~2 workgroups per CU, per-block round-up), for A/B runs
+        target = 2 * per_round
+        total = sum(n for _, _, n in blocks)
+        if len(blocks) < target and total > 0:
+            chunk = max(min_split_tiles, -(-total // target))
+    elif seq_lens is not None and blocks:   # history-dominated: round-aware split
+        nk = np.fromiter((n for _, _, n in blocks), dtype=np.int64, count=len(blocks))
+        top = int(nk.max())
+        if top > min_split_tiles:
+            # candidate chunks: the longest block cut into 1..32 equal parts
+            c = np.unique(np.maximum(-(-top // np.arange(1, 33)), min_split_tiles))
+            ns = np.maximum(-(-nk[None, :] // c[:, None]), 1)
+            n_items = ns.sum(1)
+            n_part = np.where(ns > 1, ns, 0).sum(1)
+            rounds = -(-n_items // per_round)
+            cost = rounds * (c + PREFILL_ITEM_TILES)
+            ok = (rounds <= PREFILL_MAX_ROUNDS) & (n_part <= max_partials)
+            if ok.any():
+                best = int(c[ok][np.argmin(cost[ok])])
+                chunk = best if best < top else 0
     slots = 0
     for b, s, nkt in blocks:
         ns = -(-nkt // chunk) if chunk else 1

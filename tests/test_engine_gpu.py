@@ -28,14 +28,15 @@ def _prompts(n, lens, seed=0):
 @pytest.mark.parametrize("model,quant,T,fused_rows", [
     ("tiny-gqa4", None, 40, None), ("tiny-2k", None, 40, None), ("tiny-2k", None, 7, None),
     ("tiny-2k", None, 40, 64), ("tiny-2k", "w4", 40, None), ("tiny-2k", "w4", 100, None),
-    ("tiny", "w4", 40, None)])
+    ("tiny", "w4", 40, None), ("tiny-2k", None, 300, None)])
 def test_gpu_logits_match_cpu_reference(model, quant, T, fused_rows, monkeypatch):
     """Full forward on GPU (bf16 HIP kernels; at hidden 2048 the down projection
     and LM head run on the packed-weight skinny GEMMs) vs CPU fp32 reference ops.
     bf16 <= FUSED_ROWS rows: the fused decode layer (fused_rows=64 at 40 rows runs
     the 48-row bucket, wave-split-N GEMMs).  W4: <= 64 rows run the W4A16 kernels
     (o / down into split-K slabs), 100 rows the dequantize + hipBLASLt path; the CPU
-    side holds the dequantized weights."""
+    side holds the dequantized weights.  bf16 at 300 rows: qkv / o / gate_up on
+    hipBLASLt over the resident row-major copies, down on packed_gemm."""
     if fused_rows is not None:
         from fasttalk_llm_microservice_amd.models import llama
         monkeypatch.setattr(llama, "FUSED_ROWS", fused_rows)
@@ -47,7 +48,10 @@ def test_gpu_logits_match_cpu_reference(model, quant, T, fused_rows, monkeypatch
     c.init_random(3, consistent=True)
     if quant:
         assert g.layers[0].q4 and g.layers[0].wgu is None and c.layers[0].q4 is None
-    bs, nblk = 16, 8
+    else:   # T = 300: qkv / o / gate_up on hipBLASLt over the resident row-major copies
+        assert g.layers[0].rm is not None and set(g.layers[0].rm) == {"qkv", "o", "gu"}
+    bs = 16
+    nblk = max(8, -(-T // bs))
     for m in (g, c):
         kv = m.allocate_kv_cache(nblk, bs)
         dev = m.device
@@ -118,14 +122,19 @@ def test_many_sequences_continuous_batching():
     assert eng.bm.num_free() == eng.bm.num_blocks
 
 
-def test_pipelined_decode_matches_synchronous():
+def test_pipelined_decode_matches_synchronous(monkeypatch):
     """Decode steps queued one ahead on the GPU (ids fed device-to-device) must
     give exactly the synchronous engine's tokens, including sequences that stop
-    early on a stop token, at max_tokens, or at different lengths."""
+    early on a stop token, at max_tokens, or at different lengths; also with
+    ENGINE_PIPELINE_SHRINK=1 (queued steps drop finished rows and gather the
+    survivors' ids on the device by row map)."""
     prompts = _prompts(12, [5 + 7 * i for i in range(12)], seed=3)
     outs = []
-    # pipeline depth 1 / 2 / 3 (ENGINE_PIPELINE_DEPTH: steps queued ahead), then synchronous
-    for async_output, depth in ((True, 1), (True, 2), (True, 3), (False, 1)):
+    # pipeline depth 1 / 2 / 3 (ENGINE_PIPELINE_DEPTH: steps queued ahead), shrink at
+    # depth 1 and 2, then synchronous
+    for async_output, depth, shrink in ((True, 1, "0"), (True, 2, "0"), (True, 3, "0"),
+                                        (True, 1, "1"), (True, 2, "1"), (False, 1, "0")):
+        monkeypatch.setenv("ENGINE_PIPELINE_SHRINK", shrink)
         eng = _engine(max_num_seqs=32, num_kv_blocks=1024, async_output=async_output,
                       pipeline_depth=depth)
         res = {}
@@ -138,6 +147,7 @@ def test_pipelined_decode_matches_synchronous():
         assert eng.bm.num_free() == eng.bm.num_blocks
         if async_output:
             assert eng.stats["pipelined_steps"] > 0
+            assert (eng.stats["pipeline_shrinks"] > 0) == (shrink == "1")
         outs.append([res[i] for i in range(len(prompts))])
     # Identical until the first sequence stops (step 8): from then on the pipelined
     # engine's in-flight step still carries the finished row while the synchronous
@@ -146,6 +156,46 @@ def test_pipelined_decode_matches_synchronous():
     for piped in outs[:-1]:
         assert [len(o) for o in piped] == [len(o) for o in outs[-1]]
         assert [o[:8] for o in piped] == [o[:8] for o in outs[-1]]
+
+
+def test_mixed_ahead_and_jit_topup(monkeypatch):
+    """Prompts arriving while decode steps are queued go into a mixed step queued
+    behind them (decode rows' ids gathered on the device from the last queued
+    step's sampled rows, positions ``inflight`` ahead), and the queue is topped up
+    just in time.  Against the drained/synchronous engine: every request gets its
+    full length, the first tokens agree (the mixed steps group rows differently,
+    so bf16 rounding may flip a near-tie later), all KV blocks come back, no
+    sequence keeps a stale in-flight count."""
+    prompts = _prompts(16, [20 + 9 * i for i in range(16)], seed=5)
+
+    def run(ahead: bool):
+        monkeypatch.setenv("ENGINE_MIXED_AHEAD", "1" if ahead else "0")
+        monkeypatch.setenv("ENGINE_JIT_TOPUP", "1" if ahead else "0")
+        eng = _engine(max_num_seqs=32, num_kv_blocks=1024, pipeline_depth=1)
+        res = {}
+        step = k = 0
+        for i in range(4):
+            eng.add_request(f"r{i}", prompts[i], SamplingParams(temperature=0.0, max_tokens=24,
+                                                                 ignore_eos=True),
+                            on_output=lambda o, i=i: res.setdefault(i, []).extend(o.token_ids))
+        k = 4
+        while eng.has_work() or k < len(prompts):
+            if k < len(prompts) and step % 3 == 2:
+                eng.add_request(f"r{k}", prompts[k], SamplingParams(temperature=0.0, max_tokens=24,
+                                                                     ignore_eos=True),
+                                on_output=lambda o, i=k: res.setdefault(i, []).extend(o.token_ids))
+                k += 1
+            eng.step()
+            step += 1
+        assert eng.bm.num_free() == eng.bm.num_blocks
+        return [res[i] for i in range(len(prompts))], eng
+
+    ref, _ = run(False)
+    got, eng = run(True)
+    assert eng.stats["mixed_ahead"] > 0 and eng.stats["pipelined_steps"] > 0
+    assert [len(o) for o in got] == [len(o) for o in ref] == [24] * len(prompts)
+    agree = sum(a[:3] == b[:3] for a, b in zip(got, ref))
+    assert agree >= len(prompts) - 2, (agree, got, ref)
 
 
 def test_host_swap_roundtrip_and_engine():

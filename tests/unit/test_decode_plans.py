@@ -94,3 +94,29 @@ def test_prefill_split_plan_covers_ranges():
     # slot budget: blocks that would exceed it run unsplit
     items, comb = ops.build_prefill_tiles(q_lens, 64, seq_lens=seq_lens, num_cus=256, max_partials=4)
     assert sum(c[3] for c in comb) <= 4
+
+
+def test_prefill_split_plan_fills_whole_rounds():
+    """The prefill kernel runs one workgroup per CU, so the plan counts rounds of
+    num_cus workgroups: 5 prompts x 107 new tokens over 3k cached fit ONE round
+    (the old ~2-per-CU target gave 520 workgroups: a third round for 8 of them),
+    and no plan's estimated makespan is worse than the round-blind split's."""
+    from fasttalk_llm_microservice_amd import ops
+
+    items, comb = ops.build_prefill_tiles([107] * 5, 64, seq_lens=[3107] * 5, nkv=8, num_cus=256)
+    assert len(items) * 8 <= 256 and comb
+    for S, Q, C in [(10, 100, 3000), (4, 128, 3000), (1, 512, 3000), (50, 60, 3000), (3, 300, 5000)]:
+        items, comb = ops.build_prefill_tiles([Q] * S, 64, seq_lens=[Q + C] * S, nkv=8, num_cus=256)
+        lens = [((r & 0xFFFF) - (r >> 16)) if r != 0xFFFF else None for _, _, r, _ in items]
+        assert sum(c[3] for c in comb) <= ops.PREFILL_MAX_PARTIALS
+        rounds = -(-len(items) * 8 // 256)
+        assert rounds <= ops.PREFILL_MAX_ROUNDS
+        if any(lens):
+            longest = max(x for x in lens if x)
+            # round-blind plan: ~64 items of ceil(total / 64) tiles, rounded up per block
+            nblocks = S * -(-Q // 64)
+            total = sum(-(-min(Q + C, C + s + min(64, Q - s)) // 64) for s in range(0, Q, 64)) * S
+            blind = max(4, -(-total // 64))
+            blind_items = sum(-(-min(Q + C, C + s + min(64, Q - s)) // 64 // blind) or 1
+                              for s in range(0, Q, 64)) * S
+            assert rounds * (longest + 1) <= -(-max(blind_items, nblocks) * 8 // 256) * (blind + 1) + 1

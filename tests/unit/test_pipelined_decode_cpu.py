@@ -1,0 +1,208 @@
+"""Pipelined decode (engine.py ``_speculate``) on the CPU with a device-emulating
+runner: queued steps take their input ids from the previous queued step's
+sampled rows, and a step queued after a sequence is known to have finished
+drops that row and gathers the survivors' ids by ``rowmap``.  Tokens must equal
+the synchronous engine's exactly (the fake model is deterministic in (input
+token, position)), whatever the pipeline depth and however sequences stop."""
+import pytest
+import torch
+
+from fasttalk_llm_microservice_amd.engine.config import EngineConfig
+from fasttalk_llm_microservice_amd.engine.engine import LLMEngine
+from fasttalk_llm_microservice_amd.engine.sampling_params import SamplingParams
+from fasttalk_llm_microservice_amd.models.config import MODELS
+
+EOS = 128009
+
+
+def _next(tok: int, pos: int) -> int:
+    if (tok * 31 + pos) % 23 == 0:
+        return EOS
+    return (tok * 7 + pos * 13 + 3) % 1000 + 1
+
+
+class _Handle:
+    def __init__(self, out):
+        self.out = out
+        self.event = None
+
+
+class ModelRunner:
+    """Named like the real runner: the engine pipelines only ``ModelRunner``s.
+    ``d_out`` plays the device buffer of the last queued step's sampled ids;
+    positions come from each sequence's ``inflight`` count, and a queued step
+    checks that the KV slot it would write has a block."""
+
+    def __init__(self, num_blocks=256, max_model_len=512, block_size=4):
+        self.num_blocks = num_blocks
+        self.max_model_len = max_model_len
+        self.bs = block_size
+        self.mcfg = MODELS["tiny"]
+        self.dtype = torch.float32
+        self.device = torch.device("cpu")
+        self.stats = {"steps": 0}
+        self.d_out = []
+        self.launches = []   # (rows, ahead, rowmap)
+        self.mixed = []      # (decode rows, prefill tokens, rowmap) of queued mixed steps
+
+    def execute(self, batch, masks):
+        self.stats["steps"] += 1
+        return [_next(int(s.tokens[-1]), s.n_tokens - 1) for s in batch.sampled_seqs()]
+
+    def can_pipeline(self, n: int) -> bool:
+        return n > 0
+
+    def step_done(self, h) -> bool:
+        return True
+
+    def decode_launch(self, seqs, ahead=0, masks=None, rowmap=None):
+        self.launches.append((len(seqs), ahead, None if rowmap is None else list(rowmap)))
+        if ahead:
+            rows = rowmap if rowmap is not None else range(len(seqs))
+            ids = [self.d_out[r] for r in rows]
+        else:
+            ids = [int(s.tokens[-1]) for s in seqs]
+        out = []
+        for s, tok in zip(seqs, ids):
+            pos = s.n_tokens - 1 + s.inflight
+            assert ahead or s.inflight == 0
+            assert pos // self.bs < len(s.block_ids), "KV slot of a queued step has no block"
+            out.append(_next(tok, pos))
+        self.d_out = out
+        return _Handle(out)
+
+    def decode_collect(self, h):
+        return list(h.out)
+
+    def mixed_launch(self, batch, rowmap):
+        self.mixed.append((len(batch.decode_seqs), list(batch.prefill_tokens), list(rowmap)))
+        out = []
+        for s, r in zip(batch.decode_seqs, rowmap):
+            pos = s.n_tokens - 1 + s.inflight
+            assert s.inflight >= 1 and pos // self.bs < len(s.block_ids)
+            out.append(_next(self.d_out[r], pos))
+        for s, n, smp in zip(batch.prefill_seqs, batch.prefill_tokens, batch.prefill_sample):
+            assert s.inflight == 0
+            assert (s.num_computed + n + self.bs - 1) // self.bs <= len(s.block_ids)
+            if smp:
+                assert s.num_computed + n == s.n_tokens
+                out.append(_next(int(s.tokens[-1]), s.n_tokens - 1))
+        self.d_out = out
+        return _Handle(out)
+
+    def mixed_collect(self, h):
+        return list(h.out)
+
+
+def _run(async_output: bool, depth: int, n_req: int = 9, shrink: bool = True, late: int = 0,
+         mixed_ahead: bool = False):
+    """``late`` requests arrive one every third engine step after the first ``n_req``."""
+    import os
+
+    os.environ["ENGINE_PIPELINE_SHRINK"] = "1" if shrink else "0"
+    os.environ["ENGINE_MIXED_AHEAD"] = "1" if mixed_ahead else "0"
+    cfg = EngineConfig(model="tiny", device="cpu", block_size=4, async_output=async_output,
+                       pipeline_depth=depth, max_num_seqs=32)
+    runner = ModelRunner()
+    eng = LLMEngine(cfg, runner=runner)
+    res = {}
+
+    def add(i):
+        prompt = [11 + 5 * i + j for j in range(3 + 2 * i + (i % 3) * 9)]
+        sp = SamplingParams(temperature=0.0, max_tokens=6 + 4 * (i % 9), stop_token_ids=[EOS])
+        eng.add_request(f"r{i}", prompt, sp,
+                        on_output=lambda o, i=i: res.setdefault(i, []).extend(o.token_ids))
+
+    for i in range(n_req):
+        add(i)
+    k, step = n_req, 0
+    while eng.has_work() or k < n_req + late:
+        if k < n_req + late and step % 3 == 2:   # a late prompt every third step
+            add(k)
+            k += 1
+        eng.step()
+        step += 1
+    os.environ.pop("ENGINE_PIPELINE_SHRINK", None)
+    os.environ.pop("ENGINE_MIXED_AHEAD", None)
+    assert eng.bm.num_free() == eng.bm.num_blocks
+    assert all(q.inflight == 0 for q in eng.scheduler.by_id.values())
+    return [res.get(i, []) for i in range(n_req + late)], eng, runner
+
+
+@pytest.mark.parametrize("depth", [1, 2, 3])
+def test_pipelined_decode_with_finishes_matches_synchronous(depth):
+    ref, _, _ = _run(False, 1)
+    got, eng, runner = _run(True, depth)
+    assert got == ref
+    # sequences of different lengths stop mid-pipeline: the queue shrank instead of
+    # draining, and every shrunk step gathered its ids by row map
+    assert eng.stats["pipeline_shrinks"] > 0
+    assert any(rm is not None for _, _, rm in runner.launches)
+    lens = sorted({len(o) for o in ref})
+    assert len(lens) > 2   # the finishes really are staggered
+
+
+def test_shrink_keeps_pipelining_until_last_sequence():
+    """With every request admitted up front, the only synchronous (non-queued)
+    launch is the first decode step: later stops shrink the queue."""
+    _, eng, runner = _run(True, 1)
+    first_launches = [l for l in runner.launches if l[1] == 0]
+    assert len(first_launches) == 1
+
+
+def test_default_drains_on_stop():
+    """Default (ENGINE_PIPELINE_SHRINK unset): a stop drains the queue, so the
+    session's next prompt is scheduled one step sooner; tokens are unchanged."""
+    ref, _, _ = _run(False, 1, shrink=False)
+    got, eng, runner = _run(True, 1, shrink=False)
+    assert got == ref
+    assert eng.stats["pipeline_shrinks"] == 0
+    assert all(rm is None for _, _, rm in runner.launches)
+
+
+@pytest.mark.parametrize("depth", [1, 2])
+def test_mixed_ahead_matches_synchronous(depth):
+    """Prompts that arrive while decode steps are queued are scheduled into a mixed
+    step queued behind them (decode rows' ids gathered by row map from the last
+    queued step); tokens equal the synchronous engine's, every block comes back."""
+    ref, _, _ = _run(False, 1, n_req=4, late=14)
+    got, eng, runner = _run(True, depth, n_req=4, late=14, mixed_ahead=True)
+    assert got == ref
+    assert eng.stats["mixed_ahead"] > 0 and runner.mixed
+    # decode steps were queued behind mixed ones (ids from the mixed step's rows)
+    assert eng.stats["pipelined_steps"] > 0
+    # the drained path handled the rest: no mixed step ran while another was queued
+    assert all(d > 0 for d, _, _ in runner.mixed)
+
+
+def test_mixed_ahead_with_background_warmups():
+    """Background prefix-cache warm-ups queued while decode steps run are prefilled
+    in mixed steps queued ahead too; foreground tokens are unchanged and every
+    block comes back (warm-up blocks stay cached, not held)."""
+    import os
+
+    outs = []
+    for ahead in (False, True):
+        os.environ["ENGINE_MIXED_AHEAD"] = "1" if ahead else "0"
+        cfg = EngineConfig(model="tiny", device="cpu", block_size=4, async_output=ahead,
+                           pipeline_depth=1, max_num_seqs=32)
+        runner = ModelRunner()
+        eng = LLMEngine(cfg, runner=runner)
+        res = {}
+        for i in range(5):
+            eng.add_request(f"r{i}", [7 + i + j for j in range(5 + 3 * i)],
+                            SamplingParams(temperature=0.0, max_tokens=20 + i, stop_token_ids=[EOS]),
+                            on_output=lambda o, i=i: res.setdefault(i, []).extend(o.token_ids))
+        step = 0
+        while eng.has_work():
+            if step in (3, 6, 9):
+                eng.add_request(f"w{step}", [300 + step + j for j in range(30)],
+                                SamplingParams(temperature=0.0, max_tokens=1), background=True)
+            eng.step()
+            step += 1
+        os.environ.pop("ENGINE_MIXED_AHEAD", None)
+        assert eng.bm.num_free() == eng.bm.num_blocks
+        outs.append([res.get(i, []) for i in range(5)])
+        if ahead:
+            assert eng.stats["mixed_ahead"] > 0
+    assert outs[0] == outs[1]
