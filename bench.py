@@ -325,8 +325,9 @@ def main():
             "engine_decode_step_ms": _timed_decode_ms(m_before, metrics),
             "engine_decode_step_ms_last512": round(metrics.get("decode_step_ms_avg", 0.0), 3),
             "engine_decode_batch_avg": round(metrics.get("decode_batch_avg", 0.0), 2),
-            "engine_steps": {k: metrics.get(k, 0) for k in
-                             ("decode_steps", "pipelined_steps", "mixed_steps", "mixed_ahead", "pipeline_shrinks")},
+            "engine_steps": {k: v for k, v in metrics.items() if k in
+                             ("decode_steps", "pipelined_steps", "mixed_steps", "mixed_ahead", "pipeline_shrinks")
+                             or k.startswith("mixed_ahead_skip_")},
             "engine_runner": metrics.get("runner", {}),
             "engine_decode_host_ms": metrics.get("decode_host_ms", {}),
             "init_s": round(init_s, 1),

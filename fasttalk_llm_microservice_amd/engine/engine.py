@@ -95,11 +95,15 @@ class LLMEngine:
         self.pipeline_depth = max(1, int(getattr(cfg, "pipeline_depth", 1)))
         # ENGINE_MIXED_AHEAD (default on): waiting prompts are scheduled into a mixed
         # step queued behind the running decode step instead of draining the queue.
-        # ENGINE_JIT_TOPUP (default on): the queue is topped up only when the running
-        # step is about to finish (ENGINE_JIT_MARGIN_MS before its expected end), with
-        # new requests handled meanwhile (``poll_hook``, set by AsyncEngine)
+        # ENGINE_JIT_TOPUP=1: the queue is topped up only when the running step is
+        # about to finish (ENGINE_JIT_MARGIN_MS before its expected end), with new
+        # requests handled meanwhile (``poll_hook``, set by AsyncEngine), so a prompt
+        # that arrives during a step starts in the next one.  Off by default: the
+        # host's view of step ends jitters with the GIL (the WebSocket thread streams
+        # 50 frames a step), late top-ups cost the decode step 7.6 -> 8.0 ms and p50
+        # TTFT did not improve (profiles/ab_mixed_ahead_r03.log).
         self.mixed_ahead = os.environ.get("ENGINE_MIXED_AHEAD", "1") != "0"
-        self.jit_topup = os.environ.get("ENGINE_JIT_TOPUP", "1") != "0"
+        self.jit_topup = os.environ.get("ENGINE_JIT_TOPUP", "0") == "1"
         self.jit_margin = float(os.environ.get("ENGINE_JIT_MARGIN_MS", "1.5")) / 1e3
         self.poll_hook = None
         self._ema_step = 0.0
@@ -260,28 +264,33 @@ class LLMEngine:
         (a prompt's next chunk needs the previous chunk's post-step state), and
         only for grammar-free, single-process (no TP broadcast) engines."""
         sched = self.scheduler
-        if any(e.mixed for e in self._inflight) or sched.swapped:
+
+        def skip(why: str):
+            self.stats["mixed_ahead_skip_" + why] += 1
             return None
+
+        if any(e.mixed for e in self._inflight) or sched.swapped:
+            return skip("queued_mixed" if not sched.swapped else "swapped")
         if not hasattr(self.runner, "mixed_launch") or getattr(self.runner, "bcast", None) is not None:
             return None
         if any(q.grammar is not None or q.lazy or q.jf_ids for q in sched.waiting) or \
                 any(q.grammar is not None for q in sched.background):
-            return None
+            return skip("grammar")
         running = list(sched.running)
         if not running:   # nothing to overlap: the drained path schedules it
-            return None
+            return skip("no_running")
         pos = {id(q): i for i, q in enumerate(last)}
         if any(id(q) not in pos or q.grammar is not None for q in running):
-            return None
+            return skip("rows")
         if not self._grow_for_next(running):
-            return None
+            return skip("blocks")
         pseqs, ptok, psamp, rejected = sched._schedule_prefill(sched.max_tokens - len(running),
                                                                len(running))
         for q in rejected:   # only background warm-ups are dropped while sequences run
             sched.by_id.pop(q.request_id, None)
             self._finalize(q, "abort", emit=False)
         if not pseqs:
-            return None
+            return skip("no_prefill")
         mb = ScheduledBatch(running, pseqs, ptok, psamp)
         h = self.runner.mixed_launch(mb, [pos[id(q)] for q in running])
         for q in mb.sampled_seqs():

@@ -158,7 +158,10 @@ PG_BLAS_ROWS = int(os.environ.get("FT_PG_BLAS_ROWS", "2048"))
 # soft-budgeted mixed-step sizes (300-512 rows) the library beats packed_gemm on
 # them (qkv 32.8 vs 43.4 us, o 26.5 vs 33.0, gate_up 91.7 vs 113 at 512 rows,
 # profiles/pg_probe_300_512_r02.log) while down stays packed (71.9 vs 78.7).
-# FT_ROWMAJOR_COPIES: auto (copies <= 15% of device memory) / 1 / 0.
+# FT_ROWMAJOR_COPIES: 0 (default: one weight image) / auto (copies <= 15% of device
+# memory) / 1.  At the driver config the copies were worth +1.2% tok/s, within the
+# run-to-run spread (profiles/ab_rowmajor_copies_r03.log), for 10 GB more resident
+# weights, so the single packed image stays the default.
 PG_RM_ROWS = int(os.environ.get("FT_PG_RM_ROWS", "257"))
 RM_PROJS = ("qkv", "o", "gu")
 
@@ -485,7 +488,7 @@ class LlamaModel:
     def _prepare_rowmajor(self):
         """Resident row-major copies of the RM_PROJS images (hipBLASLt from PG_RM_ROWS
         rows, see there) when they fit the memory policy."""
-        mode = os.environ.get("FT_ROWMAJOR_COPIES", "auto")
+        mode = os.environ.get("FT_ROWMAJOR_COPIES", "0")
         if mode == "0" or not self.device.type == "cuda" or not self.layers:
             return
         pk = [getattr(L, _ATTR[p] + "_pk") for L in self.layers for p in RM_PROJS]
@@ -597,8 +600,11 @@ class LlamaModel:
         for L in self.layers:
             for f in dataclasses.fields(L):
                 v = getattr(L, f.name)
-                if isinstance(v, dict):
+                if isinstance(v, dict):   # W4 projections / row-major copies
                     for q in v.values():
+                        if isinstance(q, torch.Tensor):
+                            add(q)
+                            continue
                         for t in vars(q).values():
                             add(t)
                 else:

@@ -35,11 +35,13 @@ def test_gpu_logits_match_cpu_reference(model, quant, T, fused_rows, monkeypatch
     bf16 <= FUSED_ROWS rows: the fused decode layer (fused_rows=64 at 40 rows runs
     the 48-row bucket, wave-split-N GEMMs).  W4: <= 64 rows run the W4A16 kernels
     (o / down into split-K slabs), 100 rows the dequantize + hipBLASLt path; the CPU
-    side holds the dequantized weights.  bf16 at 300 rows: qkv / o / gate_up on
-    hipBLASLt over the resident row-major copies, down on packed_gemm."""
+    side holds the dequantized weights.  bf16 at 300 rows with FT_ROWMAJOR_COPIES=1:
+    qkv / o / gate_up on hipBLASLt over resident row-major copies, down on packed_gemm."""
     if fused_rows is not None:
         from fasttalk_llm_microservice_amd.models import llama
         monkeypatch.setattr(llama, "FUSED_ROWS", fused_rows)
+    if T >= 257 and quant is None:
+        monkeypatch.setenv("FT_ROWMAJOR_COPIES", "1")
     cfg = MODELS[model]
     # consistent=True: both draw the same unsharded weights on the host from one seed
     g = LlamaModel(cfg, torch.device("cuda"), torch.bfloat16, max_model_len=512,
@@ -48,7 +50,7 @@ def test_gpu_logits_match_cpu_reference(model, quant, T, fused_rows, monkeypatch
     c.init_random(3, consistent=True)
     if quant:
         assert g.layers[0].q4 and g.layers[0].wgu is None and c.layers[0].q4 is None
-    else:   # T = 300: qkv / o / gate_up on hipBLASLt over the resident row-major copies
+    elif T >= 257:   # qkv / o / gate_up on hipBLASLt over the resident row-major copies
         assert g.layers[0].rm is not None and set(g.layers[0].rm) == {"qkv", "o", "gu"}
     bs = 16
     nblk = max(8, -(-T // bs))
