@@ -316,6 +316,24 @@ class LLMEngine:
                 return
             time.sleep(0.0002)
 
+    def _drain_wait(self, e: "_Inflight"):
+        """The queue is draining (nothing could be queued behind ``e``: a stop, or no
+        room).  While ``e`` runs, new requests are admitted (``poll_hook``), and the
+        first prompt that arrives is scheduled into a mixed step queued behind ``e``
+        (:meth:`_speculate_mixed`), so the prefill starts the moment ``e`` ends
+        instead of after the host has collected it and built the step."""
+        poll = self.poll_hook
+        while not self.runner.step_done(e.handle):
+            poll()
+            if self.scheduler.waiting:
+                nxt = self._speculate_mixed(e.batch.sampled_seqs())
+                if nxt is not None:
+                    nxt.t_launch = time.perf_counter()
+                    self._inflight.append(nxt)
+                    self.stats["mixed_ahead_drain"] += 1
+                return
+            time.sleep(0.0002)
+
     def _step_pipelined(self) -> List[RequestOutput]:
         e = self._inflight[0]
         batch, handle = e.batch, e.handle
@@ -329,6 +347,8 @@ class LLMEngine:
                 break
             nxt.t_launch = time.perf_counter()
             self._inflight.append(nxt)
+        if len(self._inflight) == 1 and not e.mixed and self.mixed_ahead and self.poll_hook is not None:
+            self._drain_wait(e)
         tl = time.perf_counter()
         toks = self.runner.mixed_collect(handle) if e.mixed else self.runner.decode_collect(handle)
         t1 = time.perf_counter()

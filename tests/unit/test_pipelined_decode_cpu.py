@@ -206,3 +206,62 @@ def test_mixed_ahead_with_background_warmups():
         if ahead:
             assert eng.stats["mixed_ahead"] > 0
     assert outs[0] == outs[1]
+
+
+def _slow_step_done(self, h) -> bool:
+    """step_done() is False for the first two polls of every queued step."""
+    polls = self.__dict__.setdefault("polls", {})
+    n = polls.get(id(h), 0)
+    polls[id(h)] = n + 1
+    return n >= 2
+
+
+# named ModelRunner too: the engine pipelines only ``ModelRunner``s
+_SlowDone = type("ModelRunner", (ModelRunner,), {"step_done": _slow_step_done})
+
+
+def test_prompt_arriving_during_drain_is_queued_behind_running_step():
+    """A stop drains the queue; a prompt admitted while the last queued step still
+    runs (AsyncEngine's poll hook) goes into a mixed step queued behind it.
+    Tokens equal the synchronous engine's; blocks all come back."""
+    import os
+
+    def run(async_output):
+        os.environ["ENGINE_MIXED_AHEAD"] = "1"
+        cfg = EngineConfig(model="tiny", device="cpu", block_size=4, async_output=async_output,
+                           pipeline_depth=1, max_num_seqs=32)
+        runner = _SlowDone()
+        eng = LLMEngine(cfg, runner=runner)
+        res = {}
+        pending = []
+
+        def add(i):
+            eng.add_request(f"r{i}", [9 + 3 * i + j for j in range(4 + 5 * (i % 4))],
+                            SamplingParams(temperature=0.0, max_tokens=5 + 3 * (i % 5),
+                                           stop_token_ids=[EOS]),
+                            on_output=lambda o, i=i: res.setdefault(i, []).extend(o.token_ids))
+
+        def poll():   # the next request "arrives" while a step runs
+            if pending:
+                add(pending.pop(0))
+
+        eng.poll_hook = poll if async_output else None
+        for i in range(4):
+            add(i)
+        nxt, step = 4, 0
+        while eng.has_work() or pending or nxt < 16:
+            if nxt < 16 and not pending and step % 3 == 0:
+                pending.append(nxt)
+                nxt += 1
+            if not async_output or not eng.has_work():
+                poll()   # between steps (AsyncEngine drains its command queue there too)
+            eng.step()
+            step += 1
+        os.environ.pop("ENGINE_MIXED_AHEAD", None)
+        assert eng.bm.num_free() == eng.bm.num_blocks
+        return [res.get(i, []) for i in range(16)], eng
+
+    ref, _ = run(False)
+    got, eng = run(True)
+    assert got == ref
+    assert eng.stats["mixed_ahead_drain"] > 0
