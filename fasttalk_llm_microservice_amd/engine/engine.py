@@ -203,7 +203,7 @@ class LLMEngine:
             q.inflight += 1
         return _Inflight(ScheduledBatch(list(seqs), [], [], []), h, False)
 
-    def _speculate(self, batch: ScheduledBatch, ahead: int):
+    def _speculate(self):
         """Queue the step after the queued ones, assuming none of their sequences
         stops.  Rows of sequences that do stop are discarded; their extra KV writes
         land in blocks beyond the sequence's end, which are not in the prefix cache
@@ -342,7 +342,7 @@ class LLMEngine:
             self._jit_wait(e)
         # top the queue up to depth + 1 steps before waiting on the oldest
         while len(self._inflight) <= self.pipeline_depth:
-            nxt = self._speculate(batch, len(self._inflight))
+            nxt = self._speculate()
             if nxt is None:
                 break
             nxt.t_launch = time.perf_counter()
