@@ -69,7 +69,8 @@ int ft_ar_export_error(int* dst, const uint64_t* peers_dev, int world, hipStream
 int ft_skinny_gemm_pk(const void* x, int x_stride, int M, const void* wpk, int N, int K, float* ws,
                       void* out, int out_stride, int splits, int nt, hipStream_t stream);
 int ft_skinny_gemm_xr(const void* x, int x_stride, int M, const void* w, int N, int K, float* ws,
-                      void* out, int out_stride, int splits, int nt, int epi, hipStream_t stream);
+                      void* out, int out_stride, int splits, int nt, int epi, int nw,
+                      hipStream_t stream);
 int ft_packed_gemm(const void* x, int x_stride, int M, const void* wpk, int N, int K, int splits,
                    int epi, int cfg, void* out, int out_stride, float* ws, hipStream_t stream);
 int ft_unpack_weight(void* out, const void* wpk, int N, int K, hipStream_t stream);
@@ -431,9 +432,10 @@ void skinny_gemm(at::Tensor x, at::Tensor w, c10::optional<at::Tensor> out,
   TORCH_CHECK(w.size(1) == K, "K mismatch");
   TORCH_CHECK(M <= (u == -4 ? 128 : 64), "skinny_gemm supports M <= 64 (pk, xr) / 128 (xc)");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0, "w alignment");
-  TORCH_CHECK(u >= -6 && u <= -3,
-              "skinny_gemm variant: -3 (pk), -4 (xc), -5 (xr), -6 (xr + SiLU), packed weights");
-  const bool silu = u == -6;
+  TORCH_CHECK(u >= -8 && u <= -3,
+              "skinny_gemm variant: -3 (pk), -4 (xc), -5 (xr), -6 (xr + SiLU), -7 / -8 (the same "
+              "xr on 8-wave workgroups), packed weights");
+  const bool silu = u == -6 || u == -8;
   TORCH_CHECK(!silu || (splits == 1 && nt == 2 && N % 32 == 0),
               "xr SiLU epilogue: one split, nt 2, interleaved gate_up image");
   float* wsp = nullptr;
@@ -454,7 +456,8 @@ void skinny_gemm(at::Tensor x, at::Tensor w, c10::optional<at::Tensor> out,
   }
   if (u <= -5)
     check_rc(ft_skinny_gemm_xr(x.data_ptr(), (int)x.stride(0), M, w.data_ptr(), N, K, wsp, op,
-                               ostride, (int)splits, (int)nt, silu ? 1 : 0, cur_stream()),
+                               ostride, (int)splits, (int)nt, silu ? 1 : 0, u <= -7 ? 8 : 4,
+                               cur_stream()),
              "skinny_gemm_xr");
   else if (u == -3)  // w is the packed [N/16][K/64][2][64][8] image (ops.pack_weight)
     check_rc(ft_skinny_gemm_pk(x.data_ptr(), (int)x.stride(0), M, w.data_ptr(), N, K, wsp, op,
@@ -469,7 +472,8 @@ void skinny_gemm(at::Tensor x, at::Tensor w, c10::optional<at::Tensor> out,
 // "xr" decode GEMM (csrc/kernels/skinny_gemm.hip): epi 0 bf16 out / fp32 slabs,
 // epi 1 SiLU of the interleaved gate/up image.
 void skinny_gemm_xr(at::Tensor x, at::Tensor w, c10::optional<at::Tensor> out,
-                    c10::optional<at::Tensor> ws, int64_t splits, int64_t nt, int64_t epi) {
+                    c10::optional<at::Tensor> ws, int64_t splits, int64_t nt, int64_t epi,
+                    int64_t nw) {
   check_bf16(x, "x");
   check_bf16(w, "w");
   check_rows(x, "x");
@@ -493,7 +497,7 @@ void skinny_gemm_xr(at::Tensor x, at::Tensor w, c10::optional<at::Tensor> out,
     wsp = ws->data_ptr<float>();
   }
   check_rc(ft_skinny_gemm_xr(x.data_ptr(), (int)x.stride(0), M, w.data_ptr(), N, K, wsp, op, ostride,
-                             (int)splits, (int)nt, (int)epi, cur_stream()),
+                             (int)splits, (int)nt, (int)epi, (int)nw, cur_stream()),
            "skinny_gemm_xr");
 }
 
@@ -808,7 +812,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("nt") = 1, py::arg("xr") = false, py::arg("silu") = false);
   m.def("w4_dequant", &w4_dequant);
   m.def("skinny_gemm_xr", &skinny_gemm_xr, py::arg("x"), py::arg("w"), py::arg("out") = py::none(),
-        py::arg("ws") = py::none(), py::arg("splits") = 1, py::arg("nt") = 2, py::arg("epi") = 0);
+        py::arg("ws") = py::none(), py::arg("splits") = 1, py::arg("nt") = 2, py::arg("epi") = 0,
+        py::arg("nw") = 4);
   m.def("skinny_gemm", &skinny_gemm, py::arg("x"), py::arg("w"), py::arg("out") = py::none(),
         py::arg("ws") = py::none(), py::arg("splits") = 1, py::arg("nt") = 1, py::arg("u") = -3);
   m.def("pkr_gemm", &pkr_gemm, py::arg("x"), py::arg("w"), py::arg("out") = py::none(),

@@ -198,22 +198,27 @@ __global__ __launch_bounds__(256) void skinny_xc_kernel(
 // (above).  (An in-launch split-K residual epilogue and an RMS-scaled SiLU variant
 // were measured slower than the separate add+RMSNorm launches they replaced --
 // profiles/ab_resid_layer_r02.log -- and removed.)
-template <int MT, int NT, int KC, int EPI>
-__global__ __launch_bounds__(256, 1) void skinny_xr_kernel(
+// NW: waves per workgroup.  8 waves share one staged x chunk between twice the
+// weight columns: the per-CU load path carries x once per 8 waves' weights
+// instead of once per 4 (at 50-64 rows x is as many bytes per workgroup as its
+// weight slice), and a 128 KiB (KC 512) workgroup gets two waves per SIMD.
+template <int MT, int NT, int KC, int EPI, int NW = 4>
+__global__ __launch_bounds__(64 * NW, 1) void skinny_xr_kernel(
     const uint16_t* __restrict__ x, int x_stride, int M, const uint16_t* __restrict__ w, int K,
     float* __restrict__ ws, uint16_t* __restrict__ out, int out_stride, int N, int k_slice) {
   constexpr bool SILU = EPI == 1;
   constexpr int KS = KC / 64;
   constexpr int ROWS = 16 * MT;
   constexpr int CPR = KC / 8;
-  constexpr int XL = ROWS * CPR / 256;
-  static_assert(XL >= 1 && (ROWS * CPR) % 256 == 0, "x chunk must tile the workgroup");
+  constexpr int NTH = 64 * NW;
+  constexpr int XL = ROWS * CPR / NTH;
+  static_assert(XL >= 1 && (ROWS * CPR) % NTH == 0, "x chunk must tile the workgroup");
   static_assert(!SILU || NT == 2, "the SiLU epilogue pairs a gate tile with its up tile");
   __shared__ __attribute__((aligned(16))) uint16_t s_x[2][ROWS * KC];
   const int tid = threadIdx.x;
   const int lane = lane_id(), wave = wave_id();
   const int l15 = lane & 15, g = lane >> 4;
-  const int n0 = (blockIdx.x * 4 + wave) * (16 * NT);
+  const int n0 = (blockIdx.x * NW + wave) * (16 * NT);
   const int s = blockIdx.y;
   const int kbeg = s * k_slice;
   const int nch = k_slice / KC;
@@ -223,11 +228,11 @@ __global__ __launch_bounds__(256, 1) void skinny_xr_kernel(
 #pragma unroll
   for (int j = 0; j < NT; ++j)
     wp[j] = w + ((size_t)(min(n0 + 16 * j, N - 16) / 16) * (K >> 6) + (kbeg >> 6)) * 1024 + lane * 8;
-  // this thread's x elements: row e / CPR, 16-B chunk e % CPR of each chunk, e = tid + 256 p
+  // this thread's x elements: row e / CPR, 16-B chunk e % CPR of each chunk, e = tid + NTH p
   const uint16_t* xsrc[XL];
 #pragma unroll
   for (int p = 0; p < XL; ++p) {
-    const int e = tid + 256 * p;
+    const int e = tid + NTH * p;
     xsrc[p] = x + (size_t)min(e / CPR, M - 1) * x_stride + kbeg + (e % CPR) * 8;
   }
 
@@ -261,7 +266,7 @@ __global__ __launch_bounds__(256, 1) void skinny_xr_kernel(
     uint16_t* sx = s_x[c & 1];
 #pragma unroll
     for (int p = 0; p < XL; ++p) {
-      const int e = tid + 256 * p;
+      const int e = tid + NTH * p;
       const int row = e / CPR, ch = e % CPR;
       const int slot = (ch & ~7) | ((ch & 7) ^ (row & 7));
       *reinterpret_cast<sk_u32x4*>(&sx[row * KC + slot * 8]) = xr[p];
@@ -478,14 +483,15 @@ extern "C" int ft_skinny_gemm_xc(const void* x, int x_stride, int M, const void*
 
 // Ring-pipelined x-chunk variant.  Requirements (checked): M <= 64,
 // N % (16*nt) == 0, K % (kc*splits) == 0 with kc = 512 (nt 2) / 256 (nt 1; two
-// 64-column workgroups per CU).  epi 0: out (one split) or ws [splits, M, N];
-// epi 1 (SiLU): nt 2, one split, out = [M, N/2].
+// 4-wave workgroups per CU).  epi 0: out (one split) or ws [splits, M, N];
+// epi 1 (SiLU): nt 2, one split, out = [M, N/2].  nw: 4 or 8 waves per workgroup.
 extern "C" int ft_skinny_gemm_xr(const void* x, int x_stride, int M, const void* w, int N, int K,
                                  float* ws, void* out, int out_stride, int splits, int nt, int epi,
-                                 hipStream_t stream) {
+                                 int nw, hipStream_t stream) {
   if (M <= 0) return 0;
   if (M > 64 || splits < 1) return -1;
   if (nt != 1 && nt != 2) return -5;
+  if (nw != 4 && nw != 8) return -7;
   if (N % (16 * nt) != 0) return -2;
   const int kc = nt == 2 ? 512 : 256;
   if (K % (kc * splits) != 0) return -3;
@@ -493,21 +499,25 @@ extern "C" int ft_skinny_gemm_xr(const void* x, int x_stride, int M, const void*
   if (epi == 1 && (nt != 2 || splits != 1)) return -6;
   if (epi == 0 && splits > 1 && ws == nullptr) return -4;
   const int mt = (M + 15) / 16;
-  const int cols = 4 * 16 * nt;
-  dim3 grid((N + cols - 1) / cols, splits), block(256);
+  const int cols = nw * 16 * nt;
+  dim3 grid((N + cols - 1) / cols, splits), block(64 * nw);
   const int k_slice = K / splits;
-#define FT_XR(MT_, NT_, KC_, E_)                                                              \
-  if (mt == MT_ && nt == NT_ && epi == E_) {                                                  \
-    hipLaunchKernelGGL((ft::skinny_xr_kernel<MT_, NT_, KC_, E_>), grid, block, 0, stream,     \
+#define FT_XR(MT_, NT_, KC_, E_, NW_)                                                         \
+  if (mt == MT_ && nt == NT_ && epi == E_ && nw == NW_) {                                     \
+    hipLaunchKernelGGL((ft::skinny_xr_kernel<MT_, NT_, KC_, E_, NW_>), grid, block, 0, stream,\
                        (const uint16_t*)x, x_stride, M, (const uint16_t*)w, K, ws,            \
                        (uint16_t*)out, out_stride, N, k_slice);                               \
     return static_cast<int>(hipGetLastError());                                               \
   }
-#define FT_XR_MT(MT_) FT_XR(MT_, 1, 256, 0) FT_XR(MT_, 2, 512, 0) FT_XR(MT_, 2, 512, 1)
-  FT_XR_MT(1)
-  FT_XR_MT(2)
-  FT_XR_MT(3)
-  FT_XR_MT(4)
+#define FT_XR_MT(MT_, NW_) FT_XR(MT_, 1, 256, 0, NW_) FT_XR(MT_, 2, 512, 0, NW_) FT_XR(MT_, 2, 512, 1, NW_)
+  FT_XR_MT(1, 4)
+  FT_XR_MT(2, 4)
+  FT_XR_MT(3, 4)
+  FT_XR_MT(4, 4)
+  FT_XR_MT(1, 8)
+  FT_XR_MT(2, 8)
+  FT_XR_MT(3, 8)
+  FT_XR_MT(4, 8)
 #undef FT_XR_MT
 #undef FT_XR
   return -5;

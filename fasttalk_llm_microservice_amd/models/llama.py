@@ -128,6 +128,13 @@ PACKED_PLAN = {
     "down": {1: (1, -3, 2), 8: (2, -3, 4), 16: (4, -3, 4), 32: (4, -3, 4), 64: (1, -5, 4)},
     "lm": {1: (1, -3, 1), 8: (2, -3, 1), 16: (4, -3, 1), 32: (1, -4, 1), 64: (2, -5, 1)},
 }
+# 33-64 rows, o / down: xr on 8-wave workgroups with 8 splits (one staged x chunk
+# feeds twice the weight columns, u = -7): cold-cache us at 50 / 64 rows o 9.8 /
+# 10.3 vs 10.4 / 10.5, down 22.8 / 23.4 vs 25.3 / 25.0 (profiles/xr8_sweep_r03.log;
+# qkv and the SiLU gate_up gain nothing there).  FT_XR8=0 keeps the 4-wave plan.
+if os.environ.get("FT_XR8", "1") != "0":
+    PACKED_PLAN["o"][64] = (1, -7, 8)
+    PACKED_PLAN["down"][64] = (1, -7, 8)
 MAX_SPLITS = 4
 
 
@@ -177,8 +184,9 @@ def pg_cfg(proj: str, rows: int, k: int) -> Tuple[int, int]:
 
 def _cfg_fits(c, n: int, k: int) -> bool:
     nt, u, sp = c
-    kq = {-4: 512, -5: 512 if nt == 2 else 256, -6: 512}.get(u, 64)
-    if u == -6 and (nt != 2 or sp != 1 or n % 32):
+    kq = {-4: 512, -5: 512 if nt == 2 else 256, -6: 512,
+          -7: 512 if nt == 2 else 256, -8: 512}.get(u, 64)
+    if u in (-6, -8) and (nt != 2 or sp != 1 or n % 32):
         return False
     return n % (16 * nt) == 0 and k % (kq * sp) == 0 and (u != -4 or n % 64 == 0)
 
@@ -693,6 +701,8 @@ class LlamaModel:
             return 0, (ops.silu_mul(y, interleaved=True) if gu else y)
         slab_ok = self._slab_ok(proj, rows) and self.ws is not None
         c = packed_cfg(proj, rows) if proj in PACKED_PLAN else None
+        while c is not None and c[2] > 1 and not _cfg_fits(c, n, k):
+            c = (c[0], c[1], c[2] // 2)   # a K the plan's split does not divide (TP shards)
         if c is not None and _cfg_fits(c, n, k):
             nt, u, sp = c
             if sp > 1 and not (slab_ok and sp * rows * n <= self.ws.numel()):
@@ -701,7 +711,7 @@ class LlamaModel:
                 ops.skinny_gemm(x, wp, ws=self.ws, splits=sp, nt=nt, u=u)
                 return sp, None
             y = ops.skinny_gemm(x, wp, splits=1, nt=nt, u=u)
-            if u == -6:  # the xr kernel's own SiLU epilogue: y is already h
+            if u in (-6, -8):  # the xr kernel's own SiLU epilogue: y is already h
                 return 0, y
             return 0, (ops.silu_mul(y, interleaved=True) if gu else y)
         if PG_BLAS_ROWS and rows >= PG_BLAS_ROWS and proj != "lm":

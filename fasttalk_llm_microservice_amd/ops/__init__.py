@@ -346,15 +346,16 @@ def skinny_gemm(x, w, out=None, ws=None, splits: int = 1, nt: int = 1, u: int = 
     slabs in ``ws`` ([splits, M, N]) for a fused epilogue; otherwise writes bf16
     ``out``.  u = -3: "pk" kernel, -4: "xc", -5: "xr" (chunk-pipelined xc),
     -6: "xr" with the SiLU epilogue on an interleave_gate_up(w, 1) image (out is
-    h = silu(gate) * up, [M, N / 2])."""
+    h = silu(gate) * up, [M, N / 2]); -7 / -8: -5 / -6 on 8-wave workgroups."""
     if splits == 1 and out is None:
-        cols = w.shape[0] // 2 if u == -6 else w.shape[0]
+        cols = w.shape[0] // 2 if u in (-6, -8) else w.shape[0]
         out = torch.empty(x.shape[0], cols, dtype=x.dtype, device=x.device)
     native().skinny_gemm(x, w, out, ws, splits, nt, u)
     return out if splits == 1 else ws
 
 
-def skinny_gemm_xr(x, w, out=None, ws=None, splits: int = 1, nt: int = 2, epi: str = "store"):
+def skinny_gemm_xr(x, w, out=None, ws=None, splits: int = 1, nt: int = 2, epi: str = "store",
+                   nw: int = 4):
     """The "xr" decode GEMM (M <= 64): epi "store": bf16 out (one split) or fp32 slabs
     [splits, M, N] in ``ws``; "silu": h = silu(gate) * up of an interleave_gate_up(w, 1)
     image, [M, N / 2]."""
@@ -362,7 +363,7 @@ def skinny_gemm_xr(x, w, out=None, ws=None, splits: int = 1, nt: int = 2, epi: s
     if out is None and (code == 1 or splits == 1):
         cols = w.shape[0] // 2 if code == 1 else w.shape[0]
         out = torch.empty(x.shape[0], cols, dtype=x.dtype, device=x.device)
-    native().skinny_gemm_xr(x, w, out, ws, splits, nt, code)
+    native().skinny_gemm_xr(x, w, out, ws, splits, nt, code, nw)
     return out if code == 1 or splits == 1 else ws
 
 

@@ -513,11 +513,12 @@ def test_w4_xr_silu_epilogue(m):
 
 @pytest.mark.parametrize("m", [1, 7, 16, 33, 64])
 @pytest.mark.parametrize("nt,u,splits", [(1, -3, 1), (2, -3, 4), (4, -3, 2), (1, -4, 1), (2, -4, 2),
-                                         (2, -5, 1), (1, -5, 1), (2, -5, 4), (1, -5, 2)])
+                                         (2, -5, 1), (1, -5, 1), (2, -5, 4), (1, -5, 2),
+                                         (2, -7, 1), (1, -7, 1), (2, -7, 4), (1, -7, 2)])
 def test_skinny_gemm(m, nt, u, splits):
     """Packed-weight decode GEMMs ("pk" u=-3, "xc" u=-4, chunk-pipelined "xr"
-    u=-5: 8 / 16 / 2 / 8 chunks per workgroup) vs fp32, bf16 out and split-K fp32
-    slabs."""
+    u=-5: 8 / 16 / 2 / 8 chunks per workgroup; u=-7 the same on 8-wave workgroups)
+    vs fp32, bf16 out and split-K fp32 slabs."""
     n, k = 1024, 4096
     w = (torch.randn(n, k, device=DEV) * 0.05).bfloat16()
     x = torch.randn(m, k, device=DEV).bfloat16()
@@ -534,15 +535,16 @@ def test_skinny_gemm(m, nt, u, splits):
 
 @pytest.mark.parametrize("m", [1, 29, 50, 64])
 @pytest.mark.parametrize("n,k", [(2048, 4096), (28672, 4096)])
-def test_skinny_gemm_xr_silu(m, n, k):
+@pytest.mark.parametrize("u", [-6, -8])
+def test_skinny_gemm_xr_silu(m, n, k, u):
     """xr with the SiLU epilogue on an interleave_gate_up(w, 1) image: h = silu(x Wg^T)
-    * (x Wu^T) straight from the GEMM (no slabs), vs fp32."""
+    * (x Wu^T) straight from the GEMM (no slabs), vs fp32; u=-8 on 8-wave workgroups."""
     wg = (torch.randn(n // 2, k, device=DEV) * 0.02).bfloat16()
     wu = (torch.randn(n // 2, k, device=DEV) * 0.02).bfloat16()
     x = torch.randn(m, k, device=DEV).bfloat16()
     ref_h = torch.nn.functional.silu(x.float() @ wg.float().t()) * (x.float() @ wu.float().t())
     wp = ops.pack_weight(ops.interleave_gate_up(torch.cat([wg, wu]), 1))
-    h = ops.skinny_gemm(x, wp, nt=2, u=-6)
+    h = ops.skinny_gemm(x, wp, nt=2, u=u)
     assert h.shape == (m, n // 2)
     _close(h.float(), ref_h, atol=3e-2, rtol=2e-2, msg="xr silu")
 
