@@ -131,7 +131,7 @@ PACKED_PLAN = {
 # 33-64 rows, o / down: xr on 8-wave workgroups with 8 splits (one staged x chunk
 # feeds twice the weight columns, u = -7): cold-cache us at 50 / 64 rows o 9.8 /
 # 10.3 vs 10.4 / 10.5, down 22.8 / 23.4 vs 25.3 / 25.0 (profiles/xr8_sweep_r03.log;
-# qkv and the SiLU gate_up gain nothing there).  FT_XR8=1 selects it (engine A/B pending).
+# qkv and the SiLU gate_up gain nothing there).  FT_XR8=1 selects it; in the decode graph it lost (7.66 vs 7.61 ms/step: the 8-split slabs cost the add+RMSNorm kernels more than the GEMMs save, profiles/ab_xr8_r03.log).
 if os.environ.get("FT_XR8", "0") == "1":
     PACKED_PLAN["o"][64] = (1, -7, 8)
     PACKED_PLAN["down"][64] = (1, -7, 8)
