@@ -8,7 +8,6 @@ processing_time_ms / tokens_per_second only, ``/health`` reports
 """
 from __future__ import annotations
 
-import json
 from typing import Any, Dict
 
 from fastapi.responses import JSONResponse
@@ -52,28 +51,20 @@ class WebSocketLLMServer(_V2):
             except Exception as e:
                 return JSONResponse(content={"status": "unhealthy", "error": str(e)}, status_code=503)
 
-    async def handle_websocket(self, websocket):
-        # v1 frame shapes are produced by filtering the v2 frames on the way out
-        orig_send = websocket.send_text
-
-        async def send_text(data: str):
-            try:
-                obj = json.loads(data)
-            except Exception:
-                return await orig_send(data)
-            t = obj.get("type")
-            if t == "session_started":
-                obj = {"type": t, "session_id": obj["session_id"]}
-            elif t == "session_configured":
-                obj = {"type": t, "config": obj.get("config", {})}
-            elif t == "response_complete":
-                s = obj.get("stats", {})
-                obj = {"type": t, "stats": {k: s[k] for k in ("tokens_generated", "processing_time_ms",
-                                                              "tokens_per_second") if k in s}}
-            return await orig_send(json.dumps(obj))
-
-        websocket.send_text = send_text
-        await super().handle_websocket(websocket)
+    def _shape_frame(self, obj: Dict[str, Any]) -> Dict[str, Any]:
+        """v1 frame shapes (reference ``websocket_server.py:160-163``, ``:232-240``), applied
+        in the server's ``send`` path so they hold on every transport -- including the
+        aiohttp socket the v2 hot path writes to directly."""
+        t = obj.get("type")
+        if t == "session_started":
+            return {"type": t, "session_id": obj["session_id"]}
+        if t == "session_configured":
+            return {"type": t, "config": obj.get("config", {})}
+        if t == "response_complete":
+            s = obj.get("stats", {})
+            return {"type": t, "stats": {k: s[k] for k in ("tokens_generated", "processing_time_ms",
+                                                           "tokens_per_second") if k in s}}
+        return obj
 
     async def _handle_message(self, session_id: str, message: Dict[str, Any], send):
         if message.get("type") == "update_config":

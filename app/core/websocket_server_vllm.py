@@ -229,8 +229,12 @@ class WebSocketLLMServer:
         # per-token cost that bounds one process's stream rate (bench/dp_ceiling.py)
         raw = (websocket.scope.get("extensions") or {}).get("fasttalk.aiohttp_ws")
 
+        shape = self._shape_frame
+
         async def send(obj: Any):
-            txt = obj if isinstance(obj, str) else json.dumps(obj)
+            # frames are shaped here, on the one path every transport shares (the v1
+            # server trims v2 frames to its shapes; token frames arrive pre-serialised)
+            txt = obj if isinstance(obj, str) else json.dumps(shape(obj))
             async with send_lock:
                 ws = raw.get("ws") if raw is not None else None
                 if ws is None:
@@ -309,6 +313,10 @@ class WebSocketLLMServer:
             self.conversation_manager.end_session(session_id)
             if self.native_handler is not None:
                 self.native_handler.forget_session(session_id)
+
+    def _shape_frame(self, obj: Dict[str, Any]) -> Dict[str, Any]:
+        """Protocol-version hook on every outgoing control frame (v2: unchanged)."""
+        return obj
 
     async def _handle_message(self, session_id: str, message: Dict[str, Any], send):
         t = message.get("type")

@@ -269,7 +269,8 @@ def main():
     client.join(timeout=30)
 
     summ = summarize(res)
-    local = {"tokens": res["tokens"], "elapsed": elapsed, "ttft": res["ttft_s"],
+    local = {"tokens": res["tokens"], "frames": res.get("frames", 0), "elapsed": elapsed,
+             "ttft": res["ttft_s"],
              "server_ttft": res.get("server_ttft_ms", []),
              "engine_ttft": res.get("engine_ttft_ms", []),
              "cached": res["cached_prompt_tokens"], "prompt": res["prompt_tokens"]}
@@ -279,6 +280,7 @@ def main():
     else:
         allr = [local]
     tokens = sum(r["tokens"] for r in allr)
+    frames = sum(r["frames"] for r in allr)
     t_max = max(r["elapsed"] for r in allr)
     ttfts = sorted(x for r in allr for x in r["ttft"])
     p = lambda q: ttfts[min(len(ttfts) - 1, int(round(q * (len(ttfts) - 1))))] if ttfts else 0.0  # noqa
@@ -315,6 +317,10 @@ def main():
             "p50_server_ttft_ms": _p50([x for r in allr for x in r["server_ttft"]]),
             "p50_engine_ttft_ms": _p50([x for r in allr for x in r["engine_ttft"]]),
             "per_session_tok_s": round(value / (a.sessions * world), 2),
+            # WS `token` frames received vs engine tokens: < 1 means the service coalesced
+            # deltas because a client fell behind (engine/sequence.py output coalescing)
+            "frames": frames,
+            "frames_per_token": round(frames / tokens, 4) if tokens else None,
             "reference_anchor": ("70B ~20 tok/s, ~1 s TTFT, multi-GPU (README.md:474,568)"
                                  if "70B" in mlabel else
                                  "8B single stream ~50-80 tok/s, ~200 ms TTFT on RTX 3090 (README.md:567)"),
@@ -402,6 +408,10 @@ def bench_tp(a, rank: int, world: int, local_rank: int):
     if a.device == "cpu":
         cfg.num_kv_blocks = cfg.num_kv_blocks or 512
         cfg.max_model_len = min(cfg.max_model_len, 2048)
+    elif cfg.tp_share_device and not cfg.num_kv_blocks:
+        # every rank's weights land on one device before any rank sizes its KV pool, so
+        # the free-memory rule would see the others' shards: a fixed pool per rank
+        cfg.num_kv_blocks = 4096
     sync = torch.cuda.synchronize if a.device == "cuda" else (lambda: None)
     eng = torchrun_tp(cfg)
     if rank != 0:
@@ -463,6 +473,8 @@ def bench_tp(a, rank: int, world: int, local_rank: int):
         "config": {"model": a.model, "global_batch": a.sessions, "seq_len": eng.max_model_len,
                    "parallelism": f"tp{world}", "custom_allreduce": a.custom_allreduce},
         "p50_ttft_ms": summ.get("p50_ttft_ms"), "p99_ttft_ms": summ.get("p99_ttft_ms"),
+        "frames": res.get("frames", 0),
+        "frames_per_token": round(res.get("frames", 0) / res["tokens"], 4) if res["tokens"] else None,
         "engine_decode_step_ms": round(metrics.get("decode_step_ms_avg", 0.0), 3),
         "engine_decode_batch_avg": round(metrics.get("decode_batch_avg", 0.0), 2),
         "init_s": round(init_s, 1),

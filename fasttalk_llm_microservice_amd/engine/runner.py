@@ -273,9 +273,14 @@ class ModelRunner:
         self._graph_msgs = 0
         self._mixed_msgs = 0
         self.stats = {"graph_replays": 0, "eager_decode": 0, "prefill_steps": 0, "captures": 0}
-        # tests: a list here collects each eager step's logits (fp32, host) -- TP-vs-TP=1
-        # numerics are compared on logits, not on greedy tokens of random weights
+        # tests: a list here collects every step's logits (fp32; eager steps on the host,
+        # graph-replayed and mixed-ahead steps as stream-ordered device copies) -- TP-vs-TP=1
+        # numerics are compared on logits, not on greedy tokens of random weights.  With
+        # logits_tap_ids a list too, each entry gets the request ids of its rows.
         self.logits_tap: Optional[list] = None
+        self.logits_tap_ids: Optional[list] = None
+        self._tap_rows: Optional[list] = None
+        self._graph_logits: Dict[int, torch.Tensor] = {}   # logits tensor of each graph
         # FT_GPU_GAPS=1: timing events around every graph-replayed decode step, so
         # gap_summary() can report how long the GPU sat idle BETWEEN consecutive
         # decode steps (the host enqueued the next one late), without a profiler
@@ -447,6 +452,8 @@ class ModelRunner:
                     num_partials=sum(c[3] for c in combine))
         sseqs = dseqs + [s for s, sm in zip(pseqs, psamp) if sm]
         host["sampling"] = self._sampling_arrays(sseqs)
+        if self.logits_tap_ids is not None:
+            self._tap_rows = [s.request_id for s in sseqs]
         return host
 
     def _mixed_run(self, host: Dict[str, object], masks) -> List[int]:
@@ -515,7 +522,7 @@ class ModelRunner:
     def _sample(self, h, sampling, masks, dev_sampling=None, dev_mask=None) -> List[int]:
         logits = self.model.compute_logits(h)
         if self.logits_tap is not None:
-            self.logits_tap.append(logits.float().cpu())
+            self._tap(logits.float().cpu())
         if dev_sampling is None:
             arrays = list(sampling) + ([masks] if masks is not None else [])
             if self.is_gpu:
@@ -544,6 +551,12 @@ class ModelRunner:
             self._comm_fault()
         return host.tolist()
 
+    def _tap(self, logits: torch.Tensor):
+        self.logits_tap.append(logits)
+        if self.logits_tap_ids is not None:
+            self.logits_tap_ids.append(self._tap_rows)
+            self._tap_rows = None
+
     # ------------------------------------------------------------------ TP fault contract
     def _arm_comm_check(self) -> Optional[torch.Tensor]:
         """Queues the fold of every rank's collective error word into the device
@@ -569,6 +582,7 @@ class ModelRunner:
             torch.cuda.synchronize(self.device)  # no graph of the old kind still running
         self.comm.disable_custom("custom collective timed out")
         self.graphs.clear()  # they captured the custom kernels; recaptured on demand
+        self._graph_logits.clear()
         if not self.comm.graph_safe():
             self.use_graphs = False
         for st in self.stg:
@@ -610,6 +624,11 @@ class ModelRunner:
                                        "rowmap": gather}, masks))
         self._set_masks(masks, n)
         self._decode_enqueue(st, nb, n, from_device=bool(ahead), gather=gather)
+        if self.logits_tap is not None and nb in self._graph_logits:
+            # copied in stream order: the next queued replay overwrites the graph's logits
+            if self.logits_tap_ids is not None:
+                self._tap_rows = [s.request_id for s in seqs]
+            self._tap(self._graph_logits[nb][:n].float().clone())
         return DecodeHandle(st, n, nb)
 
     def _set_masks(self, masks: Optional[np.ndarray], n: int):
@@ -684,6 +703,8 @@ class ModelRunner:
             meta.dec_counters = self.dec_counters
         h = self.model.forward(d["ids"], meta, self.kv)
         logits = self.model.compute_logits(h)
+        if self.logits_tap is not None:
+            self._tap(logits.float().clone())
         n = logits.shape[0]
         temp, topp, topk, seeds, steps = dev[len(names):len(names) + 5]
         ops.sample(logits, temp, topp, topk, seeds, steps, out=self.d_out[:n])
@@ -849,10 +870,12 @@ class ModelRunner:
                         dec_block_tables=self.d_bt[:nb], dec_seq_lens=self.d_seq_lens[:nb],
                         tmp_out=self.tmp_out, tmp_ml=self.tmp_ml, dec_counters=self.dec_counters)
 
-    def _graph_body(self, nb: int):
+    def _graph_body(self, nb: int, keep: bool = False):
         meta = self._decode_meta(nb)
         h = self.model.forward(self.d_input_ids[:nb], meta, self.kv)
         logits = self.model.compute_logits(h)
+        if keep:   # graph-pool memory: holds each replay's logits until the next one
+            self._graph_logits[nb] = logits
         ops.sample(logits, self.d_temp[:nb], self.d_top_p[:nb], self.d_top_k[:nb],
                    self.d_seeds[:nb], self.d_steps[:nb], out=self.d_out[:nb],
                    mask=self.d_mask[:nb] if self.d_mask is not None else None)
@@ -879,7 +902,7 @@ class ModelRunner:
             self.graph_pool = torch.cuda.graph_pool_handle()
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, pool=self.graph_pool):
-            self._graph_body(nb)
+            self._graph_body(nb, keep=True)
         self.d_slots[:nb].copy_(saved[0])
         self.d_seq_lens[:nb].copy_(saved[1])
         self.graphs[nb] = g

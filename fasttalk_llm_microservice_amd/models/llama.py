@@ -376,21 +376,29 @@ class LlamaModel:
         full unsharded tensors on the host from one seed and slices them, so TP=N
         equals TP=1 exactly; otherwise every shard is drawn on the device."""
         cfg = self.cfg
+        on_device = False
         if consistent is None and os.environ.get("FT_CONSISTENT_INIT"):
-            consistent = os.environ["FT_CONSISTENT_INIT"] == "1"  # TP-vs-TP=1 tests
+            # TP-vs-TP=1 tests; "device": the full tensors are drawn by the device's own
+            # generator (same seed -> same values in every process on the same device
+            # kind), seconds instead of minutes for 70B-shaped layers on the host
+            mode = os.environ["FT_CONSISTENT_INIT"]
+            consistent = mode in ("1", "device")
+            on_device = mode == "device" and self.device.type == "cuda"
         if consistent is None:
             consistent = cfg.num_params() < 2_000_000_000 and self.device.type == "cpu" or \
                 cfg.num_params() < 300_000_000
         if consistent:
-            g = torch.Generator().manual_seed(seed)
-            embed = (torch.randn(cfg.vocab_size, cfg.hidden_size, generator=g) * std).to(self.dtype)
+            g = torch.Generator(device=self.device if on_device else "cpu").manual_seed(seed)
+            embed = (torch.randn(cfg.vocab_size, cfg.hidden_size, generator=g, device=g.device)
+                     * std).to(self.dtype)
             shards = []
             for li in range(cfg.num_layers):
                 full = W.random_full_layer(cfg, g, std, self.dtype)
                 shards.append(W.shard_full_layer(cfg, full, self.rank, self.tp))
             self._set_layers(shards)
             lm = embed if cfg.tie_word_embeddings else \
-                (torch.randn(cfg.vocab_size, cfg.hidden_size, generator=g) * std).to(self.dtype)
+                (torch.randn(cfg.vocab_size, cfg.hidden_size, generator=g, device=g.device)
+                 * std).to(self.dtype)
             self.embed = embed.to(self.device)
             self.lm_head = W._shard_rows(lm, self.rank, self.tp).contiguous().to(self.device)
         else:

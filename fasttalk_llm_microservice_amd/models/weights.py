@@ -81,7 +81,7 @@ def random_full_layer(cfg: ModelConfig, gen: torch.Generator, std: float, dtype)
     h, i, d = cfg.hidden_size, cfg.intermediate_size, cfg.head_dim
 
     def rn(*shape):
-        return (torch.randn(*shape, generator=gen) * std).to(dtype)
+        return (torch.randn(*shape, generator=gen, device=gen.device) * std).to(dtype)
 
     return {
         "q": rn(cfg.num_heads * d, h), "k": rn(cfg.num_kv_heads * d, h),

@@ -1,5 +1,5 @@
-"""Custom xGMI collectives (csrc/kernels/custom_ar.hip) with two ranks that share
-ONE MI355X: two processes, IPC-mapped uncached regions of the same device, the
+"""Custom xGMI collectives (csrc/kernels/custom_ar.hip) with W = 2, 4 and 8 ranks
+that share ONE MI355X (every template instance of the kernels runs): W processes, IPC-mapped uncached regions of the same device, the
 same signalling protocol the TP group runs over xGMI.  Checks one-shot and
 two-shot sums and the interleaved all-gather against fp32 host references,
 eager and captured in a hipGraph (fixed kernel arguments, epochs advance on the
@@ -49,7 +49,8 @@ def _worker(rank, world, port, q):
         ar.all_reduce(x)
         torch.cuda.synchronize()
         errs.append((x.float().cpu() - expect).abs().max().item())
-    # hipGraph: the same kernel replayed with new data in the captured buffer
+    # hipGraph: the same kernel replayed with new data in the captured buffer (one-shot,
+    # then the two-shot and fused-norm forms captured in one graph as a TP layer does)
     n = 16 * 4096
     buf = torch.zeros(n, device="cuda").bfloat16()
     s = torch.cuda.Stream()
@@ -66,6 +67,35 @@ def _worker(rank, world, port, q):
         g.replay()
         torch.cuda.synchronize()
         errs.append((buf.float().cpu() - sum(x.float() for x in xs)).abs().max().item())
+    ar.two_shot_bytes = 0
+    buf2 = torch.zeros(n, device="cuda").bfloat16()
+    rows, hidden = 8, 8192
+    res = torch.zeros(rows, hidden, device="cuda").bfloat16()
+    part = torch.zeros(rows, hidden, device="cuda").bfloat16()
+    outn = torch.empty(rows, hidden, device="cuda").bfloat16()
+    wn = torch.ones(hidden, device="cuda").bfloat16()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        ar.all_reduce(buf2)
+        ar.all_reduce_add_rmsnorm(outn, res, wn, 1e-5, rows, x=part)
+    torch.cuda.current_stream().wait_stream(s)
+    g2 = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g2):
+        ar.all_reduce(buf2)
+        ar.all_reduce_add_rmsnorm(outn, res, wn, 1e-5, rows, x=part)
+    for trial in range(14, 17):
+        xs = _inputs(trial, world, n)
+        ps = [(torch.randn(rows, hidden, generator=torch.Generator().manual_seed(7 * trial + r))
+               * 0.3).bfloat16() for r in range(world)]
+        buf2.copy_(xs[rank].cuda())
+        part.copy_(ps[rank].cuda())
+        r0 = res.float().cpu()
+        g2.replay()
+        torch.cuda.synchronize()
+        errs.append((buf2.float().cpu() - sum(x.float() for x in xs)).abs().max().item())
+        r_exp = (r0 + sum(p.float() for p in ps).bfloat16().float()).bfloat16().float()
+        errs.append((res.float().cpu() - r_exp).abs().max().item())
+    ar.two_shot_bytes = 1 << 62
     # two-shot (reduce-scatter + all-gather), forced at every size
     ar.two_shot_bytes = 0
     for trial, n in enumerate([64 * 4096, 8 * 4096, 8 * 3, 50 * 4096], start=20):
@@ -86,7 +116,8 @@ def _worker(rank, world, port, q):
     # fp32 split-K slabs or bf16 rows; every rank ends with the same residual
     fused_errs = []
     for trial, (rows, hidden, splits) in enumerate([(50, 4096, 4), (1, 8192, 2), (64, 2048, 0),
-                                                    (33, 8192, 1)], start=40):
+                                                    (33, 8192, 1), (17, 8192, 0), (8, 6144, 3)],
+                                                   start=40):
         gen = lambda r: torch.Generator().manual_seed(100 * trial + r)  # noqa: E731
         if splits:
             parts = [torch.randn(splits, rows, hidden, generator=gen(r)) * 0.3 for r in range(world)]
@@ -140,20 +171,22 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_custom_allreduce_two_ranks_one_gpu():
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_custom_allreduce_ranks_share_one_gpu(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     try:
-        results = [q.get(timeout=240) for _ in procs]
+        results = [q.get(timeout=300) for _ in procs]
     finally:
         for p in procs:
             p.join(timeout=60)
             if p.is_alive():
                 p.kill()
+    assert sorted(r[0] for r in results) == list(range(world))
     for rank, errs, healthy, spin_us, unreduced, fast, flagged in results:
         assert healthy, f"rank {rank}: a wait ran out of spin budget"
         assert max(errs) < 0.07, f"rank {rank}: max abs err {max(errs)} ({errs})"

@@ -22,16 +22,20 @@ def _cfg(**kw):
     return EngineConfig(**base)
 
 
-def test_tp2_generation_matches_tp1():
+@pytest.mark.parametrize("tp", [2, 4])
+def test_tp_generation_matches_tp1(tp):
+    """TP=4 splits tiny's 2 kv heads over 4 ranks: each kv head is replicated on two
+    ranks (weights.kv_head_range) and the step ring has 3 readers."""
     from fasttalk_llm_microservice_amd.parallel.tp import spawn_tp_engine
 
     rng = np.random.default_rng(0)
     prompts = [rng.integers(0, 120000, n).tolist() for n in (9, 70, 30)]
     sp = SamplingParams(temperature=0, max_tokens=6, ignore_eos=True)
     ref = LLMEngine(_cfg()).generate(prompts, sp)
-    eng = spawn_tp_engine(_cfg(tp_size=2))
+    eng = spawn_tp_engine(_cfg(tp_size=tp))
     try:
-        assert eng.runner.model.nq == 4 and eng.runner.model.nkv == 1  # half the heads per rank
+        assert eng.runner.model.nq == 8 // tp and eng.runner.model.nkv == 1  # heads per rank
+        assert len(eng.tp_group.procs) == tp - 1
         out = eng.generate(prompts, sp)
         # seeded sampling is identical across ranks too (every rank samples the gathered logits)
         sp2 = SamplingParams(temperature=0.8, top_p=0.9, max_tokens=4, seed=7, ignore_eos=True)

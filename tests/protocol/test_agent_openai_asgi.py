@@ -288,6 +288,52 @@ def test_aiohttp_asgi_transport_serves_ws_and_http(monkeypatch, engine):
     asyncio.run(main())
 
 
+def test_v1_frames_hold_on_the_aiohttp_transport(monkeypatch, engine):
+    """the v1 server's frame shapes (reference
+    websocket_server.py:160-163) must survive the raw-socket send path of the
+    production transport, not only Starlette's TestClient."""
+    import aiohttp
+
+    from app.core.websocket_server import WebSocketLLMServer as V1
+    from app.server.asgi_aiohttp import AiohttpASGIServer
+    from app.utils.config import Config
+
+    monkeypatch.setenv("LLM_PROVIDER", "native")
+    monkeypatch.setenv("ENABLE_PYDANTIC_AI", "false")
+    srv = V1(Config(), engine=engine)
+
+    async def main():
+        asgi = AiohttpASGIServer(srv.app, "127.0.0.1", 0)
+        await asgi.start()
+        try:
+            async with aiohttp.ClientSession() as s:
+                async with s.get(f"http://127.0.0.1:{asgi.port}/health") as r:
+                    h = await r.json()
+                    assert "ollama_connection" in h and "provider" not in h
+                async with s.ws_connect(f"ws://127.0.0.1:{asgi.port}/ws/llm") as ws:
+                    hello = json.loads((await ws.receive()).data)
+                    await ws.send_str(json.dumps({"type": "start_session", "config": {
+                        "max_tokens": 3, "temperature": 0, "ignore_eos": True}}))
+                    conf = json.loads((await ws.receive()).data)
+                    await ws.send_str(json.dumps({"type": "user_message", "text": "hi"}))
+                    while True:
+                        f = json.loads((await ws.receive()).data)
+                        if f["type"] == "response_complete":
+                            break
+                    await ws.send_str(json.dumps({"type": "update_config", "config": {}}))
+                    err = json.loads((await ws.receive()).data)
+                    return hello, conf, f, err
+        finally:
+            await asgi.stop()
+
+    hello, conf, done, err = asyncio.run(main())
+    assert set(hello) == {"type", "session_id"}
+    assert set(conf) == {"type", "config"}
+    assert set(done["stats"]) == {"tokens_generated", "processing_time_ms", "tokens_per_second"}
+    assert done["stats"]["tokens_generated"] == 3
+    assert err["type"] == "error" and err["error"]["code"] == "unknown_message_type"
+
+
 # ----------------------------------------------------------------------------- monitoring
 def test_service_monitor_metrics_and_prometheus(monkeypatch, engine):
     from app.core.websocket_server_vllm import WebSocketLLMServer
