@@ -70,12 +70,22 @@ class WebSocketLauncher:
 
             self._pool = WorkerPool(n, self.config.host, self.config.port,
                                     tp=int(getattr(self.config, "engine_tp_size", 1) or 1),
-                                    max_restarts=int(os.environ.get("ENGINE_MAX_RESTARTS", "3")))
+                                    max_restarts=int(os.environ.get("ENGINE_MAX_RESTARTS", "3")),
+                                    max_connections=self.config.max_connections)
+            if self.monitor is not None and hasattr(self.monitor, "attach_node"):
+                self.monitor.attach_node(self._pool.board)   # :9092 reports every worker
             self._pool.start()
             try:
+                if not self._pool.wait_ready():
+                    # a worker failed its backend check (or died) before serving: exit 1
+                    # like the single-process launcher (reference websocket_launcher.py:105)
+                    sys.exit(1)
                 self._pool.run()
-            except (KeyboardInterrupt, SystemExit):
+            except KeyboardInterrupt:
                 pass
+            finally:
+                self._pool.stop()
+                self._pool.close()
             return
         logger.info(f"Starting LLM WebSocket server (provider: {self.config.llm_provider})")
         self.server = self._create_server()

@@ -80,6 +80,10 @@ class WebSocketLLMServer:
         self.ollama_handler = None
         self.use_pydantic_ai = False
         self._engine = engine
+        # DP service workers (app/server/workers.py): the node board makes /health and
+        # /stats describe the whole node; None = this process is the whole service
+        self.node = None
+        self.node_index: Optional[int] = None
         self._init_llm_handler()
         self._register_routes()
 
@@ -168,6 +172,16 @@ class WebSocketLLMServer:
                     "active_connections": self.connection_manager.get_active_count(),
                     "active_sessions": self.conversation_manager.get_session_count(),
                 }
+                if self.node is not None:
+                    # one service: healthy only while every worker is up and serving
+                    workers = self.node.workers()
+                    node_ok = all(w["alive"] and w["ready"] and w["heartbeat_fresh"]
+                                  and w["backend_ok"] for w in workers)
+                    ok = ok and node_ok
+                    body["status"] = "healthy" if ok else "degraded"
+                    body["active_connections"] = self.node.node_active()
+                    body["worker"] = self.node_index
+                    body["workers"] = workers
                 return JSONResponse(content=body, status_code=200 if ok else 503)
             except Exception as e:
                 return JSONResponse(content={"status": "unhealthy", "error": str(e)}, status_code=503)
@@ -181,6 +195,16 @@ class WebSocketLLMServer:
                 "provider": self.provider,
                 "pydantic_ai_enabled": self.use_pydantic_ai,
             }
+            if self.node is not None:
+                from app.server.node_state import merge_service_stats
+
+                alive = {w["index"] for w in self.node.workers() if w["alive"]}
+                parts = [body] + [s for s in self.node.snapshots()
+                                  if s and s.get("index") != self.node_index
+                                  and s.get("index") in alive]
+                body.update(merge_service_stats(parts, self.node.max_connections,
+                                                active=self.node.node_active()))
+                body["workers"] = self.node.workers()
             eng = self.engine_metrics()
             if eng is not None:
                 body["engine"] = eng

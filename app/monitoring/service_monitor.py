@@ -41,10 +41,24 @@ class ServiceMonitor:
         self._ttft = deque(maxlen=2048)
         self._lock = threading.Lock()
         self.server = None  # WebSocketLLMServer, for engine gauges
+        self.node = None    # app.server.node_state.NodeBoard: DP workers feed this monitor
 
     def attach_server(self, server):
         self.server = server
         server.monitor = self
+
+    def attach_node(self, board):
+        """Parent of the DP service workers: /metrics sums the workers' counters
+        (each worker publishes its own ServiceMonitor through the node board)."""
+        self.node = board
+
+    def counters(self) -> Dict[str, Any]:
+        """Raw counters (published by a DP worker, summed by the parent)."""
+        with self._lock:
+            return {"requests": self.request_count, "generations": self.generation_count,
+                    "errors": self.error_count, "total_tokens_generated": self.total_tokens_generated,
+                    "total_processing_time": self.total_processing_time,
+                    "ttft": list(self._ttft)[-256:]}
 
     def record_request(self):
         with self._lock:
@@ -66,19 +80,32 @@ class ServiceMonitor:
         return time.time() - self.start_time
 
     def get_metrics(self) -> Dict[str, Any]:
-        with self._lock:
-            n = self.generation_count
-            ttft = list(self._ttft)
-            m = {
-                "uptime_seconds": self.get_uptime(),
-                "requests": self.request_count,
-                "generations": n,
-                "errors": self.error_count,
-                "total_tokens_generated": self.total_tokens_generated,
-                "avg_processing_time_seconds": self.total_processing_time / n if n else 0.0,
-                "ttft_p50_ms": 1e3 * _pct(ttft, 0.5),
-                "ttft_p99_ms": 1e3 * _pct(ttft, 0.99),
-            }
+        c = self.counters()
+        snaps = []
+        if self.node is not None:
+            from app.server.node_state import merge_monitor
+
+            snaps = [s for s in self.node.snapshots() if s]
+            c = merge_monitor([c] + [s.get("monitor", {}) for s in snaps])
+        n = c["generations"]
+        m = {
+            "uptime_seconds": self.get_uptime(),
+            "requests": c["requests"],
+            "generations": n,
+            "errors": c["errors"],
+            "total_tokens_generated": c["total_tokens_generated"],
+            "avg_processing_time_seconds": c["total_processing_time"] / n if n else 0.0,
+            "ttft_p50_ms": 1e3 * _pct(c["ttft"], 0.5),
+            "ttft_p99_ms": 1e3 * _pct(c["ttft"], 0.99),
+        }
+        if self.node is not None:
+            m["workers"] = self.node.workers()
+            by = {s.get("index"): s for s in snaps}
+            for w in m["workers"]:
+                s = by.get(w["index"]) or {}
+                w["generations"] = s.get("monitor", {}).get("generations", 0)
+                if s.get("engine"):
+                    w["engine"] = s["engine"]
         if self.server is not None:
             try:
                 eng = self.server.engine_metrics()
@@ -124,6 +151,12 @@ def prometheus_text(metrics: Dict[str, Any], prefix: str = "fasttalk") -> str:
                         emit(f"engine_{ek}_{sk}", sv)
                 else:
                     emit(f"engine_{ek}", ev)
+        elif k == "workers" and isinstance(v, list):
+            for w in v:
+                lab = f'{{worker="{w["index"]}"}}'
+                for wk in ("alive", "ready", "active_connections", "generations", "restarts"):
+                    if wk in w:
+                        emit(f"worker_{wk}", w[wk], lab)
         elif k == "gpus" and isinstance(v, list):
             for g in v:
                 emit("gpu_hbm_used_gb", g["hbm_used_gb"], f'{{gpu="{g["index"]}"}}')

@@ -72,8 +72,11 @@ class ConnectionManager:
     """Thread-safe registry enforcing ``max_connections``; per-connection counters
     are folded into the global totals when a connection is removed."""
 
-    def __init__(self, max_connections: int = 50):
+    def __init__(self, max_connections: int = 50, admission: Any = None):
         self.max_connections = max_connections
+        # node-wide gate of the DP service workers (app/server/node_state.py): an object
+        # with try_admit() / release(); None = this process is the whole service
+        self.admission = admission
         self.active_connections: Dict[str, ConnectionInfo] = {}
         self._lock = Lock()
         self.total_connections = 0
@@ -94,6 +97,12 @@ class ConnectionManager:
             if session_id in self.active_connections:
                 logger.warning("Session %s already exists; replacing it", session_id)
                 del self.active_connections[session_id]
+                if self.admission is not None:
+                    self.admission.release()
+            if self.admission is not None and not self.admission.try_admit():
+                logger.warning("Max connections (%d) reached on the node; rejecting %s",
+                               self.max_connections, session_id)
+                return None
             info = ConnectionInfo(session_id=session_id, websocket=websocket,
                                   state=ConnectionState.ACTIVE, config=dict(config or {}))
             self.active_connections[session_id] = info
@@ -105,6 +114,8 @@ class ConnectionManager:
             info = self.active_connections.pop(session_id, None)
             if info is None:
                 return False
+            if self.admission is not None:
+                self.admission.release()
             self.total_disconnections += 1
             for name in _TOTALS:
                 setattr(self, "total_" + name, getattr(self, "total_" + name) + getattr(info, name))
@@ -170,6 +181,8 @@ class ConnectionManager:
                      if c.get_idle_time() > idle_timeout]
             for sid in stale:
                 del self.active_connections[sid]
+                if self.admission is not None:
+                    self.admission.release()
         if stale:
             logger.info("Cleaned up %d idle connections", len(stale))
         return len(stale)

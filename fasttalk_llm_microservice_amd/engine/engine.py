@@ -92,6 +92,7 @@ class LLMEngine:
         # queued decode steps, oldest first: [(batch, DecodeHandle)], at most
         # cfg.pipeline_depth + 1 of them (ENGINE_PIPELINE_DEPTH)
         self._inflight: List[_Inflight] = []
+        self._executing: Optional[ScheduledBatch] = None   # drained step being executed
         self.pipeline_depth = max(1, int(getattr(cfg, "pipeline_depth", 1)))
         # ENGINE_MIXED_AHEAD (default on): waiting prompts are scheduled into a mixed
         # step queued behind the running decode step instead of draining the queue.
@@ -145,7 +146,10 @@ class LLMEngine:
             else:
                 # the grammar's fixed head (e.g. '{"name": "' of a tool call) is output the
                 # model cannot choose: appended now, prefilled with the prompt
-                seq.jf_text, seq.jf_ids = self._jump_forward(seq, room=params.max_tokens - 1)
+                # bounded by max_model_len too: the head is prefilled with the prompt, and
+                # positions past max_model_len have no RoPE row / KV room
+                room = min(params.max_tokens - 1, self.max_model_len - 1 - len(prompt_ids))
+                seq.jf_text, seq.jf_ids = self._jump_forward(seq, room=max(0, room))
         self.scheduler.add(seq)
         self.stats["requests"] += 1
         return seq
@@ -414,10 +418,23 @@ class LLMEngine:
         the failing step was the swap itself their host copies may be garbage).
         ``reset_cache`` (a collective fault: KV written from un-reduced partial sums
         may sit in committed blocks) also empties the prefix cache."""
+        # sequences of queued / executing steps first: a mixed-ahead step's prompts left
+        # `waiting` when it was scheduled and join `running` only in post_step, so
+        # without this they would never finish and their KV blocks would leak (ADVICE r3)
+        limbo = []
+        for e in self._inflight:
+            limbo += list(e.batch.prefill_seqs) + list(e.batch.sampled_seqs())
+        if self._executing is not None:
+            limbo += list(self._executing.prefill_seqs) + list(self._executing.decode_seqs)
+            self._executing = None
         self.reset_inflight()
         sched = self.scheduler
-        for seq in list(sched.running) + list(sched.waiting) + list(sched.swapped) + \
+        seen = set()
+        for seq in limbo + list(sched.running) + list(sched.waiting) + list(sched.swapped) + \
                 list(sched.background):
+            if id(seq) in seen or seq.status == SeqStatus.FINISHED:
+                continue
+            seen.add(id(seq))
             self._finalize(seq, "error", emit=True, error=error)
         if reset_cache and hasattr(self.bm, "reset_prefix_cache"):
             self.bm.reset_prefix_cache()
@@ -453,7 +470,9 @@ class LLMEngine:
             return self._step_pipelined()
         sampled_seqs = batch.sampled_seqs()
         masks = self._masks_for(sampled_seqs)
+        self._executing = batch
         toks = self.runner.execute(batch, masks)
+        self._executing = None
         t1 = time.perf_counter()
         self.scheduler.post_step(batch)
         for seq, tok in zip(sampled_seqs, toks):
@@ -728,9 +747,13 @@ class AsyncEngine:
     @classmethod
     def from_config(cls, cfg: EngineConfig) -> "AsyncEngine":
         if cfg.tp_size > 1:
+            import os as _os
+
             from ..parallel.tp import spawn_tp_engine
 
-            return cls(spawn_tp_engine(cfg))
+            # a DP service worker owns GPUs [ENGINE_DEVICE_BASE, +tp) (app/server/workers.py)
+            base = int(_os.environ.get("ENGINE_DEVICE_BASE", "0") or 0)
+            return cls(spawn_tp_engine(cfg, device_base=base))
         return cls(LLMEngine(cfg))
 
     # ------------------------------------------------------------------ lifecycle

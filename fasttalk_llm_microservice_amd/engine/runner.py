@@ -9,6 +9,7 @@ run eagerly (variable token counts) through the same HIP kernels.
 """
 from __future__ import annotations
 
+import contextlib
 import logging
 import math
 import os
@@ -272,6 +273,11 @@ class ModelRunner:
             if stall else (None, 0.0)
         self._graph_msgs = 0
         self._mixed_msgs = 0
+        # the first eager steps and graph warm-ups of a TP group wait for peers with a
+        # long spin budget (every rank counts the same steps: same message order)
+        self._warm_left = int(os.environ.get("ENGINE_TP_WARM_STEPS", "4")) \
+            if comm.world_size > 1 else 0
+        self._trace_tp = os.environ.get("FT_TP_TRACE", "0") == "1" and comm.world_size > 1
         self.stats = {"graph_replays": 0, "eager_decode": 0, "prefill_steps": 0, "captures": 0}
         # tests: a list here collects every step's logits (fp32; eager steps on the host,
         # graph-replayed and mixed-ahead steps as stream-ordered device copies) -- TP-vs-TP=1
@@ -456,7 +462,23 @@ class ModelRunner:
             self._tap_rows = [s.request_id for s in sseqs]
         return host
 
+    def _long_waits(self):
+        """Context: the custom collectives' first-steps spin budget while warm steps last."""
+        if self._warm_left <= 0 or self.comm.custom is None:
+            return contextlib.nullcontext()
+        self._warm_left -= 1
+        return self.comm.custom.long_waits()
+
     def _mixed_run(self, host: Dict[str, object], masks) -> List[int]:
+        t0 = time.perf_counter() if self._trace_tp else 0.0
+        with self._long_waits():
+            out = self._mixed_run_inner(host, masks)
+        if self._trace_tp:
+            log.warning("TP trace rank %d: mixed step %d rows in %.1f ms", self.comm.rank,
+                        len(host["ids"]), 1e3 * (time.perf_counter() - t0))
+        return out
+
+    def _mixed_run_inner(self, host: Dict[str, object], masks) -> List[int]:
         self.stats["prefill_steps"] += 1
         nd = host["nd"]
         qsl = host["qsl"]
@@ -895,7 +917,7 @@ class ModelRunner:
         self.d_seq_lens[:nb].fill_(0)
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
-        with torch.cuda.stream(s):
+        with torch.cuda.stream(s), self._long_waits():
             self._graph_body(nb)  # warm-up (allocator, lazy init)
         torch.cuda.current_stream(self.device).wait_stream(s)
         if self.graph_pool is None:

@@ -26,11 +26,13 @@ this module owns the IPC plumbing and the fault contract:
   the whole group switches to RCCL (:meth:`disable` on every rank, graphs
   recaptured).
 
-Opt-in (``ENGINE_CUSTOM_ALLREDUCE=1``): messages above ``max_bytes`` (prefill)
-always go through RCCL.
+On by default for tensor parallelism on GPUs (``ENGINE_CUSTOM_ALLREDUCE=0`` turns it
+off, engine/config.py); messages above ``max_bytes`` (long prefills) always go
+through RCCL.
 """
 from __future__ import annotations
 
+import contextlib
 import logging
 import os
 from typing import List, Optional
@@ -55,8 +57,14 @@ class CustomAllReduce:
         self.rank, self.world = rank, world
         self.max_bytes = int(max_bytes)
         if spin_budget is None:
-            spin_budget = int(os.environ.get("ENGINE_CUSTOM_AR_SPIN", str(1 << 23)))  # ~1.6 s (0.19 us/spin measured)
+            # 0.19 us per spin with 2 ranks, 0.36 us with 8 ranks sharing one MI355X:
+            # 2^25 spins = 6-12 s before a missing peer is declared dead
+            spin_budget = int(os.environ.get("ENGINE_CUSTOM_AR_SPIN", str(1 << 25)))
         self.spin_budget = int(spin_budget)
+        # the group's first steps (lazy library / code-object loads, allocator growth on
+        # one rank while the others already wait) get a budget of minutes: long_waits()
+        self.first_spin_budget = max(self.spin_budget,
+                                     int(os.environ.get("ENGINE_CUSTOM_AR_SPIN_FIRST", str(1 << 28))))
         if two_shot_bytes is None:
             env = os.environ.get("ENGINE_CUSTOM_AR_TWO_SHOT")
             two_shot_bytes = int(env) if env else {8: 512 << 10, 4: 1 << 20}.get(world, 1 << 62)
@@ -117,6 +125,16 @@ class CustomAllReduce:
         self._C.custom_ar_allgather(out, x, self.peers, self.rank, self.world, self.max_bytes,
                                     self.spin_budget)
         return out
+
+    @contextlib.contextmanager
+    def long_waits(self):
+        """Eager collectives issued inside use the first-steps spin budget."""
+        saved = self.spin_budget
+        self.spin_budget = self.first_spin_budget
+        try:
+            yield
+        finally:
+            self.spin_budget = saved
 
     def export_error(self):
         """err_flag <- OR of every rank's error word (stream ordered, graph-safe)."""

@@ -82,3 +82,130 @@ def test_dp_workers_share_one_port_and_restart(monkeypatch):
     finally:
         pool.stop()
     assert not any(pool.alive())
+
+
+def _http_json(port, path):
+    import json
+    import urllib.error
+    import urllib.request
+
+    try:
+        with urllib.request.urlopen(f"http://127.0.0.1:{port}{path}", timeout=10) as r:
+            return r.status, json.loads(r.read())
+    except urllib.error.HTTPError as e:
+        return e.code, json.loads(e.read())
+
+
+def _wait_health(port, code, timeout=120):
+    t0 = time.time()
+    while time.time() - t0 < timeout:
+        try:
+            st, body = _http_json(port, "/health")
+            if st == code:
+                return body
+        except OSError:
+            pass
+        time.sleep(0.3)
+    raise TimeoutError(f"/health never answered {code}")
+
+
+def test_dp_workers_behave_as_one_service(monkeypatch):
+    """(i) the node-wide LLM_MAX_CONNECTIONS cap, (ii) the parent's
+    :9092 /metrics counts generations from every worker, /stats sums them, (iii) a
+    killed worker turns /health 503 on the survivors until it is back."""
+    import json
+
+    import aiohttp
+
+    from app.monitoring.service_monitor import MonitoringServer, ServiceMonitor
+    from app.server.workers import WorkerPool
+
+    for k, v in {"ENGINE_SYNTHETIC_STEP_MS": "2", "COMPUTE_DEVICE": "cpu", "LLM_PROVIDER": "native",
+                 "ENGINE_MODEL": "tiny", "ENABLE_PYDANTIC_AI": "false", "LOG_LEVEL": "WARNING",
+                 "LLM_MAX_CONNECTIONS": "5"}.items():
+        monkeypatch.setenv(k, v)
+    port = _free_port()
+    pool = WorkerPool(2, "127.0.0.1", port, max_restarts=1, max_connections=5)
+    mon = ServiceMonitor()
+    mon.attach_node(pool.board)
+    ms = MonitoringServer(port=0, monitor=mon).app.test_client()
+    pool.start()
+    try:
+        assert pool.wait_ready(180)
+        body = _wait_health(port, 200)
+        assert len(body["workers"]) == 2 and all(w["ready"] for w in body["workers"])
+
+        # (i) 5 sessions fill the node whichever worker accepted them; the 6th is refused
+        async def cap():
+            async with aiohttp.ClientSession() as s:
+                socks = []
+                for _ in range(5):
+                    ws = await s.ws_connect(f"ws://127.0.0.1:{port}/ws/llm")
+                    assert json.loads((await ws.receive()).data)["type"] == "session_started"
+                    socks.append(ws)
+                extra = await s.ws_connect(f"ws://127.0.0.1:{port}/ws/llm")
+                refused = json.loads((await extra.receive()).data)
+                await extra.close()
+                st, stats = _http_json(port, "/stats")
+                await socks[0].close()
+                await asyncio.sleep(0.5)
+                again = await s.ws_connect(f"ws://127.0.0.1:{port}/ws/llm")
+                ok = json.loads((await again.receive()).data)
+                for ws in socks[1:] + [again]:
+                    await ws.close()
+                return refused, stats, ok
+        refused, stats, ok = asyncio.run(cap())
+        assert refused["type"] == "error" and refused["error"]["code"] == "max_connections"
+        assert stats["connections"]["active_connections"] == 5
+        assert stats["connections"]["max_connections"] == 5
+        assert ok["type"] == "session_started", "a closed session must free its slot"
+
+        # (ii) generations from both workers reach the parent's monitor and /stats
+        time.sleep(1.0)
+        r = _sessions(port, 4, turns=2)
+        assert r["turns"] == 8
+        time.sleep(1.5)   # two snapshot periods
+        m = ms.get("/metrics").get_json()
+        assert m["generations"] == 8 and m["total_tokens_generated"] == 8 * 6, m
+        per = [w["generations"] for w in m["workers"]]
+        assert sum(per) == 8 and min(per) >= 1, per
+        st, stats = _http_json(port, "/stats")
+        assert stats["connections"]["total_generations_completed"] == 8
+        assert b"fasttalk_worker_ready" in ms.get("/metrics/prometheus").data
+
+        # (iii) a dead worker: 503 on the survivor until the respawned worker serves
+        victim = pool.procs[0]
+        victim.kill()
+        victim.join(10)
+        pool.supervise_once()
+        body = _wait_health(port, 503, timeout=30)
+        assert not body["workers"][0]["ready"] and body["status"] == "degraded"
+        body = _wait_health(port, 200, timeout=180)
+        assert body["workers"][0]["restarts"] == 1
+        r = _sessions(port, 4)
+        assert r["turns"] == 4
+    finally:
+        pool.stop()
+        pool.close()
+
+
+def test_dp_worker_startup_check_fails_before_serving(monkeypatch):
+    """A worker whose backend is unreachable exits 1 before opening the port
+    (reference websocket_launcher.py:104-105); the pool reports the failed start."""
+    from app.server.workers import STARTUP_FAILED, WorkerPool
+
+    dead = _free_port()
+    for k, v in {"LLM_PROVIDER": "vllm", "VLLM_BASE_URL": f"http://127.0.0.1:{dead}/v1",
+                 "ENABLE_PYDANTIC_AI": "false", "LOG_LEVEL": "WARNING", "COMPUTE_DEVICE": "cpu"}.items():
+        monkeypatch.setenv(k, v)
+    port = _free_port()
+    pool = WorkerPool(1, "127.0.0.1", port, max_restarts=0).start()
+    try:
+        assert not pool.wait_ready(120)
+        pool.procs[0].join(10)
+        assert pool.procs[0].exitcode == STARTUP_FAILED
+        with pytest.raises(OSError):
+            socket.create_connection(("127.0.0.1", port), timeout=1).close()
+    finally:
+        pool.stop()
+        pool.close()

@@ -80,6 +80,7 @@ def test_tp2_on_one_gpu_matches_tp1_and_survives_an_allreduce_timeout(tp1_tokens
     # stalls until rank 0's all-reduce has timed out (<= 60 s)
     monkeypatch.setenv("FT_FAULT_TP_STALL", "20:60")
     monkeypatch.setenv("ENGINE_CUSTOM_AR_SPIN", str(1 << 20))
+    monkeypatch.setenv("ENGINE_TP_WARM_STEPS", "0")
     eng = spawn_tp_engine(_cfg(tp_size=2, tp_share_device=True, custom_allreduce=True))
     try:
         r = eng.runner
@@ -205,6 +206,7 @@ def test_tp2_allreduce_timeout_in_a_no_logits_prefill_chunk(monkeypatch):
     monkeypatch.setenv("FT_CONSISTENT_INIT", "1")
     monkeypatch.setenv("FT_FAULT_TP_STALL", "m1:60")   # the worker's first eager step
     monkeypatch.setenv("ENGINE_CUSTOM_AR_SPIN", str(1 << 20))
+    monkeypatch.setenv("ENGINE_TP_WARM_STEPS", "0")    # no long first-step waits
     eng = spawn_tp_engine(_cfg(tp_size=2, tp_share_device=True, custom_allreduce=True,
                                enable_prefix_caching=True, max_num_batched_tokens=64))
     try:

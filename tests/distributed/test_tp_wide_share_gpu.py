@@ -67,7 +67,8 @@ def _tp1_teacher_forced(model, seqs):
     return torch.stack(rows)
 
 
-@pytest.mark.parametrize("tp,model", [(4, "tiny-2k"), (8, "tiny-2k"), (8, "llama3-70b-2l")])
+@pytest.mark.parametrize("tp,model", [(4, "tiny-2k"), (8, "tiny-2k"), (4, "llama3-70b-2l"),
+                                      (8, "llama3-70b-2l")])
 def test_tp_wide_one_gpu_every_step_logits_match_tp1(tp, model, monkeypatch):
     import torch
 

@@ -511,3 +511,23 @@ def test_lazy_tool_grammar_binds_only_when_the_model_opens_a_call(opens_call):
     else:
         assert text.startswith(" hello") and len(ids) == 40
         assert eng.stats["lazy_grammar_bound"] == 0
+
+
+def test_jump_forward_head_stays_within_max_model_len(tiny_engine):
+    """the forced tool-call head appended at admission is bounded by
+    max_model_len (it is prefilled with the prompt; RoPE has max_model_len + 1 rows)."""
+    from fasttalk_llm_microservice_amd.engine.guided import tool_call_ast
+
+    tools = [{"type": "function", "function": {"name": "duckduckgo_search", "parameters": {
+        "type": "object", "properties": {"query": {"type": "string"}}, "required": ["query"]}}}]
+    spec = GuidedSpec(tool_call_ast(tools))
+    eng = tiny_engine
+    n = eng.max_model_len - 2
+    sp = SamplingParams(temperature=1.0, max_tokens=64, seed=1, guided=spec)
+    seq = eng.add_request("jf-edge", [7] * n, sp)
+    assert 0 < len(seq.jf_ids) <= 1 and seq.n_tokens <= eng.max_model_len - 1
+    outs = []
+    while eng.has_work():
+        outs += [o for o in eng.step() if o.request_id == "jf-edge"]
+    assert outs and outs[-1].finished and outs[-1].finish_reason == "length"
+    assert eng.bm.num_free() == eng.bm.num_blocks or eng.bm.num_cached() > 0

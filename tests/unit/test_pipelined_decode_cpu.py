@@ -265,3 +265,56 @@ def test_prompt_arriving_during_drain_is_queued_behind_running_step():
     got, eng = run(True)
     assert got == ref
     assert eng.stats["mixed_ahead_drain"] > 0
+
+
+def _failing_collect(self, h):
+    """decode_collect fails once a mixed step has been queued behind the step."""
+    if self.mixed and not self.__dict__.get("failed"):
+        self.failed = True
+        raise RuntimeError("injected device error")
+    return list(h.out)
+
+
+_FailBehindMixed = type("ModelRunner", (ModelRunner,), {"decode_collect": _failing_collect})
+
+
+def test_failure_with_a_queued_mixed_step_finishes_every_request():
+    """a step that fails while a mixed-ahead step is queued behind it.
+    The mixed step's prompts had left `waiting` and would only join `running` in
+    post_step; fail_unfinished must end them too (an error output each) and every
+    KV block must come back."""
+    import os
+
+    os.environ["ENGINE_MIXED_AHEAD"] = "1"
+    try:
+        cfg = EngineConfig(model="tiny", device="cpu", block_size=4, async_output=True,
+                           pipeline_depth=1, max_num_seqs=32)
+        runner = _FailBehindMixed()
+        eng = LLMEngine(cfg, runner=runner)
+        done = {}
+
+        def add(i):
+            eng.add_request(f"r{i}", [5 + 2 * i + j for j in range(6 + 3 * i)],
+                            SamplingParams(temperature=0.0, max_tokens=40),
+                            on_output=lambda o, i=i: done.__setitem__(i, o) if o.finished else None)
+
+        for i in range(3):
+            add(i)
+        err = None
+        for step in range(60):
+            if step == 4:
+                add(3)
+                add(4)
+            try:
+                eng.step()
+            except RuntimeError as e:
+                err = e
+                break
+        assert err is not None and runner.mixed, "the failure must hit with a mixed step queued"
+        eng.fail_unfinished(str(err))
+    finally:
+        os.environ.pop("ENGINE_MIXED_AHEAD", None)
+    assert sorted(done) == [0, 1, 2, 3, 4]
+    assert all(o.finish_reason == "error" for o in done.values())
+    assert not eng.has_work()
+    assert eng.bm.num_free() == eng.bm.num_blocks
