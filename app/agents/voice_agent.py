@@ -14,7 +14,10 @@ pydantic-ai is not installable offline, so the agent loop is native:
 Differences from the reference (Appendix D): multi-turn history is passed as
 real chat messages to the native engine (prefix-cache friendly, Q18; the
 reference's flattened "Previous conversation:" prompt is still available as
-``_build_prompt_with_history`` and is used for remote backends); ``temperature
+``_build_prompt_with_history`` and is used for remote backends, which run the
+same tool loop over the OpenAI API: schemas sent, streamed ``tool_calls`` deltas
+assembled, tools run here, results re-prompted -- the reference's PydanticAI path);
+``temperature
 = 0`` means greedy (Q5); with ``guided_tool_calls`` (or ``tool_choice=
 "required"``) the tool call is decoded under a JSON-schema token FSM, so even
 random-init weights produce a valid call (BASELINE config 5).
@@ -211,13 +214,9 @@ class VoiceAgent:
         tp = self.config.top_p if top_p is None else top_p
         backend = self._get_backend()
         if not self.is_native:
-            prompt = self._build_prompt_with_history(user_message, context)
-            msgs = [{"role": "system", "content": self.config.system_prompt},
-                    {"role": "user", "content": prompt}]
-            async for text in backend.generate_stream_async(messages=msgs, temperature=temp,
-                                                            max_tokens=mt, top_p=tp,
-                                                            request_id=context.session_id):
-                yield AgentEvent(text=text, num_tokens=1)
+            async for ev in self._remote_events(backend, user_message, context, temp, mt, tp, top_k,
+                                                stop, seed, tool_choice, ignore_eos, min_tokens):
+                yield ev
             return
 
         from fasttalk_llm_microservice_amd.engine.guided import GuidedSpec
@@ -305,6 +304,74 @@ class VoiceAgent:
                     yield AgentEvent(text=text, num_tokens=held_tokens)
             yield AgentEvent(finish_reason=finish or "stop")
             return
+        yield AgentEvent(finish_reason="length")
+
+    async def _remote_events(self, backend, user_message: str, context: ConversationContext,
+                             temp, mt, tp, top_k, stop, seed, tool_choice, ignore_eos, min_tokens
+                             ) -> AsyncGenerator[AgentEvent, None]:
+        """The reference's default path (PydanticAI over the vLLM OpenAI API,
+        ``/root/reference/app/agents/voice_agent.py:141-164,219-229``): the flattened
+        history prompt, the tool schemas sent with every request (the server parses
+        calls: ``--enable-auto-tool-choice``), streamed ``tool_calls`` deltas
+        assembled, the tools run here, their results appended as ``tool`` messages
+        and the model re-prompted until it answers in text."""
+        prompt = self._build_prompt_with_history(user_message, context)
+        messages: List[Dict[str, Any]] = [{"role": "system", "content": self.config.system_prompt},
+                                          {"role": "user", "content": prompt}]
+        schemas = self.tool_schemas()
+        tools_by_name = self.tools()
+        force = self._wants_tool(user_message, tool_choice)
+        extra = {"top_k": top_k, "seed": seed, "ignore_eos": True if ignore_eos else None,
+                 "min_tokens": min_tokens or None}
+        chat = getattr(backend, "stream_chat_async", None)
+        for rnd in range(self.config.max_tool_rounds + 1):
+            offer = bool(schemas) and rnd < self.config.max_tool_rounds and chat is not None
+            choice = None
+            if offer:
+                if force == "required" and rnd == 0:
+                    choice = "required"
+                elif force and rnd == 0:
+                    choice = {"type": "function", "function": {"name": force}}
+                else:
+                    choice = "auto"
+            if chat is None:   # a backend without the chat/tool API: text only
+                async for text in backend.generate_stream_async(
+                        messages=messages, temperature=temp, max_tokens=mt, top_p=tp,
+                        request_id=context.session_id):
+                    yield AgentEvent(text=text, num_tokens=1)
+                yield AgentEvent(finish_reason="stop")
+                return
+            calls: List[Dict[str, Any]] = []
+            finish = "stop"
+            forced = choice not in (None, "auto")
+            # a forced call is a finite JSON language: room to finish it, and no ignore_eos
+            rx = dict(extra, ignore_eos=None) if forced else extra
+            async for ev in chat(messages, temperature=temp, max_tokens=max(mt, 256) if forced else mt,
+                                 top_p=tp, stop=stop, tools=schemas if offer else None,
+                                 tool_choice=choice, request_id=context.session_id, extra=rx):
+                if ev["type"] == "text":
+                    yield AgentEvent(text=ev["text"], num_tokens=1)
+                elif ev["type"] == "tool_calls":
+                    calls = [c for c in ev["calls"] if c.get("name") in tools_by_name]
+                else:
+                    finish = ev["reason"]
+            if not calls or finish == "abort":
+                yield AgentEvent(finish_reason=finish)
+                return
+            messages.append({"role": "assistant", "content": "", "tool_calls": [
+                {"id": c["id"], "type": "function",
+                 "function": {"name": c["name"], "arguments": c["arguments"] or "{}"}} for c in calls]})
+            for c in calls:
+                try:
+                    args = json.loads(c["arguments"] or "{}")
+                    if not isinstance(args, dict):
+                        raise ValueError("tool arguments must be a JSON object")
+                    result = await tools_by_name[c["name"]](context, **args)
+                except Exception as e:   # surfaced to the model, like the reference's handler
+                    args = {}
+                    result = f"[Error executing tool: {e}]"
+                yield AgentEvent(tool_call={"name": c["name"], "arguments": args}, tool_result=result)
+                messages.append({"role": "tool", "tool_call_id": c["id"], "content": str(result)})
         yield AgentEvent(finish_reason="length")
 
     async def generate_stream(self, user_message: str, context: ConversationContext,

@@ -55,7 +55,8 @@ def register_openai_routes(app, handler) -> None:
         kw = dict(temperature=body.get("temperature", 1.0), max_tokens=body.get("max_tokens")
                   or body.get("max_completion_tokens"), top_p=body.get("top_p"),
                   top_k=body.get("top_k"), stop=stop, tools=tools, guided=guided,
-                  seed=body.get("seed"), ignore_eos=bool(body.get("ignore_eos", False)))
+                  seed=body.get("seed"), ignore_eos=bool(body.get("ignore_eos", False)),
+                  min_tokens=int(body.get("min_tokens") or 0))
         rid = f"chatcmpl-{uuid.uuid4().hex[:24]}"
         created = int(time.time())
         model = body.get("model") or handler.model

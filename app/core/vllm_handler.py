@@ -71,10 +71,16 @@ class VLLMHandler:
                                   severity=ErrorSeverity.MEDIUM)
 
     # ------------------------------------------------------------------ request tracking
-    def _params(self, messages, temperature, max_tokens, top_p, stop, tools) -> Dict[str, Any]:
+    def _params(self, messages, temperature, max_tokens, top_p, stop, tools,
+                tool_choice=None, extra: Optional[Dict[str, Any]] = None) -> Dict[str, Any]:
         body: Dict[str, Any] = {"model": self.model, "messages": messages, "stream": True}
         for k, v in (("temperature", temperature), ("max_tokens", max_tokens), ("top_p", top_p),
                      ("stop", stop), ("tools", tools)):
+            if v is not None:
+                body[k] = v
+        if tools and tool_choice is not None:
+            body["tool_choice"] = tool_choice
+        for k, v in (extra or {}).items():   # vLLM sampling extensions: top_k, seed, ignore_eos ...
             if v is not None:
                 body[k] = v
         return body
@@ -153,6 +159,66 @@ class VLLMHandler:
         finally:
             self._unregister(req_id)
 
+    async def stream_chat_async(self, messages: List[Dict[str, Any]], temperature: Optional[float] = None,
+                                max_tokens: Optional[int] = None, top_p: Optional[float] = None,
+                                stop: Optional[List[str]] = None, tools: Optional[List[Dict]] = None,
+                                tool_choice: Any = None, request_id: Optional[str] = None,
+                                extra: Optional[Dict[str, Any]] = None
+                                ) -> AsyncGenerator[Dict[str, Any], None]:
+        """One streamed chat completion with tools (what the reference's PydanticAI
+        agent sends, ``/root/reference/app/agents/voice_agent.py:219``): yields
+        ``{"type": "text", "text"}`` per content delta, then -- when the server
+        answered with calls -- one ``{"type": "tool_calls", "calls": [{"id",
+        "name", "arguments"}]}`` assembled from the streamed ``tool_calls`` deltas
+        (keyed by ``index``; the id and name come first, argument fragments after),
+        and finally ``{"type": "finish", "reason"}``."""
+        req_id = request_id or f"vllm-chat-{uuid.uuid4()}"
+        self._register(req_id)
+        calls: Dict[int, Dict[str, Any]] = {}
+        finish = None
+        try:
+            async with httpx.AsyncClient(timeout=self.timeout, headers=self._headers) as c:
+                body = self._params(messages, temperature, max_tokens, top_p, stop, tools,
+                                    tool_choice, extra)
+                async with c.stream("POST", self.base_url + "/chat/completions", json=body) as r:
+                    r.raise_for_status()
+                    async for line in r.aiter_lines():
+                        if self._cancelled(req_id):
+                            finish = "abort"
+                            break
+                        for chunk in _sse_payloads([line]):
+                            ch = (chunk.get("choices") or [{}])[0]
+                            delta = ch.get("delta") or {}
+                            if delta.get("content"):
+                                yield {"type": "text", "text": delta["content"]}
+                            for tc in delta.get("tool_calls") or []:
+                                slot = calls.setdefault(int(tc.get("index", len(calls))),
+                                                        {"id": None, "name": None, "arguments": ""})
+                                if tc.get("id"):
+                                    slot["id"] = tc["id"]
+                                fn = tc.get("function") or {}
+                                if fn.get("name"):
+                                    slot["name"] = fn["name"]
+                                if fn.get("arguments"):
+                                    slot["arguments"] += fn["arguments"]
+                            if ch.get("finish_reason"):
+                                finish = ch["finish_reason"]
+        except LLMServiceError:
+            raise
+        except Exception as e:
+            raise LLMServiceError(f"vLLM chat error: {e}", category=ErrorCategory.PROCESSING,
+                                  severity=ErrorSeverity.HIGH)
+        finally:
+            self._unregister(req_id)
+        if calls:
+            out = []
+            for i in sorted(calls):
+                cinfo = calls[i]
+                out.append({"id": cinfo["id"] or f"call_{uuid.uuid4().hex[:12]}",
+                            "name": cinfo["name"], "arguments": cinfo["arguments"]})
+            yield {"type": "tool_calls", "calls": out}
+        yield {"type": "finish", "reason": finish or "stop"}
+
     def cancel_generation(self, request_id: str) -> bool:
         with self._requests_lock:
             info = self._active_requests.get(request_id)
@@ -178,33 +244,32 @@ class VLLMWithToolsHandler(VLLMHandler):
                                    max_rounds: int = 4) -> Generator[str, None, None]:
         req_id = request_id or f"vllm-tools-{uuid.uuid4()}"
         for _ in range(max_rounds):
-            calls: Dict[str, Dict[str, str]] = {}
-            order: List[str] = []
+            # streamed tool_calls deltas are keyed by `index` (OpenAI / vLLM): the first
+            # delta of a call carries its id and name, later ones argument fragments
+            calls: Dict[int, Dict[str, Any]] = {}
             body = self._params(messages, temperature, max_tokens, None, None, tools)
             with httpx.Client(timeout=self.timeout, headers=self._headers) as c:
                 with c.stream("POST", self.base_url + "/chat/completions", json=body) as r:
                     r.raise_for_status()
-                    current = None
                     for chunk in _sse_payloads(r.iter_lines()):
                         delta = ((chunk.get("choices") or [{}])[0].get("delta") or {})
                         for tc in delta.get("tool_calls") or []:
+                            slot = calls.setdefault(int(tc.get("index", len(calls))),
+                                                    {"id": None, "name": None, "arguments": ""})
                             if tc.get("id"):
-                                current = tc["id"]
-                                if current not in calls:
-                                    calls[current] = {"name": None, "arguments": ""}
-                                    order.append(current)
+                                slot["id"] = tc["id"]
                             fn = tc.get("function") or {}
-                            if current is not None:
-                                if fn.get("name"):
-                                    calls[current]["name"] = fn["name"]
-                                if fn.get("arguments"):
-                                    calls[current]["arguments"] += fn["arguments"]
+                            if fn.get("name"):
+                                slot["name"] = fn["name"]
+                            if fn.get("arguments"):
+                                slot["arguments"] += fn["arguments"]
                         if delta.get("content"):
                             yield delta["content"]
             if not calls:
                 return
-            for cid in order:
-                info = calls[cid]
+            for i in sorted(calls):
+                info = calls[i]
+                cid = info["id"] or f"call_{uuid.uuid4().hex[:12]}"
                 fn = tool_functions.get(info["name"])
                 if fn is None:
                     continue

@@ -398,3 +398,107 @@ def test_tool_hints_force_one_tool_when_unambiguous(engine):
     assert agent._wants_tool("what is the current weather", None) == "required"
     assert agent._wants_tool("tell me a story", None) is None
     assert agent._wants_tool("search news", "get_session_info") == "get_session_info"
+
+
+# ----------------------------------------------------------------------------- remote provider
+def _serve_facade(engine):
+    """This repo's own OpenAI facade (/v1) on a real socket, in a thread."""
+    import threading
+
+    from app.core.websocket_server_vllm import WebSocketLLMServer
+    from app.server.asgi_aiohttp import AiohttpASGIServer
+    from app.utils.config import Config
+
+    cfg = Config()
+    cfg.llm_provider = "native"
+    cfg.enable_pydantic_ai = False
+    srv = WebSocketLLMServer(cfg, engine=engine)
+    asgi = AiohttpASGIServer(srv.app, "127.0.0.1", 0)
+    loop = asyncio.new_event_loop()
+    ready = threading.Event()
+
+    def run():
+        asyncio.set_event_loop(loop)
+        loop.run_until_complete(asgi.start())
+        ready.set()
+        loop.run_forever()
+
+    threading.Thread(target=run, daemon=True).start()
+    assert ready.wait(30)
+
+    def stop():
+        asyncio.run_coroutine_threadsafe(asgi.stop(), loop).result(15)
+        loop.call_soon_threadsafe(loop.stop)
+    return asgi.port, stop
+
+
+def test_agent_tool_loop_over_remote_openai_provider(monkeypatch, engine):
+    """LLM_PROVIDER=openai with VLLM_BASE_URL at this repo's own
+    OpenAI facade (AiohttpASGIServer): the agent sends its tools with
+    tool_choice="required", assembles the streamed tool_calls deltas, runs the tool,
+    re-prompts with the result and streams the answer (reference
+    app/agents/voice_agent.py:141-164,219-229 over vllm_handler.py)."""
+    from app.core.vllm_handler import VLLMHandler
+
+    monkeypatch.setenv("WEB_SEARCH_BACKEND", "stub")
+    port, stop = _serve_facade(engine)
+    try:
+        base = f"http://127.0.0.1:{port}/v1"
+        handler = VLLMHandler(base, "fasttalk-native")
+        assert handler.check_connection()
+        agent = VoiceAgent(AgentConfig(vllm_base_url=base, max_tokens=12, temperature=0.7,
+                                       duckduckgo_rate_limit=0.0), backend=handler)
+        assert not agent.is_native
+
+        async def run(choice):
+            return [ev async for ev in agent.generate_events(
+                "Search the web for the latest tea news", _ctx("remote1"), tool_choice=choice,
+                seed=3, max_tokens=12, ignore_eos=True)]
+
+        events = asyncio.run(run("required"))
+        calls = [e for e in events if e.tool_call]
+        assert calls and calls[0].tool_call["name"] in agent.tools() and calls[0].tool_result
+        after = events[events.index(calls[-1]) + 1:]
+        assert sum(e.num_tokens for e in after if e.text) >= 1, "the answer must stream after the tool"
+        assert events[-1].finish_reason in ("stop", "length")
+        # a named tool: the server is told which one
+        events = asyncio.run(run("get_current_time"))
+        named = [e for e in events if e.tool_call]
+        assert named and named[0].tool_call["name"] == "get_current_time"
+        assert "current date" in named[0].tool_result
+    finally:
+        stop()
+
+
+def test_ws_agent_over_remote_openai_provider(monkeypatch, engine):
+    """The whole reference default path: /ws/llm -> VoiceAgent -> remote OpenAI API
+    (this repo's facade) with guided tool calls for a search-worded message."""
+    from app.core.websocket_server_vllm import WebSocketLLMServer
+    from app.utils.config import Config
+
+    monkeypatch.setenv("WEB_SEARCH_BACKEND", "stub")
+    port, stop = _serve_facade(engine)
+    try:
+        for k, v in {"LLM_PROVIDER": "openai", "VLLM_BASE_URL": f"http://127.0.0.1:{port}/v1",
+                     "ENABLE_PYDANTIC_AI": "true", "AGENT_GUIDED_TOOL_CALLS": "true",
+                     "DUCKDUCKGO_RATE_LIMIT": "0"}.items():
+            monkeypatch.setenv(k, v)
+        srv = WebSocketLLMServer(Config())
+        assert srv.voice_agent is not None and srv.vllm_handler is not None
+        with TestClient(srv.app) as c, c.websocket_connect("/ws/llm") as ws:
+            assert ws.receive_json()["type"] == "session_started"
+            ws.send_json({"type": "start_session", "config": {"max_tokens": 10, "temperature": 0.7,
+                                                              "seed": 1, "ignore_eos": True}})
+            ws.receive_json()
+            ws.send_json({"type": "user_message", "text": "Search the web for the weather news"})
+            n = 0
+            while True:
+                f = ws.receive_json()
+                if f["type"] == "token":
+                    n += 1
+                    continue
+                assert f["type"] == "response_complete", f
+                break
+        assert n >= 1 and f["stats"]["tokens_generated"] >= 1 and f["stats"]["pydantic_ai_used"]
+    finally:
+        stop()
