@@ -51,6 +51,7 @@ int ft_skinny_gemm_xc(const void* x, int x_stride, int M, const void* w, int N, 
 int ft_embed_rmsnorm(void* out, void* residual, const int* ids, const void* table, const void* w,
                      int rows, int hidden, int vocab, float eps, hipStream_t stream);
 size_t ft_ar_header_bytes();
+void ft_ar_set_max_blocks(int n);
 int ft_ar_alloc(size_t bytes, void** ptr);
 int ft_ar_free(void* ptr);
 int ft_ar_ipc_handle(void* ptr, char* out64);
@@ -826,6 +827,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("w"), py::arg("rows"), py::arg("eps"));
   m.def("embed_rmsnorm", &embed_rmsnorm);
   m.def("custom_ar_header_bytes", []() { return (int64_t)ft_ar_header_bytes(); });
+  m.def("custom_ar_set_max_blocks", [](int64_t n) { ft_ar_set_max_blocks((int)n); });
   m.def("custom_ar_alloc", &custom_ar_alloc);
   m.def("custom_ar_free", &custom_ar_free);
   m.def("custom_ar_handle", &custom_ar_handle);

@@ -277,42 +277,43 @@ __global__ __launch_bounds__(256) void ar_add_rmsnorm_kernel(
 #pragma unroll
   for (int r = 0; r < W; ++r)
     in[r] = reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(peers[r]) + slot);
+  // Two passes per row, each column block in its own (non-unrolled) iteration, so at
+  // most W peer loads are in flight per thread and nothing is live across blocks:
+  // hoisting all VPT * W loads took 256 VGPRs + 82 AGPRs at W = 8, VPT = 4 (one wave
+  // per SIMD: every spinning block held a whole CU, and ranks sharing one GPU starved
+  // the one still computing).  Pass 1 writes the new residual; pass 2 re-reads this
+  // thread's own stores (same thread, no fence) for the normalised output.
   for (int row = blockIdx.x; row < rows; row += gridDim.x) {
-    float v[VPT][8];
-    uint4 wv[VPT];
-#pragma unroll
+    uint4* rr = reinterpret_cast<uint4*>(residual + (size_t)row * hidden);
+    float ss = 0.f;
+#pragma unroll 1
     for (int c = 0; c < VPT; ++c) {
       const int e = row * h8 + c * 256 + threadIdx.x;
       uint4 raw[W];
 #pragma unroll
       for (int r = 0; r < W; ++r) raw[r] = in[r][e];   // W peer loads in flight
-      load8(raw[0], v[c]);
+      float v[8];
+      load8(raw[0], v);
 #pragma unroll
       for (int r = 1; r < W; ++r) {
         float t[8];
         load8(raw[r], t);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[c][j] += t[j];
+        for (int j = 0; j < 8; ++j) v[j] += t[j];
       }
-      wv[c] = *reinterpret_cast<const uint4*>(weight + (c * 256 + threadIdx.x) * 8);
-    }
-    uint4* rr = reinterpret_cast<uint4*>(residual + (size_t)row * hidden);
-    float ss = 0.f;
-#pragma unroll
-    for (int c = 0; c < VPT; ++c) {
       // the reduced partial is rounded to bf16 first, exactly as the separate
       // all-reduce would store it: fused, unfused and RCCL-fallback TP steps (and the
       // retried steps after a collective fault) produce the same bits
       float rv[8];
-      load8(store8(v[c]), v[c]);
+      load8(store8(v), v);
       load8(rr[c * 256 + threadIdx.x], rv);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[c][j] += rv[j];
-      const uint4 rb = store8(v[c]);
+      for (int j = 0; j < 8; ++j) v[j] += rv[j];
+      const uint4 rb = store8(v);
       rr[c * 256 + threadIdx.x] = rb;
-      load8(rb, v[c]);   // continue from the bf16-rounded residual
+      load8(rb, v);   // continue from the bf16-rounded residual
 #pragma unroll
-      for (int j = 0; j < 8; ++j) ss += v[c][j] * v[c][j];
+      for (int j = 0; j < 8; ++j) ss += v[j] * v[j];
     }
     ss = wave_sum(ss);
     __syncthreads();
@@ -320,13 +321,14 @@ __global__ __launch_bounds__(256) void ar_add_rmsnorm_kernel(
     __syncthreads();
     const float inv = rsqrtf((red[0] + red[1] + red[2] + red[3]) / (float)hidden + eps);
     uint4* orow = reinterpret_cast<uint4*>(out + (size_t)row * out_stride);
-#pragma unroll
+#pragma unroll 1
     for (int c = 0; c < VPT; ++c) {
-      float wf[8];
-      load8(wv[c], wf);
+      float v[8], wf[8];
+      load8(rr[c * 256 + threadIdx.x], v);
+      load8(*reinterpret_cast<const uint4*>(weight + (c * 256 + threadIdx.x) * 8), wf);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[c][j] = bf16_to_f32(f32_to_bf16(v[c][j] * inv)) * wf[j];
-      orow[c * 256 + threadIdx.x] = store8(v[c]);
+      for (int j = 0; j < 8; ++j) v[j] = bf16_to_f32(f32_to_bf16(v[j] * inv)) * wf[j];
+      orow[c * 256 + threadIdx.x] = store8(v);
     }
   }
 }
@@ -380,7 +382,16 @@ extern "C" int ft_ar_read_error(void* mine, int* err) {
   return 0;
 }
 
-static int ar_blocks(int n8) { return (int)std::min<long>(ft::ceil_div(n8, 256), 128); }
+// Grid cap of every collective (all loops are grid-strided).  128 by default; ranks
+// that share ONE device (tests / rehearsals) lower it so the W-1 kernels that spin
+// while a peer is still computing leave that peer CUs to compute on.
+static int g_ar_max_blocks = 128;
+
+extern "C" void ft_ar_set_max_blocks(int n) { g_ar_max_blocks = std::max(1, std::min(n, 128)); }
+
+static int ar_blocks(int n8) {
+  return (int)std::min<long>(ft::ceil_div(n8, 256), g_ar_max_blocks);
+}
 
 // x (bf16, n elements, n % 8 == 0, n*2 <= max_bytes) is summed over the W
 // ranks into out (may alias x).  peers: device array of W region base pointers.
@@ -451,7 +462,7 @@ extern "C" int ft_ar_add_rmsnorm(void* out, int out_stride, void* residual, cons
   if (hidden % 2048 != 0 || hidden > 8192) return -3;
   if ((size_t)(rows * hidden) * 2 > max_bytes) return -1;
   if ((ws == nullptr) == (x == nullptr) || (ws != nullptr && splits < 1)) return -4;
-  const int blocks = (int)std::min<long>(rows, 128);
+  const int blocks = (int)std::min<long>(rows, g_ar_max_blocks);
   const int vpt = (int)(hidden / 2048);
 #define FT_ARN(WW, VV)                                                                         \
   if (world == WW && vpt == VV) {                                                              \

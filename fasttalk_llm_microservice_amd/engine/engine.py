@@ -96,26 +96,18 @@ class LLMEngine:
         self.pipeline_depth = max(1, int(getattr(cfg, "pipeline_depth", 1)))
         # ENGINE_MIXED_AHEAD (default on): waiting prompts are scheduled into a mixed
         # step queued behind the running decode step instead of draining the queue.
-        # ENGINE_JIT_TOPUP=1: the queue is topped up only when the running step is
-        # about to finish (ENGINE_JIT_MARGIN_MS before its expected end), with new
-        # requests handled meanwhile (``poll_hook``, set by AsyncEngine), so a prompt
-        # that arrives during a step starts in the next one.  Off by default: the
-        # host's view of step ends jitters with the GIL (the WebSocket thread streams
-        # 50 frames a step), late top-ups cost the decode step 7.6 -> 8.0 ms and p50
-        # TTFT did not improve (profiles/ab_mixed_ahead_r03.log).
+        # (A just-in-time queue top-up was built and measured in round 3: the host's view
+        # of step ends jitters with the GIL, late top-ups cost the decode step 7.6 ->
+        # 8.0 ms, p50 TTFT did not improve -- profiles/ab_mixed_ahead_r03.log; removed.)
         self.mixed_ahead = os.environ.get("ENGINE_MIXED_AHEAD", "1") != "0"
-        self.jit_topup = os.environ.get("ENGINE_JIT_TOPUP", "0") == "1"
-        self.jit_margin = float(os.environ.get("ENGINE_JIT_MARGIN_MS", "1.5")) / 1e3
         self.poll_hook = None
-        self._ema_step = 0.0
-        self._t_prev_done = 0.0
         # ENGINE_PIPELINE_SHRINK=1: a stop shrinks the queued steps instead of draining
         # them.  Off by default: in the voice-agent loop the session's next prompt
         # follows its stop within a step, and a drained queue lets it start one step
         # sooner (driver config, same box: p50 TTFT 36-41 ms drained vs 50-51 ms shrunk
         # at equal tok/s, profiles/ab_pipeline_shrink_r03.log).  Workloads with think
         # time between turns keep the GPU busy with it on.
-        self.pipeline_shrink = os.environ.get("ENGINE_PIPELINE_SHRINK", "1" if self.jit_topup else "0") == "1"
+        self.pipeline_shrink = os.environ.get("ENGINE_PIPELINE_SHRINK", "0") == "1"
         self._last_complete = 0.0
         from .debug import FaultInjector, StepProfiler
 
@@ -302,24 +294,6 @@ class LLMEngine:
         self.stats["mixed_ahead"] += 1
         return _Inflight(mb, h, True)
 
-    def _jit_wait(self, e: "_Inflight"):
-        """Delays the queue top-up until the running step is about to finish (its
-        start + the mean step time - ``jit_margin``), handling new requests
-        meanwhile: a prompt that arrives during the step is then scheduled into
-        the very next step instead of behind one more queued decode step."""
-        est = max(e.t_launch, self._t_prev_done) + self._ema_step - self.jit_margin
-        poll = self.poll_hook
-        while time.perf_counter() < est:
-            if poll is not None:
-                poll()
-            # no early return on a new prompt: the mixed step could not start before
-            # the running step ends anyway, and the prompts arriving meanwhile join it
-            # (returning at the first prompt gave mixed steps of fewer prompts and
-            # p50 TTFT 43-44 vs 35-39 ms, profiles/ab_mixed_ahead_r03.log)
-            if self.runner.step_done(e.handle):
-                return
-            time.sleep(0.0002)
-
     def _drain_wait(self, e: "_Inflight"):
         """The queue is draining (nothing could be queued behind ``e``: a stop, or no
         room).  While ``e`` runs, new requests are admitted (``poll_hook``), and the
@@ -342,8 +316,6 @@ class LLMEngine:
         e = self._inflight[0]
         batch, handle = e.batch, e.handle
         t0 = time.perf_counter()
-        if self.jit_topup and not e.mixed and len(self._inflight) == 1 and self._ema_step > 0:
-            self._jit_wait(e)
         # top the queue up to depth + 1 steps before waiting on the oldest
         while len(self._inflight) <= self.pipeline_depth:
             nxt = self._speculate()
@@ -356,10 +328,6 @@ class LLMEngine:
         tl = time.perf_counter()
         toks = self.runner.mixed_collect(handle) if e.mixed else self.runner.decode_collect(handle)
         t1 = time.perf_counter()
-        if not e.mixed:   # GPU time of a decode step ~ completion - max(launch, previous completion)
-            d = t1 - max(e.t_launch, self._t_prev_done)
-            self._ema_step = d if self._ema_step <= 0 else 0.8 * self._ema_step + 0.2 * d
-        self._t_prev_done = t1
         self._inflight.pop(0)
         sampled = batch.sampled_seqs()
         for q in sampled:
@@ -824,8 +792,8 @@ class AsyncEngine:
     def _run(self):
         eng = self.engine
         if hasattr(eng, "poll_hook"):
-            # requests that arrive while a queued step runs are admitted before the
-            # queue is topped up (LLMEngine._jit_wait)
+            # requests that arrive while the last queued step runs are admitted and
+            # scheduled into a mixed step behind it (LLMEngine._drain_wait)
             eng.poll_hook = self._poll_cmds
         while not self._stop:
             self.heartbeat = time.time()

@@ -128,13 +128,12 @@ PACKED_PLAN = {
     "down": {1: (1, -3, 2), 8: (2, -3, 4), 16: (4, -3, 4), 32: (4, -3, 4), 64: (1, -5, 4)},
     "lm": {1: (1, -3, 1), 8: (2, -3, 1), 16: (4, -3, 1), 32: (1, -4, 1), 64: (2, -5, 1)},
 }
-# 33-64 rows, o / down: xr on 8-wave workgroups with 8 splits (one staged x chunk
-# feeds twice the weight columns, u = -7): cold-cache us at 50 / 64 rows o 9.8 /
-# 10.3 vs 10.4 / 10.5, down 22.8 / 23.4 vs 25.3 / 25.0 (profiles/xr8_sweep_r03.log;
-# qkv and the SiLU gate_up gain nothing there).  FT_XR8=1 selects it; in the decode graph it lost (7.66 vs 7.61 ms/step: the 8-split slabs cost the add+RMSNorm kernels more than the GEMMs save, profiles/ab_xr8_r03.log).
-if os.environ.get("FT_XR8", "0") == "1":
-    PACKED_PLAN["o"][64] = (1, -7, 8)
-    PACKED_PLAN["down"][64] = (1, -7, 8)
+# (33-64 rows, o / down on 8-wave workgroups with 8 splits -- one staged x chunk
+# feeding twice the weight columns -- won the cold-cache sweep, o 9.8 vs 10.4 us, down
+# 22.8 vs 25.3 us at 50 rows (profiles/xr8_sweep_r03.log), but lost in the decode graph,
+# 7.66 vs 7.61 ms/step: the 8-split slabs cost the add+RMSNorm kernels more than the
+# GEMMs save (profiles/ab_xr8_r03.log).  The kernel keeps the 8-wave form (u = -7 / -8)
+# for plans that want it; the env switch is gone.)
 MAX_SPLITS = 4
 
 

@@ -48,13 +48,19 @@ class CustomAllReduce:
 
     def __init__(self, group, rank: int, world: int, device: torch.device,
                  max_bytes: int = 8 << 20, spin_budget: Optional[int] = None,
-                 two_shot_bytes: Optional[int] = None):
+                 two_shot_bytes: Optional[int] = None, max_blocks: Optional[int] = None):
         from .. import ops
 
         if world not in self.SUPPORTED_WORLD:
             raise ValueError(f"custom all-reduce supports world sizes {self.SUPPORTED_WORLD}")
         self._C = ops.native()
         self.rank, self.world = rank, world
+        # grid cap of the collectives: ranks that share one device keep it small, so the
+        # kernels spinning for a late peer leave that peer CUs to compute on
+        if max_blocks is None:
+            max_blocks = int(os.environ.get("ENGINE_CUSTOM_AR_BLOCKS", "128"))
+        self.max_blocks = int(max_blocks)
+        self._C.custom_ar_set_max_blocks(self.max_blocks)
         self.max_bytes = int(max_bytes)
         if spin_budget is None:
             # 0.19 us per spin with 2 ranks, 0.36 us with 8 ranks sharing one MI355X:

@@ -141,6 +141,28 @@ def _worker(rank, world, port, q):
         fused_errs.append(max((res.float().cpu() - r_exp).abs().max().item(),
                               (out.float().cpu() - x_exp).abs().max().item()))
     errs.append(max(fused_errs))
+    # a 3-workgroup grid cap (what ranks sharing one device use): every loop is
+    # grid-strided, so one-shot, two-shot and the fused norm must still be exact
+    ar._C.custom_ar_set_max_blocks(3)
+    for two in (False, True):
+        ar.two_shot_bytes = 0 if two else 1 << 62
+        xs = _inputs(50 + two, world, 64 * 4096)
+        x = xs[rank].cuda()
+        ar.all_reduce(x)
+        torch.cuda.synchronize()
+        errs.append((x.float().cpu() - sum(v.float() for v in xs)).abs().max().item())
+    ar.two_shot_bytes = 1 << 62
+    rows, hidden = 9, 8192
+    parts = [(torch.randn(rows, hidden, generator=torch.Generator().manual_seed(60 + r)) * 0.3)
+             .bfloat16() for r in range(world)]
+    res = torch.zeros(rows, hidden, device="cuda").bfloat16()
+    out = torch.empty(rows, hidden, device="cuda").bfloat16()
+    ar.all_reduce_add_rmsnorm(out, res, torch.ones(hidden, device="cuda").bfloat16(), 1e-5, rows,
+                              x=parts[rank].cuda())
+    torch.cuda.synchronize()
+    errs.append((res.float().cpu() - sum(p.float() for p in parts).bfloat16().float())
+                .abs().max().item())
+    ar._C.custom_ar_set_max_blocks(128)
     healthy = ar.healthy()
     ar.export_error()
     flag_ok = int(ar.err_flag.item()) == 0

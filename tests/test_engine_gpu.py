@@ -160,42 +160,68 @@ def test_pipelined_decode_matches_synchronous(monkeypatch):
         assert [o[:8] for o in piped] == [o[:8] for o in outs[-1]]
 
 
-def test_mixed_ahead_and_jit_topup(monkeypatch):
+def test_mixed_ahead_matches_teacher_forced_logits(monkeypatch):
     """Prompts arriving while decode steps are queued go into a mixed step queued
     behind them (decode rows' ids gathered on the device from the last queued
-    step's sampled rows, positions ``inflight`` ahead), and the queue is topped up
-    just in time.  Against the drained/synchronous engine: every request gets its
-    full length, the first tokens agree (the mixed steps group rows differently,
-    so bf16 rounding may flip a near-tie later), all KV blocks come back, no
-    sequence keeps a stale in-flight count."""
+    step's sampled rows, positions ``inflight`` ahead).  Every request gets its full
+    length and all KV blocks come back; and -- ADVICE r3: token agreement alone is
+    weak evidence for the device-side id gather, the in-flight positions and the
+    block growth of queued steps -- the logits of EVERY step of the mixed-ahead run
+    (prefill rows of mixed-ahead steps, their decode rows, graph-replayed decode
+    steps) must match a fresh engine's eager prefill of the same prefix (the run's
+    own tokens teacher-forced): an off-by-one position or slot breaks that at once."""
     prompts = _prompts(16, [20 + 9 * i for i in range(16)], seed=5)
+    n_tok = 12
 
     def run(ahead: bool):
         monkeypatch.setenv("ENGINE_MIXED_AHEAD", "1" if ahead else "0")
-        monkeypatch.setenv("ENGINE_JIT_TOPUP", "1" if ahead else "0")
-        eng = _engine(max_num_seqs=32, num_kv_blocks=1024, pipeline_depth=1)
+        eng = _engine(model="tiny-2k", max_num_seqs=32, num_kv_blocks=1024, pipeline_depth=1)
+        r = eng.runner
+        r.logits_tap, r.logits_tap_ids = [], []
         res = {}
         step = k = 0
         for i in range(4):
-            eng.add_request(f"r{i}", prompts[i], SamplingParams(temperature=0.0, max_tokens=24,
+            eng.add_request(f"r{i}", prompts[i], SamplingParams(temperature=0.0, max_tokens=n_tok,
                                                                  ignore_eos=True),
                             on_output=lambda o, i=i: res.setdefault(i, []).extend(o.token_ids))
         k = 4
         while eng.has_work() or k < len(prompts):
             if k < len(prompts) and step % 3 == 2:
-                eng.add_request(f"r{k}", prompts[k], SamplingParams(temperature=0.0, max_tokens=24,
+                eng.add_request(f"r{k}", prompts[k], SamplingParams(temperature=0.0,
+                                                                     max_tokens=n_tok,
                                                                      ignore_eos=True),
                                 on_output=lambda o, i=k: res.setdefault(i, []).extend(o.token_ids))
                 k += 1
             eng.step()
             step += 1
         assert eng.bm.num_free() == eng.bm.num_blocks
-        return [res[i] for i in range(len(prompts))], eng
+        assert all(q.inflight == 0 for q in eng.scheduler.by_id.values())
+        tap = {}
+        for logits, ids in zip(r.logits_tap, r.logits_tap_ids):
+            for row, rid in enumerate(ids or []):
+                tap.setdefault(rid, []).append(logits[row].float().cpu())
+        r.logits_tap = r.logits_tap_ids = None
+        return [res[i] for i in range(len(prompts))], eng, tap
 
-    ref, _ = run(False)
-    got, eng = run(True)
+    ref, _, _ = run(False)
+    got, eng, tap = run(True)
     assert eng.stats["mixed_ahead"] > 0 and eng.stats["pipelined_steps"] > 0
-    assert [len(o) for o in got] == [len(o) for o in ref] == [24] * len(prompts)
+    assert [len(o) for o in got] == [len(o) for o in ref] == [n_tok] * len(prompts)
+    # teacher-forced reference: step k of request i predicted got[i][k] from prompt + got[i][:k]
+    fresh = _engine(model="tiny-2k", max_num_seqs=4, num_kv_blocks=256, enable_prefix_caching=False)
+    fresh.runner.logits_tap = []
+    rows, refs = [], []
+    for i, p in enumerate(prompts):
+        assert len(tap[f"r{i}"]) >= n_tok, (i, len(tap[f"r{i}"]))
+        for k in range(n_tok):
+            fresh.runner.logits_tap.clear()
+            fresh.generate([p + got[i][:k]], SamplingParams(temperature=0.0, max_tokens=1,
+                                                            ignore_eos=True))
+            refs.append(fresh.runner.logits_tap[-1][-1])
+            rows.append(tap[f"r{i}"][k])
+    cos = torch.nn.functional.cosine_similarity(torch.stack(rows), torch.stack(refs), dim=-1)
+    print(f"mixed-ahead vs teacher-forced eager logits: {len(rows)} steps, min cos {cos.min():.6f}")
+    assert cos.min().item() > 0.999, cos
     agree = sum(a[:3] == b[:3] for a, b in zip(got, ref))
     assert agree >= len(prompts) - 2, (agree, got, ref)
 
