@@ -58,6 +58,21 @@ def _free_port(base: int) -> int:
     raise RuntimeError("no free port")
 
 
+def _heartbeat(state: dict, period: float = 30.0):
+    """A progress line on stderr every ``period`` s (long TP / multi-rank runs stay
+    visibly alive while weights load and graphs capture)."""
+    t0 = time.time()
+
+    def run():
+        while not state.get("done"):
+            time.sleep(period)
+            if not state.get("done"):
+                print(f"bench: {state.get('phase', '?')} ({time.time() - t0:.0f} s)", file=sys.stderr,
+                      flush=True)
+
+    threading.Thread(target=run, daemon=True, name="bench-heartbeat").start()
+
+
 def _launch_ranks(n: int, argv) -> int:
     """Start ``n`` bench ranks (this file, same arguments) with the torch.distributed
     env contract and wait for them.  Runs before this process imports torch, so it
@@ -172,6 +187,10 @@ def main():
     # ---- load generator child first (before this process touches the GPU) ----------
     from ws_load import client_process, summarize
 
+    hb = {"phase": "init"}
+    if rank == 0:
+        _heartbeat(hb)
+
     port = a.port or _free_port(18100 + 10 * local_rank)
     sess_cfg = {"system_prompt": "You are a helpful voice assistant. Keep responses concise and "
                                  "conversational.",
@@ -250,8 +269,10 @@ def main():
         return r.get("result")
 
     cmd("open")
+    hb["phase"] = "warmup turns"
     if a.warmup > 0:
         cmd(("run", a.warmup))
+    hb["phase"] = "timed turns"
 
     def barrier():
         if world > 1:
@@ -265,6 +286,7 @@ def main():
     res = cmd(("run", a.steps))
     barrier()
     elapsed = time.perf_counter() - t0
+    hb["done"] = True
     cmd("close")
     client.join(timeout=30)
 
@@ -373,6 +395,9 @@ def bench_tp(a, rank: int, world: int, local_rank: int):
     TP workers replaying rank 0's steps."""
     if a.tp != world:
         raise SystemExit(f"--tp {a.tp} needs exactly {a.tp} ranks (got {world})")
+    hb = {"phase": "init"}
+    if rank == 0:
+        _heartbeat(hb)
     from ws_load import client_process, summarize
 
     port = a.port or _free_port(18100)
@@ -413,9 +438,11 @@ def bench_tp(a, rank: int, world: int, local_rank: int):
         # the free-memory rule would see the others' shards: a fixed pool per rank
         cfg.num_kv_blocks = 4096
     sync = torch.cuda.synchronize if a.device == "cuda" else (lambda: None)
+    hb["phase"] = "weights + KV cache"
     eng = torchrun_tp(cfg)
     if rank != 0:
         return  # worker: returned after rank 0 sent "stop"
+    hb["phase"] = "decode graph capture"
     eng.runner.warmup([b for b in eng.runner.graph_sizes if b <= 2 * a.sessions])
     aeng = AsyncEngine(eng).start()
     from app.core.websocket_server_vllm import WebSocketLLMServer
@@ -449,13 +476,16 @@ def bench_tp(a, rank: int, world: int, local_rank: int):
         return r.get("result")
 
     cmd("open")
+    hb["phase"] = "warmup turns"
     if a.warmup > 0:
         cmd(("run", a.warmup))
     sync()
+    hb["phase"] = "timed turns"
     t0 = time.perf_counter()
     res = cmd(("run", a.steps))
     sync()
     elapsed = time.perf_counter() - t0
+    hb["done"] = True
     cmd("close")
     client.join(timeout=30)
     summ = summarize(res)

@@ -19,7 +19,7 @@ __global__ __launch_bounds__(256, 2) void attn_loads(const uint16_t* __restrict_
   if (wave_id() == 0) dec_prefix(s_pre, seq_lens, batch);
   __syncthreads();
   const int total = nkv * s_pre[batch];
-  const int nw = dec_num_waves(total, gridDim.x * 4);
+  const int nw = dec_num_waves(total, gridDim.x * 4, kDecMinTiles);
   const int w = wave_id() * gridDim.x + blockIdx.x;
   if (total == 0 || w >= nw) return;
   int f = (int)(((long long)w * total) / nw);

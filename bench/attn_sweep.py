@@ -5,7 +5,10 @@ unless --uniform; KV blocks are scattered (random permutation), like a pool
 that has served many sessions.
 
 python bench/attn_sweep.py [--nq 32 --nkv 8] [--uniform]
-FT_DECODE_RING=2|3|4 selects the kernel's register-ring depth (default 2).
+FT_DECODE_RING=2|3|4 selects the kernel's register-ring depth (default 2);
+FT_DECODE_MIN_TILES the partition's minimum 16-token tiles per wave (default 4).
+--fused: the in-launch combine the engine uses (decode tickets) instead of the
+separate combine kernel.  --shapes "1:512,1:3000" overrides the shape list.
 """
 from __future__ import annotations
 
@@ -32,10 +35,13 @@ def main():
     ap.add_argument("--nkv", type=int, default=8)
     ap.add_argument("--d", type=int, default=128)
     ap.add_argument("--uniform", action="store_true")
+    ap.add_argument("--fused", action="store_true")
+    ap.add_argument("--shapes", default="")
     a = ap.parse_args()
+    shapes = [tuple(int(v) for v in x.split(":")) for x in a.shapes.split(",")] if a.shapes else SHAPES
     nq, nkv, d, bs = a.nq, a.nkv, a.d, 16
     dev = "cuda"
-    for B, ctx in SHAPES:
+    for B, ctx in shapes:
         nblk = math.ceil(ctx / bs)
         nblocks = B * nblk + 8
         kc = torch.randn(nblocks, nkv, bs, d, device=dev).bfloat16()
@@ -52,10 +58,13 @@ def main():
         tmp_o = torch.empty(n_out, device=dev)
         tmp_ml = torch.empty(n_ml, device=dev)
         nbytes = int(sl.sum().item()) * nkv * d * 2 * 2
+        cnt = ops.decode_counters(B, nkv, dev) if a.fused else None
         us = timeit(lambda: ops.decode_attention(out, q, kc, vc, bt, sl, tmp_o, tmp_ml, nq, nkv, d,
-                                                 d ** -0.5), iters=100, warmup=10)
+                                                 d ** -0.5, counters=cnt), iters=100, warmup=10)
         print(json.dumps({"B": B, "ctx": ctx, "uniform": a.uniform,
                           "ring": int(os.environ.get("FT_DECODE_RING", "2")),
+                          "min_tiles": int(os.environ.get("FT_DECODE_MIN_TILES", "4")),
+                          "fused": a.fused,
                           "us": round(us, 2), "GBps": round(nbytes / us / 1e3, 1)}), flush=True)
         del kc, vc
 

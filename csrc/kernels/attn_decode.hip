@@ -53,7 +53,7 @@ typedef short short4_t __attribute__((ext_vector_type(4)));
 typedef float floatx4_t __attribute__((ext_vector_type(4)));
 
 constexpr int kDecMaxBatch = 1024;
-constexpr int kDecMinTiles = 4;   // >= 64 tokens per wave: short contexts use fewer waves
+constexpr int kDecMinTiles = 4;   // default: >= 64 tokens per wave (short contexts use fewer waves)
 // deferred-rescale threshold (log2 units): p = exp2(score - reference max) stays <= 2^8,
 // exact in fp32 and in bf16's range
 constexpr float kDecRescaleThr = 8.f;
@@ -76,8 +76,11 @@ __device__ __forceinline__ void dec_prefix(int* s_pre, const int* __restrict__ s
   if (lane == 0) s_pre[0] = 0;
 }
 
-__device__ __forceinline__ int dec_num_waves(int total, int nw_grid) {
-  return max(1, min(nw_grid, (total + kDecMinTiles - 1) / kDecMinTiles));
+// waves the flattened partition uses: at least min_tiles 16-token tiles each (a
+// launch argument: fewer, longer ranges mean fewer partials for the last arriver to
+// merge -- the latency that dominates short batches)
+__device__ __forceinline__ int dec_num_waves(int total, int nw_grid, int min_tiles) {
+  return max(1, min(nw_grid, (total + min_tiles - 1) / min_tiles));
 }
 
 // one 16-token tile of one kv head in registers: K rows (A operand of QK^T, one
@@ -252,14 +255,15 @@ __global__ __launch_bounds__(256, WPC) void paged_decode_kernel(
     float* __restrict__ tmp_ml, const uint16_t* __restrict__ q, int q_stride,
     uint16_t* __restrict__ k_cache, uint16_t* __restrict__ v_cache,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ seq_lens,
-    int batch, int nkv, int bs_shift, float scale_log2, int* __restrict__ counters) {
+    int batch, int nkv, int bs_shift, float scale_log2, int* __restrict__ counters,
+    int min_tiles) {
   static_assert(G >= 1 && G <= 16, "GQA group must fit the 16 MFMA columns");
   constexpr int KC = D / 32, ND = D / 16;
   __shared__ int s_pre[kDecMaxBatch + 1];
   if (wave_id() == 0) dec_prefix(s_pre, seq_lens, batch);
   __syncthreads();
   const int total = nkv * s_pre[batch];
-  const int nw = dec_num_waves(total, gridDim.x * 4);
+  const int nw = dec_num_waves(total, gridDim.x * 4, min_tiles);
   const int w = wave_id() * gridDim.x + blockIdx.x;  // spreads low wave ids over CUs
   if (FC && blockIdx.x == 0) {
     // fused-combine mode has no combine kernel to define empty sequences' outputs
@@ -407,13 +411,13 @@ template <int D, int G>
 __global__ __launch_bounds__(256) void paged_decode_combine_kernel(
     uint16_t* __restrict__ out, int out_stride, const float* __restrict__ tmp_out,
     const float* __restrict__ tmp_ml, const int* __restrict__ seq_lens, int batch, int nkv,
-    int nw_grid) {
+    int nw_grid, int min_tiles) {
   __shared__ int s_pre[kDecMaxBatch + 1];
   __shared__ float s_M[G], s_den[G];
   if (wave_id() == 0) dec_prefix(s_pre, seq_lens, batch);
   __syncthreads();
   const int total = nkv * s_pre[batch];
-  const int nw = dec_num_waves(total, nw_grid);
+  const int nw = dec_num_waves(total, nw_grid, min_tiles);
   const int seg = blockIdx.x;
   const int b = seg / nkv, h = seg - b * nkv;
   const int nb = s_pre[b + 1] - s_pre[b];
@@ -515,13 +519,19 @@ extern "C" int ft_paged_decode_attention(void* out, int out_stride, float* tmp_o
     const int r = e ? atoi(e) : 2;
     return (r >= 2 && r <= 4) ? r : 2;
   }();
+  // minimum tiles per wave of the partition; FT_DECODE_MIN_TILES overrides (sweeps)
+  static const int min_tiles_env = [] {
+    const char* e = getenv("FT_DECODE_MIN_TILES");
+    return e ? max(1, atoi(e)) : 0;
+  }();
+  const int min_tiles = min_tiles_env ? min_tiles_env : ft::kDecMinTiles;
   // 1 workgroup per CU, or the register-limited maximum for the ring depth
   const int wpc = min(dec_wg_per_cu(), ring == 2 ? 3 : 2);
   int nwg = 0;
 #define FT_DEC_ARGS                                                                             \
   (uint16_t*)out, out_stride, tmp_out, tmp_ml, (const uint16_t*)q, q_stride, (uint16_t*)k_cache, \
       (uint16_t*)v_cache, block_tables, bt_stride, seq_lens, batch, nkv, bs_shift, scale_log2,   \
-      counters
+      counters, min_tiles
 #define FT_DEC_LAUNCH(DD, GG, RR, FCC)                                                  \
   if (wpc == 1)                                                                                \
     hipLaunchKernelGGL((ft::paged_decode_kernel<DD, GG, RR, FCC, 1>), dim3(nwg), dim3(256),      \
@@ -538,7 +548,7 @@ extern "C" int ft_paged_decode_attention(void* out, int out_stride, float* tmp_o
       FT_DEC_LAUNCH(DD, GG, RR, false);                                                        \
       hipLaunchKernelGGL((ft::paged_decode_combine_kernel<DD, GG>), dim3(batch * nkv), dim3(256),\
                          0, stream, (uint16_t*)out, out_stride, tmp_out, tmp_ml, seq_lens, batch,\
-                         nkv, nwg * 4);                                                          \
+                         nkv, nwg * 4, min_tiles);                                               \
     }                                                                                            \
     return static_cast<int>(hipGetLastError());                                                  \
   }
