@@ -10,6 +10,9 @@ python bench/layer_timeline.py gpurun_out/prof/run_results.db [--steps 200]
 from __future__ import annotations
 
 import argparse
+import csv
+import glob
+import os
 import re
 import sqlite3
 from collections import defaultdict
@@ -21,14 +24,35 @@ def _short(name: str) -> str:
     return name[:60]
 
 
+def _load(path: str):
+    """(name, start_ns, end_ns) rows in start order from a rocprofv3 output: a
+    directory (its first *kernel_trace.csv, else its first .db), a CSV or a rocpd db."""
+    if os.path.isdir(path):
+        found = sorted(glob.glob(os.path.join(path, "**", "*kernel_trace.csv"), recursive=True))
+        found = found or sorted(glob.glob(os.path.join(path, "**", "*.db"), recursive=True))
+        if not found:
+            raise SystemExit(f"no kernel trace under {path}")
+        path = found[0]
+    if path.endswith(".csv"):
+        with open(path, newline="") as f:
+            rows = [(r["Kernel_Name"], int(r["Start_Timestamp"]), int(r["End_Timestamp"]))
+                    for r in csv.DictReader(f)]
+        return sorted(rows, key=lambda r: r[1])
+    c = sqlite3.connect(path)
+    try:
+        return c.execute("select name, start, end from kernels order by start").fetchall()
+    except sqlite3.Error:
+        tabs = [r[0] for r in c.execute("select name from sqlite_master")]
+        raise SystemExit(f"no 'kernels' view in {path}; objects: {tabs}")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("db")
     ap.add_argument("--steps", type=int, default=200, help="decode steps averaged (the last N)")
     ap.add_argument("--first", default="embed_rmsnorm", help="kernel that opens a step")
     a = ap.parse_args()
-    c = sqlite3.connect(a.db)
-    rows = c.execute("select name, start, end from kernels order by start").fetchall()
+    rows = _load(a.db)
     # split into steps at the step-opening kernel
     steps, cur = [], []
     for name, s, e in rows:

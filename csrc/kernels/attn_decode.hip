@@ -53,7 +53,10 @@ typedef short short4_t __attribute__((ext_vector_type(4)));
 typedef float floatx4_t __attribute__((ext_vector_type(4)));
 
 constexpr int kDecMaxBatch = 1024;
-constexpr int kDecMinTiles = 4;   // default: >= 64 tokens per wave (short contexts use fewer waves)
+// default: >= 128 tokens per wave (short contexts use fewer waves).  Swept on MI355X
+// (profiles/attn_min_tiles_r04.log): 8 vs 4 is 14.6 vs 21.4 us at 1 x 4k, 12.5 vs
+// 13.4 at 1 x 2k, 20.0 vs 21.2 at 8 x 2k, even at 50 x 3k, 0.8 us slower at 1 x 512
+constexpr int kDecMinTiles = 8;
 // deferred-rescale threshold (log2 units): p = exp2(score - reference max) stays <= 2^8,
 // exact in fp32 and in bf16's range
 constexpr float kDecRescaleThr = 8.f;

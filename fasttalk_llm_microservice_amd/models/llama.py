@@ -236,8 +236,11 @@ FUSED_PLAN = {
 _SILU_CONFIGS = ((2, 2), (2, 3), (2, 4), (4, 2), (4, 3))
 # QKV with the RoPE + paged K/V epilogue in the same launch (ops.pkr_qkv_rope: one
 # workgroup per head, split-K reduced in the launch) instead of the ring GEMM's slabs
-# + slab_rope_kv: (splits, depth) per row bucket; FT_FUSED_QKV_ROPE=0 keeps two launches.
-FUSED_QKV_ROPE = os.environ.get("FT_FUSED_QKV_ROPE", "1") == "1"
+# + slab_rope_kv: (splits, depth) per row bucket.  Off by default: measured on MI355X
+# the in-launch split-K seam (48 head tiles x 8 splits for Llama-3-8B) costs more than
+# the launch it saves -- 3.52 vs 3.25 ms per single-session decode step
+# (profiles/qkv_rope_ab_r04.log); FT_FUSED_QKV_ROPE=1 selects it.
+FUSED_QKV_ROPE = os.environ.get("FT_FUSED_QKV_ROPE", "0") == "1"
 QKV_ROPE_PLAN = {1: (8, 2), 8: (8, 2), 16: (8, 2), 32: (8, 2)}
 if os.environ.get("FT_QKV_ROPE_PLAN"):   # "splits:depth" for every bucket (sweeps)
     _sp, _dp = (int(v) for v in os.environ["FT_QKV_ROPE_PLAN"].split(":"))
