@@ -79,11 +79,6 @@ int ft_pkr_gemm(const void* x, int x_stride, int M, const void* wpk, int N, int 
                 void* out, int out_stride, void* residual, int res_stride, int* tickets,
                 int splits, int nt, int depth, int epi, int norm, int wn, float eps,
                 hipStream_t stream);
-int ft_pkr_qkv_rope(const void* x, int x_stride, int M, const void* wpk, int N, int K, float* ws,
-                    int* tickets, int splits, int depth, void* q_out, int q_stride,
-                    const int* positions, const float* cos_sin, const int* slot_mapping,
-                    void* k_cache, void* v_cache, int nq, int nkv, int head_dim, int block_size,
-                    float eps, hipStream_t stream);
 int ft_row_rmsnorm(const void* x, int x_stride, const float* ws, int splits, void* out,
                    int out_stride, void* residual, const void* w, int rows, int hidden, float eps,
                    hipStream_t stream);
@@ -795,47 +790,6 @@ void slab_rope_kv(at::Tensor ws, int64_t splits, int64_t rows, int64_t cols, at:
                            cur_stream()), "slab_rope_kv");
 }
 
-// QKV projection of the fused decode layer with RoPE + the paged K/V write in its
-// epilogue (skinny_pkr.hip EPI_ROPE): q heads -> q_out, k / v heads -> the caches.
-void pkr_qkv_rope(at::Tensor x, at::Tensor w, c10::optional<at::Tensor> ws,
-                  c10::optional<at::Tensor> tickets, int64_t splits, int64_t depth,
-                  at::Tensor q_out, at::Tensor positions, at::Tensor cos_sin,
-                  at::Tensor slot_mapping, at::Tensor k_cache, at::Tensor v_cache, int64_t nq,
-                  int64_t nkv, int64_t head_dim, double eps) {
-  check_bf16(x, "x");
-  check_bf16(w, "w");
-  check_rows(x, "x");
-  TORCH_CHECK(w.dim() == 2 && w.is_contiguous(), "w must be contiguous [N, K]");
-  const int M = (int)x.size(0), K = (int)x.size(1), N = (int)w.size(0);
-  TORCH_CHECK(w.size(1) == K, "K mismatch");
-  TORCH_CHECK(M <= 32, "pkr_qkv_rope supports M <= 32");
-  TORCH_CHECK(N == (nq + 2 * nkv) * head_dim, "N must be (nq + 2 nkv) * head_dim");
-  float* wsp = nullptr;
-  int* tp = nullptr;
-  if (splits > 1) {
-    TORCH_CHECK(ws.has_value() && tickets.has_value(), "splits > 1 needs ws and tickets");
-    check_ws(*ws, splits * M * N + splits * M);
-    wsp = ws->data_ptr<float>();
-    check_i32(*tickets, "tickets");
-    TORCH_CHECK(tickets->numel() >= N / head_dim, "tickets too small");
-    tp = tickets->data_ptr<int>();
-  }
-  check_bf16(q_out, "q_out");
-  check_rows(q_out, "q_out");
-  TORCH_CHECK(q_out.size(0) >= M && q_out.size(1) >= nq * head_dim, "q_out shape");
-  check_i32(positions, "positions");
-  check_i32(slot_mapping, "slot_mapping");
-  TORCH_CHECK(positions.numel() >= M && slot_mapping.numel() >= M, "metadata length");
-  TORCH_CHECK(cos_sin.scalar_type() == at::kFloat && cos_sin.size(1) == head_dim, "cos_sin");
-  check_kv_caches(k_cache, v_cache, nkv, head_dim);
-  check_rc(ft_pkr_qkv_rope(x.data_ptr(), (int)x.stride(0), M, w.data_ptr(), N, K, wsp, tp,
-                           (int)splits, (int)depth, q_out.data_ptr(), (int)q_out.stride(0),
-                           positions.data_ptr<int>(), cos_sin.data_ptr<float>(),
-                           slot_mapping.data_ptr<int>(), k_cache.data_ptr(), v_cache.data_ptr(),
-                           (int)nq, (int)nkv, (int)head_dim, (int)k_cache.size(2), (float)eps,
-                           cur_stream()), "pkr_qkv_rope");
-}
-
 }  // namespace
 
 PYBIND11_MODULE(_C, m) {
@@ -888,7 +842,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("custom_ar_export_error", &custom_ar_export_error);
   m.def("slab_silu", &slab_silu);
   m.def("slab_store", &slab_store);
-  m.def("pkr_qkv_rope", &pkr_qkv_rope);
   m.def("slab_rope_kv", &slab_rope_kv, py::arg("ws"), py::arg("splits"), py::arg("rows"),
         py::arg("cols"), py::arg("q_out"), py::arg("positions"), py::arg("cos_sin"),
         py::arg("slot_mapping"), py::arg("k_cache"), py::arg("v_cache"), py::arg("nq"),

@@ -22,16 +22,6 @@
 //              from the streamed x fragments (v_dot2) and the norm weight is
 //              folded into W -- so the post-attention RMSNorm, gate_up and
 //              SiLU-mul are one launch.
-//   EPI_ROPE   the QKV projection of the fused layer with RoPE + the paged K/V write
-//              in its epilogue (replaces the slab_rope_kv launch): a workgroup's
-//              16*NT columns are one head (NT = D/16), so every RoPE pair (c, c+D/2)
-//              sits in one lane (tiles j and j + NT/2); x is the raw residual
-//              stream (the input-norm weight is folded into W) and the RMS scale
-//              comes from the streamed x fragments (NORM) summed over the waves and
-//              -- through a small per-split array behind the slabs -- the splits.
-//              Split-K partials are reduced in the launch like EPI_RESID; q heads
-//              go to `out`, k heads to the paged K cache, v heads to the transposed
-//              V cache.
 //   EPI_RESID  residual[m][n] += y in place (fp32 add, bf16 store).  Split-K
 //              partials are reduced inside the launch: each split stores its slab,
 //              publishes it (agent-scope release), takes a ticket, and the last
@@ -55,7 +45,7 @@ typedef __bf16 pr_bf16x2 __attribute__((ext_vector_type(2)));
 typedef float pr_floatx4 __attribute__((ext_vector_type(4)));
 typedef unsigned int pr_u32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int kEpiStore = 0, kEpiSilu = 1, kEpiResid = 2, kEpiRope = 3;
+constexpr int kEpiStore = 0, kEpiSilu = 1, kEpiResid = 2;
 
 struct PrArgs {
   const uint16_t* x;
@@ -66,13 +56,6 @@ struct PrArgs {
   int* tickets;
   int x_stride, M, K, N, k_slice, out_stride, res_stride;
   float eps;
-  // EPI_ROPE: q / paged K-V destinations of the QKV projection
-  const int* positions;
-  const float* cos_sin;
-  const int* slot_mapping;
-  uint16_t* k_cache;
-  uint16_t* v_cache;
-  int nq, nkv, block_size;
 };
 
 __device__ __forceinline__ pr_bf16x8 pr_frag(const uint4& v) {
@@ -259,105 +242,6 @@ __global__ __launch_bounds__(256) void skinny_pkr_kernel(PrArgs a) {
     return;
   }
 
-  if constexpr (EPI == kEpiRope) {
-    constexpr int D = 16 * NT, HALF = D / 2, NH = NT / 2;
-    float ssw[MT][4];   // this split's sums of squares of rows 16 i + 4 g + r
-#pragma unroll
-    for (int i = 0; i < MT; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int q = i * 16 + 4 * g + r;
-        ssw[i][r] = s_ss[0][q] + s_ss[1][q] + s_ss[2][q] + s_ss[3][q];
-      }
-    if (gridDim.y > 1) {
-      float* slab = a.ws + (size_t)s * M * N;
-      float* ssp = a.ws + (size_t)gridDim.y * M * N + (size_t)s * M;   // per-split sums
-#pragma unroll
-      for (int i = 0; i < MT; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int m = 16 * i + 4 * g + r;
-          if (m < M) {
-#pragma unroll
-            for (int j = 0; j < NT; ++j) slab[(size_t)m * N + n0 + 16 * j + l15] = acc[i][j][r];
-            if (l15 == 0) ssp[m] = ssw[i][r];
-          }
-        }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      int prev = 0;
-      if (lane == 0)
-        prev = __hip_atomic_fetch_add(a.tickets + tile, 1, __ATOMIC_RELAXED,
-                                      __HIP_MEMORY_SCOPE_AGENT);
-      prev = __shfl(prev, 0, 64);
-      if (prev != (int)gridDim.y - 1) return;
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      // every split's slab and sums in split order (deterministic whoever is last)
-#pragma unroll
-      for (int i = 0; i < MT; ++i) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) ssw[i][r] = 0.f;
-#pragma unroll
-        for (int j = 0; j < NT; ++j) acc[i][j] = pr_floatx4{0.f, 0.f, 0.f, 0.f};
-      }
-      for (int sp = 0; sp < (int)gridDim.y; ++sp) {
-        const float* sl = a.ws + (size_t)sp * M * N;
-        const float* sq = a.ws + (size_t)gridDim.y * M * N + (size_t)sp * M;
-#pragma unroll
-        for (int i = 0; i < MT; ++i)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int m = min(16 * i + 4 * g + r, M - 1);
-            ssw[i][r] += sq[m];
-#pragma unroll
-            for (int j = 0; j < NT; ++j) acc[i][j][r] += sl[(size_t)m * N + n0 + 16 * j + l15];
-          }
-      }
-      if (lane == 0) a.tickets[tile] = 0;  // re-arm for the next launch
-    }
-    const int head = tile;                 // 16 * NT columns = one head
-    const bool is_v = head >= a.nq + a.nkv;
-#pragma unroll
-    for (int i = 0; i < MT; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = 16 * i + 4 * g + r;
-        if (m >= M) continue;
-        const float rs = rsqrtf(ssw[i][r] / (float)a.K + a.eps);
-        const int slot = a.slot_mapping[m];
-        const int blk = slot >= 0 ? slot / a.block_size : 0;
-        const int off = slot >= 0 ? slot - blk * a.block_size : 0;
-        if (is_v) {
-          if (slot < 0) continue;
-          const int kh = head - a.nq - a.nkv;
-          uint16_t* vp = a.v_cache + ((size_t)blk * a.nkv + kh) * D * a.block_size + off;
-#pragma unroll
-          for (int j = 0; j < NT; ++j)
-            vp[(size_t)(16 * j + l15) * a.block_size] = f32_to_bf16(acc[i][j][r] * rs);
-          continue;
-        }
-        const float* cs = a.cos_sin + (size_t)a.positions[m] * D;
-        uint16_t* dst;
-        if (head < a.nq) {
-          dst = a.out + (size_t)m * a.out_stride + head * D;
-        } else {
-          if (slot < 0) continue;
-          dst = a.k_cache + (((size_t)blk * a.nkv + (head - a.nq)) * a.block_size + off) * D;
-        }
-#pragma unroll
-        for (int j = 0; j < NH; ++j) {
-          const int c = 16 * j + l15;
-          const float x1 = acc[i][j][r] * rs, x2 = acc[i][j + NH][r] * rs;
-          const float co = cs[c], si = cs[HALF + c];
-          dst[c] = f32_to_bf16(x1 * co - x2 * si);
-          dst[HALF + c] = f32_to_bf16(x2 * co + x1 * si);
-        }
-      }
-    return;
-  }
-
   if constexpr (EPI == kEpiStore) {
     const bool bf16_out = a.out != nullptr && gridDim.y == 1;
     float* slab = a.ws + (size_t)s * M * N;
@@ -451,37 +335,6 @@ __global__ __launch_bounds__(256) void skinny_pkr_kernel(PrArgs a) {
 
 }  // namespace ft
 
-// QKV projection with the RoPE + paged K/V epilogue (EPI_ROPE): one workgroup per head
-// (nt = head_dim / 16), x = the raw residual rows (input-norm weight folded into W).
-// ws: splits * M * N + splits * M floats (splits > 1); tickets: N / head_dim zeroed.
-extern "C" int ft_pkr_qkv_rope(const void* x, int x_stride, int M, const void* wpk, int N, int K,
-                               float* ws, int* tickets, int splits, int depth, void* q_out,
-                               int q_stride, const int* positions, const float* cos_sin,
-                               const int* slot_mapping, void* k_cache, void* v_cache, int nq,
-                               int nkv, int head_dim, int block_size, float eps,
-                               hipStream_t stream) {
-  if (M <= 0) return 0;
-  if (M > 32 || splits < 1 || splits > 64) return -1;
-  if (head_dim != 128 && head_dim != 64) return -2;
-  if (N != (nq + 2 * nkv) * head_dim || K % (64 * splits) != 0) return -3;
-  if (splits > 1 && (ws == nullptr || tickets == nullptr)) return -4;
-  const int nt = head_dim / 16;
-  const int mt = (M + 15) / 16;
-  ft::PrArgs a{(const uint16_t*)x, (const uint16_t*)wpk, ws, (uint16_t*)q_out, nullptr, tickets,
-               x_stride, M, K, N, K / splits, q_stride, 0, eps, positions, cos_sin, slot_mapping,
-               (uint16_t*)k_cache, (uint16_t*)v_cache, nq, nkv, block_size};
-  dim3 grid(N / head_dim, splits), block(256);
-#define FT_PQR(MT_, NT_, S_)                                                                  \
-  if (mt == MT_ && nt == NT_ && depth == S_) {                                                \
-    hipLaunchKernelGGL((ft::skinny_pkr_kernel<MT_, NT_, S_, ft::kEpiRope, true, false>), grid, \
-                       block, 0, stream, a);                                                  \
-    return static_cast<int>(hipGetLastError());                                               \
-  }
-  FT_PQR(1, 8, 2) FT_PQR(2, 8, 2) FT_PQR(1, 4, 2) FT_PQR(2, 4, 2) FT_PQR(1, 4, 3) FT_PQR(2, 4, 3)
-#undef FT_PQR
-  return -5;
-}
-
 // Requirements (checked): M <= 64, N % (16*nt) == 0, K % (64*splits) == 0.
 //   epi 0 (store): out (one split) or ws [splits, M, N]
 //   epi 1 (silu):  one split, nt even, out [M, N/2]; norm: x rows RMS-normalised
@@ -504,8 +357,7 @@ extern "C" int ft_pkr_gemm(const void* x, int x_stride, int M, const void* wpk, 
   const int mt = (M + 15) / 16;
   if (wn && (N % (64 * nt) != 0 || mt < 3)) return -9;
   ft::PrArgs a{(const uint16_t*)x, (const uint16_t*)wpk, ws, (uint16_t*)out, (uint16_t*)residual,
-               tickets, x_stride, M, K, N, K / splits, out_stride, res_stride, eps,
-               nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, 0};
+               tickets, x_stride, M, K, N, K / splits, out_stride, res_stride, eps};
   dim3 grid(N / (16 * nt) / (wn ? 4 : 1), splits), block(256);
 #define FT_PRW(MT_, NT_, S_, E_, N_, W_)                                                     \
   if (mt == MT_ && nt == NT_ && depth == S_ && epi == E_ && (norm != 0) == N_ &&             \

@@ -234,17 +234,13 @@ FUSED_PLAN = {
              48: (4, 2, 4, 0), 64: (4, 2, 4, 0)},
 }
 _SILU_CONFIGS = ((2, 2), (2, 3), (2, 4), (4, 2), (4, 3))
-# QKV with the RoPE + paged K/V epilogue in the same launch (ops.pkr_qkv_rope: one
-# workgroup per head, split-K reduced in the launch) instead of the ring GEMM's slabs
-# + slab_rope_kv: (splits, depth) per row bucket.  Off by default: measured on MI355X
-# the in-launch split-K seam (48 head tiles x 8 splits for Llama-3-8B) costs more than
-# the launch it saves -- 3.52 vs 3.25 ms per single-session decode step
-# (profiles/qkv_rope_ab_r04.log); FT_FUSED_QKV_ROPE=1 selects it.
-FUSED_QKV_ROPE = os.environ.get("FT_FUSED_QKV_ROPE", "0") == "1"
-QKV_ROPE_PLAN = {1: (8, 2), 8: (8, 2), 16: (8, 2), 32: (8, 2)}
-if os.environ.get("FT_QKV_ROPE_PLAN"):   # "splits:depth" for every bucket (sweeps)
-    _sp, _dp = (int(v) for v in os.environ["FT_QKV_ROPE_PLAN"].split(":"))
-    QKV_ROPE_PLAN = {b: (_sp, _dp) for b in QKV_ROPE_PLAN}
+# (Measured negatives, removed: the QKV projection with RoPE + the paged K/V write
+# in its own epilogue -- 3.52 vs 3.25 ms per single-session decode step, the
+# in-launch split-K seam costs more than the launch it saves
+# (profiles/qkv_rope_ab_r04.log); and RoPE + the K/V write inside the decode
+# attention launch -- 4.03 vs 3.27 ms single-session, 6.38 vs 6.23 ms at 50
+# sessions: every attention wave rebuilding its q from the slabs puts two dependent
+# memory round trips in front of its KV stream (profiles/rope_in_attention_ab_r04.log).)
 _FUSED_PLAN_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "fused_plan.json")
 
 
@@ -606,8 +602,7 @@ class LlamaModel:
             return
         for L in self.layers:
             L.fqkv, L.fo, L.fgu, L.fd = L.wqkv_pk, L.wo_pk, L.wgu_pk, L.wd_pk
-        # (+ one float per split and row: the RoPE epilogue's per-split sums of squares)
-        need = MAX_FUSED_SPLITS * FUSED_ROWS * (max(nqkv, H) + 1)
+        need = MAX_FUSED_SPLITS * FUSED_ROWS * max(nqkv, H)
         if self.ws is None or self.ws.numel() < need:
             self.ws = torch.empty(need, dtype=torch.float32, device=self.device)
         if self.tickets is None:
@@ -804,24 +799,13 @@ class LlamaModel:
         cg = fused_cfg("gu", t, 2 * I, H, nt_fixed=self.gu_nt)
         cd = fused_cfg("down", t, H, I)
         ws, tk = self.ws, self.tickets
-        rope_fused = FUSED_QKV_ROPE and t <= 32 and d in (64, 128)
-        if rope_fused:
-            rsp, rdp = QKV_ROPE_PLAN[fused_bucket(t)]
-            rsp = min(rsp, MAX_FUSED_SPLITS)
-            if H % (64 * rsp):
-                rsp = 1
         for li, L in enumerate(self.layers):
             kc, vc = kv_caches[li]
             qkv = torch.empty(t, nqkv, dtype=self.dtype, device=self.device)
-            if rope_fused:   # one launch: GEMM + RMS scale + RoPE + paged K/V write
-                ops.pkr_qkv_rope(residual, L.fqkv, qkv, meta.positions, self.cos_sin,
-                                 meta.slot_mapping, kc, vc, nq, nkv, d, eps, ws=ws, tickets=tk,
-                                 splits=rsp, depth=rdp)
-            else:
-                nt, dp, sp, wn = cq
-                ops.pkr_gemm(residual, L.fqkv, "store", ws=ws, splits=sp, nt=nt, depth=dp, wn=wn)
-                ops.slab_rope_kv(ws, sp, t, nqkv, qkv, meta.positions, self.cos_sin,
-                                 meta.slot_mapping, kc, vc, nq, nkv, d, residual=residual, eps=eps)
+            nt, dp, sp, wn = cq
+            ops.pkr_gemm(residual, L.fqkv, "store", ws=ws, splits=sp, nt=nt, depth=dp, wn=wn)
+            ops.slab_rope_kv(ws, sp, t, nqkv, qkv, meta.positions, self.cos_sin,
+                             meta.slot_mapping, kc, vc, nq, nkv, d, residual=residual, eps=eps)
             attn = self._attention(qkv, meta, kc, vc)
             nt, dp, sp, wn = co
             ops.pkr_gemm(attn, L.fo, "resid", residual=residual, ws=ws, tickets=tk, splits=sp,

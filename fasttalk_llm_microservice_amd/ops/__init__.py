@@ -430,19 +430,6 @@ def slab_rope_kv(ws, splits, rows, cols, q_out, positions, cos_sin, slot_mapping
     return q_out
 
 
-def pkr_qkv_rope(x, w_pk, q_out, positions, cos_sin, slot_mapping, k_cache, v_cache, nq, nkv,
-                 head_dim, eps: float, ws=None, tickets=None, splits: int = 1, depth: int = 2):
-    """The fused decode layer's QKV projection (M <= 32) with the RMS scale, RoPE and
-    the paged K/V write in its epilogue -- one launch instead of the ring GEMM +
-    slab_rope_kv.  x = the raw residual rows (the input-norm weight is folded into
-    ``w_pk``); q heads land in ``q_out`` (row stride kept), k / v heads in the caches.
-    splits > 1: split-K reduced in the launch (``ws`` >= splits * M * (N + 1) floats,
-    ``tickets`` >= N / head_dim zeroed int32, left zeroed)."""
-    native().pkr_qkv_rope(x, w_pk, ws, tickets, splits, depth, q_out, positions, cos_sin,
-                          slot_mapping, k_cache, v_cache, nq, nkv, head_dim, eps)
-    return q_out
-
-
 # ---------------------------------------------------------------------------------
 # fused decode layer GEMMs (csrc/kernels/skinny_pkr.hip)
 # ---------------------------------------------------------------------------------

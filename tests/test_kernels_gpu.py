@@ -734,47 +734,6 @@ def test_slab_rope_kv_residual_norm():
     _close(v1, v2, atol=3e-2, rtol=2e-2, msg="v")
 
 
-@pytest.mark.parametrize("m", [1, 7, 19, 32])
-@pytest.mark.parametrize("splits", [1, 4, 8])
-@pytest.mark.parametrize("nq,nkv,d,hidden", [(16, 4, 128, 2048), (32, 8, 128, 4096),
-                                             (8, 2, 64, 1024)])
-def test_pkr_qkv_rope_fused_epilogue(m, splits, nq, nkv, d, hidden):
-    """QKV GEMM + RMS scale + RoPE + paged K/V write in one launch (fused decode layer,
-    skinny_pkr.hip EPI_ROPE) vs fp32: x W^T * rsqrt(mean(x^2) + eps), rotated, q to
-    q_out, k / v into the paged caches; a padding row (slot -1) writes no K/V; split-K
-    reduced in the launch (bit-identical on repeat, tickets re-armed)."""
-    eps, bs, nblocks = 1e-5, 16, 8
-    n = (nq + 2 * nkv) * d
-    w = (torch.randn(n, hidden, device=DEV) * 0.02).bfloat16()
-    x = torch.randn(m, hidden, device=DEV).bfloat16()
-    wp = ops.pack_weight(w)
-    pos = torch.randint(0, 4000, (m,), device=DEV, dtype=torch.int32)
-    cs = ref.rope_cos_sin(d, 8192, 500000.0, None, DEV)
-    slots = torch.randperm(nblocks * bs, device=DEV)[:m].int()
-    if m > 1:
-        slots[-1] = -1
-    k1, v1 = _alloc_cache(nblocks, nkv, bs, d)
-    k0, v0 = k1.clone(), v1.clone()
-    ws = torch.empty(splits * m * (n + 1), device=DEV)
-    tickets = torch.zeros(256, dtype=torch.int32, device=DEV)
-    qs = []
-    for _ in range(2):
-        q_out = torch.zeros(m, n, device=DEV).bfloat16()   # row stride = n, like the qkv buffer
-        ops.pkr_qkv_rope(x, wp, q_out, pos, cs, slots, k1, v1, nq, nkv, d, eps, ws=ws,
-                         tickets=tickets, splits=splits, depth=2)
-        qs.append(q_out)
-    torch.cuda.synchronize()
-    assert int(tickets.abs().sum().item()) == 0
-    assert torch.equal(qs[0], qs[1])
-    r = torch.rsqrt(x.float().pow(2).mean(-1, keepdim=True) + eps)
-    qkv = ((x.float() @ w.float().t()) * r).bfloat16()
-    k2, v2 = k0.clone(), v0.clone()
-    ref.rope_kv_write(qkv, pos, cs, slots, k2, v2, nq, nkv, d)
-    _close(qs[0][:, : nq * d], qkv[:, : nq * d], atol=4e-2, rtol=3e-2, msg="q")
-    _close(k1, k2, atol=4e-2, rtol=3e-2, msg="k")
-    _close(v1, v2, atol=4e-2, rtol=3e-2, msg="v")
-
-
 @pytest.mark.parametrize("m", [65, 80, 200, 256, 300, 700])
 @pytest.mark.parametrize("cfg", [0, 1, 2, 3])
 def test_packed_gemm_matches_fp32(m, cfg):
