@@ -6,7 +6,8 @@ that has served many sessions.
 
 python bench/attn_sweep.py [--nq 32 --nkv 8] [--uniform]
 FT_DECODE_RING=2|3|4 selects the kernel's register-ring depth (default 2);
-FT_DECODE_MIN_TILES the partition's minimum 16-token tiles per wave (default 4).
+FT_DECODE_MIN_TILES the partition's minimum 16-token tiles per wave (default 8);
+FT_DECODE_WPC workgroups per CU (1-3, default 1).
 --fused: the in-launch combine the engine uses (decode tickets) instead of the
 separate combine kernel.  --shapes "1:512,1:3000" overrides the shape list.
 """
@@ -63,7 +64,8 @@ def main():
                                                  d ** -0.5, counters=cnt), iters=100, warmup=10)
         print(json.dumps({"B": B, "ctx": ctx, "uniform": a.uniform,
                           "ring": int(os.environ.get("FT_DECODE_RING", "2")),
-                          "min_tiles": int(os.environ.get("FT_DECODE_MIN_TILES", "4")),
+                          "min_tiles": int(os.environ.get("FT_DECODE_MIN_TILES", "8")),
+                          "wpc": int(os.environ.get("FT_DECODE_WPC", "1")),
                           "fused": a.fused,
                           "us": round(us, 2), "GBps": round(nbytes / us / 1e3, 1)}), flush=True)
         del kc, vc
