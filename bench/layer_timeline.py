@@ -46,6 +46,27 @@ def _load(path: str):
         raise SystemExit(f"no 'kernels' view in {path}; objects: {tabs}")
 
 
+def _mixed_summary(mixed):
+    """Mixed (prefill + decode) steps run eagerly: how much of their span the GPU
+    is busy (the rest is the host enqueueing kernels one by one), and where their
+    kernel time goes."""
+    span = busy = 0.0
+    agg = defaultdict(lambda: [0, 0.0])
+    for st in mixed:
+        span += (st[-1][2] - st[0][1]) / 1e3
+        for n, s, e in st:
+            busy += (e - s) / 1e3
+            agg[n][0] += 1
+            agg[n][1] += (e - s) / 1e3
+    m = len(mixed)
+    print(f"{m} mixed steps: mean span {span / m:.1f} us, kernel time {busy / m:.1f} us "
+          f"({100 * busy / max(span, 1e-9):.1f}% busy), {sum(len(st) for st in mixed) / m:.0f} kernels")
+    print(f"{'kernel (mixed steps)':60s} {'calls/step':>10} {'us/step':>9} {'avg_us':>8}")
+    for n, (k, d) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:20]:
+        print(f"{n:60s} {k / m:10.1f} {d / m:9.1f} {d / k:8.2f}")
+    print()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("db")
@@ -62,6 +83,9 @@ def main():
         cur.append((_short(name), s, e))
     if cur:
         steps.append(cur)
+    mixed = [st for st in steps if any("prefill" in n for n, _, _ in st)]
+    if mixed:
+        _mixed_summary(mixed)
     # decode steps: no prefill kernels, and the most common kernel count
     dec = [st for st in steps if not any("prefill" in n or "packed_gemm" in n for n, _, _ in st)]
     if not dec:
