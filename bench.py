@@ -292,7 +292,7 @@ def main():
 
     summ = summarize(res)
     local = {"tokens": res["tokens"], "frames": res.get("frames", 0), "elapsed": elapsed,
-             "ttft": res["ttft_s"],
+             "ttft": res["ttft_s"], "tool_ttft": res.get("tool_ttft_s", []),
              "server_ttft": res.get("server_ttft_ms", []),
              "engine_ttft": res.get("engine_ttft_ms", []),
              "cached": res["cached_prompt_tokens"], "prompt": res["prompt_tokens"]}
@@ -360,6 +360,16 @@ def main():
             "engine_decode_host_ms": metrics.get("decode_host_ms", {}),
             "init_s": round(init_s, 1),
         }
+        if a.agent_tools >= 0:
+            # TTFT of the turns that asked for a web search (the guided call, the tool and
+            # the re-prompt all sit before their first token) vs the plain turns
+            tt = sorted(x for r in allr for x in r["tool_ttft"])
+            pt = lambda q: tt[min(len(tt) - 1, int(round(q * (len(tt) - 1))))] if tt else 0.0  # noqa
+            out["tool_turns"] = {"n": len(tt), "p50_ttft_ms": round(1e3 * pt(0.5), 2),
+                                 "p99_ttft_ms": round(1e3 * pt(0.99), 2)}
+            out["guided_output_tokens"] = metrics.get("guided_output_tokens", {})
+            out["engine_guided"] = {k: v for k, v in metrics.items()
+                                    if k in ("jump_forward_tokens", "grammar_complete_stops")}
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

@@ -69,8 +69,8 @@ class Session:
 
     async def turn(self) -> Dict[str, Any]:
         t0 = time.perf_counter()
-        await self.ws.send_json({"type": "user_message",
-                                 "text": user_text(self.rng, self.words, self.tool_frac)})
+        text = user_text(self.rng, self.words, self.tool_frac)
+        await self.ws.send_json({"type": "user_message", "text": text})
         first = None
         frames = 0
         while True:
@@ -89,7 +89,9 @@ class Session:
                        "server_ttft_ms": st.get("ttft_ms"),
                        "engine_ttft_ms": st.get("engine_ttft_ms"),
                        "cached_prompt_tokens": st.get("cached_prompt_tokens", 0),
-                       "prompt_tokens": st.get("prompt_tokens", 0)}
+                       "prompt_tokens": st.get("prompt_tokens", 0),
+                       # a turn that asks for a web search (config 5: the agent's tool round)
+                       "tool": text.startswith("Search the web")}
                 self.turns.append(rec)
                 return rec
             elif t == "error":
@@ -140,6 +142,7 @@ class LoadClient:
         recs = [r for rs in res for r in rs]
         return {"elapsed_s": dt, "tokens": sum(r["tokens"] for r in recs),
                 "frames": sum(r["frames"] for r in recs), "ttft_s": [r["ttft_s"] for r in recs],
+                "tool_ttft_s": [r["ttft_s"] for r in recs if r["tool"]],
                 "latency_s": [r["latency_s"] for r in recs],
                 "server_ttft_ms": [r["server_ttft_ms"] for r in recs if r["server_ttft_ms"] is not None],
                 "engine_ttft_ms": [r["engine_ttft_ms"] for r in recs if r["engine_ttft_ms"] is not None],

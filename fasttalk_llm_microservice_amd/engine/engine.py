@@ -81,7 +81,10 @@ class LLMEngine:
         self._trie = None
         # jump-forward over grammar-forced runs (ENGINE_JUMP_FORWARD=0 disables)
         self.jump_forward = os.environ.get("ENGINE_JUMP_FORWARD", "1") != "0"
+        # a grammar that is complete ends the sequence without decoding its EOS
+        self.grammar_eos_shortcut = self.jump_forward
         self._jf_cache: Dict[bytes, List[int]] = {}
+        self._guided_lens = collections.deque(maxlen=4096)
         self.stats = collections.Counter()
         self.step_times = collections.deque(maxlen=512)
         # FT_STEP_TRACE=<path>: per-step timeline (kind, rows, tokens, start/end) and
@@ -551,6 +554,14 @@ class LLMEngine:
                 jtext, post_ids = self._jump_forward(seq, room)
                 delta += jtext
                 n_out = seq.num_output
+                # the grammar is complete (accepting, no byte can follow: the mask would
+                # allow EOS alone): end here instead of decoding that EOS -- for a tool
+                # call the step that prefills its forced closing and samples the EOS is
+                # skipped (the uncomputed tail is never committed to the prefix cache)
+                if self.grammar_eos_shortcut and n_out >= p.min_tokens and \
+                        seq.grammar.complete(seq.grammar_state):
+                    reason = "stop"
+                    self.stats["grammar_complete_stops"] += 1
         if reason is None:
             if n_out >= p.max_tokens or seq.n_tokens >= self.max_model_len:
                 reason = "length"
@@ -603,6 +614,8 @@ class LLMEngine:
         if seq.status != SeqStatus.FINISHED or seq.block_ids:
             self.scheduler.finish(seq, reason)
         seq.finish_reason = reason
+        if seq.grammar is not None:   # output lengths of guided sequences (tool calls, JSON)
+            self._guided_lens.append(seq.num_output)
         tail = ""
         if seq.detok_stream >= 0:
             if reason != "abort":
@@ -684,7 +697,18 @@ class LLMEngine:
                           if getattr(self.runner, "_gaps", None) else {})},
             "decode_host_ms": {k: round(1e3 * v / max(1, self.host_prof["steps"]), 3)
                                for k, v in self.host_prof.items() if k != "steps"},
+            "guided_output_tokens": self._len_summary(self._guided_lens),
         }
+
+    @staticmethod
+    def _len_summary(lens) -> Dict[str, Any]:
+        if not lens:
+            return {}
+        v = sorted(lens)
+        q = lambda f: v[min(len(v) - 1, int(round(f * (len(v) - 1))))]  # noqa: E731
+        hist = collections.Counter(min(64, (x + 7) // 8 * 8) for x in v)
+        return {"n": len(v), "p50": q(0.5), "p90": q(0.9), "max": v[-1],
+                "hist_le": {str(k): hist[k] for k in sorted(hist)}}
 
 
 class AsyncEngine:
