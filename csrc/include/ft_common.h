@@ -87,6 +87,29 @@ __device__ __forceinline__ float group_max(float v) {
   return v;
 }
 
+// reduce over the 4 lanes {l, l^16, l^32, l^48} (the k groups of an MFMA 16x16
+// C-layout column): gfx950 VALU lane swaps -- v_permlane16_swap exchanges the odd
+// rows of one copy with the even rows of the other (the xor-16 partners),
+// v_permlane32_swap the wave halves (xor 32) -- instead of ds_bpermute round trips,
+// which put two waited LDS latencies on an attention tile's critical path
+__device__ __forceinline__ float kgroups_max(float x) {
+  const unsigned u = __float_as_uint(x);
+  const auto r16 = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+  x = fmaxf(__uint_as_float(r16[0]), __uint_as_float(r16[1]));
+  const unsigned v = __float_as_uint(x);
+  const auto r32 = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  return fmaxf(__uint_as_float(r32[0]), __uint_as_float(r32[1]));
+}
+
+__device__ __forceinline__ float kgroups_sum(float x) {
+  const unsigned u = __float_as_uint(x);
+  const auto r16 = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+  x = __uint_as_float(r16[0]) + __uint_as_float(r16[1]);
+  const unsigned v = __float_as_uint(x);
+  const auto r32 = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  return __uint_as_float(r32[0]) + __uint_as_float(r32[1]);
+}
+
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 __device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
 

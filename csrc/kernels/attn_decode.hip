@@ -136,8 +136,7 @@ __device__ __forceinline__ void dec_finish(floatx4_t (&o)[ND], float l_run, floa
                                            float* __restrict__ tmp_out, float* __restrict__ tmp_ml,
                                            int* __restrict__ counters, int lane, int g, int n) {
   // head n's sum over the 4 token groups
-  float l_tot = l_run + __shfl_xor(l_run, 16, 64);
-  l_tot += __shfl_xor(l_tot, 32, 64);
+  const float l_tot = kgroups_sum(l_run);
   // C-layout rows of O: lane (g, n) holds heads 4g+i, dim n (+16 nd)
   const int seg = b * nkv + h;
   if (t0 == 0 && cnt == nb) {   // the whole segment: final bf16 output
@@ -356,8 +355,7 @@ __global__ __launch_bounds__(256, WPC) void paged_decode_kernel(
             if (4 * g + i4 >= valid) s[i4] = -INFINITY;
         }
         float tm = fmaxf(fmaxf(s[0], s[1]), fmaxf(s[2], s[3]));
-        tm = fmaxf(tm, __shfl_xor(tm, 16, 64));
-        tm = fmaxf(tm, __shfl_xor(tm, 32, 64));
+        tm = kgroups_max(tm);   // over the 4 token groups of head n
         // deferred rescale (guide T13): the reference max m_run (raw score units) moves
         // only when some head's tile max passes it by more than kDecRescaleThr (log2
         // units), so p <= 2^thr and most tiles skip alpha, the O rescale and the l

@@ -54,15 +54,10 @@ constexpr float kPrefillRescaleThr = 8.f;
 constexpr int kPrefillRows = 256; // query rows (token x head) per workgroup
 constexpr int kPrefillMaxBlocks = 4096;  // block-table entries staged in LDS (checked on the host)
 
-// max over aligned groups of 4 lanes that differ in bits 4..5 (the k groups)
-__device__ __forceinline__ float kgroup_max(float v) {
-  v = fmaxf(v, __shfl_xor(v, 16, 64));
-  return fmaxf(v, __shfl_xor(v, 32, 64));
-}
-__device__ __forceinline__ float kgroup_sum(float v) {
-  v += __shfl_xor(v, 16, 64);
-  return v + __shfl_xor(v, 32, 64);
-}
+// max / sum over aligned groups of 4 lanes that differ in bits 4..5 (the k groups):
+// ft_common.h kgroups_max / kgroups_sum (VALU lane swaps)
+__device__ __forceinline__ float kgroup_max(float v) { return kgroups_max(v); }
+__device__ __forceinline__ float kgroup_sum(float v) { return kgroups_sum(v); }
 
 template <int D, int G>
 __global__ __launch_bounds__(512, 1) void prefill_attn_kernel(

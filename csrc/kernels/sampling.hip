@@ -176,6 +176,7 @@ constexpr int kSlThreads = 256;
 // keeps its own top-k candidates (the global top-k is a subset of their union)
 constexpr int kTopkMax = 64;
 constexpr int kTopkKept = 256;   // kept set (top-k + ties) the merge kernel holds
+static_assert(kTopkKept <= kSlThreads, "one merge thread per kept rank");
 // per-row fp32 scratch: slice stats [kSlices][4] (M_p, Z_p, key, id) | M, Z |
 // cand (key, id) x 2 | above [kSlices][2] | flag | top-k candidate counts
 // [kSlices] | top-k candidates [kSlices][kTopkMax] (key, id)
@@ -931,8 +932,9 @@ __global__ __launch_bounds__(kSlThreads) void samp_above_kernel(
 // slices' candidates, keep key >= t* (t* = largest key with count(key >= t*) >= k,
 // the single-workgroup kernel's rule: ties at the threshold stay), then top-p over
 // the kept ids (an id is in the nucleus iff the mass of strictly more likely kept
-// ids is < top_p * Z) and one inverse-CDF draw in (key desc, id asc) order --
-// deterministic whatever order the candidates were appended in.  Rows whose
+// ids is < top_p * Z) and one inverse-CDF draw in (key desc, id asc) order over a
+// rank-ordered prefix sum -- deterministic whatever order the candidates were
+// appended in.  Rows whose
 // candidates or kept set overflow go to the one-workgroup kernel (flag 2).
 __global__ __launch_bounds__(kSlThreads) void samp_topk_kernel(
     int* __restrict__ out_tokens, int vocab, const float* __restrict__ temperature,
@@ -946,6 +948,7 @@ __global__ __launch_bounds__(kSlThreads) void samp_topk_kernel(
   __shared__ uint32_t s_k[kTopkKept];
   __shared__ int s_i[kTopkKept];
   __shared__ float s_e[kTopkKept];
+  __shared__ float s_c[kTopkKept];
   const int row = blockIdx.x, tid = threadIdx.x;
   if (!mw_topk_row(top_k, temperature, row, vocab)) return;
   float* wr = ws + (long)row * kWsRow;
@@ -1028,20 +1031,37 @@ __global__ __launch_bounds__(kSlThreads) void samp_topk_kernel(
   }
   const bool member = tid < nk && (tp >= 1.f || above < tp * Z);
   __syncthreads();
-  if (tid < nk) s_e[tid] = member ? e : 0.f;   // nucleus masses
-  const float Zn = wg_sum(member ? e : 0.f, sf);
-  // mass of the members ranked before this one
-  float cum = 0.f;
-  if (member)
-    for (int j = 0; j < nk; ++j) {
-      const uint32_t kj = s_k[j];
-      if (kj > mk || (kj == mk && s_i[j] < mi)) cum += s_e[j];
-    }
+  // nucleus masses in (key desc, id asc) rank order (the ranks are a permutation of
+  // 0..nk-1), then ONE prefix sum over that order: the members' intervals
+  // [cum, cum + e) tile [0, Zn) exactly and every sum has a fixed order, whatever
+  // order the candidates were appended in (a seeded draw reproduces bit for bit)
+  if (tid < nk) s_e[rank] = member ? e : 0.f;
+  __syncthreads();
+  float incl = tid < nk ? s_e[tid] : 0.f;   // the mass of rank tid, then its inclusive prefix
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const float y = __shfl_up(incl, o, 64);
+    if (lane_id() >= o) incl += y;
+  }
+  if (lane_id() == 63) sf[wave_id()] = incl;
+  __syncthreads();
+  float wbase = 0.f;
+  for (int w = 0; w < wave_id(); ++w) wbase += sf[w];
+  float Zn = 0.f;
+  for (int w = 0; w < kSlThreads / 64; ++w) Zn += sf[w];
+  float excl = __shfl_up(incl, 1, 64);
+  if (lane_id() == 0) excl = 0.f;
+  // the start of rank tid's interval; an interval ends where the next one starts, so
+  // consecutive boundaries tile [0, Zn) with no gap or overlap under any rounding
+  if (tid < nk) s_c[tid] = wbase + excl;
+  __syncthreads();
+  const float cum = member ? s_c[rank] : 0.f;
   const uint64_t s0 =
       splitmix64((uint64_t)seeds[row] ^ (0x632BE59BD9B4E019ull * (uint64_t)(steps[row] + 1)));
   const uint64_t h = splitmix64(s0);
   const float T = ((float)(h >> 40) + 0.5f) * (1.0f / 16777216.0f) * Zn;
-  if (member && T >= cum && T < cum + e) s_pick = mi;
+  const float hi = rank + 1 < nk ? s_c[rank + 1] : Zn;   // the next rank's start
+  if (member && e > 0.f && T >= cum && T < hi) s_pick = mi;
   if (member) atomicMax(&s_last, rank);   // rounding tail: the last-ranked member
   __syncthreads();
   if (s_pick < 0 && member && rank == s_last) s_pick = mi;
