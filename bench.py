@@ -369,7 +369,8 @@ def main():
                                  "p99_ttft_ms": round(1e3 * pt(0.99), 2)}
             out["guided_output_tokens"] = metrics.get("guided_output_tokens", {})
             out["engine_guided"] = {k: v for k, v in metrics.items()
-                                    if k in ("jump_forward_tokens", "grammar_complete_stops")}
+                                    if k in ("jump_forward_tokens", "grammar_complete_stops",
+                                             "guided_pipelined_steps", "pipelined_jump_drops")}
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

@@ -187,17 +187,24 @@ class LLMEngine:
         return (self.cfg.async_output and not batch.has_prefill and bool(batch.decode_seqs)
                 and self.runner.__class__.__name__ == "ModelRunner"
                 and self.runner.can_pipeline(len(batch.decode_seqs))
-                and all(s.grammar is None for s in batch.decode_seqs))
+                and (all(s.grammar is None for s in batch.decode_seqs) or self._guided_pipeline()))
 
-    def _launch_decode(self, seqs, from_device: bool, rowmap=None):
+    def _guided_pipeline(self) -> bool:
+        """Guided (grammar-masked) batches pipeline too: the next step's forward pass
+        is queued before this step's tokens are known, and only its sampler waits
+        for the masks the tokens decide (runner.sample_launch)."""
+        return getattr(self.runner, "can_defer_sample", lambda: False)()
+
+    def _launch_decode(self, seqs, from_device: bool, rowmap=None, masks=None):
         """Queues a graph-replayed decode step.  Positions come from each sequence's
         ``inflight`` count (steps queued ahead of it); with ``from_device`` the
         input ids are the previous queued step's sampled rows (``rowmap``: the row
-        of that step each sequence sat in; None = the same rows)."""
-        if rowmap is None:
-            h = self.runner.decode_launch(seqs, ahead=int(from_device))
-        else:
-            h = self.runner.decode_launch(seqs, ahead=1, rowmap=rowmap)
+        of that step each sequence sat in; None = the same rows).  A guided batch
+        queued ahead (``from_device``) defers its sampler until its masks are known."""
+        defer = from_device and any(q.grammar is not None for q in seqs)
+        h = self.runner.decode_launch(seqs, ahead=int(from_device), masks=masks,
+                                      rowmap=rowmap if from_device else None,
+                                      **({"defer_sample": True} if defer else {}))
         for q in seqs:
             q.inflight += 1
         return _Inflight(ScheduledBatch(list(seqs), [], [], []), h, False)
@@ -218,6 +225,8 @@ class LLMEngine:
           the queue drains (the session's next prompt usually follows within a
           step and then starts sooner)."""
         sched = self.scheduler
+        if getattr(self._inflight[-1].handle, "pending", False):
+            return None   # its sampled ids (the next step's inputs) are not queued yet
         last = self._inflight[-1].batch.sampled_seqs()
         # a background warm-up ends the pipeline unless the batch is full (it could
         # not join a step anyway)
@@ -230,7 +239,13 @@ class LLMEngine:
             if not self.pipeline_shrink or not seqs or not self.runner.can_pipeline(len(seqs)):
                 return None
             rowmap = [i for i, q in enumerate(last) if q.status != SeqStatus.FINISHED]
-        if not self.runner.can_pipeline(len(seqs)) or any(q.grammar is not None for q in seqs):
+        if not self.runner.can_pipeline(len(seqs)):
+            return None
+        if any(q.grammar is not None for q in seqs) and not self._guided_pipeline():
+            return None
+        # a jump-forward appended forced tokens behind a queued step: they are
+        # prefilled by the drained path (their sequence's queued sample is dropped)
+        if any(q.drop_next for q in seqs):
             return None
         if not self._grow_for_next(seqs):
             return None
@@ -336,6 +351,12 @@ class LLMEngine:
         for q in sampled:
             q.inflight -= 1
         outs = self._complete(batch, sampled, toks)
+        # the guided step queued behind this one: its forward pass is running; its
+        # sampler goes in now that this step's tokens have moved the grammars
+        if self._inflight and getattr(self._inflight[0].handle, "pending", False):
+            nxt = self._inflight[0]
+            self.runner.sample_launch(nxt.handle, self._masks_for(nxt.batch.sampled_seqs()))
+            self.stats["guided_pipelined_steps"] += 1
         t2 = time.perf_counter()
         dt = t2 - self._last_complete if self._last_complete else t2 - t0
         self._last_complete = t2
@@ -361,6 +382,10 @@ class LLMEngine:
         outs: List[RequestOutput] = []
         self.scheduler.post_step(batch)
         for seq, tok in zip(sampled_seqs, toks):
+            if seq.drop_next:   # its forced tokens replaced this sample (jump-forward)
+                seq.drop_next -= 1
+                self.stats["pipelined_jump_drops"] += 1
+                continue
             o = self._process_token(seq, int(tok))
             if o is not None:
                 outs.append(o)
@@ -381,6 +406,7 @@ class LLMEngine:
         for e in self._inflight:
             for q in e.batch.sampled_seqs():
                 q.inflight = 0
+                q.drop_next = 0
         self._inflight = []
 
     def fail_unfinished(self, error: str, reset_cache: bool = False):
@@ -435,7 +461,8 @@ class LLMEngine:
         if not batch.decode_seqs and not batch.prefill_seqs:
             return outs
         if not outs and self._pipeline_ok(batch):
-            e = self._launch_decode(batch.decode_seqs, False)
+            e = self._launch_decode(batch.decode_seqs, False,
+                                    masks=self._masks_for(batch.decode_seqs))
             e.t_launch = time.perf_counter()
             self._inflight = [e]
             return self._step_pipelined()
@@ -554,6 +581,10 @@ class LLMEngine:
                 jtext, post_ids = self._jump_forward(seq, room)
                 delta += jtext
                 n_out = seq.num_output
+                if post_ids and seq.inflight:
+                    # steps already queued behind this one sampled past a position the
+                    # grammar has now filled with forced tokens: drop their samples
+                    seq.drop_next = seq.inflight
                 # the grammar is complete (accepting, no byte can follow: the mask would
                 # allow EOS alone): end here instead of decoding that EOS -- for a tool
                 # call the step that prefills its forced closing and samples the EOS is

@@ -140,12 +140,15 @@ class MixedHandle:
 
 
 class DecodeHandle:
-    __slots__ = ("stage", "n", "nb")
+    """A queued graph-replayed decode step.  ``pending``: only its forward pass is
+    queued; its sampler waits for the allow-masks (``ModelRunner.sample_launch``)."""
+    __slots__ = ("stage", "n", "nb", "pending")
 
-    def __init__(self, stage: "_Staging", n: int, nb: int):
+    def __init__(self, stage: "_Staging", n: int, nb: int, pending: bool = False):
         self.stage = stage
         self.n = n
         self.nb = nb
+        self.pending = pending
 
 
 class ModelRunner:
@@ -259,6 +262,13 @@ class ModelRunner:
             if self.is_gpu and os.environ.get("FT_DECODE_FUSED_COMBINE", "1") == "1" else None
         self._done_event = torch.cuda.Event() if self.is_gpu else None
         self.graphs: Dict[int, torch.cuda.CUDAGraph] = {}
+        # guided decoding, pipelined: per bucket a forward graph (-> logits) and a
+        # sampler graph, so the next step's forward is queued before this step's
+        # tokens are known and only its sampler waits for the grammar masks
+        self.graphs_split: Dict[int, tuple] = {}
+        self._fwd_logits: Dict[int, torch.Tensor] = {}
+        # ENGINE_GUIDED_PIPELINE=0: guided batches run one synchronous step at a time
+        self.guided_pipeline = os.environ.get("ENGINE_GUIDED_PIPELINE", "1") != "0"
         self.graph_pool = None
         self.use_graphs = self.is_gpu and not cfg.enforce_eager and comm.graph_safe()
         # FT_FAULT_TP_STALL="<n>:<seconds>" (TP workers): before executing the n-th
@@ -605,6 +615,8 @@ class ModelRunner:
         self.comm.disable_custom("custom collective timed out")
         self.graphs.clear()  # they captured the custom kernels; recaptured on demand
         self._graph_logits.clear()
+        self.graphs_split.clear()
+        self._fwd_logits.clear()
         if not self.comm.graph_safe():
             self.use_graphs = False
         for st in self.stg:
@@ -622,14 +634,23 @@ class ModelRunner:
     def can_pipeline(self, n: int) -> bool:
         return self.use_graphs and self._bucket(n) is not None
 
+    def can_defer_sample(self) -> bool:
+        """Can a decode step be queued with its sampler deferred until its allow-masks
+        are known (pipelined guided decoding)?  Single process only (TP workers replay
+        whole steps from the broadcast)."""
+        return self.use_graphs and self.guided_pipeline and self.bcast is None \
+            and not self.checks_comm and self.d_mask is not None
+
     def decode_launch(self, seqs, ahead: int = 0, masks: Optional[np.ndarray] = None,
-                      rowmap: Optional[List[int]] = None) -> DecodeHandle:
+                      rowmap: Optional[List[int]] = None, defer_sample: bool = False
+                      ) -> DecodeHandle:
         """Fills a staging set and queues a graph-replayed decode step (returns at
         once).  Positions are ``inflight`` tokens past each sequence's collected
         state (steps queued ahead of it); with ``ahead`` the input ids are the last
         queued step's sampled ids, copied device-to-device, so the host never waits
         between steps.  ``rowmap[i]`` (with ``ahead``): the row of that step that
-        sequence i sat in (None: the same row)."""
+        sequence i sat in (None: the same row).  ``defer_sample``: queue the forward
+        pass only; ``sample_launch`` queues its sampler once the masks are known."""
         n = len(seqs)
         nb = self._bucket(n)
         st = self.stg[self._stg_next]
@@ -639,6 +660,10 @@ class ModelRunner:
         if ahead and rowmap is not None:
             gather = np.zeros(nb, dtype=np.int64)   # padding rows read row 0 (ignored)
             gather[:n] = rowmap
+        if defer_sample:
+            assert self.can_defer_sample()
+            self._decode_enqueue(st, nb, n, from_device=bool(ahead), gather=gather, fwd_only=True)
+            return DecodeHandle(st, n, nb, pending=True)
         if self.bcast is not None:
             self.bcast.send(("graph", {"nb": nb, "n": n, "small": st.hs.copy(),
                                        "bt": st.hbt[:nb, :maxblk].copy(), "f32": st.hf.copy(),
@@ -652,6 +677,20 @@ class ModelRunner:
                 self._tap_rows = [s.request_id for s in seqs]
             self._tap(self._graph_logits[nb][:n].float().clone())
         return DecodeHandle(st, n, nb)
+
+    def sample_launch(self, h: DecodeHandle, masks: Optional[np.ndarray]):
+        """Queues the sampler of a step whose forward pass ``decode_launch(...,
+        defer_sample=True)`` queued: its allow-masks go up, the sampler graph reads
+        the forward graph's logits, the ids land in ``d_out`` (the next step's
+        inputs) and in the staging set's pinned copy."""
+        assert h.pending
+        self._set_masks(masks, h.n)
+        self.graphs_split[h.nb][1].replay()
+        st = h.stage
+        st.h_out[:h.n].copy_(self.d_out[:h.n], non_blocking=True)
+        st.err_armed = False
+        st.event.record()
+        h.pending = False
 
     def _set_masks(self, masks: Optional[np.ndarray], n: int):
         """Uploads the step's allow-masks into the graph's static mask rows (stream
@@ -814,9 +853,9 @@ class ModelRunner:
                 "steps": len(busy)}
 
     def _decode_enqueue(self, st: "_Staging", nb: int, n: int, from_device: bool = False,
-                        gather: Optional[np.ndarray] = None):
+                        gather: Optional[np.ndarray] = None, fwd_only: bool = False):
         nw = 10 * self.max_decode_batch + nb * self.max_blocks_per_seq
-        if self._gaps is not None:
+        if self._gaps is not None and not fwd_only:
             self._gap_mark(True)
         self.d_in[:nw].copy_(st.h_in[:nw], non_blocking=True)
         if from_device:  # the previous step's sampled ids feed this step
@@ -826,6 +865,14 @@ class ModelRunner:
                 st.h_map[:nb].numpy()[:] = gather
                 self.d_map[:nb].copy_(st.h_map[:nb], non_blocking=True)
                 torch.index_select(self.d_out, 0, self.d_map[:nb], out=self.d_input_ids[:nb])
+        if fwd_only:
+            pair = self.graphs_split.get(nb)
+            if pair is None:
+                pair = self._capture_split(nb)
+            pair[0].replay()
+            self.stats["graph_replays"] += 1
+            self.stats["deferred_samples"] = self.stats.get("deferred_samples", 0) + 1
+            return
         g = self.graphs.get(nb)
         if g is None:
             g = self._capture(nb)
@@ -905,6 +952,48 @@ class ModelRunner:
             self.comm.export_error()
 
     @torch.inference_mode()
+    def _capture_split(self, nb: int):
+        """The forward graph (-> logits, held in ``_fwd_logits``) and the sampler graph
+        of bucket ``nb`` for pipelined guided decoding, captured like ``_capture``.
+        Nothing replays between a step's two halves (its sampler is queued before
+        the next forward), so the pool may share their temporaries with every other
+        graph; the logits stay allocated."""
+        t0 = time.time()
+        saved = (self.d_slots[:nb].clone(), self.d_seq_lens[:nb].clone())
+        self.d_slots[:nb].fill_(-1)
+        self.d_seq_lens[:nb].fill_(0)
+
+        def fwd():
+            h = self.model.forward(self.d_input_ids[:nb], self._decode_meta(nb), self.kv)
+            return self.model.compute_logits(h)
+
+        def samp(lg):
+            ops.sample(lg, self.d_temp[:nb], self.d_top_p[:nb], self.d_top_k[:nb],
+                       self.d_seeds[:nb], self.d_steps[:nb], out=self.d_out[:nb],
+                       mask=self.d_mask[:nb])
+
+        s = torch.cuda.Stream(self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            samp(fwd())  # warm-up (allocator, lazy init)
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        if self.graph_pool is None:
+            self.graph_pool = torch.cuda.graph_pool_handle()
+        gf = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gf, pool=self.graph_pool):
+            lg = fwd()
+        self._fwd_logits[nb] = lg
+        gs = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gs, pool=self.graph_pool):
+            samp(lg)
+        self.d_slots[:nb].copy_(saved[0])
+        self.d_seq_lens[:nb].copy_(saved[1])
+        self.graphs_split[nb] = (gf, gs)
+        self.stats["captures"] += 1
+        log.info("captured split decode graphs batch=%d in %.2fs", nb, time.time() - t0)
+        return gf, gs
+
+    @torch.inference_mode()
     def _capture(self, nb: int):
         """Captures the decode graph of batch bucket ``nb``.  Always under
         inference mode, whichever path triggers it (pipelined launches run outside
@@ -946,8 +1035,12 @@ class ModelRunner:
         if self.bcast is not None:
             self.bcast.send(("warmup", list(batch_sizes or self.graph_sizes), None))
         t0 = time.time()
+        split = self.can_defer_sample() and self.guided_pipeline
         for b in batch_sizes or self.graph_sizes:
             b = self._bucket(b)
             if b is not None and b not in self.graphs:
                 self._capture(b)
-        log.info("decode graphs ready (%d) in %.1fs", len(self.graphs), time.time() - t0)
+            if b is not None and split and b not in self.graphs_split:
+                self._capture_split(b)
+        log.info("decode graphs ready (%d + %d split) in %.1fs", len(self.graphs),
+                 len(self.graphs_split), time.time() - t0)

@@ -38,7 +38,8 @@ class Sequence:
                  "num_computed", "num_committed_blocks", "num_cached_tokens", "arrival",
                  "first_token_time", "finish_reason", "detok_stream", "on_output", "grammar",
                  "grammar_state", "stop_buf", "text_len", "aborted", "preemptions", "admit_order",
-                 "meta", "host_slots", "background", "jf_text", "jf_ids", "lazy", "inflight")
+                 "meta", "host_slots", "background", "jf_text", "jf_ids", "lazy", "inflight",
+                 "drop_next")
 
     def __init__(self, request_id: str, prompt_ids: List[int], params: SamplingParams,
                  on_output: Optional[Callable[[RequestOutput], None]] = None, meta: Any = None):
@@ -77,6 +78,9 @@ class Sequence:
         # queued (launched, not yet collected) steps that sample this sequence: its
         # next step's position / sampling step run this many tokens ahead of n_tokens
         self.inflight = 0
+        # samples of queued steps to discard: a jump-forward (pipelined guided decoding)
+        # appended forced tokens after the step behind it was already queued
+        self.drop_next = 0
 
     # ---------------------------------------------------------------- tokens
     @property

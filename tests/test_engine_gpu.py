@@ -295,6 +295,47 @@ def test_guided_rows_stay_on_the_decode_graph():
     assert eng.runner._mask_rows == 0 or eng.scheduler.has_work()
 
 
+def test_guided_decoding_pipelines_with_a_deferred_sampler(monkeypatch):
+    """Guided rows pipeline: the next step's forward graph is queued before this
+    step's tokens are known and only its sampler graph waits for the grammar masks
+    (runner.sample_launch).  Tool calls stay schema-valid (including forced runs
+    that land while a step is queued: that step's sample is dropped), plain rows run
+    their full length, nothing falls back to eager decoding.  (Token equality with
+    the synchronous engine is pinned on the CPU, tests/unit/test_pipelined_decode_cpu.py:
+    on the GPU a finished row still rides in the step queued behind it, and outputs
+    are not batch-invariant.)"""
+    import json
+
+    from fasttalk_llm_microservice_amd.engine.guided import GuidedSpec, tool_call_ast
+
+    tools = [{"type": "function", "function": {"name": "duckduckgo_search", "parameters": {
+        "type": "object", "properties": {"query": {"type": "string", "maxLength": 24},
+                                         "max_results": {"type": "integer"}},
+        "required": ["query", "max_results"]}}}]
+    spec = GuidedSpec(tool_call_ast(tools))
+    monkeypatch.setenv("ENGINE_GUIDED_PIPELINE", "1")
+    eng = _engine(max_num_seqs=16)
+    prompts = _prompts(8, [12, 20, 28, 9, 33, 17, 40, 5], seed=7)
+    res = {}
+    for i, p in enumerate(prompts):
+        guided = i % 3 == 0
+        sp = SamplingParams(temperature=0.8, seed=30 + i, max_tokens=80 if guided else 48,
+                            guided=spec if guided else None, ignore_eos=not guided)
+        eng.add_request(f"p{i}", p, sp, on_output=lambda o, i=i: res.setdefault(i, []).extend(o.token_ids))
+    while eng.has_work():
+        eng.step()
+    st = eng.runner.stats
+    assert st["eager_decode"] == 0 and st.get("deferred_samples", 0) > 0, st
+    assert eng.stats["guided_pipelined_steps"] > 0, dict(eng.stats)
+    for i in range(8):
+        if i % 3 == 0:
+            call = json.loads(eng.tokenizer.decode(res[i]))
+            assert call["name"] == "duckduckgo_search" and isinstance(call["parameters"]["max_results"], int)
+        else:
+            assert len(res[i]) == 48
+    assert eng.bm.num_free() == eng.bm.num_blocks or eng.bm.num_cached() > 0
+
+
 def test_single_weight_image_llama3_8b():
     """the GPU holds ONE image of the weights (packed, with the
     input norms folded in); resident weights <= 1.1x the model's bf16 size."""

@@ -318,3 +318,119 @@ def test_failure_with_a_queued_mixed_step_finishes_every_request():
     assert all(o.finish_reason == "error" for o in done.values())
     assert not eng.has_work()
     assert eng.bm.num_free() == eng.bm.num_blocks
+
+
+# ---- pipelined guided decoding (deferred sampler) --------------------------------
+
+def _pick(tok: int, pos: int, mask_row) -> int:
+    """The fake model's sample under an allow-mask row: unguided rows (all ones)
+    follow _next; guided rows pick deterministically among the allowed ids."""
+    import numpy as np
+
+    if mask_row is None or (mask_row == -1).all():
+        return _next(tok, pos)
+    allowed = np.nonzero(np.unpackbits(mask_row.view(np.uint8), bitorder="little"))[0]
+    assert len(allowed), "an empty allow-mask row"
+    return int(allowed[(tok * 131 + pos * 7) % len(allowed)])
+
+
+class _GHandle(_Handle):
+    def __init__(self, ids, pos, pending):
+        super().__init__(None)
+        self.ids, self.pos, self.pending = ids, pos, pending
+
+
+class _GuidedRunner(ModelRunner):
+    """Emulates the split decode graphs: a deferred launch runs the 'forward'
+    (fixes input ids and positions) and leaves the sample to sample_launch, which
+    gets the masks the engine computes from the previous step's tokens."""
+
+    def can_defer_sample(self) -> bool:
+        return True
+
+    def execute(self, batch, masks):
+        self.stats["steps"] += 1
+        return [_pick(int(s.tokens[-1]), s.n_tokens - 1, None if masks is None else masks[i])
+                for i, s in enumerate(batch.sampled_seqs())]
+
+    def decode_launch(self, seqs, ahead=0, masks=None, rowmap=None, defer_sample=False):
+        self.launches.append((len(seqs), ahead, None if rowmap is None else list(rowmap)))
+        if ahead:
+            rows = rowmap if rowmap is not None else range(len(seqs))
+            ids = [self.d_out[r] for r in rows]
+        else:
+            ids = [int(s.tokens[-1]) for s in seqs]
+        pos = [s.n_tokens - 1 + s.inflight for s in seqs]
+        for s, p in zip(seqs, pos):
+            assert p // self.bs < len(s.block_ids), "KV slot of a queued step has no block"
+        h = _GHandle(ids, pos, defer_sample)
+        if defer_sample:
+            self.d_out = None   # the next step may not read ids that are not sampled yet
+            self.stats["deferred"] = self.stats.get("deferred", 0) + 1
+        else:
+            self._sample(h, masks)
+        return h
+
+    def _sample(self, h, masks):
+        h.out = [_pick(t, p, None if masks is None else masks[i])
+                 for i, (t, p) in enumerate(zip(h.ids, h.pos))]
+        self.d_out = h.out
+        h.pending = False
+
+    def sample_launch(self, h, masks):
+        assert h.pending
+        self._sample(h, masks)
+
+    def decode_collect(self, h):
+        assert not h.pending, "collected a step whose sampler never ran"
+        return list(h.out)
+
+
+_GuidedRunner.__name__ = "ModelRunner"
+
+
+def test_guided_batches_pipeline_with_deferred_sampler():
+    """Guided (tool-call grammar) and free sequences decode together pipelined: the
+    step behind the running one is queued without its sampler, which goes in once
+    the running step's tokens moved the grammars.  Tokens equal the synchronous
+    engine's; forced runs (jump-forward) drop the queued sample and drain."""
+    import json
+    import os
+
+    from fasttalk_llm_microservice_amd.engine.guided import GuidedSpec, tool_call_ast
+
+    tools = [{"type": "function", "function": {"name": "duckduckgo_search", "parameters": {
+        "type": "object", "properties": {"query": {"type": "string", "maxLength": 24},
+                                         "max_results": {"type": "integer"}},
+        "required": ["query", "max_results"]}}}]
+    spec = GuidedSpec(tool_call_ast(tools))
+
+    def run(async_output):
+        os.environ["ENGINE_MIXED_AHEAD"] = "0"
+        cfg = EngineConfig(model="tiny", device="cpu", block_size=4, async_output=async_output,
+                           pipeline_depth=1, max_num_seqs=32)
+        runner = _GuidedRunner()
+        eng = LLMEngine(cfg, runner=runner)
+        res = {}
+        for i in range(6):
+            guided = i % 2 == 0
+            sp = SamplingParams(temperature=0.0, max_tokens=60 if guided else 10 + 3 * i,
+                                stop_token_ids=None if guided else [EOS],
+                                guided=spec if guided else None)
+            eng.add_request(f"r{i}", [20 + 3 * i + j for j in range(4 + i)], sp,
+                            on_output=lambda o, i=i: res.setdefault(i, []).extend(o.token_ids))
+        while eng.has_work():
+            eng.step()
+        os.environ.pop("ENGINE_MIXED_AHEAD", None)
+        assert eng.bm.num_free() == eng.bm.num_blocks
+        assert all(q.inflight == 0 and q.drop_next == 0 for q in eng.scheduler.by_id.values())
+        return [res.get(i, []) for i in range(6)], eng, runner
+
+    ref, _, _ = run(False)
+    got, eng, runner = run(True)
+    assert got == ref
+    for i in (0, 2, 4):   # the guided ones are valid calls
+        call = json.loads(eng.tokenizer.decode(got[i]))
+        assert call["name"] == "duckduckgo_search"
+    assert eng.stats["guided_pipelined_steps"] > 0 and runner.stats.get("deferred", 0) > 0
+    assert eng.stats["jump_forward_tokens"] > 0 and eng.stats["pipelined_jump_drops"] > 0
