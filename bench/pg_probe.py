@@ -42,7 +42,7 @@ def main():
     ap.add_argument("--rows", default="80,128,256,512,1024,4096")
     ap.add_argument("--only", default="")
     ap.add_argument("--iters", type=int, default=10)
-    ap.add_argument("--cfgs", default="0,1,2,3,4")
+    ap.add_argument("--cfgs", default="0,1,2,3,4,5,6")
     ap.add_argument("--splits", default="1,2,4,8,16")
     a = ap.parse_args()
     torch.manual_seed(0)
@@ -68,7 +68,8 @@ def main():
                         cands.append((f"xc{nt}/{sp}", lambda nt=nt, sp=sp: ops.native().skinny_gemm(
                             x, wp, out, ws, sp, nt, -4), sp))
             for cfg in [int(c) for c in a.cfgs.split(",")]:
-                bm, bn = [(256, 256), (128, 256), (256, 128), (256, 256), (256, 256)][cfg]
+                bm, bn = [(256, 256), (128, 256), (256, 128), (256, 256), (256, 256),
+                          (192, 256), (192, 128)][cfg]
                 tiles = -(-m // bm) * -(-n // bn)
                 for sp in [int(v) for v in a.splits.split(",")]:
                     if k % (64 * sp) or (sp > 1 and tiles * sp > 2048) or (sp > 1 and tiles >= 512):

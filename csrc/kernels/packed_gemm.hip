@@ -482,7 +482,8 @@ __global__ __launch_bounds__(256) void unpack_weight_kernel(uint16_t* __restrict
 }  // namespace ft
 
 // cfg: 0 = 256x256 tile (2x4 waves of 128x64, 2 LDS slots), 1 = 128x256 (2x4 waves
-// of 64x64, 3 slots), 2 = 256x128 (4x2 waves of 64x64, 3 slots), 3 = 256x256 phased.
+// of 64x64, 3 slots), 2 = 256x128 (4x2 waves of 64x64, 3 slots), 3 = 256x256 phased,
+// 5 = 192x256 (2x4 waves of 96x64, 2 slots), 6 = 192x128 (4x2 waves of 48x64, 3 slots).
 // epi: 0 bf16 out, 1 fp32 slabs (splits > 1), 2 SiLU-mul of interleaved gate/up.
 // Requirements (checked): N % 16 == 0 (N % 32 for SiLU), K % (64 * splits) == 0.
 extern "C" int ft_packed_gemm(const void* x, int x_stride, int M, const void* wpk, int N, int K,
@@ -501,6 +502,8 @@ extern "C" int ft_packed_gemm(const void* x, int x_stride, int M, const void* wp
     case 2: bm = 256; bn = 128; break;
     case 3: bm = 256; bn = 256; break;
     case 4: bm = 256; bn = 256; break;
+    case 5: bm = 192; bn = 256; break;
+    case 6: bm = 192; bn = 128; break;
     default: return -5;
   }
   const int tiles = ((M + bm - 1) / bm) * ((N + bn - 1) / bn);
@@ -540,6 +543,10 @@ extern "C" int ft_packed_gemm(const void* x, int x_stride, int M, const void* wp
   FT_PG(4, 2, 2, 8, 8, 2)
   FT_PG(1, 2, 4, 4, 4, 3)
   FT_PG(2, 4, 2, 4, 4, 3)
+  // 192-row tiles: mixed steps of 129-192 / 257-384 rows pad to 192 / 384 instead of
+  // 256 / 512 (a third fewer MFMA rows computed for nothing)
+  FT_PG(5, 2, 4, 6, 4, 2)
+  FT_PG(6, 4, 2, 3, 4, 3)
 #undef FT_PG
   return -5;
 }

@@ -172,12 +172,20 @@ PG_RM_ROWS = int(os.environ.get("FT_PG_RM_ROWS", "257"))
 RM_PROJS = ("qkv", "o", "gu")
 
 
+# 192-row twins of the 256-row tiles (cfg 0 -> 5, 2 -> 6): used when they pad the
+# step's rows to fewer MFMA rows (129-192 rows: 192 instead of 256; 257-384: 384
+# instead of 512).  FT_PG_192=0 keeps the 256-row tiles.
+PG_192 = {0: 5, 2: 6} if os.environ.get("FT_PG_192", "1") == "1" else {}
+
+
 def pg_cfg(proj: str, rows: int, k: int) -> Tuple[int, int]:
     for lim, cfg, sp in PG_PLAN[proj]:
         if rows <= lim:
             break
     while sp > 1 and k % (64 * sp):
         sp //= 2
+    if cfg in PG_192 and -(-rows // 192) * 192 < -(-rows // 256) * 256:
+        cfg = PG_192[cfg]
     return cfg, sp
 
 
