@@ -256,7 +256,9 @@ class VoiceAgent:
                     request_id=sid, session_id=sid if (rnd == 0 and (guided is None or lazy)) else None,
                     prefix_session=sid, assistant_prefix=head, tools=schemas or None, guided=guided,
                     seed=seed, guided_lazy=lazy,
-                    ignore_eos=ignore_eos and (guided is None or lazy), min_tokens=min_tokens):
+                    ignore_eos=ignore_eos and (guided is None or lazy), min_tokens=min_tokens,
+                    # a re-prompt after a tool ran: its user has waited through the call
+                    **({"priority": 1} if rnd > 0 else {})):
                 if out.finished:
                     finish = out.finish_reason
                 n = len(out.token_ids)

@@ -322,7 +322,7 @@ class NativeHandler:
 
     # ------------------------------------------------------------------ generation
     def _params(self, temperature, max_tokens, top_p, top_k=None, stop=None, seed=None,
-                guided=None, ignore_eos=False, min_tokens=0, guided_lazy=False):
+                guided=None, ignore_eos=False, min_tokens=0, guided_lazy=False, priority=0):
         from fasttalk_llm_microservice_amd.engine.sampling_params import SamplingParams
 
         return SamplingParams(
@@ -331,7 +331,7 @@ class NativeHandler:
             top_k=0 if top_k in (None, -1) else int(top_k),
             max_tokens=int(max_tokens or self.default_max_tokens),
             stop=stop, seed=seed, guided=guided, ignore_eos=ignore_eos, min_tokens=min_tokens,
-            guided_lazy=bool(guided_lazy and guided is not None))
+            guided_lazy=bool(guided_lazy and guided is not None), priority=int(priority))
 
     async def stream_events(self, messages: List[Dict[str, Any]], temperature: Optional[float] = None,
                             max_tokens: Optional[int] = None, top_p: Optional[float] = None,
@@ -340,14 +340,16 @@ class NativeHandler:
                             prompt_ids: Optional[List[int]] = None, tools=None, guided=None,
                             seed: Optional[int] = None, ignore_eos: bool = False,
                             min_tokens: int = 0, prefix_session: Optional[str] = None,
-                            assistant_prefix: str = "", guided_lazy: bool = False) -> AsyncIterator[Any]:
+                            assistant_prefix: str = "", guided_lazy: bool = False,
+                            priority: int = 0) -> AsyncIterator[Any]:
         """``prefix_session`` (with ``session_id=None``): build the prompt on that
         session's token stream without making this request the session's turn.
         ``assistant_prefix``: text the assistant turn starts with (written into the
-        prompt; the output stream holds only what follows it)."""
+        prompt; the output stream holds only what follows it).  ``priority``: > 0
+        prefills ahead of waiting prompts of lower priority."""
         mt = int(max_tokens or self.default_max_tokens)
         params = self._params(temperature, mt, top_p, top_k, stop, seed, guided, ignore_eos,
-                              min_tokens, guided_lazy)
+                              min_tokens, guided_lazy, priority)
         if prompt_ids is None:
             if session_id is None and prefix_session is not None:
                 prompt_ids = self.build_prompt(messages, mt, prefix_session, tools, remember=False)

@@ -25,6 +25,9 @@ class SamplingParams:
     # the model chose to open a tool call with '{"'); otherwise the reply is free text
     guided_lazy: bool = False
     skip_special_tokens: bool = True
+    # scheduling priority: waiting prompts of a higher priority are prefilled first
+    # (an agent's post-tool re-prompt: its user has already waited through the call)
+    priority: int = 0
 
     def __post_init__(self):
         if self.temperature is None:

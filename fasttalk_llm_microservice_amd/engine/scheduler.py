@@ -122,7 +122,22 @@ class Scheduler:
     # ------------------------------------------------------------------ queue ops
     def add(self, seq: Sequence):
         self.by_id[seq.request_id] = seq
-        (self.background if seq.background else self.waiting).append(seq)
+        if seq.background:
+            self.background.append(seq)
+            return
+        pr = getattr(seq.params, "priority", 0)
+        if pr > 0 and self.waiting:
+            # ahead of every lower-priority prompt that has not started its prefill (a
+            # chunked prefill in progress keeps its place)
+            i = 0
+            for i, q in enumerate(self.waiting):
+                if q.num_computed == 0 and getattr(q.params, "priority", 0) < pr:
+                    break
+            else:
+                i = len(self.waiting)
+            self.waiting.insert(i, seq)
+            return
+        self.waiting.append(seq)
 
     def has_work(self) -> bool:
         return bool(self.waiting) or bool(self.running) or bool(self.swapped) or bool(self.background)

@@ -578,3 +578,24 @@ def test_jump_forward_head_stays_within_max_model_len(tiny_engine):
         outs += [o for o in eng.step() if o.request_id == "jf-edge"]
     assert outs and outs[-1].finished and outs[-1].finish_reason == "length"
     assert eng.bm.num_free() == eng.bm.num_blocks or eng.bm.num_cached() > 0
+
+
+def test_priority_prompts_prefill_first():
+    """An agent's post-tool re-prompt (priority 1) goes ahead of waiting prompts of
+    lower priority that have not started; a chunked prefill in progress keeps its
+    place; equal priorities stay FIFO."""
+    from fasttalk_llm_microservice_amd.engine.scheduler import Scheduler
+    from fasttalk_llm_microservice_amd.engine.sequence import Sequence
+    from fasttalk_llm_microservice_amd.runtime import rt
+
+    bm = rt().BlockManager(64, 4, True)
+    sch = Scheduler(bm, 4, 8, 256, 512)
+    mk = lambda rid, pr=0: Sequence(rid, [1, 2, 3], SamplingParams(max_tokens=4, priority=pr))  # noqa
+    a, b = mk("a"), mk("b")
+    sch.add(a)
+    sch.add(b)
+    a.num_computed = 2          # a's chunked prefill is under way
+    sch.add(mk("t1", 1))
+    sch.add(mk("t2", 1))
+    sch.add(mk("c"))
+    assert [q.request_id for q in sch.waiting] == ["a", "t1", "t2", "b", "c"]
