@@ -276,7 +276,9 @@ class LLMEngine:
         queued step, ids gathered from its sampled rows on the device), prefill
         rows as the scheduler picks them.  At most one mixed step is in flight
         (a prompt's next chunk needs the previous chunk's post-step state), and
-        only for grammar-free, single-process (no TP broadcast) engines."""
+        only for single-process (no TP broadcast) engines; guided decode rows defer
+        the step's sampler until their masks are known, guided prompts wait for
+        the drained path."""
         sched = self.scheduler
 
         def skip(why: str):
@@ -294,7 +296,9 @@ class LLMEngine:
         if not running:   # nothing to overlap: the drained path schedules it
             return skip("no_running")
         pos = {id(q): i for i, q in enumerate(last)}
-        if any(id(q) not in pos or q.grammar is not None for q in running):
+        guided_rows = any(q.grammar is not None for q in running)
+        if any(id(q) not in pos or q.drop_next for q in running) or \
+                (guided_rows and not self._guided_pipeline()):
             return skip("rows")
         if not self._grow_for_next(running):
             return skip("blocks")
@@ -306,7 +310,9 @@ class LLMEngine:
         if not pseqs:
             return skip("no_prefill")
         mb = ScheduledBatch(running, pseqs, ptok, psamp)
-        h = self.runner.mixed_launch(mb, [pos[id(q)] for q in running])
+        # guided decode rows: the sampler waits for their masks (this step's tokens)
+        h = self.runner.mixed_launch(mb, [pos[id(q)] for q in running],
+                                     **({"defer_sample": True} if guided_rows else {}))
         for q in mb.sampled_seqs():
             q.inflight += 1
         self.stats["mixed_ahead"] += 1
