@@ -681,6 +681,7 @@ class ModelRunner:
             self._tap(self._graph_logits[nb][:n].float().clone())
         return DecodeHandle(st, n, nb)
 
+    @torch.inference_mode()
     def sample_launch(self, h, masks: Optional[np.ndarray]):
         """Queues the sampler of a step whose forward pass ``decode_launch(...,
         defer_sample=True)`` queued: its allow-masks go up, the sampler graph reads

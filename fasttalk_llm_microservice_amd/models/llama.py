@@ -145,12 +145,19 @@ MAX_SPLITS = 4
 # 512 rows: profiles/pg_probe_300_512_r02.log).  Up to 2047 rows the M = 1024
 # measurements rule: split-K keeps o / down at 512 workgroups (whole tiles there:
 # 80 workgroups on 256 CUs, 2-3x slower).
+# 129-192 and 257-384 rows: the 192-row tiles (cfg 5 = 192x256, 6 = 192x128) pad the
+# step to 192 / 384 MFMA rows instead of 256 / 512 -- profiles/pg_probe_192_r04.log:
+# gate_up 54.8 vs 67.8 us at 145 rows, 81.4 vs 102.4 at 300, 88.2 vs 105.3 at 384;
+# down 36.2 vs 43.7 / 54.3 vs 63.8 / 57.5 vs 66.3; LM head 233 vs 263 / 376 vs 463.
 PG_PLAN = {
-    "qkv": ((128, 1, 8), (256, 2, 4), (512, 2, 2), (2047, 0, 2), (1 << 30, 2, 1)),
-    "o": ((128, 2, 8), (256, 1, 8), (512, 2, 4), (2047, 1, 2), (1 << 30, 0, 1)),
-    "gu": ((128, 1, 2), (256, 2, 1), (1 << 30, 0, 1)),
-    "down": ((128, 1, 16), (256, 1, 8), (512, 0, 8), (2047, 0, 4), (1 << 30, 3, 1)),
-    "lm": ((128, 1, 1), (256, 3, 1), (1 << 30, 0, 1)),
+    "qkv": ((128, 1, 8), (192, 6, 4), (256, 2, 4), (384, 6, 2), (512, 2, 2), (2047, 0, 2),
+            (1 << 30, 2, 1)),
+    "o": ((128, 2, 8), (192, 6, 8), (256, 1, 8), (384, 6, 4), (512, 2, 4), (2047, 1, 2),
+          (1 << 30, 0, 1)),
+    "gu": ((128, 1, 2), (192, 6, 1), (256, 2, 1), (384, 5, 1), (1 << 30, 0, 1)),
+    "down": ((128, 1, 16), (192, 6, 8), (256, 1, 8), (384, 5, 8), (512, 0, 8), (2047, 0, 4),
+             (1 << 30, 3, 1)),
+    "lm": ((128, 1, 1), (192, 5, 1), (256, 3, 1), (384, 5, 1), (1 << 30, 0, 1)),
 }
 PG_MAX_SLAB_ROWS = 2048
 # At prefill-burst sizes hipBLASLt's tiles beat packed_gemm (1.35-1.66 vs 1.1-1.2
@@ -172,20 +179,12 @@ PG_RM_ROWS = int(os.environ.get("FT_PG_RM_ROWS", "257"))
 RM_PROJS = ("qkv", "o", "gu")
 
 
-# 192-row twins of the 256-row tiles (cfg 0 -> 5, 2 -> 6): used when they pad the
-# step's rows to fewer MFMA rows (129-192 rows: 192 instead of 256; 257-384: 384
-# instead of 512).  FT_PG_192=0 keeps the 256-row tiles.
-PG_192 = {0: 5, 2: 6} if os.environ.get("FT_PG_192", "1") == "1" else {}
-
-
 def pg_cfg(proj: str, rows: int, k: int) -> Tuple[int, int]:
     for lim, cfg, sp in PG_PLAN[proj]:
         if rows <= lim:
             break
     while sp > 1 and k % (64 * sp):
         sp //= 2
-    if cfg in PG_192 and -(-rows // 192) * 192 < -(-rows // 256) * 256:
-        cfg = PG_192[cfg]
     return cfg, sp
 
 

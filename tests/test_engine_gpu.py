@@ -314,19 +314,30 @@ def test_guided_decoding_pipelines_with_a_deferred_sampler(monkeypatch):
         "required": ["query", "max_results"]}}}]
     spec = GuidedSpec(tool_call_ast(tools))
     monkeypatch.setenv("ENGINE_GUIDED_PIPELINE", "1")
+    monkeypatch.setenv("ENGINE_MIXED_AHEAD", "1")
     eng = _engine(max_num_seqs=16)
     prompts = _prompts(8, [12, 20, 28, 9, 33, 17, 40, 5], seed=7)
     res = {}
-    for i, p in enumerate(prompts):
+
+    def add(i):
         guided = i % 3 == 0
         sp = SamplingParams(temperature=0.8, seed=30 + i, max_tokens=80 if guided else 48,
                             guided=spec if guided else None, ignore_eos=not guided)
-        eng.add_request(f"p{i}", p, sp, on_output=lambda o, i=i: res.setdefault(i, []).extend(o.token_ids))
-    while eng.has_work():
+        eng.add_request(f"p{i}", prompts[i], sp,
+                        on_output=lambda o, i=i: res.setdefault(i, []).extend(o.token_ids))
+
+    for i in range(4):
+        add(i)
+    step = 0
+    while eng.has_work() or step < 12:
+        if step in (3, 5, 7, 9):   # prompts arriving while guided rows decode: mixed steps
+            add(4 + (step - 3) // 2)  # queued behind the running step, sampler deferred
         eng.step()
+        step += 1
     st = eng.runner.stats
     assert st["eager_decode"] == 0 and st.get("deferred_samples", 0) > 0, st
     assert eng.stats["guided_pipelined_steps"] > 0, dict(eng.stats)
+    assert eng.stats["mixed_ahead"] > 0, dict(eng.stats)
     for i in range(8):
         if i % 3 == 0:
             call = json.loads(eng.tokenizer.decode(res[i]))
