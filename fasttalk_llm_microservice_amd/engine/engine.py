@@ -103,6 +103,7 @@ class LLMEngine:
         # of step ends jitters with the GIL, late top-ups cost the decode step 7.6 ->
         # 8.0 ms, p50 TTFT did not improve -- profiles/ab_mixed_ahead_r03.log; removed.)
         self.mixed_ahead = os.environ.get("ENGINE_MIXED_AHEAD", "1") != "0"
+        self.guided_mixed_ahead = os.environ.get("ENGINE_GUIDED_MIXED_AHEAD", "1") != "0"
         self.poll_hook = None
         # ENGINE_PIPELINE_SHRINK=1: a stop shrinks the queued steps instead of draining
         # them.  Off by default: in the voice-agent loop the session's next prompt
@@ -298,7 +299,7 @@ class LLMEngine:
         pos = {id(q): i for i, q in enumerate(last)}
         guided_rows = any(q.grammar is not None for q in running)
         if any(id(q) not in pos or q.drop_next for q in running) or \
-                (guided_rows and not self._guided_pipeline()):
+                (guided_rows and not (self._guided_pipeline() and self.guided_mixed_ahead)):
             return skip("rows")
         if not self._grow_for_next(running):
             return skip("blocks")
