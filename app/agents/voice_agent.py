@@ -38,7 +38,6 @@ from app.agents.tools import Tool, make_search_tool, make_session_tool, make_tim
 
 logger = logging.getLogger(__name__)
 
-_REPROMPT_PRIORITY = os.environ.get("AGENT_REPROMPT_PRIORITY", "1") != "0"
 _TOOL_HINTS = re.compile(r"\b(search|look up|lookup|news|weather|latest|current|today|time|date|"
                          r"session|google|find)\b", re.I)
 # hint words that name one tool: a message whose hints all point at one tool forces
@@ -257,9 +256,7 @@ class VoiceAgent:
                     request_id=sid, session_id=sid if (rnd == 0 and (guided is None or lazy)) else None,
                     prefix_session=sid, assistant_prefix=head, tools=schemas or None, guided=guided,
                     seed=seed, guided_lazy=lazy,
-                    ignore_eos=ignore_eos and (guided is None or lazy), min_tokens=min_tokens,
-                    # a re-prompt after a tool ran: its user has waited through the call
-                    **({"priority": 1} if rnd > 0 and _REPROMPT_PRIORITY else {})):
+                    ignore_eos=ignore_eos and (guided is None or lazy), min_tokens=min_tokens):
                 if out.finished:
                     finish = out.finish_reason
                 n = len(out.token_ids)

@@ -38,9 +38,10 @@ def main():
     ap.add_argument("--uniform", action="store_true")
     ap.add_argument("--fused", action="store_true")
     ap.add_argument("--shapes", default="")
+    ap.add_argument("--bs", type=int, default=16, help="KV block size (tokens)")
     a = ap.parse_args()
     shapes = [tuple(int(v) for v in x.split(":")) for x in a.shapes.split(",")] if a.shapes else SHAPES
-    nq, nkv, d, bs = a.nq, a.nkv, a.d, 16
+    nq, nkv, d, bs = a.nq, a.nkv, a.d, a.bs
     dev = "cuda"
     for B, ctx in shapes:
         nblk = math.ceil(ctx / bs)
@@ -62,7 +63,7 @@ def main():
         cnt = ops.decode_counters(B, nkv, dev) if a.fused else None
         us = timeit(lambda: ops.decode_attention(out, q, kc, vc, bt, sl, tmp_o, tmp_ml, nq, nkv, d,
                                                  d ** -0.5, counters=cnt), iters=100, warmup=10)
-        print(json.dumps({"B": B, "ctx": ctx, "uniform": a.uniform,
+        print(json.dumps({"B": B, "ctx": ctx, "uniform": a.uniform, "bs": bs,
                           "ring": int(os.environ.get("FT_DECODE_RING", "2")),
                           "min_tiles": int(os.environ.get("FT_DECODE_MIN_TILES", "8")),
                           "wpc": int(os.environ.get("FT_DECODE_WPC", "1")),

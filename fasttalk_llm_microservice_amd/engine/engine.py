@@ -103,7 +103,6 @@ class LLMEngine:
         # of step ends jitters with the GIL, late top-ups cost the decode step 7.6 ->
         # 8.0 ms, p50 TTFT did not improve -- profiles/ab_mixed_ahead_r03.log; removed.)
         self.mixed_ahead = os.environ.get("ENGINE_MIXED_AHEAD", "1") != "0"
-        self.guided_mixed_ahead = os.environ.get("ENGINE_GUIDED_MIXED_AHEAD", "1") != "0"
         self.poll_hook = None
         # ENGINE_PIPELINE_SHRINK=1: a stop shrinks the queued steps instead of draining
         # them.  Off by default: in the voice-agent loop the session's next prompt
@@ -277,9 +276,7 @@ class LLMEngine:
         queued step, ids gathered from its sampled rows on the device), prefill
         rows as the scheduler picks them.  At most one mixed step is in flight
         (a prompt's next chunk needs the previous chunk's post-step state), and
-        only for single-process (no TP broadcast) engines; guided decode rows defer
-        the step's sampler until their masks are known, guided prompts wait for
-        the drained path."""
+        only for grammar-free, single-process (no TP broadcast) engines."""
         sched = self.scheduler
 
         def skip(why: str):
@@ -297,9 +294,11 @@ class LLMEngine:
         if not running:   # nothing to overlap: the drained path schedules it
             return skip("no_running")
         pos = {id(q): i for i, q in enumerate(last)}
-        guided_rows = any(q.grammar is not None for q in running)
-        if any(id(q) not in pos or q.drop_next for q in running) or \
-                (guided_rows and not (self._guided_pipeline() and self.guided_mixed_ahead)):
+        # (guided decode rows: a mixed step queued behind them with its sampler deferred
+        # until their masks were known was built and measured in round 4 -- more, smaller
+        # mixed steps and a worse tool-turn tail, p99 462 / 541 vs 408 / 398 ms on one
+        # box, profiles/ab_guided_mixed_ahead_r04.log -- and removed)
+        if any(id(q) not in pos or q.grammar is not None or q.drop_next for q in running):
             return skip("rows")
         if not self._grow_for_next(running):
             return skip("blocks")
@@ -311,9 +310,7 @@ class LLMEngine:
         if not pseqs:
             return skip("no_prefill")
         mb = ScheduledBatch(running, pseqs, ptok, psamp)
-        # guided decode rows: the sampler waits for their masks (this step's tokens)
-        h = self.runner.mixed_launch(mb, [pos[id(q)] for q in running],
-                                     **({"defer_sample": True} if guided_rows else {}))
+        h = self.runner.mixed_launch(mb, [pos[id(q)] for q in running])
         for q in mb.sampled_seqs():
             q.inflight += 1
         self.stats["mixed_ahead"] += 1

@@ -130,16 +130,13 @@ class _Staging:
 
 class MixedHandle:
     """A queued mixed step's sampled ids (pinned host copy) and completion event;
-    two alternate (at most one mixed step is queued at a time).  ``pending``: its
-    sampler waits for the allow-masks (``deferred`` = logits + sampling inputs)."""
-    __slots__ = ("host", "event", "n", "pending", "deferred")
+    two alternate (at most one mixed step is queued at a time)."""
+    __slots__ = ("host", "event", "n")
 
     def __init__(self, rows: int, pin: bool, gpu: bool):
         self.host = torch.zeros(rows, dtype=torch.int32, pin_memory=pin)
         self.event = torch.cuda.Event() if gpu else None
         self.n = 0
-        self.pending = False
-        self.deferred = None
 
 
 class DecodeHandle:
@@ -682,18 +679,12 @@ class ModelRunner:
         return DecodeHandle(st, n, nb)
 
     @torch.inference_mode()
-    def sample_launch(self, h, masks: Optional[np.ndarray]):
+    def sample_launch(self, h: DecodeHandle, masks: Optional[np.ndarray]):
         """Queues the sampler of a step whose forward pass ``decode_launch(...,
         defer_sample=True)`` queued: its allow-masks go up, the sampler graph reads
         the forward graph's logits, the ids land in ``d_out`` (the next step's
-        inputs) and in the staging set's pinned copy.  For a deferred mixed step the
-        sampler runs eagerly on its logits with the masks uploaded alongside."""
+        inputs) and in the staging set's pinned copy."""
         assert h.pending
-        if isinstance(h, MixedHandle):
-            logits, samp = h.deferred
-            dmask = self._upload([masks])[0] if masks is not None else None
-            self._mixed_sample(h, logits, samp, dmask)
-            return
         self._set_masks(masks, h.n)
         self.graphs_split[h.nb][1].replay()
         st = h.stage
@@ -732,8 +723,7 @@ class ModelRunner:
         return ev is None or ev.query()
 
     @torch.inference_mode()
-    def mixed_launch(self, batch: ScheduledBatch, rowmap: List[int],
-                     defer_sample: bool = False) -> "MixedHandle":
+    def mixed_launch(self, batch: ScheduledBatch, rowmap: List[int]) -> "MixedHandle":
         """Queues a mixed (decode + prefill) step behind the queued decode step(s)
         without waiting (engine ``_speculate_mixed``): decode row i's input id is
         row ``rowmap[i]`` of the last queued step's sampled ids (``d_out``),
@@ -778,27 +768,17 @@ class ModelRunner:
         if self.logits_tap is not None:
             self._tap(logits.float().clone())
         n = logits.shape[0]
-        samp = dev[len(names):len(names) + 5]
+        temp, topp, topk, seeds, steps = dev[len(names):len(names) + 5]
+        ops.sample(logits, temp, topp, topk, seeds, steps, out=self.d_out[:n])
         mh = self._mx_handles[self._mx_next]
         self._mx_next ^= 1
         if mh.host.shape[0] < n:
             mh.host = torch.zeros(2 * n, dtype=torch.int32, pin_memory=self.is_gpu)
         mh.n = n
-        if defer_sample:
-            assert self.can_defer_sample()
-            mh.pending, mh.deferred = True, (logits, samp)
-            return mh
-        self._mixed_sample(mh, logits, samp, None)
-        return mh
-
-    def _mixed_sample(self, mh: "MixedHandle", logits, samp, dmask):
-        n = mh.n
-        temp, topp, topk, seeds, steps = samp
-        ops.sample(logits, temp, topp, topk, seeds, steps, out=self.d_out[:n], mask=dmask)
         mh.host[:n].copy_(self.d_out[:n], non_blocking=self.is_gpu)
         if mh.event is not None:
             mh.event.record()
-        mh.pending, mh.deferred = False, None
+        return mh
 
     def mixed_collect(self, h: "MixedHandle") -> List[int]:
         if h.event is not None:

@@ -385,31 +385,6 @@ class _GuidedRunner(ModelRunner):
         assert not h.pending, "collected a step whose sampler never ran"
         return list(h.out)
 
-    def mixed_launch(self, batch, rowmap, defer_sample=False):
-        self.mixed.append((len(batch.decode_seqs), list(batch.prefill_tokens), list(rowmap)))
-        ids, pos = [], []
-        for s, r in zip(batch.decode_seqs, rowmap):
-            assert s.inflight >= 1 and self.d_out is not None
-            ids.append(self.d_out[r])
-            pos.append(s.n_tokens - 1 + s.inflight)
-        for s, n, smp in zip(batch.prefill_seqs, batch.prefill_tokens, batch.prefill_sample):
-            if smp:
-                assert s.num_computed + n == s.n_tokens
-                ids.append(int(s.tokens[-1]))
-                pos.append(s.n_tokens - 1)
-        h = _GHandle(ids, pos, defer_sample)
-        if defer_sample:
-            self.d_out = None
-            self.stats["deferred_mixed"] = self.stats.get("deferred_mixed", 0) + 1
-        else:
-            self._sample(h, None)
-        return h
-
-    def mixed_collect(self, h):
-        assert not h.pending, "collected a mixed step whose sampler never ran"
-        return list(h.out)
-
-
 _GuidedRunner.__name__ = "ModelRunner"
 
 
@@ -459,50 +434,3 @@ def test_guided_batches_pipeline_with_deferred_sampler():
     assert eng.stats["guided_pipelined_steps"] > 0 and runner.stats.get("deferred", 0) > 0
     assert eng.stats["jump_forward_tokens"] > 0 and eng.stats["pipelined_jump_drops"] > 0
 
-
-def test_mixed_ahead_with_guided_rows_defers_its_sampler():
-    """Prompts arriving while guided sequences decode pipelined go into a mixed step
-    queued behind the running step; its sampler waits for the guided rows' masks.
-    Tokens equal the synchronous engine's."""
-    import os
-
-    from fasttalk_llm_microservice_amd.engine.guided import GuidedSpec, tool_call_ast
-
-    tools = [{"type": "function", "function": {"name": "duckduckgo_search", "parameters": {
-        "type": "object", "properties": {"query": {"type": "string", "maxLength": 40}},
-        "required": ["query"]}}}]
-    spec = GuidedSpec(tool_call_ast(tools))
-
-    def run(async_output):
-        os.environ["ENGINE_MIXED_AHEAD"] = "1"
-        cfg = EngineConfig(model="tiny", device="cpu", block_size=4, async_output=async_output,
-                           pipeline_depth=1, max_num_seqs=32)
-        runner = _GuidedRunner()
-        eng = LLMEngine(cfg, runner=runner)
-        res = {}
-
-        def add(i):
-            guided = i % 3 == 0
-            sp = SamplingParams(temperature=0.0, max_tokens=80 if guided else 12 + i,
-                                stop_token_ids=None if guided else [EOS],
-                                guided=spec if guided else None)
-            eng.add_request(f"r{i}", [40 + 5 * i + j for j in range(3 + i % 5)], sp,
-                            on_output=lambda o, i=i: res.setdefault(i, []).extend(o.token_ids))
-
-        for i in range(4):
-            add(i)
-        k, step = 4, 0
-        while eng.has_work() or k < 14:
-            if k < 14 and step % 2 == 1:
-                add(k)
-                k += 1
-            eng.step()
-            step += 1
-        os.environ.pop("ENGINE_MIXED_AHEAD", None)
-        assert eng.bm.num_free() == eng.bm.num_blocks
-        return [res.get(i, []) for i in range(14)], eng, runner
-
-    ref, _, _ = run(False)
-    got, eng, runner = run(True)
-    assert got == ref
-    assert runner.stats.get("deferred_mixed", 0) > 0 and eng.stats["mixed_ahead"] > 0
