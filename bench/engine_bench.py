@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--eager", action="store_true")
     ap.add_argument("--temperature", type=float, default=0.7)
     ap.add_argument("--kv-blocks", type=int, default=None)
+    ap.add_argument("--batch-invariant", action="store_true")
     a = ap.parse_args()
 
     import numpy as np
@@ -33,7 +34,8 @@ def main():
     from fasttalk_llm_microservice_amd.engine.engine import LLMEngine
     from fasttalk_llm_microservice_amd.engine.sampling_params import SamplingParams
 
-    cfg = EngineConfig(model=a.model, enforce_eager=a.eager, num_kv_blocks=a.kv_blocks)
+    cfg = EngineConfig(model=a.model, enforce_eager=a.eager, num_kv_blocks=a.kv_blocks,
+                       batch_invariant=a.batch_invariant)
     t0 = time.time()
     eng = LLMEngine(cfg)
     print(f"engine up in {time.time() - t0:.1f}s", flush=True)

@@ -23,14 +23,15 @@ int ft_paged_decode_attention(void* out, int out_stride, float* tmp_out, float* 
                               const void* q, int q_stride, const void* k_cache,
                               const void* v_cache, const int* block_tables, int bt_stride,
                               const int* seq_lens, int batch, int nq, int nkv, int head_dim,
-                              int block_size, float scale, int* counters, hipStream_t stream);
+                              int block_size, float scale, int* counters, int piece,
+                              int slot_cap, hipStream_t stream);
 int ft_prefill_tile_tokens(int nq, int nkv);
 int ft_prefill_attention(void* out, int out_stride, const void* q, int q_stride,
                          const void* k_cache, const void* v_cache, const int* block_tables,
                          int bt_stride, const int* seq_lens, const int* q_start_loc,
                          const int* tile_info, int num_tiles, int nq, int nkv, int head_dim,
                          int block_size, float scale, float* part_o, float* part_ml,
-                         const int* combine, int num_combine, hipStream_t stream);
+                         const int* combine, int num_combine, int invariant, hipStream_t stream);
 int ft_sample(int* out_tokens, const void* logits, int logits_is_bf16, long logit_stride,
               int batch, int vocab, const float* temperature, const float* top_p,
               const int* top_k, const long long* seeds, const int* steps,
@@ -199,7 +200,7 @@ void rope_kv_write(at::Tensor qkv, at::Tensor positions, at::Tensor cos_sin,
 void paged_decode_attention(at::Tensor out, at::Tensor q, at::Tensor k_cache, at::Tensor v_cache,
                             at::Tensor block_tables, at::Tensor seq_lens, at::Tensor tmp_out,
                             at::Tensor tmp_ml, int64_t nq, int64_t nkv, int64_t head_dim,
-                            double scale, c10::optional<at::Tensor> counters) {
+                            double scale, c10::optional<at::Tensor> counters, int64_t piece) {
   check_bf16(out, "out");
   check_bf16(q, "q");
   check_rows(out, "out");
@@ -225,12 +226,20 @@ void paged_decode_attention(at::Tensor out, at::Tensor q, at::Tensor k_cache, at
     TORCH_CHECK(counters->numel() >= (int64_t)batch * nkv, "decode counters too small");
     cnt = counters->data_ptr<int>();
   }
+  const int64_t slot_cap = std::min(tmp_out.numel() / ((nq / nkv) * head_dim), tmp_ml.numel() / ((nq / nkv) * 2));
+  if (piece > 0) {  // batch-invariant pieces: one slot per piece of the longest possible segment
+    TORCH_CHECK(cnt != nullptr, "piece mode merges in-launch: counters required");
+    const int64_t max_tiles = (block_tables.size(1) * k_cache.size(2) + 15) / 16;
+    TORCH_CHECK(slot_cap >= (int64_t)batch * nkv * ((max_tiles + piece - 1) / piece),
+                "decode workspace too small for piece mode (ops.decode_workspace pieces=)");
+  }
   check_rc(ft_paged_decode_attention(out.data_ptr(), (int)out.stride(0), tmp_out.data_ptr<float>(),
                                      tmp_ml.data_ptr<float>(), q.data_ptr(), (int)q.stride(0),
                                      k_cache.data_ptr(), v_cache.data_ptr(),
                                      block_tables.data_ptr<int>(), (int)block_tables.stride(0),
                                      seq_lens.data_ptr<int>(), batch, (int)nq, (int)nkv,
                                      (int)head_dim, (int)k_cache.size(2), (float)scale, cnt,
+                                     (int)piece, (int)std::min<int64_t>(slot_cap, INT32_MAX),
                                      cur_stream()),
            "paged_decode_attention");
 }
@@ -240,7 +249,7 @@ void prefill_attention(at::Tensor out, at::Tensor q, at::Tensor k_cache, at::Ten
                        at::Tensor tile_info, int64_t num_tiles, int64_t nq, int64_t nkv,
                        int64_t head_dim, double scale, c10::optional<at::Tensor> part_o,
                        c10::optional<at::Tensor> part_ml, c10::optional<at::Tensor> combine,
-                       int64_t num_combine, int64_t num_partials) {
+                       int64_t num_combine, int64_t num_partials, bool invariant) {
   check_bf16(out, "out");
   check_bf16(q, "q");
   check_rows(out, "out");
@@ -279,7 +288,7 @@ void prefill_attention(at::Tensor out, at::Tensor q, at::Tensor k_cache, at::Ten
                                 seq_lens.data_ptr<int>(), q_start_loc.data_ptr<int>(),
                                 tile_info.data_ptr<int>(), (int)num_tiles, (int)nq, (int)nkv,
                                 (int)head_dim, (int)k_cache.size(2), (float)scale, po, pml, cb,
-                                (int)num_combine, cur_stream()),
+                                (int)num_combine, (int)invariant, cur_stream()),
            "prefill_attention");
 }
 
@@ -798,10 +807,18 @@ PYBIND11_MODULE(_C, m) {
   m.def("fused_add_rmsnorm", &fused_add_rmsnorm);
   m.def("silu_mul", &silu_mul);
   m.def("rope_kv_write", &rope_kv_write);
-  m.def("paged_decode_attention", &paged_decode_attention);
+  m.def("paged_decode_attention", &paged_decode_attention, py::arg("out"), py::arg("q"),
+        py::arg("k_cache"), py::arg("v_cache"), py::arg("block_tables"), py::arg("seq_lens"),
+        py::arg("tmp_out"), py::arg("tmp_ml"), py::arg("nq"), py::arg("nkv"), py::arg("head_dim"),
+        py::arg("scale"), py::arg("counters") = py::none(), py::arg("piece") = 0);
   m.def("decode_waves", []() { return ft_decode_waves(); });
   m.def("decode_max_batch", []() { return ft_decode_max_batch(); });
-  m.def("prefill_attention", &prefill_attention);
+  m.def("prefill_attention", &prefill_attention, py::arg("out"), py::arg("q"), py::arg("k_cache"),
+        py::arg("v_cache"), py::arg("block_tables"), py::arg("seq_lens"), py::arg("q_start_loc"),
+        py::arg("tile_info"), py::arg("num_tiles"), py::arg("nq"), py::arg("nkv"),
+        py::arg("head_dim"), py::arg("scale"), py::arg("part_o") = py::none(),
+        py::arg("part_ml") = py::none(), py::arg("combine") = py::none(),
+        py::arg("num_combine") = 0, py::arg("num_partials") = 0, py::arg("invariant") = false);
   m.def("prefill_tile_tokens", [](int64_t nq, int64_t nkv) { return ft_prefill_tile_tokens((int)nq, (int)nkv); });
   m.def("sample", &sample, py::arg("out_tokens"), py::arg("logits"), py::arg("temperature"),
         py::arg("top_p"), py::arg("top_k"), py::arg("seeds"), py::arg("steps"),

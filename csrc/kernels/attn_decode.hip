@@ -61,13 +61,16 @@ constexpr int kDecMinTiles = 8;
 // exact in fp32 and in bf16's range
 constexpr float kDecRescaleThr = 8.f;
 
-// s_pre[b] = sum_{b' < b} ceil(L_b' / 16) (tiles per kv head), b = 0..batch; wave-wide scan
-__device__ __forceinline__ void dec_prefix(int* s_pre, const int* __restrict__ seq_lens, int batch) {
+// s_pre[b] = sum_{b' < b} ceil(ceil(L_b' / 16) / per) (tiles, or pieces of `per` tiles,
+// per kv head), b = 0..batch; wave-wide scan
+__device__ __forceinline__ void dec_prefix(int* s_pre, const int* __restrict__ seq_lens, int batch,
+                                           int per) {
   const int lane = lane_id();
   int run = 0;
   for (int b0 = 0; b0 < batch; b0 += 64) {
     const int b = b0 + lane;
     int x = b < batch ? (max(seq_lens[b], 0) + 15) >> 4 : 0;
+    if (per > 1) x = (x + per - 1) / per;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
       const int y = __shfl_up(x, o, 64);
@@ -129,17 +132,19 @@ __device__ __forceinline__ void mt_load(MTile<D>& t, const uint16_t* __restrict_
 // End of a wave's piece of segment (b, h): the whole segment -> bf16 output;
 // otherwise an fp32 (acc, m, l) partial at slot segment + wave, and with FC the
 // in-launch combine by the last arriving wave (see the header comment).
+// whole: this wave covered the segment alone; otherwise its partial goes to slot
+// `slot` and the segment's np partials sit at slots first .. first + np - 1.
 template <int D, int G, int ND, bool FC>
 __device__ __forceinline__ void dec_finish(floatx4_t (&o)[ND], float l_run, float m_run, int b, int h,
-                                           int t0, int cnt, int nb, int w, int nw, int total, int nkv,
-                                           const int* s_pre, uint16_t* __restrict__ out, int out_stride,
+                                           bool whole, int slot_i, int first, int np, int nkv,
+                                           uint16_t* __restrict__ out, int out_stride,
                                            float* __restrict__ tmp_out, float* __restrict__ tmp_ml,
                                            int* __restrict__ counters, int lane, int g, int n) {
   // head n's sum over the 4 token groups
   const float l_tot = kgroups_sum(l_run);
   // C-layout rows of O: lane (g, n) holds heads 4g+i, dim n (+16 nd)
   const int seg = b * nkv + h;
-  if (t0 == 0 && cnt == nb) {   // the whole segment: final bf16 output
+  if (whole) {   // the whole segment: final bf16 output
 #pragma unroll
     for (int i4 = 0; i4 < 4; ++i4) {
       const int r = 4 * g + i4;
@@ -152,7 +157,7 @@ __device__ __forceinline__ void dec_finish(floatx4_t (&o)[ND], float l_run, floa
       }
     }
   } else {
-    const size_t slot = (size_t)(seg + w);
+    const size_t slot = (size_t)slot_i;
 #pragma unroll
     for (int i4 = 0; i4 < 4; ++i4) {
       const int r = 4 * g + i4;
@@ -193,14 +198,9 @@ __device__ __forceinline__ void dec_finish(floatx4_t (&o)[ND], float l_run, floa
       if (lane == 0)
         prev = __hip_atomic_fetch_add(counters + seg, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       prev = __shfl(prev, 0, 64);
-      // waves sharing the segment: the first and last whose tile range meets it
-      const int S = nkv * s_pre[b] + h * nb, E = S + nb;
-      const int wf = (int)(((long long)(S + 1) * nw - 1) / total);
-      const int wl = (int)(((long long)E * nw - 1) / total);
-      const int np = wl - wf + 1;
       if (prev == np - 1) {   // last arriver: merge the np partials of this segment
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keep the loads below the ticket
-        const size_t base = (size_t)(seg + wf);
+        const size_t base = (size_t)first;
         uint16_t* op = out + (size_t)b * out_stride + h * G * D;
         // lane (r, c): head r, dims c + 16 nd of the permuted partials; the
         // partial slots are read in batches of 8 with every load of a batch in
@@ -251,21 +251,24 @@ __device__ __forceinline__ void dec_finish(floatx4_t (&o)[ND], float l_run, floa
   }
 }
 
-template <int D, int G, int R, bool FC, int WPC>
+template <int D, int G, int R, bool FC, int WPC, bool PIECE = false>
 __global__ __launch_bounds__(256, WPC) void paged_decode_kernel(
     uint16_t* __restrict__ out, int out_stride, float* __restrict__ tmp_out,
     float* __restrict__ tmp_ml, const uint16_t* __restrict__ q, int q_stride,
     uint16_t* __restrict__ k_cache, uint16_t* __restrict__ v_cache,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ seq_lens,
     int batch, int nkv, int bs_shift, float scale_log2, int* __restrict__ counters,
-    int min_tiles) {
+    int min_tiles, int piece, int slot_cap) {
   static_assert(G >= 1 && G <= 16, "GQA group must fit the 16 MFMA columns");
   constexpr int KC = D / 32, ND = D / 16;
-  __shared__ int s_pre[kDecMaxBatch + 1];
-  if (wave_id() == 0) dec_prefix(s_pre, seq_lens, batch);
+  // s_pre: tile prefix; s_pre + kDecMaxBatch + 1: piece prefix (piece mode)
+  __shared__ int s_pre[2 * (kDecMaxBatch + 1)];
+  int* s_pp = s_pre + kDecMaxBatch + 1;
+  if (wave_id() == 0) dec_prefix(s_pre, seq_lens, batch, 1);
+  if (PIECE && wave_id() == 1) dec_prefix(s_pp, seq_lens, batch, piece);
   __syncthreads();
   const int total = nkv * s_pre[batch];
-  const int nw = dec_num_waves(total, gridDim.x * 4, min_tiles);
+  const int nw = PIECE ? gridDim.x * 4 : dec_num_waves(total, gridDim.x * 4, min_tiles);
   const int w = wave_id() * gridDim.x + blockIdx.x;  // spreads low wave ids over CUs
   if (FC && blockIdx.x == 0) {
     // fused-combine mode has no combine kernel to define empty sequences' outputs
@@ -279,8 +282,6 @@ __global__ __launch_bounds__(256, WPC) void paged_decode_kernel(
     }
   }
   if (total == 0 || w >= nw) return;
-  int f = (int)(((long long)w * total) / nw);
-  const int f1 = (int)(((long long)(w + 1) * total) / nw);
 
   const int lane = lane_id();
   const float thr_raw = kDecRescaleThr / scale_log2;   // the threshold in raw score units
@@ -294,19 +295,8 @@ __global__ __launch_bounds__(256, WPC) void paged_decode_kernel(
   const int voff_b = 2 * (n * bsz + 4 * g);   // bytes: V^T row n (+16 nd), tokens 4g..4g+3
   const int vstep_b = 2 * 16 * bsz;           // bytes between the V^T dim tiles
 
-  while (f < f1) {
-    // segment (b, h) holding flattened tile f: b = last sequence with nkv * pre[b] <= f
-    int lo = 0, hi = batch - 1;
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (nkv * s_pre[mid] <= f) lo = mid; else hi = mid - 1;
-    }
-    const int b = lo;
-    const int nb = s_pre[b + 1] - s_pre[b];
-    const int rel = f - nkv * s_pre[b];
-    const int h = rel / nb;
-    const int t0 = rel - h * nb;
-    const int cnt = min(f1 - f, nb - t0);
+  // tiles [t0, t0 + cnt) of segment (b, h), then dec_finish
+  auto run = [&](int b, int h, int t0, int cnt, int nb, bool whole, int slot_i, int first, int np) {
     const int L = seq_lens[b];
 
     // Q^T fragments (B operand): lane (g, n) = head n of this kv head, dims 8g.. (+32 kc)
@@ -400,9 +390,53 @@ __global__ __launch_bounds__(256, WPC) void paged_decode_kernel(
       }
     }
 
-    dec_finish<D, G, ND, FC>(o, l_run, m_run * scale_log2, b, h, t0, cnt, nb, w, nw, total, nkv, s_pre, out,
+    dec_finish<D, G, ND, FC>(o, l_run, m_run * scale_log2, b, h, whole, slot_i, first, np, nkv, out,
                              out_stride, tmp_out, tmp_ml, counters, lane, g, n);
+  };
+  // b = last sequence with nkv * pre[b] <= f
+  auto find_seq = [&](const int* pre, int f) {
+    int lo = 0, hi = batch - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (nkv * pre[mid] <= f) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+  };
+
+  if constexpr (PIECE) {
+    // batch-invariant partition: segment (b, h) is cut into pieces of `piece` tiles
+    // from its first token, whatever the rest of the batch; piece p of the flattened
+    // piece space writes partial slot p and the segment's last arriver merges its
+    // pieces in order, so a sequence's output depends on its own length only
+    const int npieces = nkv * s_pp[batch];
+    for (int p = w; p < npieces && p < slot_cap; p += nw) {
+      const int b = find_seq(s_pp, p);
+      const int npb = s_pp[b + 1] - s_pp[b];
+      const int rel = p - nkv * s_pp[b];
+      const int h = rel / npb, k = rel - h * npb;
+      const int nb = s_pre[b + 1] - s_pre[b];
+      const int t0 = k * piece;
+      run(b, h, t0, min(piece, nb - t0), nb, npb == 1, p, p - k, npb);
+    }
+  } else {
+  int f = (int)(((long long)w * total) / nw);
+  const int f1 = (int)(((long long)(w + 1) * total) / nw);
+  while (f < f1) {
+    // segment (b, h) holding flattened tile f
+    const int b = find_seq(s_pre, f);
+    const int nb = s_pre[b + 1] - s_pre[b];
+    const int rel = f - nkv * s_pre[b];
+    const int h = rel / nb;
+    const int t0 = rel - h * nb;
+    const int cnt = min(f1 - f, nb - t0);
+    // waves sharing the segment: the first and last whose tile range meets it
+    const int S = nkv * s_pre[b] + h * nb, E = S + nb;
+    const int wf = (int)(((long long)(S + 1) * nw - 1) / total);
+    const int wl = (int)(((long long)E * nw - 1) / total);
+    const int seg = b * nkv + h;
+    run(b, h, t0, cnt, nb, t0 == 0 && cnt == nb, seg + w, seg + wf, wl - wf + 1);
     f += cnt;
+  }
   }
 }
 
@@ -415,7 +449,7 @@ __global__ __launch_bounds__(256) void paged_decode_combine_kernel(
     int nw_grid, int min_tiles) {
   __shared__ int s_pre[kDecMaxBatch + 1];
   __shared__ float s_M[G], s_den[G];
-  if (wave_id() == 0) dec_prefix(s_pre, seq_lens, batch);
+  if (wave_id() == 0) dec_prefix(s_pre, seq_lens, batch, 1);
   __syncthreads();
   const int total = nkv * s_pre[batch];
   const int nw = dec_num_waves(total, nw_grid, min_tiles);
@@ -505,9 +539,11 @@ extern "C" int ft_paged_decode_attention(void* out, int out_stride, float* tmp_o
                                          const void* v_cache, const int* block_tables,
                                          int bt_stride, const int* seq_lens, int batch, int nq,
                                          int nkv, int head_dim, int block_size, float scale,
-                                         int* counters, hipStream_t stream) {
+                                         int* counters, int piece, int slot_cap,
+                                         hipStream_t stream) {
   if (batch <= 0) return 0;
   if (nq % nkv != 0) return -1;
+  if (piece < 0 || (piece > 0 && counters == nullptr)) return -6;  // pieces merge in-launch
   if (batch > ft::kDecMaxBatch) return -5;
   if (block_size < 16 || (block_size & (block_size - 1))) return -4;
   const int bs_shift = __builtin_ctz(block_size);
@@ -532,7 +568,7 @@ extern "C" int ft_paged_decode_attention(void* out, int out_stride, float* tmp_o
 #define FT_DEC_ARGS                                                                             \
   (uint16_t*)out, out_stride, tmp_out, tmp_ml, (const uint16_t*)q, q_stride, (uint16_t*)k_cache, \
       (uint16_t*)v_cache, block_tables, bt_stride, seq_lens, batch, nkv, bs_shift, scale_log2,   \
-      counters, min_tiles
+      counters, min_tiles, piece, slot_cap
 #define FT_DEC_LAUNCH(DD, GG, RR, FCC)                                                  \
   if (wpc == 1)                                                                                \
     hipLaunchKernelGGL((ft::paged_decode_kernel<DD, GG, RR, FCC, 1>), dim3(nwg), dim3(256),      \
@@ -543,7 +579,11 @@ extern "C" int ft_paged_decode_attention(void* out, int out_stride, float* tmp_o
 #define FT_DEC_CASE(DD, GG, RR)                                                                \
   if (head_dim == DD && G == GG) {                                                             \
     nwg = ft_num_cus() * wpc;                                                                  \
-    if (counters != nullptr) {                                                                 \
+    if (piece > 0) {                                                                           \
+      nwg = ft_num_cus();                                                                      \
+      hipLaunchKernelGGL((ft::paged_decode_kernel<DD, GG, 2, true, 1, true>), dim3(nwg),      \
+                         dim3(256), 0, stream, FT_DEC_ARGS);                                   \
+    } else if (counters != nullptr) {                                                          \
       FT_DEC_LAUNCH(DD, GG, RR, true);                                                         \
     } else {                                                                                   \
       FT_DEC_LAUNCH(DD, GG, RR, false);                                                        \

@@ -59,7 +59,10 @@ constexpr int kPrefillMaxBlocks = 4096;  // block-table entries staged in LDS (c
 __device__ __forceinline__ float kgroup_max(float v) { return kgroups_max(v); }
 __device__ __forceinline__ float kgroup_sum(float v) { return kgroups_sum(v); }
 
-template <int D, int G>
+// INV (batch-invariant mode): the deferred rescale is decided per query row (lane)
+// instead of wave-wide, so a row's rounding never depends on the rows that share its
+// wave -- which change with chunking and prefix-cache hits.
+template <int D, int G, bool INV>
 __global__ __launch_bounds__(512, 1) void prefill_attn_kernel(
     uint16_t* __restrict__ out, int out_stride, const uint16_t* __restrict__ q, int q_stride,
     const uint16_t* __restrict__ k_cache, const uint16_t* __restrict__ v_cache,
@@ -266,7 +269,8 @@ __global__ __launch_bounds__(512, 1) void prefill_attn_kernel(
       for (int n = 1; n < 4; ++n)
         mt = fmaxf(mt, fmaxf(fmaxf(s[m][n][0], s[m][n][1]), fmaxf(s[m][n][2], s[m][n][3])));
       mt = kgroup_max(mt);
-      if (__builtin_amdgcn_ballot_w64(mt > m_run[m] + thr_raw) != 0) {
+      const bool up = mt > m_run[m] + thr_raw;
+      if (INV ? up : __builtin_amdgcn_ballot_w64(up) != 0) {
         const float mn = fmaxf(m_run[m], mt);
         const float alpha = mn == -INFINITY ? 1.f : __builtin_amdgcn_exp2f((m_run[m] - mn) * scale_log2);
         m_run[m] = mn;
@@ -446,7 +450,7 @@ extern "C" int ft_prefill_attention(void* out, int out_stride, const void* q, in
                                     const int* q_start_loc, const int* tile_info, int num_tiles,
                                     int nq, int nkv, int head_dim, int block_size, float scale,
                                     float* part_o, float* part_ml, const int* combine,
-                                    int num_combine, hipStream_t stream) {
+                                    int num_combine, int invariant, hipStream_t stream) {
   if (num_tiles <= 0) return 0;
   if (nq % nkv != 0) return -1;
   if (num_combine > 0 && (part_o == nullptr || part_ml == nullptr || combine == nullptr)) return -3;
@@ -455,11 +459,18 @@ extern "C" int ft_prefill_attention(void* out, int out_stride, const void* q, in
   dim3 grid(num_tiles, nkv), block(512);
 #define FT_PF_CASE(DD, GG)                                                                   \
   if (head_dim == DD && G == GG) {                                                           \
-    hipLaunchKernelGGL((ft::prefill_attn_kernel<DD, GG>), grid, block, 0, stream,            \
-                       (uint16_t*)out, out_stride, (const uint16_t*)q, q_stride,             \
-                       (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables,     \
-                       bt_stride, seq_lens, q_start_loc, tile_info, nkv, block_size,         \
-                       scale_log2, part_o, part_ml);                                         \
+    if (invariant)                                                                           \
+      hipLaunchKernelGGL((ft::prefill_attn_kernel<DD, GG, true>), grid, block, 0, stream,    \
+                         (uint16_t*)out, out_stride, (const uint16_t*)q, q_stride,           \
+                         (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables,   \
+                         bt_stride, seq_lens, q_start_loc, tile_info, nkv, block_size,       \
+                         scale_log2, part_o, part_ml);                                       \
+    else                                                                                     \
+      hipLaunchKernelGGL((ft::prefill_attn_kernel<DD, GG, false>), grid, block, 0, stream,   \
+                         (uint16_t*)out, out_stride, (const uint16_t*)q, q_stride,           \
+                         (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables,   \
+                         bt_stride, seq_lens, q_start_loc, tile_info, nkv, block_size,       \
+                         scale_log2, part_o, part_ml);                                       \
     if (num_combine > 0)                                                                     \
       hipLaunchKernelGGL((ft::prefill_combine_kernel<DD, GG>),                               \
                          dim3(num_combine, nkv, ft::kPrefillRows / (256 / (DD / 4))),         \

@@ -62,6 +62,9 @@ class EngineConfig:
     tp_share_device: bool = False      # TP ranks all on device_base (tests: gloo control + IPC data)
     max_restarts: int = 3              # separate-process engines: respawns after a replica dies
     quantization: Optional[str] = None  # None | "awq" | "w4" (W4A16, group 128; --quantization awq)
+    # a sequence's tokens independent of what else shares its steps (fixed GEMM splits,
+    # fixed-piece attention partitions; TP=1, bf16; slower decode attention)
+    batch_invariant: bool = False
 
     def resolved_device(self) -> str:
         if self.device != "auto":
@@ -113,6 +116,7 @@ class EngineConfig:
             tp_share_device=_env(["ENGINE_TP_SHARE_DEVICE"], False, _bool),
             max_restarts=_env(["ENGINE_MAX_RESTARTS"], 3, int),
             quantization=_env(["ENGINE_QUANTIZATION", "VLLM_QUANTIZATION"], None) or None,
+            batch_invariant=_env(["ENGINE_BATCH_INVARIANT", "VLLM_BATCH_INVARIANT"], False, _bool),
         )
         for k, v in overrides.items():
             setattr(c, k, v)

@@ -178,6 +178,12 @@ class ModelRunner:
             torch.cuda.synchronize(self.device)
         log.info("weights ready in %.1fs", time.time() - t0)
 
+        # batch-invariant numerics (cfg.batch_invariant): rows of a step up to the token
+        # budget plus a decode row per sequence
+        self.invariant = bool(getattr(cfg, "batch_invariant", False))
+        if self.invariant:
+            self.model.set_batch_invariant(max(cfg.max_num_batched_tokens, cfg.max_num_seqs)
+                                           + cfg.max_num_seqs)
         self.num_blocks = self._decide_num_blocks()
         self.kv = self.model.allocate_kv_cache(self.num_blocks, self.bs)
         # E6 host swap pool (--swap-space): capped at 2x the device pool, allocated
@@ -244,22 +250,34 @@ class ModelRunner:
         # of the kernel's grid (any step has at most max_num_seqs decode rows)
         self.max_decode_rows = max(mb, cfg.max_num_seqs)
         n_out, n_ml = ops.decode_workspace(self.max_decode_rows, nq, self.model.nkv, d,
-                                           waves=None if self.is_gpu else 0)
+                                           waves=None if self.is_gpu else 0,
+                                           piece=ops.DECODE_INV_PIECE if self.invariant else 0,
+                                           max_len=self.max_blocks_per_seq * self.bs)
         self.tmp_out = torch.empty(max(1, n_out), dtype=torch.float32, device=dv)
         self.tmp_ml = torch.empty(max(1, n_ml), dtype=torch.float32, device=dv)
         # split-KV prefill partials (ops.build_prefill_tiles): 128 slots = 128 MiB fp32
         # for Llama-3-8B; FT_PREFILL_SPLIT=0 keeps one workgroup per query block
         self.num_cus = torch.cuda.get_device_properties(dv).multi_processor_count if self.is_gpu else 256
         self.pf_part_o = self.pf_part_ml = None
-        if self.is_gpu and os.environ.get("FT_PREFILL_SPLIT", "1") == "1":
-            n_po, n_pml = ops.prefill_partials(self.model.nkv, d)
+        # batch-invariant plans cut every KV range at fixed pieces and never fall back
+        # to an unsplit item: room for every query block of a full step (the budget's
+        # 64-token blocks + a partial one per prompt) times the pieces of max_model_len
+        self.pf_max_partials = ops.PREFILL_MAX_PARTIALS
+        if self.invariant:
+            pieces = -(-self.max_model_len // (ops.PREFILL_BK * ops.PREFILL_INV_CHUNK))
+            qblocks = -(-cfg.max_num_batched_tokens // ops.prefill_tile_tokens(nq, self.model.nkv))
+            self.pf_max_partials = max(ops.PREFILL_MAX_PARTIALS,
+                                       (qblocks + cfg.max_num_seqs) * pieces)
+        if self.is_gpu and (self.invariant or os.environ.get("FT_PREFILL_SPLIT", "1") == "1"):
+            n_po, n_pml = ops.prefill_partials(self.model.nkv, d, self.pf_max_partials)
             self.pf_part_o = torch.empty(n_po, dtype=torch.float32, device=dv)
             self.pf_part_ml = torch.empty(n_pml, dtype=torch.float32, device=dv)
         # in-launch combine tickets (FT_DECODE_FUSED_COMBINE=0: separate combine kernel):
         # with the kernel at one workgroup per CU the last-arriver merge matches or beats
         # the combine kernel and saves a launch per layer (csrc/kernels/attn_decode.hip)
         self.dec_counters = ops.decode_counters(self.max_decode_rows, self.model.nkv, dv) \
-            if self.is_gpu and os.environ.get("FT_DECODE_FUSED_COMBINE", "1") == "1" else None
+            if self.is_gpu and (self.invariant or os.environ.get("FT_DECODE_FUSED_COMBINE", "1") == "1") \
+            else None
         self._done_event = torch.cuda.Event() if self.is_gpu else None
         self.graphs: Dict[int, torch.cuda.CUDAGraph] = {}
         # guided decoding, pipelined: per bucket a forward graph (-> logits) and a
@@ -457,7 +475,8 @@ class ModelRunner:
         tiles, combine = ops.build_prefill_tiles(
             ntoks, ops.prefill_tile_tokens(self.model.nq, self.model.nkv),
             seq_lens=seq_lens if self.pf_part_o is not None else None, nkv=self.model.nkv,
-            num_cus=self.num_cus)
+            num_cus=self.num_cus, max_partials=self.pf_max_partials,
+            fixed_chunk=ops.PREFILL_INV_CHUNK if self.invariant else 0)
         # logits rows: every decode row + the last row of each prompt that completes
         lrows = list(range(nd)) + [nd + int(qsl[i + 1]) - 1 for i, sm in enumerate(psamp) if sm]
         host.update(ids=np.concatenate(ids).astype(np.int32), pos=np.concatenate(pos).astype(np.int32),

@@ -107,6 +107,11 @@ _ATTR = {"qkv": "wqkv", "o": "wo", "gu": "wgu", "down": "wd"}
 # Split-K partial sums stay fp32 in one workspace and are reduced inside the
 # residual-add + RMSNorm that follows (row_rmsnorm from slabs): no extra kernel.
 PACKED_ROWS = 64
+# Batch-invariant mode (ENGINE_BATCH_INVARIANT): one (nt, splits) per projection at
+# EVERY row count -- the xr decode kernel up to 64 rows, packed_gemm above -- so a
+# row's sums run over the same K slices in the same order (k-steps ascending, fp32
+# slabs summed 0..splits-1 by the consumer) whatever else is in the step.
+INV_PLAN = {"qkv": (1, 2), "o": (1, 4), "gu": (2, 1), "down": (1, 4), "lm": (2, 1)}
 _M_BUCKETS = (1, 8, 16, 32, 64)
 PACKED_PLAN = {
     # qkv 32 / 64: split-K slabs reduced by slab_rope_kv (the bf16 image is the only
@@ -359,6 +364,8 @@ class LlamaModel:
                                         cfg.rope_scaling, device=self.device)
         self.lm_head_pk: Optional[torch.Tensor] = None
         self.ws: Optional[torch.Tensor] = None
+        self.invariant = False          # set_batch_invariant()
+        self.inv_plan: Dict[str, Tuple[int, int]] = {}
         self.use_packed = (self.device.type == "cuda" and dtype == torch.bfloat16
                            and os.environ.get("FT_PACKED_GEMM", "1") != "0")
         # "awq" / "w4": layer projections as W4A16 (group 128).  On the GPU only the
@@ -642,6 +649,55 @@ class LlamaModel:
             add(t)
         return total
 
+    def set_batch_invariant(self, max_rows: int):
+        """Batch-invariant numerics: INV_PLAN GEMMs at every row count, no fused decode
+        layer, fixed-piece decode attention and per-row prefill rescales (the caller
+        plans prefill with ops.build_prefill_tiles(fixed_chunk=...)).  A sequence's
+        tokens then do not depend on what else shares its steps."""
+        if self.tp != 1 or self.quant:
+            raise ValueError("batch-invariant mode needs TP=1 and bf16 weights")
+        self.fused = False
+        self.invariant = True
+        if self.layers[0].wqkv_pk is None:   # CPU / row-major reference path
+            return
+        nqkv = (self.nq + 2 * self.nkv) * self.d
+        shapes = {"qkv": (nqkv, self.cfg.hidden_size), "o": (self.cfg.hidden_size, self.nq * self.d),
+                  "gu": (2 * self.cfg.intermediate_size, self.cfg.hidden_size),
+                  "down": (self.cfg.hidden_size, self.cfg.intermediate_size)}
+        need = 0
+        self.inv_plan = {"lm": INV_PLAN["lm"]}
+        for proj, (n, k) in shapes.items():
+            nt, sp = INV_PLAN[proj]
+            kc = 512 if nt == 2 else 256
+            while sp > 1 and k % (kc * sp):   # fewer slices for a K the plan does not divide
+                sp //= 2
+            if n % (16 * nt) or k % (kc * sp) or (proj == "gu" and (nt != 2 or sp != 1)):
+                raise ValueError(f"batch-invariant plan does not fit {proj} {n}x{k}")
+            self.inv_plan[proj] = (nt, sp)
+            if sp > 1:
+                need = max(need, sp * max_rows * n)
+        if self.ws is None or self.ws.numel() < need:
+            self.ws = torch.empty(need, dtype=torch.float32, device=self.device)
+
+    def _packed_invariant(self, x: torch.Tensor, wp: torch.Tensor, proj: str):
+        rows = x.shape[0]
+        n, k = wp.shape
+        nt, sp = self.inv_plan[proj]
+        gu = proj == "gu"
+        if sp > 1 and sp * rows * n > self.ws.numel():
+            raise RuntimeError(f"batch-invariant workspace too small for {rows} rows")
+        if rows <= PACKED_ROWS:
+            u = -6 if gu else -5
+            if sp > 1:
+                ops.skinny_gemm(x, wp, ws=self.ws, splits=sp, nt=nt, u=u)
+                return sp, None
+            return 0, ops.skinny_gemm(x, wp, splits=1, nt=nt, u=u)
+        cfg = pg_cfg(proj, rows, k)[0]
+        if sp > 1:
+            ops.packed_gemm(x, wp, ws=self.ws, splits=sp, epi="slab", cfg=cfg)
+            return sp, None
+        return 0, ops.packed_gemm(x, wp, epi="silu" if gu else "store", cfg=cfg)
+
     # ------------------------------------------------------------------ projections
     def _tp_fused(self, rows: int) -> bool:
         """TP decode-size steps: the row-parallel o / down outputs go through ONE
@@ -714,6 +770,8 @@ class LlamaModel:
         """y = x W^T on the packed image: the decode kernels up to PACKED_ROWS rows
         (skinny_gemm.hip), the tiled MFMA GEMM above (packed_gemm.hip); hipBLASLt on
         the resident row-major copy ``rm`` from PG_RM_ROWS rows."""
+        if self.invariant:
+            return self._packed_invariant(x, wp, proj)
         rows = x.shape[0]
         n, k = wp.shape
         gu = proj == "gu"
@@ -783,12 +841,14 @@ class LlamaModel:
         if nd > 0:
             ops.decode_attention(attn[:nd], qkv[:nd], kc, vc, meta.dec_block_tables,
                                  meta.dec_seq_lens, meta.tmp_out, meta.tmp_ml, nq, nkv, d,
-                                 self.scale, counters=meta.dec_counters)
+                                 self.scale, counters=meta.dec_counters,
+                                 piece=ops.DECODE_INV_PIECE if self.invariant else 0)
         if t > nd:
             ops.prefill_attention(attn[nd:], qkv[nd:], kc, vc, meta.block_tables, meta.seq_lens,
                                   meta.q_start_loc, meta.tile_info, meta.num_tiles, nq, nkv, d,
                                   self.scale, meta.pf_part_o, meta.pf_part_ml, meta.pf_combine,
-                                  meta.pf_num_combine, meta.pf_num_partials)
+                                  meta.pf_num_combine, meta.pf_num_partials,
+                                  invariant=self.invariant)
         return attn
 
     def _forward_fused(self, input_ids: torch.Tensor, meta: AttnMeta, kv_caches) -> torch.Tensor:

@@ -120,13 +120,24 @@ def rope_kv_write(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, nq, n
                           head_dim)
 
 
-def decode_workspace(batch: int, nq: int, nkv: int, head_dim: int, waves: Optional[int] = None):
+# Batch-invariant decode attention: every (sequence, kv head) is cut into pieces of
+# this many 16-token tiles from its first token (csrc/kernels/attn_decode.hip piece
+# mode), whatever the rest of the batch.
+DECODE_INV_PIECE = 32
+
+
+def decode_workspace(batch: int, nq: int, nkv: int, head_dim: int, waves: Optional[int] = None,
+                     piece: int = 0, max_len: int = 0):
     """(tmp_out, tmp_ml) element counts of the decode kernel's partial workspace:
     one fp32 slot per (sequence, kv head) plus one per wave of the grid
-    (csrc/kernels/attn_decode.hip), each holding the G = nq / nkv heads."""
+    (csrc/kernels/attn_decode.hip), each holding the G = nq / nkv heads.  With
+    ``piece`` (batch-invariant mode) one slot per piece of a ``max_len`` sequence."""
     if waves is None:
         waves = native().decode_waves() if native_available() else 0
     slots = batch * nkv + waves
+    if piece > 0:
+        tiles = -(-max_len // 16)
+        slots = max(slots, batch * nkv * -(-tiles // piece))
     g = nq // nkv
     return slots * g * head_dim, slots * g * 2
 
@@ -143,14 +154,16 @@ def decode_counters(batch: int, nkv: int, device) -> torch.Tensor:
 
 
 def decode_attention(out, q, k_cache, v_cache, block_tables, seq_lens, tmp_out, tmp_ml, nq, nkv,
-                     head_dim, scale, counters: Optional[torch.Tensor] = None):
+                     head_dim, scale, counters: Optional[torch.Tensor] = None, piece: int = 0):
     """out[b] = attention of the single new query of sequence b (q: [B, >=nq*D] rows).
     k_cache [blocks, nkv, bs, D]; v_cache [blocks, nkv, D, bs] (transposed blocks).
     ``counters`` (decode_counters): merge shared segments inside the launch instead
-    of a second combine kernel."""
+    of a second combine kernel.  ``piece`` > 0: batch-invariant partition (fixed
+    pieces of that many tiles per sequence; needs counters and a workspace from
+    decode_workspace(piece=...))."""
     if q.is_cuda:
         native().paged_decode_attention(out, q, k_cache, v_cache, block_tables, seq_lens, tmp_out,
-                                        tmp_ml, nq, nkv, head_dim, scale, counters)
+                                        tmp_ml, nq, nkv, head_dim, scale, counters, piece)
         return out
     b = q.shape[0]
     qq = q[:, : nq * head_dim].reshape(b, nq, head_dim)
@@ -162,15 +175,16 @@ def decode_attention(out, q, k_cache, v_cache, block_tables, seq_lens, tmp_out, 
 
 def prefill_attention(out, q, k_cache, v_cache, block_tables, seq_lens, q_start_loc, tile_info,
                       num_tiles, nq, nkv, head_dim, scale, part_o=None, part_ml=None, combine=None,
-                      num_combine: int = 0, num_partials: int = 0):
+                      num_combine: int = 0, num_partials: int = 0, invariant: bool = False):
     """Varlen causal attention of the new tokens over their paged history.
     ``tile_info``: the work items of build_prefill_tiles (4 int32 each); split-KV
     items leave fp32 partials in ``part_o`` / ``part_ml`` (prefill_partials) that
-    the ``combine`` list merges (csrc/kernels/attn_prefill.hip)."""
+    the ``combine`` list merges (csrc/kernels/attn_prefill.hip).  ``invariant``:
+    per-row rescale decisions (batch-invariant mode, with a fixed_chunk plan)."""
     if q.is_cuda:
         native().prefill_attention(out, q, k_cache, v_cache, block_tables, seq_lens, q_start_loc,
                                    tile_info, num_tiles, nq, nkv, head_dim, scale, part_o, part_ml,
-                                   combine, num_combine, num_partials)
+                                   combine, num_combine, num_partials, invariant)
         return out
     t = q.shape[0]
     qq = q[:, : nq * head_dim].reshape(t, nq, head_dim)
@@ -196,9 +210,21 @@ PREFILL_MAX_ROUNDS = 4
 PREFILL_ROUND_BLIND = os.environ.get("FT_PREFILL_ROUND_BLIND", "0") == "1"
 
 
+# Batch-invariant prefill plan: KV ranges cut at absolute multiples of this many
+# 64-token tiles (1024 tokens), so a query row sees the same pieces in the same
+# order whatever chunk, query block or batch it is computed in.
+PREFILL_INV_CHUNK = 16
+
+
 def build_prefill_tiles(q_lens, tile_tokens: int, seq_lens=None, nkv: int = 8, num_cus: int = 256,
-                        max_partials: int = PREFILL_MAX_PARTIALS, min_split_tiles: int = 4):
+                        max_partials: int = PREFILL_MAX_PARTIALS, min_split_tiles: int = 4,
+                        fixed_chunk: int = 0):
     """Host plan of the prefill kernel grid: (items, combine).
+
+    ``fixed_chunk`` (batch-invariant mode): every block's KV range is cut at
+    absolute multiples of that many tiles (pieces past a row's position are masked
+    no-ops in the merge) and the plan never falls back to an unsplit item; raises
+    if the partial slots run out.
 
     items: [(seq, first query token, kv_lo_tile << 16 | kv_hi_tile, partial slot)],
     one per (query block, KV range); combine: [(seq, first query token, first slot,
@@ -226,6 +252,22 @@ def build_prefill_tiles(q_lens, tile_tokens: int, seq_lens=None, nkv: int = 8, n
                 nkt = (kv_end + PREFILL_BK - 1) // PREFILL_BK
             blocks.append((b, s, nkt))
     items, combine = [], []
+    if fixed_chunk > 0:
+        slots = 0
+        for b, s, nkt in blocks:
+            ns = -(-nkt // fixed_chunk)
+            if ns <= 1 or seq_lens is None:
+                items.append((b, s, 0xFFFF, -1))
+                continue
+            if slots + ns > max_partials:
+                raise RuntimeError(f"batch-invariant prefill plan needs more than {max_partials} "
+                                   "partial slots (fewer batched tokens per step)")
+            combine.append((b, s, slots, ns))
+            for j in range(ns):
+                items.append((b, s, ((j * fixed_chunk) << 16) | min((j + 1) * fixed_chunk, nkt),
+                              slots + j))
+            slots += ns
+        return items, combine
     per_round = max(1, num_cus // max(1, nkv))
     chunk = 0
     nk_lo = min(n for _, _, n in blocks) if blocks else 0

@@ -120,3 +120,35 @@ def test_prefill_split_plan_fills_whole_rounds():
             blind_items = sum(-(-min(Q + C, C + s + min(64, Q - s)) // 64 // blind) or 1
                               for s in range(0, Q, 64)) * S
             assert rounds * (longest + 1) <= -(-max(blind_items, nblocks) * 8 // 256) * (blind + 1) + 1
+
+
+def test_prefill_fixed_chunk_plan_is_absolute():
+    """Batch-invariant prefill plan (fixed_chunk): a block's KV range is cut at
+    absolute multiples of the chunk, whatever the other blocks of the step, so the
+    same query rows see the same pieces in any batch; it never silently falls back
+    to an unsplit item when the partial slots run out."""
+    from fasttalk_llm_microservice_amd import ops
+
+    C = 4
+    a, comb_a = ops.build_prefill_tiles([100], 64, seq_lens=[3000], fixed_chunk=C)
+    b, comb_b = ops.build_prefill_tiles([37, 100, 5], 64, seq_lens=[900, 3000, 4000], fixed_chunk=C)
+    ranges = lambda items, seq: sorted((s, r >> 16, r & 0xFFFF) for bb, s, r, _ in items if bb == seq)
+    assert ranges(a, 0) == ranges(b, 1)
+    for s, lo, hi in ranges(a, 0):
+        assert lo % C == 0 and (hi - lo == C or hi == -(-min(3000, 2900 + s + min(64, 100 - s)) // 64))
+    assert [c[3] for c in comb_a] == [c[3] for c in comb_b if c[0] == 1]
+    with pytest.raises(RuntimeError):
+        ops.build_prefill_tiles([100] * 8, 64, seq_lens=[3000] * 8, fixed_chunk=C, max_partials=8)
+    # no seq_lens (CPU path): nothing is split
+    items, comb = ops.build_prefill_tiles([100], 64, fixed_chunk=C)
+    assert comb == [] and all(r == 0xFFFF for _, _, r, _ in items)
+
+
+def test_decode_workspace_piece_mode_slots():
+    """Piece mode needs one partial slot per piece of the longest sequence."""
+    from fasttalk_llm_microservice_amd import ops
+
+    n_out, n_ml = ops.decode_workspace(4, 32, 8, 128, waves=16, piece=32, max_len=2048)
+    assert n_out == 4 * 8 * 4 * 4 * 128 and n_ml == 4 * 8 * 4 * 4 * 2   # 128 tiles -> 4 pieces
+    n0, _ = ops.decode_workspace(4, 32, 8, 128, waves=16)
+    assert n0 == (4 * 8 + 16) * 4 * 128
