@@ -174,24 +174,26 @@ def test_prefill_attention_invariant_to_chunking_and_batch():
     assert ((got - expect).abs() <= 2e-2 + 2e-2 * expect.abs()).all()
 
 
-def test_engine_batch_invariant_greedy_tokens():
-    """Greedy tokens of a prompt alone == the same prompt while other prompts of
-    other lengths arrive around it (mixed steps, decode batches of changing size)."""
+def _target_logits(batch_invariant: bool):
+    """(alone, mixed) per-step logits rows of one greedy prompt: decoded alone, then
+    with other prompts of other lengths arriving around it."""
     from fasttalk_llm_microservice_amd.engine.config import EngineConfig
     from fasttalk_llm_microservice_amd.engine.engine import LLMEngine
     from fasttalk_llm_microservice_amd.engine.sampling_params import SamplingParams
 
     eng = LLMEngine(EngineConfig(model="tiny-2k", device="cuda", num_kv_blocks=1024,
-                                 max_model_len=4096, max_num_seqs=16, batch_invariant=True,
-                                 enable_prefix_caching=False))
-    assert eng.runner.model.invariant and not eng.runner.model.fused
+                                 max_model_len=4096, max_num_seqs=16,
+                                 batch_invariant=batch_invariant, enable_prefix_caching=False))
+    assert eng.runner.model.invariant == batch_invariant
     rng = np.random.default_rng(5)
     target = rng.integers(0, 120000, 1300).tolist()
     others = [rng.integers(0, 120000, n).tolist() for n in (40, 700, 2100, 9, 333)]
+    r = eng.runner
 
     def run(schedule):
-        outs = {}
+        toks = []
         step = 0
+        r.logits_tap, r.logits_tap_ids = [], []
         eng.add_request("t", target, SamplingParams(temperature=0.0, max_tokens=40, ignore_eos=True))
         while eng.has_work() or schedule:
             while schedule and schedule[0][0] <= step:
@@ -200,11 +202,37 @@ def test_engine_batch_invariant_greedy_tokens():
                                 SamplingParams(temperature=0.0, max_tokens=30, ignore_eos=True))
             for o in eng.step():
                 if o.request_id == "t":
-                    outs.setdefault("t", []).extend(o.token_ids)
+                    toks.extend(o.token_ids)
             step += 1
-        return outs["t"]
+        torch.cuda.synchronize()
+        logits = [lg[row].float().cpu() for lg, ids in zip(r.logits_tap, r.logits_tap_ids)
+                  for row, rid in enumerate(ids or []) if rid == "t"]
+        shared = max(len(ids) for ids in r.logits_tap_ids if ids and "t" in ids)
+        r.logits_tap = r.logits_tap_ids = None
+        return toks, logits, shared
 
     alone = run([])
-    assert len(alone) == 40
     mixed = run([(0, 0), (0, 1), (2, 2), (5, 3), (9, 4), (20, 1)])
-    assert mixed == alone
+    return alone, mixed
+
+
+def test_engine_batch_invariant_logits():
+    """Batch-invariant engine: every step's logits row of the target is bit-identical
+    alone and while 6 other prompts share its steps (mixed prefill steps, decode
+    batches of changing size), so its greedy tokens are too."""
+    (ta, la, n1), (tm, lm, n2) = _target_logits(True)
+    # (a pipelined run may tap one queued step past the last token: >= 40 rows)
+    assert len(ta) == 40 and len(la) >= 40 and len(lm) >= 40 and n1 == 1
+    assert n2 >= 4, n2   # the target really shared its steps
+    assert tm == ta
+    for k, (a, b) in enumerate(zip(la[:40], lm[:40])):
+        assert torch.equal(a, b), f"step {k}"
+
+
+def test_engine_default_mode_is_not_batch_invariant():
+    """Control for the test above: the default plans (fused decode layer for small
+    batches, packed_gemm rows in mixed steps, batch-dependent attention splits)
+    change the target's logits bits when others share its steps."""
+    (_, la, _), (_, lm, n2) = _target_logits(False)
+    assert n2 >= 4
+    assert any(not torch.equal(a, b) for a, b in zip(la, lm))
