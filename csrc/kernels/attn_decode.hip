@@ -268,7 +268,8 @@ __global__ __launch_bounds__(256, WPC) void paged_decode_kernel(
   if (PIECE && wave_id() == 1) dec_prefix(s_pp, seq_lens, batch, piece);
   __syncthreads();
   const int total = nkv * s_pre[batch];
-  const int nw = PIECE ? gridDim.x * 4 : dec_num_waves(total, gridDim.x * 4, min_tiles);
+  const int wpg = blockDim.x >> 6;   // waves per workgroup (FT_DECODE_WAVES sweeps 2 / 4)
+  const int nw = PIECE ? gridDim.x * wpg : dec_num_waves(total, gridDim.x * wpg, min_tiles);
   const int w = wave_id() * gridDim.x + blockIdx.x;  // spreads low wave ids over CUs
   if (FC && blockIdx.x == 0) {
     // fused-combine mode has no combine kernel to define empty sequences' outputs
@@ -564,6 +565,15 @@ extern "C" int ft_paged_decode_attention(void* out, int out_stride, float* tmp_o
   const int min_tiles = min_tiles_env ? min_tiles_env : ft::kDecMinTiles;
   // 1 workgroup per CU, or the register-limited maximum for the ring depth
   const int wpc = min(dec_wg_per_cu(), ring == 2 ? 3 : 2);
+  // waves per workgroup: 2 (one 128-thread workgroup per CU, 512 waves) -- engine A/B
+  // at 50 x 3k: decode step 7.15-7.17 vs 7.29 ms with 4 waves, 8.71 with 1; the bare
+  // kernel 130.7-135 vs 138-145 us at 64 x 4k (profiles/attn_waves_per_wg_r04.log).
+  // FT_DECODE_WAVES (1 / 2 / 4) overrides for sweeps.
+  static const int nwv = [] {
+    const char* e = getenv("FT_DECODE_WAVES");
+    const int v = e ? atoi(e) : 2;
+    return (v == 1 || v == 2 || v == 4) ? v : 2;
+  }();
   int nwg = 0;
 #define FT_DEC_ARGS                                                                             \
   (uint16_t*)out, out_stride, tmp_out, tmp_ml, (const uint16_t*)q, q_stride, (uint16_t*)k_cache, \
@@ -571,11 +581,11 @@ extern "C" int ft_paged_decode_attention(void* out, int out_stride, float* tmp_o
       counters, min_tiles, piece, slot_cap
 #define FT_DEC_LAUNCH(DD, GG, RR, FCC)                                                  \
   if (wpc == 1)                                                                                \
-    hipLaunchKernelGGL((ft::paged_decode_kernel<DD, GG, RR, FCC, 1>), dim3(nwg), dim3(256),      \
+    hipLaunchKernelGGL((ft::paged_decode_kernel<DD, GG, RR, FCC, 1>), dim3(nwg), dim3(64 * nwv), \
                        0, stream, FT_DEC_ARGS);                                                \
   else                                                                                         \
     hipLaunchKernelGGL((ft::paged_decode_kernel<DD, GG, RR, FCC, (RR == 2 ? 3 : 2)>),          \
-                       dim3(nwg), dim3(256), 0, stream, FT_DEC_ARGS)
+                       dim3(nwg), dim3(64 * nwv), 0, stream, FT_DEC_ARGS)
 #define FT_DEC_CASE(DD, GG, RR)                                                                \
   if (head_dim == DD && G == GG) {                                                             \
     nwg = ft_num_cus() * wpc;                                                                  \
@@ -589,7 +599,7 @@ extern "C" int ft_paged_decode_attention(void* out, int out_stride, float* tmp_o
       FT_DEC_LAUNCH(DD, GG, RR, false);                                                        \
       hipLaunchKernelGGL((ft::paged_decode_combine_kernel<DD, GG>), dim3(batch * nkv), dim3(256),\
                          0, stream, (uint16_t*)out, out_stride, tmp_out, tmp_ml, seq_lens, batch,\
-                         nkv, nwg * 4, min_tiles);                                               \
+                         nkv, nwg * nwv, min_tiles);                                             \
     }                                                                                            \
     return static_cast<int>(hipGetLastError());                                                  \
   }
