@@ -402,6 +402,26 @@ def test_tiny_cpu_chunked_prefill_and_prefix_cache(tiny_engine):
     assert chunked.generate([p + first + [7, 8, 9]], sp)[0] == again
 
 
+def test_batch_invariant_config_plumbing():
+    """ENGINE_BATCH_INVARIANT reaches the model: invariant plans on, the fused small-batch
+    layer off (GPU kernels: tests/test_batch_invariance_gpu.py), and the CPU path still
+    generates the same greedy tokens as the default engine."""
+    import os
+
+    os.environ["ENGINE_BATCH_INVARIANT"] = "1"
+    try:
+        cfg = EngineConfig.from_env(model="tiny", device="cpu", num_kv_blocks=128, max_model_len=512)
+    finally:
+        del os.environ["ENGINE_BATCH_INVARIANT"]
+    assert cfg.batch_invariant
+    inv = LLMEngine(cfg)
+    assert inv.runner.invariant and inv.runner.model.invariant and not inv.runner.model.fused
+    base = LLMEngine(EngineConfig(model="tiny", device="cpu", num_kv_blocks=128, max_model_len=512))
+    assert not base.runner.model.invariant
+    sp = SamplingParams(temperature=0, max_tokens=5, ignore_eos=True)
+    assert inv.generate([[4, 5, 6, 7]], sp) == base.generate([[4, 5, 6, 7]], sp)
+
+
 def test_tiny_cpu_seeded_sampling_reproducible(tiny_engine):
     sp = SamplingParams(temperature=0.9, top_p=0.9, top_k=50, max_tokens=5, seed=11, ignore_eos=True)
     a = tiny_engine.generate([[1, 2, 3]], sp)[0]
