@@ -835,10 +835,15 @@ class AsyncEngine:
         self._pending = {}
 
     def _dispatch(self, items: List[RequestOutput]):
-        for o in items:
-            q = self._streams.get(o.request_id)
-            if q is not None:
-                q.put_nowait(o)
+        # a request's first output (a new turn's first token) wakes its consumer
+        # ahead of the step's streaming deltas: the loop runs woken consumers in
+        # put order, and ~50 deltas of the other sessions share each step
+        for first in (True, False):
+            for o in items:
+                if (o.ttft_s is not None) == first:
+                    q = self._streams.get(o.request_id)
+                    if q is not None:
+                        q.put_nowait(o)
 
     def _poll_cmds(self):
         while True:
