@@ -204,8 +204,10 @@ def prefill_partials(nkv: int, head_dim: int, max_partials: int = PREFILL_MAX_PA
 
 
 # per-work-item overhead of the prefill kernel in 64-token KV tiles (Q load, DMA ramp,
-# partial store + its combine), for the round-aware split plan below
-PREFILL_ITEM_TILES = float(os.environ.get("FT_PREFILL_ITEM_TILES", "1.0"))
+# partial store + its combine), for the round-aware split plan below.  Swept on MI355X
+# (profiles/prefill_item_tiles_r04.log): 2 = 1 at every chat-turn shape but one, where it
+# plans one round instead of two (4 x 150 new over 1.5k: 46.9 vs 58.9 us)
+PREFILL_ITEM_TILES = float(os.environ.get("FT_PREFILL_ITEM_TILES", "2.0"))
 PREFILL_MAX_ROUNDS = 4
 PREFILL_ROUND_BLIND = os.environ.get("FT_PREFILL_ROUND_BLIND", "0") == "1"
 
