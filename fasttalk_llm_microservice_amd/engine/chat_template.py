@@ -58,9 +58,15 @@ def _content_text(m: Dict[str, Any]) -> str:
 
 
 class ChatTemplate:
+    # rendered messages kept (role, text) -> ids: a conversation re-renders the same
+    # history messages at every window cut and for the cut-window warm-up, and each
+    # encode runs on the service's event loop (~0.25 ms per message)
+    MSG_CACHE = 16384
+
     def __init__(self, tokenizer: Tokenizer):
         self.tok = tokenizer
         self._hdr_cache: Dict[str, List[int]] = {}
+        self._msg_cache: Dict[tuple, List[int]] = {}
 
     def _header(self, role: str) -> List[int]:
         h = self._hdr_cache.get(role)
@@ -74,7 +80,18 @@ class ChatTemplate:
         role = m.get("role", "user")
         if role == "tool":
             role = "ipython"
-        return self._header(role) + self.tok.encode(_content_text(m)) + [self.tok.eot_id]
+        text = _content_text(m)
+        key = (role, text)
+        ids = self._msg_cache.get(key)
+        if ids is None:
+            ids = self._header(role) + self.tok.encode(text) + [self.tok.eot_id]
+            while len(self._msg_cache) >= self.MSG_CACHE:   # FIFO: drop the oldest entries
+                try:
+                    self._msg_cache.pop(next(iter(self._msg_cache)))
+                except (RuntimeError, KeyError, StopIteration):   # a concurrent render
+                    self._msg_cache.clear()
+            self._msg_cache[key] = ids
+        return list(ids)
 
     def render(self, messages: Sequence[Dict[str, Any]], add_generation_prompt: bool = True,
                tools: Optional[Sequence[Dict[str, Any]]] = None) -> List[int]:

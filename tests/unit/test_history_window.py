@@ -183,3 +183,25 @@ def test_tool_rounds_continue_the_session_stream_without_becoming_its_state():
     # a full re-render (what these rounds used before) diverges at the first reply
     full = h.template.render(msgs)
     assert full[:len(stream)] != stream
+
+
+def test_chat_template_message_cache_is_transparent():
+    """Rendered message ids are cached by (role, text): a re-render gives the same ids,
+    callers may mutate what they get back, and the cache stays bounded."""
+    from fasttalk_llm_microservice_amd.engine.chat_template import ChatTemplate
+    from fasttalk_llm_microservice_amd.engine.tokenizer import get_tokenizer
+
+    t = ChatTemplate(get_tokenizer())
+    msgs = [{"role": "system", "content": "be brief"}, {"role": "user", "content": "hello there"},
+            {"role": "assistant", "content": "hi"}, {"role": "tool", "content": "result 1"}]
+    a = t.render(msgs)
+    a2 = t.render(msgs)
+    assert a == a2
+    ids = t.message_ids(msgs[1])
+    ids.append(-1)
+    assert t.message_ids(msgs[1])[-1] != -1
+    t.MSG_CACHE = 3
+    for i in range(10):
+        t.message_ids({"role": "user", "content": f"m{i}"})
+    assert len(t._msg_cache) <= 3
+    assert t.render(msgs) == a
