@@ -91,7 +91,7 @@ class AgentConfig(BaseModel):
     model_tool_choice: bool = False
 
 
-@dataclass
+@dataclass(slots=True)
 class AgentEvent:
     text: str = ""
     num_tokens: int = 0

@@ -259,14 +259,16 @@ class WebSocketLLMServer:
             # frames are shaped here, on the one path every transport shares (the v1
             # server trims v2 frames to its shapes; token frames arrive pre-serialised)
             txt = obj if isinstance(obj, str) else json.dumps(shape(obj))
-            async with send_lock:
-                ws = raw.get("ws") if raw is not None else None
-                if ws is None:
-                    await websocket.send_text(txt)
-                elif ws.closed:
+            ws = raw.get("ws") if raw is not None else None
+            if ws is not None:
+                # aiohttp writes each frame whole, synchronously, before any drain await,
+                # so concurrent senders cannot split a frame: no lock on the per-token path
+                if ws.closed:
                     raise WebSocketDisconnect(1006)
-                else:
-                    await ws.send_str(txt)
+                await ws.send_str(txt)
+                return
+            async with send_lock:
+                await websocket.send_text(txt)
 
         if self.connection_manager.add_connection(session_id, websocket) is None:
             await send({"type": "error", "error": {"code": "max_connections",
