@@ -7,7 +7,8 @@ that has served many sessions.
 python bench/attn_sweep.py [--nq 32 --nkv 8] [--uniform]
 FT_DECODE_RING=2|3|4 selects the kernel's register-ring depth (default 2);
 FT_DECODE_MIN_TILES the partition's minimum 16-token tiles per wave (default 8);
-FT_DECODE_WPC workgroups per CU (1-3, default 1).
+FT_DECODE_WPC workgroups per CU (1-3, default 1); FT_DECODE_WAVES waves per workgroup (1 / 2 / 4,
+default 2).
 --fused: the in-launch combine the engine uses (decode tickets) instead of the
 separate combine kernel.  --shapes "1:512,1:3000" overrides the shape list.
 """
