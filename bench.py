@@ -354,7 +354,8 @@ def main():
             "engine_decode_step_ms_last512": round(metrics.get("decode_step_ms_avg", 0.0), 3),
             "engine_decode_batch_avg": round(metrics.get("decode_batch_avg", 0.0), 2),
             "engine_steps": {k: v for k, v in metrics.items() if k in
-                             ("decode_steps", "pipelined_steps", "mixed_steps", "mixed_ahead", "pipeline_shrinks")
+                             ("decode_steps", "pipelined_steps", "mixed_steps", "mixed_ahead", "pipeline_shrinks",
+                              "mixed_ahead_drain")
                              or k.startswith("mixed_ahead_skip_")},
             "engine_runner": metrics.get("runner", {}),
             "engine_decode_host_ms": metrics.get("decode_host_ms", {}),
