@@ -249,8 +249,19 @@ def main():
     loop = asyncio.new_event_loop()
     ready = threading.Event()
 
+    # FT_BENCH_LOOP_PROFILE=<path>: cProfile of the service event-loop thread (the asyncio
+    # loop that runs the WebSocket handlers and the voice agent), dumped after the timed turns
+    loop_prof_path = os.environ.get("FT_BENCH_LOOP_PROFILE")
+    loop_prof = None
+
     def serve():
+        nonlocal loop_prof
         asyncio.set_event_loop(loop)
+        if loop_prof_path:
+            import cProfile
+
+            loop_prof = cProfile.Profile()
+            loop_prof.enable()
         loop.run_until_complete(asgi.start())
         ready.set()
         loop.run_forever()
@@ -287,6 +298,16 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     hb["done"] = True
+    if loop_prof is not None:
+        dumped = threading.Event()
+
+        def dump():
+            loop_prof.disable()
+            loop_prof.dump_stats(loop_prof_path)
+            dumped.set()
+
+        loop.call_soon_threadsafe(dump)
+        dumped.wait(30)
     cmd("close")
     client.join(timeout=30)
 
@@ -469,8 +490,19 @@ def bench_tp(a, rank: int, world: int, local_rank: int):
     loop = asyncio.new_event_loop()
     ready = threading.Event()
 
+    # FT_BENCH_LOOP_PROFILE=<path>: cProfile of the service event-loop thread (the asyncio
+    # loop that runs the WebSocket handlers and the voice agent), dumped after the timed turns
+    loop_prof_path = os.environ.get("FT_BENCH_LOOP_PROFILE")
+    loop_prof = None
+
     def serve():
+        nonlocal loop_prof
         asyncio.set_event_loop(loop)
+        if loop_prof_path:
+            import cProfile
+
+            loop_prof = cProfile.Profile()
+            loop_prof.enable()
         loop.run_until_complete(asgi.start())
         ready.set()
         loop.run_forever()
@@ -498,6 +530,16 @@ def bench_tp(a, rank: int, world: int, local_rank: int):
     sync()
     elapsed = time.perf_counter() - t0
     hb["done"] = True
+    if loop_prof is not None:
+        dumped = threading.Event()
+
+        def dump():
+            loop_prof.disable()
+            loop_prof.dump_stats(loop_prof_path)
+            dumped.set()
+
+        loop.call_soon_threadsafe(dump)
+        dumped.wait(30)
     cmd("close")
     client.join(timeout=30)
     summ = summarize(res)
