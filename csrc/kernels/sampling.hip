@@ -4,7 +4,7 @@
 // Rows without top-k (greedy, temperature, top-p: the serving default) take the
 // multi-workgroup path further down (samp_*_kernel: 32 vocabulary slices per row,
 // 28.6 vs 84.6 us for top-p at 50 rows, profiles/sampler_probe_r02.log); top-k
-// rows and the rare rows whose two nucleus candidates were both rejected run the
+// rows and the rare rows whose nucleus candidates were all rejected run the
 // one-workgroup-per-row kernel described here.
 //
 // Design (measured: the first version, a 4-pass radix select with LDS-atomic
@@ -178,10 +178,14 @@ constexpr int kTopkMax = 64;
 constexpr int kTopkKept = 256;   // kept set (top-k + ties) the merge kernel holds
 static_assert(kTopkKept <= kSlThreads, "one merge thread per kept rank");
 // per-row fp32 scratch: slice stats [kSlices][4] (M_p, Z_p, key, id) | M, Z |
-// cand (key, id) x 2 | above [kSlices][2] | flag | top-k candidate counts
+// cand (key, id) x kCand | above [kSlices][kCand] | flag | top-k candidate counts
 // [kSlices] | top-k candidates [kSlices][kTopkMax] (key, id)
-constexpr int kWsStats = 0, kWsMZ = 4 * kSlices, kWsCand = kWsMZ + 2, kWsAbove = kWsCand + 4,
-              kWsFlag = kWsAbove + 2 * kSlices, kWsTkCnt = kWsFlag + 1,
+// kCand inverse-CDF candidates per top-p row: all rejected with probability <= (1 - top_p)^kCand
+// (1e-4 at top_p 0.9), so the one-workgroup fallback -- a ~30 us tail the whole sampler launch
+// waits for -- almost never runs (with 2 candidates: 1% of rows, ~40% of 50-row steps)
+constexpr int kCand = 4;
+constexpr int kWsStats = 0, kWsMZ = 4 * kSlices, kWsCand = kWsMZ + 2, kWsAbove = kWsCand + 2 * kCand,
+              kWsFlag = kWsAbove + kCand * kSlices, kWsTkCnt = kWsFlag + 1,
               kWsTk = kWsTkCnt + kSlices, kWsRow = kWsTk + 2 * kSlices * kTopkMax;
 
 template <typename T>
@@ -195,7 +199,7 @@ __global__ __launch_bounds__(kSampThreads) void sample_kernel(
   __shared__ float chunk_mass[kChunks * kSampThreads];  // 64 KiB
   const int row = blockIdx.x;
   // multi-workgroup path (flags != null): 0 = row already sampled there, 1 = both of
-  // its candidates were rejected (run here on fresh uniforms, rounds 2..), 2 = top-k row
+  // its candidates were rejected (run here on fresh uniforms, rounds kCand..), 2 = top-k row
   int fl = flags ? flags[(long)row * flag_stride] : 2;
   if (fl == 0) return;
   if (fl == 3) {
@@ -203,19 +207,19 @@ __global__ __launch_bounds__(kSampThreads) void sample_kernel(
     // mass strictly above it (samp_above_kernel, per slice) is < top_p * Z
     if (threadIdx.x == 0) {
       const float* wr = reinterpret_cast<const float*>(flags) + (long)row * flag_stride - kWsFlag;
-      float a0 = 0.f, a1 = 0.f;
+      float a[kCand] = {};
       for (int p = 0; p < kSlices; ++p) {
-        a0 += wr[kWsAbove + 2 * p];
-        a1 += wr[kWsAbove + 2 * p + 1];
+#pragma unroll
+        for (int c = 0; c < kCand; ++c) a[c] += wr[kWsAbove + kCand * p + c];
       }
       const float lim = top_p[row] * wr[kWsMZ + 1];
       int res = 1;
-      if (a0 < lim) {
-        out_tokens[row] = __float_as_int(wr[kWsCand + 1]);
-        res = 0;
-      } else if (a1 < lim) {
-        out_tokens[row] = __float_as_int(wr[kWsCand + 3]);
-        res = 0;
+#pragma unroll
+      for (int c = 0; c < kCand; ++c) {
+        if (res && a[c] < lim) {   // the first accepted candidate is the sample
+          out_tokens[row] = __float_as_int(wr[kWsCand + 2 * c + 1]);
+          res = 0;
+        }
       }
       sh.winner = res;
     }
@@ -224,7 +228,7 @@ __global__ __launch_bounds__(kSampThreads) void sample_kernel(
     __syncthreads();
     if (fl == 0) return;
   }
-  const int r0 = fl == 1 ? 2 : 0;
+  const int r0 = fl == 1 ? kCand : 0;
   const int tid = threadIdx.x;
   const T* x = logits + (long)row * logit_stride;
   const uint32_t* mrow = allow_mask ? allow_mask + (long)row * mask_words : nullptr;
@@ -465,7 +469,7 @@ __global__ __launch_bounds__(kSampThreads) void sample_kernel(
 //   K1 slice stats     (rows x kSlices): argmax key / id, and the slice's mass
 //                      Z_p = sum exp2((x - M_p) c) relative to its own max M_p
 //   K2 draw            (rows): M, Z = sum Z_p 2^((M_p - M) c); greedy rows end
-//                      here; two inverse-CDF candidates (uniforms u0, u1 of the
+//                      here; kCand inverse-CDF candidates (uniforms u0..u3 of the
 //                      same splitmix64 stream): slice by the prefix of the Z_p,
 //                      then the id inside that slice (one pass over 1/kSlices)
 //   K3 above-mass      (rows x kSlices): per slice, the mass of ids strictly more
@@ -473,8 +477,8 @@ __global__ __launch_bounds__(kSampThreads) void sample_kernel(
 //   accept             (sample_kernel's first step, rows): candidate r is in the
 //                      nucleus iff its above-mass < top_p * Z; the first accepted
 //                      one is the sample
-// A row whose two candidates are both rejected (probability (1 - top_p)^2) is
-// finished by the one-workgroup kernel on uniforms 2.. (independent of u0, u1,
+// A row whose kCand candidates are all rejected (probability (1 - top_p)^kCand) is
+// finished by the one-workgroup kernel on uniforms kCand.. (independent of u0..u3,
 // so the mixture is exactly the renormalised nucleus); top-k rows go there too.
 
 
@@ -714,10 +718,11 @@ __global__ __launch_bounds__(kSampThreads) void samp_draw_kernel(
     const int* __restrict__ steps, const uint32_t* __restrict__ allow_mask, int mask_words,
     float* __restrict__ ws) {
   static_assert(kSlices <= 64, "one lane per slice");
-  constexpr int HALF = kSampThreads / 2;   // candidate r is searched by threads [r * HALF, ...)
-  __shared__ float s_scan[2][HALF / 64];
-  __shared__ float s_M, s_cexp, s_tgt[2];
-  __shared__ int s_ps[2], s_done, s_last[2], s_found[2];
+  // top-p rows: candidate r is searched by threads [r * per, (r + 1) * per), per = kSampThreads /
+  // kCand; without a nucleus only candidate 0 is drawn, by the whole workgroup
+  __shared__ float s_scan[kSampThreads / 64];
+  __shared__ float s_M, s_cexp, s_tgt[kCand];
+  __shared__ int s_ps[kCand], s_done, s_last[kCand], s_found[kCand];
   const int row = blockIdx.x, tid = threadIdx.x, lane = lane_id();
   float* wr = ws + (long)row * kWsRow;
   int* flag = reinterpret_cast<int*>(wr + kWsFlag);
@@ -779,7 +784,7 @@ __global__ __launch_bounds__(kSampThreads) void samp_draw_kernel(
       const uint64_t s0 =
           splitmix64((uint64_t)seeds[row] ^ (0x632BE59BD9B4E019ull * (uint64_t)(steps[row] + 1)));
 #pragma unroll
-      for (int r = 0; r < 2; ++r) {
+      for (int r = 0; r < kCand; ++r) {
         const uint64_t h = splitmix64(s0 + (uint64_t)r * 0xD1B54A32D192ED03ull);
         const float u = ((float)(h >> 40) + 0.5f) * (1.0f / 16777216.0f);
         const float T0 = u * Z;
@@ -800,23 +805,25 @@ __global__ __launch_bounds__(kSampThreads) void samp_draw_kernel(
         s_done = 0;
         wr[kWsMZ] = M;
         wr[kWsMZ + 1] = Z;
-        wr[kWsCand] = __uint_as_float(bestk);   // defined even if a search finds nothing
-        wr[kWsCand + 1] = __int_as_float(besti);
-        wr[kWsCand + 2] = __uint_as_float(bestk);
-        wr[kWsCand + 3] = __int_as_float(besti);
+#pragma unroll
+        for (int c = 0; c < kCand; ++c) {   // defined even if a search finds nothing
+          wr[kWsCand + 2 * c] = __uint_as_float(bestk);
+          wr[kWsCand + 2 * c + 1] = __int_as_float(besti);
+        }
       }
     }
   }
-  if (tid < 2) {
+  if (tid < kCand) {
     s_last[tid] = -1;
     s_found[tid] = 0;
   }
   __syncthreads();
   if (s_done) return;
-  // inverse CDF inside the chosen slice, both candidates at once (one half each),
+  // inverse CDF inside the chosen slice, all candidates at once (kSampThreads / kCand each),
   // in (thread, chunk, id) order; the first chunk's keys stay in registers
-  const int r = tid / HALF, lt = tid - r * HALF, w = lt >> 6;
-  const bool active = r == 0 || tp < 1.f;
+  const int per = tp < 1.f ? kSampThreads / kCand : kSampThreads;
+  const int r = tid / per, lt = tid - r * per, w = lt >> 6;
+  float* scan = s_scan + r * (per >> 6);
   const float M = s_M, cexp = s_cexp, tgt = s_tgt[r];
   const int S = slice_len(vocab);
   const int beg = s_ps[r] * S, end = min(vocab, beg + S);
@@ -825,10 +832,10 @@ __global__ __launch_bounds__(kSampThreads) void samp_draw_kernel(
   uint32_t k0[8];
   float mass = 0.f;
   {
-    load_keys8<T>(x, mrow, active && beg + lt * 8 < end ? beg + lt * 8 : vocab, vocab, k0);
+    load_keys8<T>(x, mrow, beg + lt * 8 < end ? beg + lt * 8 : vocab, vocab, k0);
 #pragma unroll
     for (int j = 0; j < 8; ++j) mass += k0[j] > kNegInfKey ? exp2f((key_to_f32(k0[j]) - M) * cexp) : 0.f;
-    for (int b2 = beg + (lt + HALF) * 8; active && b2 < end; b2 += HALF * 8) {
+    for (int b2 = beg + (lt + per) * 8; b2 < end; b2 += per * 8) {
       uint32_t key[8];
       load_keys8<T>(x, mrow, b2, vocab, key);
 #pragma unroll
@@ -841,13 +848,13 @@ __global__ __launch_bounds__(kSampThreads) void samp_draw_kernel(
     const float y = __shfl_up(incl, o, 64);
     if (lane >= o) incl += y;
   }
-  if (lane == 63) s_scan[r][w] = incl;
+  if (lane == 63) scan[w] = incl;
   if (mass > 0.f) atomicMax(&s_last[r], lt);
   __syncthreads();
   float wbase = 0.f;
-  for (int w2 = 0; w2 < w; ++w2) wbase += s_scan[r][w2];
+  for (int w2 = 0; w2 < w; ++w2) wbase += scan[w2];
   const float excl = wbase + incl - mass;
-  const bool mine = active && mass > 0.f &&
+  const bool mine = mass > 0.f &&
                     ((tgt >= excl && tgt < excl + mass) || (lt == s_last[r] && tgt >= excl + mass));
   if (mine) {
     float a = excl;
@@ -869,7 +876,7 @@ __global__ __launch_bounds__(kSampThreads) void samp_draw_kernel(
       }
     };
     walk(k0, beg + lt * 8);
-    for (int b2 = beg + (lt + HALF) * 8; pick < 0 && b2 < end; b2 += HALF * 8) {
+    for (int b2 = beg + (lt + per) * 8; pick < 0 && b2 < end; b2 += per * 8) {
       uint32_t key[8];
       load_keys8<T>(x, mrow, b2, vocab, key);
       walk(key, b2);
@@ -906,25 +913,29 @@ __global__ __launch_bounds__(kSlThreads) void samp_above_kernel(
   const uint32_t* mrow = allow_mask ? allow_mask + (long)row * mask_words : nullptr;
   const float M = wr[kWsMZ];
   const float cexp = 1.4426950408889634f / temperature[row];
-  const uint32_t k0 = __float_as_uint(wr[kWsCand]), k1 = __float_as_uint(wr[kWsCand + 2]);
+  uint32_t kc[kCand], kmin = 0xffffffffu;
+#pragma unroll
+  for (int c = 0; c < kCand; ++c) {
+    kc[c] = __float_as_uint(wr[kWsCand + 2 * c]);
+    kmin = min(kmin, kc[c]);
+  }
   const int S = slice_len(vocab);
   const int beg = p * S, end = min(vocab, beg + S);
-  float a0 = 0.f, a1 = 0.f;
+  float a[kCand] = {};
   for (int base = beg + threadIdx.x * 8; base < end; base += kSlThreads * 8) {
     uint32_t key[8];
     load_keys8<T>(x, mrow, base, vocab, key);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const float e = key[j] > k1 || key[j] > k0 ? exp2f((key_to_f32(key[j]) - M) * cexp) : 0.f;
-      a0 += key[j] > k0 ? e : 0.f;
-      a1 += key[j] > k1 ? e : 0.f;
+      const float e = key[j] > kmin ? exp2f((key_to_f32(key[j]) - M) * cexp) : 0.f;
+#pragma unroll
+      for (int c = 0; c < kCand; ++c) a[c] += key[j] > kc[c] ? e : 0.f;
     }
   }
-  a0 = wg_sum(a0, sf);
-  a1 = wg_sum(a1, sf);
-  if (threadIdx.x == 0) {
-    wr[kWsAbove + 2 * p] = a0;
-    wr[kWsAbove + 2 * p + 1] = a1;
+#pragma unroll
+  for (int c = 0; c < kCand; ++c) {
+    a[c] = wg_sum(a[c], sf);
+    if (threadIdx.x == 0) wr[kWsAbove + kCand * p + c] = a[c];
   }
 }
 
