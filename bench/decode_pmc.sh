@@ -13,3 +13,4 @@ timeout -s KILL 170 rocprofv3 --pmc WRITE_SIZE SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_C
 for d in a b; do
   python3 $R/bench/pmc_summary.py $(find $O/$d -name "*.db") --match=ft:: > $O/$d.txt || exit $?
 done
+rm -rf $O/a $O/b   # the databases exceed what gpurun copies back; the summaries stay
