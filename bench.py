@@ -329,6 +329,7 @@ def main():
     p = lambda q: ttfts[min(len(ttfts) - 1, int(round(q * (len(ttfts) - 1))))] if ttfts else 0.0  # noqa
     value = tokens / t_max
     metrics = engine.engine.metrics()
+    ctx = _timed_ctx(m_before, metrics)
     mlabel = _model_label(a.model)
     if rank == 0:
         out = {
@@ -351,7 +352,11 @@ def main():
             "data": f"synthetic (random-init {mlabel} weights, synthetic English prompts, "
                     "synthetic Llama-3 tokenizer)",
             "config": {"model": mlabel, "global_batch": a.sessions * world,
-                       "seq_len": engine.engine.max_model_len, "parallelism": f"dp{world}",
+                       # measured context: mean tokens a decode row attended over in the
+                       # timed turns (max_model_len is the engine's cap, not the workload)
+                       "seq_len": ctx["ctx_mean"], "ctx_mean": ctx["ctx_mean"],
+                       "ctx_max": ctx["ctx_max"], "max_model_len": engine.engine.max_model_len,
+                       "parallelism": f"dp{world}",
                        "sessions_per_gpu": a.sessions, "tokens_per_turn": a.gen,
                        "path": "ws/llm -> " + ("direct engine" if a.no_agent else "voice agent") +
                                " -> in-process engine"},
@@ -403,6 +408,16 @@ def main():
         pass
     loop.call_soon_threadsafe(loop.stop)
     engine.shutdown()
+
+
+def _timed_ctx(before, after):
+    """Mean / max context (tokens attended over) of the decode rows between two engine
+    metric snapshots (engine counters; ctx_max is the run's longest, reached in the
+    timed turns since histories only grow)."""
+    rows = after.get("ctx_rows", 0) - before.get("ctx_rows", 0)
+    toks = after.get("ctx_tokens", 0) - before.get("ctx_tokens", 0)
+    return {"ctx_mean": round(toks / rows, 1) if rows > 0 else None,
+            "ctx_max": after.get("ctx_max") if rows > 0 else None}
 
 
 def _timed_decode_ms(before, after):
@@ -525,6 +540,7 @@ def bench_tp(a, rank: int, world: int, local_rank: int):
         cmd(("run", a.warmup))
     sync()
     hb["phase"] = "timed turns"
+    m0 = eng.metrics()
     t0 = time.perf_counter()
     res = cmd(("run", a.steps))
     sync()
@@ -544,6 +560,7 @@ def bench_tp(a, rank: int, world: int, local_rank: int):
     client.join(timeout=30)
     summ = summarize(res)
     metrics = eng.metrics()
+    ctx = _timed_ctx(m0, metrics)
     value = res["tokens"] / elapsed
     out = {
         "metric": "output tokens/sec (node) + p50 TTFT over WebSocket, "
@@ -554,7 +571,9 @@ def bench_tp(a, rank: int, world: int, local_rank: int):
         "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
         "dtype": ("w4a16 (bf16 compute)" if a.quant else "bf16") if a.device == "cuda" else "fp32",
         "data": "synthetic (random-init weights, synthetic English prompts, synthetic Llama-3 tokenizer)",
-        "config": {"model": a.model, "global_batch": a.sessions, "seq_len": eng.max_model_len,
+        "config": {"model": a.model, "global_batch": a.sessions,
+                   "seq_len": ctx["ctx_mean"], "ctx_mean": ctx["ctx_mean"], "ctx_max": ctx["ctx_max"],
+                   "max_model_len": eng.max_model_len,
                    "parallelism": f"tp{world}", "custom_allreduce": a.custom_allreduce},
         "p50_ttft_ms": summ.get("p50_ttft_ms"), "p99_ttft_ms": summ.get("p99_ttft_ms"),
         "frames": res.get("frames", 0),

@@ -375,6 +375,7 @@ class LLMEngine:
         self.stats["decode_ms_sum"] += 1e3 * dt
         self.stats["decode_steps"] += 1
         self.stats["pipelined_steps"] += 1
+        self._count_ctx(batch.decode_seqs)
         hp = self.host_prof
         hp["launch_next"] += tl - t0
         hp["collect"] += t1 - tl
@@ -405,6 +406,22 @@ class LLMEngine:
         finally:
             self._profiler.after_step()
 
+    def _count_ctx(self, seqs):
+        """Decode-step context counters: rows, tokens attended over, longest context
+        (bench.py reports the measured mean / max context of the timed turns)."""
+        st = self.stats
+        m = 0
+        tot = 0
+        for q in seqs:
+            c = q.n_tokens
+            tot += c
+            if c > m:
+                m = c
+        st["ctx_rows"] += len(seqs)
+        st["ctx_tokens"] += tot
+        if m > st["ctx_max"]:
+            st["ctx_max"] = m
+
     def reset_inflight(self):
         """Forget the queued steps (after a failed step)."""
         for e in self._inflight:
@@ -412,6 +429,9 @@ class LLMEngine:
                 q.inflight = 0
                 q.drop_next = 0
         self._inflight = []
+        discard = getattr(self.runner, "discard_pending", None)
+        if discard is not None:
+            discard()
 
     def fail_unfinished(self, error: str, reset_cache: bool = False):
         """After a failed step: every unfinished sequence ends with an error and
@@ -492,6 +512,7 @@ class LLMEngine:
         self.step_times.append((batch.has_prefill, len(batch.decode_seqs), batch.total_tokens, dt))
         if not batch.has_prefill:
             self.stats["decode_ms_sum"] += 1e3 * dt
+            self._count_ctx(batch.decode_seqs)
         if self._trace_path:
             self._trace.append(("mixed" if batch.has_prefill else "decode", ts, t2,
                                 len(batch.decode_seqs), sum(batch.prefill_tokens),

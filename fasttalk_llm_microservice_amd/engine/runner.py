@@ -285,6 +285,7 @@ class ModelRunner:
         # tokens are known and only its sampler waits for the grammar masks
         self.graphs_split: Dict[int, tuple] = {}
         self._fwd_logits: Dict[int, torch.Tensor] = {}
+        self._pending_split: Optional["DecodeHandle"] = None   # forward queued, sampler not yet
         # ENGINE_GUIDED_PIPELINE=0: guided batches run one synchronous step at a time
         self.guided_pipeline = os.environ.get("ENGINE_GUIDED_PIPELINE", "1") != "0"
         self.graph_pool = None
@@ -399,6 +400,7 @@ class ModelRunner:
 
         Decode-only steps replay a hipGraph; steps that carry prefill chunks run
         eagerly as one mixed forward pass (decode rows first)."""
+        self._assert_no_pending_split("execute")
         if batch.has_prefill:
             if self._gaps is not None:
                 self._gaps.append([None, None])
@@ -636,6 +638,7 @@ class ModelRunner:
         self._graph_logits.clear()
         self.graphs_split.clear()
         self._fwd_logits.clear()
+        self._pending_split = None   # the in-flight step is discarded with its graphs
         if not self.comm.graph_safe():
             self.use_graphs = False
         for st in self.stg:
@@ -679,10 +682,13 @@ class ModelRunner:
         if ahead and rowmap is not None:
             gather = np.zeros(nb, dtype=np.int64)   # padding rows read row 0 (ignored)
             gather[:n] = rowmap
+        self._assert_no_pending_split("decode_launch")
         if defer_sample:
             assert self.can_defer_sample()
             self._decode_enqueue(st, nb, n, from_device=bool(ahead), gather=gather, fwd_only=True)
-            return DecodeHandle(st, n, nb, pending=True)
+            h = DecodeHandle(st, n, nb, pending=True)
+            self._pending_split = h
+            return h
         if self.bcast is not None:
             self.bcast.send(("graph", {"nb": nb, "n": n, "small": st.hs.copy(),
                                        "bt": st.hbt[:nb, :maxblk].copy(), "f32": st.hf.copy(),
@@ -703,14 +709,28 @@ class ModelRunner:
         defer_sample=True)`` queued: its allow-masks go up, the sampler graph reads
         the forward graph's logits, the ids land in ``d_out`` (the next step's
         inputs) and in the staging set's pinned copy."""
-        assert h.pending
+        assert h.pending and self._pending_split is h
         self._set_masks(masks, h.n)
         self.graphs_split[h.nb][1].replay()
+        self._pending_split = None
         st = h.stage
         st.h_out[:h.n].copy_(self.d_out[:h.n], non_blocking=True)
         st.err_armed = False
         st.event.record()
         h.pending = False
+
+    def discard_pending(self):
+        """Forget a deferred-sample step whose sampler will never be queued (the
+        engine dropped its in-flight steps after a failure)."""
+        self._pending_split = None
+
+    def _assert_no_pending_split(self, where: str):
+        """A split step's logits (``_fwd_logits``) live in the graph pool every graph
+        shares: nothing may be replayed or run between its forward and its sampler, or
+        that work can overwrite them before they are sampled."""
+        if self._pending_split is not None:
+            raise RuntimeError(f"{where}: a deferred-sample decode step is pending; "
+                               "sample_launch() must be queued first")
 
     def _set_masks(self, masks: Optional[np.ndarray], n: int):
         """Uploads the step's allow-masks into the graph's static mask rows (stream
@@ -750,6 +770,7 @@ class ModelRunner:
         sampled ids land in ``d_out`` (rows = ``batch.sampled_seqs()``) for the
         decode step queued next, and in a pinned host buffer for the collect.
         Single process only (no TP broadcast), no allow-masks."""
+        self._assert_no_pending_split("mixed_launch")
         host = self._mixed_host(batch)
         nd = host["nd"]
         self.stats["prefill_steps"] += 1
@@ -978,6 +999,7 @@ class ModelRunner:
         Nothing replays between a step's two halves (its sampler is queued before
         the next forward), so the pool may share their temporaries with every other
         graph; the logits stay allocated."""
+        self._assert_no_pending_split("split-graph capture")
         t0 = time.time()
         saved = (self.d_slots[:nb].clone(), self.d_seq_lens[:nb].clone())
         self.d_slots[:nb].fill_(-1)
@@ -1019,6 +1041,7 @@ class ModelRunner:
         inference mode, whichever path triggers it (pipelined launches run outside
         ``execute``): the CUDA generator's graph-safe RNG state is created by the
         first capture and must be of the same kind for every later one."""
+        self._assert_no_pending_split("graph capture")
         t0 = time.time()
         # inputs must be valid for the warm-up/capture run: no KV writes, empty contexts
         saved = (self.d_slots[:nb].clone(), self.d_seq_lens[:nb].clone())
@@ -1047,6 +1070,18 @@ class ModelRunner:
 
         return self._mixed(_SB(list(seqs), [], [], []), masks)
 
+    @staticmethod
+    def _warm_split_graphs() -> bool:
+        """Pre-capture the split (forward | sampler) graphs of pipelined guided decoding?
+        Guided rows come from grammar-constrained tool calls or JSON-schema requests.
+        ``ENGINE_WARM_SPLIT_GRAPHS`` decides when set; otherwise only a service with
+        guided tool calls on (``AGENT_GUIDED_TOOL_CALLS``) pays for them at start-up, and
+        any other deployment captures a bucket's pair on its first guided step."""
+        env = os.environ.get("ENGINE_WARM_SPLIT_GRAPHS")
+        if env is not None:
+            return env.strip().lower() not in ("0", "false", "no", "off", "")
+        return os.environ.get("AGENT_GUIDED_TOOL_CALLS", "false").strip().lower() == "true"
+
     def warmup(self, batch_sizes=None):
         """Pre-capture decode graphs (one per batch bucket, any context length) so
         serving never pays for a capture."""
@@ -1055,7 +1090,7 @@ class ModelRunner:
         if self.bcast is not None:
             self.bcast.send(("warmup", list(batch_sizes or self.graph_sizes), None))
         t0 = time.time()
-        split = self.can_defer_sample() and self.guided_pipeline
+        split = self.can_defer_sample() and self._warm_split_graphs()
         for b in batch_sizes or self.graph_sizes:
             b = self._bucket(b)
             if b is not None and b not in self.graphs:

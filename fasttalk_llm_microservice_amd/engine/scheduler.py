@@ -125,13 +125,17 @@ class Scheduler:
         if seq.background:
             self.background.append(seq)
             return
+        # SamplingParams.priority (opt-in, default 0; NativeHandler.stream_events(priority=)):
+        # a prompt of priority p > 0 is prefilled ahead of every waiting prompt of lower
+        # priority that has not started yet.  A chunked prefill in progress keeps its place,
+        # and so does a sequence re-queued by preemption (it was admitted before the new
+        # prompt arrived; jumping it again would starve it under memory pressure).
         pr = getattr(seq.params, "priority", 0)
         if pr > 0 and self.waiting:
-            # ahead of every lower-priority prompt that has not started its prefill (a
-            # chunked prefill in progress keeps its place)
             i = 0
             for i, q in enumerate(self.waiting):
-                if q.num_computed == 0 and getattr(q.params, "priority", 0) < pr:
+                if q.num_computed == 0 and q.preemptions == 0 and \
+                        getattr(q.params, "priority", 0) < pr:
                     break
             else:
                 i = len(self.waiting)

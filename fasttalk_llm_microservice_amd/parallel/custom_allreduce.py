@@ -48,7 +48,8 @@ class CustomAllReduce:
 
     def __init__(self, group, rank: int, world: int, device: torch.device,
                  max_bytes: int = 8 << 20, spin_budget: Optional[int] = None,
-                 two_shot_bytes: Optional[int] = None, max_blocks: Optional[int] = None):
+                 two_shot_bytes: Optional[int] = None, max_blocks: Optional[int] = None,
+                 shared_device: bool = False):
         from .. import ops
 
         if world not in self.SUPPORTED_WORLD:
@@ -62,15 +63,20 @@ class CustomAllReduce:
         self.max_blocks = int(max_blocks)
         self._C.custom_ar_set_max_blocks(self.max_blocks)
         self.max_bytes = int(max_bytes)
+        # spin budgets: ~0.19 us per spin on a GPU of its own.  Ranks on separate GPUs
+        # declare a missing peer dead after 2^23 spins (~1.6 s) and give the group's
+        # first steps (lazy library / code-object loads, allocator growth on one rank
+        # while the others already wait) 2^26 (~13 s).  Ranks time-sharing ONE device
+        # (tests / rehearsals: 0.36 us per spin at 8 ranks, and a peer may not be
+        # scheduled for seconds) get 2^25 / 2^28.
+        self.shared_device = bool(shared_device)
+        default_spin, default_first = (1 << 25, 1 << 28) if shared_device else (1 << 23, 1 << 26)
         if spin_budget is None:
-            # 0.19 us per spin with 2 ranks, 0.36 us with 8 ranks sharing one MI355X:
-            # 2^25 spins = 6-12 s before a missing peer is declared dead
-            spin_budget = int(os.environ.get("ENGINE_CUSTOM_AR_SPIN", str(1 << 25)))
+            spin_budget = int(os.environ.get("ENGINE_CUSTOM_AR_SPIN", str(default_spin)))
         self.spin_budget = int(spin_budget)
-        # the group's first steps (lazy library / code-object loads, allocator growth on
-        # one rank while the others already wait) get a budget of minutes: long_waits()
         self.first_spin_budget = max(self.spin_budget,
-                                     int(os.environ.get("ENGINE_CUSTOM_AR_SPIN_FIRST", str(1 << 28))))
+                                     int(os.environ.get("ENGINE_CUSTOM_AR_SPIN_FIRST",
+                                                        str(default_first))))
         if two_shot_bytes is None:
             env = os.environ.get("ENGINE_CUSTOM_AR_TWO_SHOT")
             two_shot_bytes = int(env) if env else {8: 512 << 10, 4: 1 << 20}.get(world, 1 << 62)

@@ -88,7 +88,8 @@ def _maybe_custom_ar(cfg, comm: TPComm, device: str):
         # CUs the last rank computes on -- cap their grids at 16 workgroups
         ar = CustomAllReduce(comm.group, comm.rank, comm.world_size,
                              torch.device("cuda", torch.cuda.current_device()),
-                             max_blocks=16 if getattr(cfg, "tp_share_device", False) else None)
+                             max_blocks=16 if getattr(cfg, "tp_share_device", False) else None,
+                             shared_device=bool(getattr(cfg, "tp_share_device", False)))
     except Exception as e:  # e.g. IPC mapping refused: the group stays on RCCL
         log.warning("custom all-reduce unavailable on rank %d: %s", comm.rank, e)
         ok = 0

@@ -7,10 +7,9 @@
 set -euo pipefail
 cd "$(dirname "$0")"
 [ -f .env.remote ] || cp .env.remote.example .env.remote
-# variables given on the command line win over the file
-overrides=$(env | grep -E '^(LLM_PROVIDER|VLLM_BASE_URL|VLLM_MODEL|OLLAMA_BASE_URL|LLM_PORT)=' || true)
-set -a; source .env.remote; set +a
-while IFS= read -r kv; do [ -n "$kv" ] && export "$kv"; done <<< "$overrides"
+# variables given on the command line win over the file (load_env_file keeps them)
+source scripts/load_env.sh
+load_env_file .env.remote
 export COMPUTE_DEVICE=cpu
 # the launcher verifies the backend before serving and exits 1 if it is unreachable
 exec python main.py websocket "$@"

@@ -7,7 +7,8 @@
 set -euo pipefail
 cd "$(dirname "$0")"
 [ -f .env ] || cp .env.example .env
-set -a; source .env; set +a
+source scripts/load_env.sh
+load_env_file .env
 export COMPUTE_DEVICE=${COMPUTE_DEVICE:-rocm} HSA_ENABLE_IPC_MODE_LEGACY=0 PYTORCH_ROCM_ARCH=gfx950
 python -m fasttalk_llm_microservice_amd.ops.build
 exec python main.py websocket "$@"

@@ -40,7 +40,7 @@ def _worker(rank, world, port, q):
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
                             world_size=world)
     ar = CustomAllReduce(dist.group.WORLD, rank, world, torch.device("cuda:0"),
-                         max_bytes=1 << 20, spin_budget=1 << 24)
+                         max_bytes=1 << 20, spin_budget=1 << 24, shared_device=True)
     errs = []
     for trial, n in enumerate([64 * 4096, 8 * 4096, 4096, 50 * 4096]):
         xs = _inputs(trial, world, n)

@@ -619,3 +619,21 @@ def test_priority_prompts_prefill_first():
     sch.add(mk("t2", 1))
     sch.add(mk("c"))
     assert [q.request_id for q in sch.waiting] == ["a", "t1", "t2", "b", "c"]
+
+
+def test_priority_does_not_jump_preempted_sequences():
+    """A sequence re-queued by recompute preemption (num_computed back to 0) keeps its
+    place in front of a later high-priority prompt."""
+    from fasttalk_llm_microservice_amd.engine.scheduler import Scheduler
+    from fasttalk_llm_microservice_amd.engine.sequence import Sequence
+    from fasttalk_llm_microservice_amd.runtime import rt
+
+    bm = rt().BlockManager(64, 4, True)
+    sch = Scheduler(bm, 4, 8, 256, 512)
+    mk = lambda rid, pr=0: Sequence(rid, [1, 2, 3], SamplingParams(max_tokens=4, priority=pr))  # noqa
+    victim, fresh = mk("victim"), mk("fresh")
+    victim.preemptions = 1      # preempted once, re-queued with num_computed == 0
+    sch.add(victim)
+    sch.add(fresh)
+    sch.add(mk("t", 1))
+    assert [q.request_id for q in sch.waiting] == ["victim", "t", "fresh"]
