@@ -227,12 +227,18 @@ class AiohttpASGIServer:
                 self._lifespan_task.cancel()
 
     # ------------------------------------------------------------------ run
-    async def start(self):
+    async def start(self, listen: bool = True):
+        """``listen=False``: set the server up without a listening socket; connections
+        accepted elsewhere (the DP front door, app/server/front_door.py) are adopted
+        with ``loop.connect_accepted_socket(self.protocol_factory(), sock=...)``."""
         await self._lifespan_startup()
         web_app = web.Application(client_max_size=self.max_msg_size)
         web_app.router.add_route("*", "/{tail:.*}", self._dispatch)
         self._runner = web.AppRunner(web_app, access_log=None, handle_signals=False)
         await self._runner.setup()
+        if not listen:
+            logger.info("serving adopted connections (no listening socket)")
+            return
         site = web.TCPSite(self._runner, self.host, self.port, reuse_address=True,
                            reuse_port=self.reuse_port or None)
         await site.start()
@@ -242,6 +248,11 @@ class AiohttpASGIServer:
                 if srv is not None and srv.sockets:
                     self.port = srv.sockets[0].getsockname()[1]
         logger.info("serving on %s:%s", self.host, self.port)
+
+    def protocol_factory(self):
+        """aiohttp's low-level server (a protocol factory) once ``start`` ran."""
+        assert self._runner is not None and self._runner.server is not None
+        return self._runner.server
 
     async def stop(self):
         if self._runner is not None:

@@ -35,7 +35,10 @@ from typing import Any, Dict, List, Optional
 
 import numpy as np
 
-FIELDS = ("alive", "ready", "pid", "heartbeat", "active", "restarts", "backend_ok", "started")
+# conns / recv: the front door's load signal (app/server/front_door.py) -- TCP connections
+# a worker currently holds, and connections it has received from the door in total
+FIELDS = ("alive", "ready", "pid", "heartbeat", "active", "restarts", "backend_ok", "started",
+          "conns", "recv")
 _F = {k: i for i, k in enumerate(FIELDS)}
 HEARTBEAT_S = 0.5          # snapshot + heartbeat period of a worker
 STALE_S = 5.0              # a worker whose heartbeat is older is reported down
@@ -99,6 +102,13 @@ class NodeBoard:
     def set(self, index: int, field: str, value: float):
         self.t[index, _F[field]] = float(value)
 
+    def get(self, index: int, field: str) -> float:
+        return float(self.t[index, _F[field]])
+
+    def add(self, index: int, field: str, delta: float):
+        """Single-writer counter update (each worker owns its row's conns / recv)."""
+        self.t[index, _F[field]] += delta
+
     def beat(self, index: int, backend_ok: bool):
         self.t[index, _F["backend_ok"]] = 1.0 if backend_ok else 0.0
         self.t[index, _F["heartbeat"]] = time.time()
@@ -125,6 +135,8 @@ class NodeBoard:
         with self._locked():
             row = self.t[index]
             row[_F["active"]] = 0
+            row[_F["conns"]] = 0
+            row[_F["recv"]] = 0
             row[_F["ready"]] = 0
             row[_F["backend_ok"]] = 0
             row[_F["heartbeat"]] = 0
@@ -139,6 +151,7 @@ class NodeBoard:
             row[_F["alive"]] = 0
             row[_F["ready"]] = 0
             row[_F["active"]] = 0   # its sockets died with it
+            row[_F["conns"]] = 0
 
     # ------------------------------------------------------------------ queries
     def workers(self, now: Optional[float] = None) -> List[Dict[str, Any]]:
@@ -151,6 +164,7 @@ class NodeBoard:
                         "ready": bool(r[_F["ready"]]), "heartbeat_fresh": bool(fresh),
                         "backend_ok": bool(r[_F["backend_ok"]]),
                         "active_connections": int(r[_F["active"]]),
+                        "open_sockets": int(r[_F["conns"]]),
                         "restarts": int(r[_F["restarts"]])})
         return out
 

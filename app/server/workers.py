@@ -4,10 +4,13 @@
 provider): the launcher starts N worker processes.  Worker i owns GPUs
 [i*tp, (i+1)*tp) and runs the whole stack -- the FastAPI ``/ws/llm`` app on the
 aiohttp ASGI transport, the session / conversation managers, the voice agent and
-an in-process engine -- and every worker listens on the service port with
-``SO_REUSEPORT``, so the kernel spreads incoming connections over them.  A
-WebSocket session lives on the worker that accepted it, which is also where its
-KV cache (multi-turn prefix reuse) lives: session affinity comes for free.
+an in-process engine.  The parent's front door (``app/server/front_door.py``,
+``ENGINE_DP_FRONT=door``, the default) accepts every connection on the service port
+and hands its file descriptor to the least-loaded ready worker; with
+``ENGINE_DP_FRONT=reuseport`` every worker listens on the port with
+``SO_REUSEPORT`` and the kernel's hash places connections instead.  A WebSocket
+session lives on the worker that received it, which is also where its KV cache
+(multi-turn prefix reuse) lives: session affinity comes for free.
 
 Why not one process in front of N engine replicas (``ENGINE_DP_MODE=router``,
 parallel/dp_router.py)?  Every token frame costs the service process tens of
@@ -43,6 +46,7 @@ import threading
 import time
 from typing import Dict, List, Optional
 
+from app.server.front_door import DoorWorker, FrontDoor, dp_front_mode
 from app.server.node_state import HEARTBEAT_S, NodeBoard
 
 log = logging.getLogger("fasttalk.workers")
@@ -95,10 +99,15 @@ def _publisher(board: NodeBoard, index: int, server, monitor, stop: threading.Ev
         stop.wait(HEARTBEAT_S)
 
 
+def worker_env(index: int, world: int, tp: int) -> Dict[str, str]:
+    """Environment of DP service worker ``index``: one engine (no nested DP) whose TP
+    group owns GPUs [index*tp, (index+1)*tp) (parallel/tp.py tp_device_index)."""
+    return {"ENGINE_DP_SIZE": "1", "ENGINE_DEVICE_BASE": str(index * max(1, tp)),
+            "FASTTALK_WORKER": f"{index}/{world}"}
+
+
 def _worker_main(index: int, world: int, host: str, port: int, tp: int, board_spec=None):
-    os.environ["ENGINE_DP_SIZE"] = "1"
-    os.environ["ENGINE_DEVICE_BASE"] = str(index * tp)
-    os.environ["FASTTALK_WORKER"] = f"{index}/{world}"
+    os.environ.update(worker_env(index, world, tp))
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     import asyncio
 
@@ -134,14 +143,31 @@ def _worker_main(index: int, world: int, host: str, port: int, tp: int, board_sp
         server.connection_manager.admission = _Gate(board, index)
         threading.Thread(target=_publisher, args=(board, index, server, monitor, stop),
                          name="fasttalk-node-publisher", daemon=True).start()
-    asgi = AiohttpASGIServer(server.app, host, port, reuse_port=True)
+    door = board is not None and dp_front_mode() == "door"
+    asgi = AiohttpASGIServer(server.app, host, port, reuse_port=not door)
 
     async def serve():
-        await asgi.start()
+        door_worker = None
+        if door:
+            # the parent's front door accepts and hands this worker its connections
+            await asgi.start(listen=False)
+            door_worker = DoorWorker(asgi, board, index)
+            await door_worker.start()
+        else:
+            await asgi.start()
         if board is not None:
             board.set(index, "ready", 1)
-        log.info("DP worker %d/%d serving on %s:%d", index, world, host, port)
+        log.info("DP worker %d/%d serving on %s:%d (%s)", index, world, host, port,
+                 "front door" if door else "SO_REUSEPORT")
         while True:
+            if door_worker is not None:
+                try:
+                    await asyncio.wait_for(door_worker.lost.wait(), 3600)
+                except asyncio.TimeoutError:
+                    continue
+                # the parent is gone: nothing can reach this worker any more
+                log.error("DP worker %d: front door closed; exiting", index)
+                return
             await asyncio.sleep(3600)
 
     try:
@@ -174,6 +200,10 @@ class WorkerPool:
         self.procs: List[Optional[mp.Process]] = [None] * world
         self.restarts: Dict[int, int] = {i: 0 for i in range(world)}
         self._stop = False
+        # ENGINE_DP_FRONT=door (default): one acceptor here places every connection on the
+        # least-loaded worker; reuseport: the workers share the port (kernel hash)
+        self.front_mode = dp_front_mode()
+        self.door: Optional[FrontDoor] = None
 
     def _spawn(self, i: int):
         p = self.ctx.Process(target=_worker_main,
@@ -184,6 +214,8 @@ class WorkerPool:
         self.board.worker_started(i, p.pid, self.restarts[i])
 
     def start(self) -> "WorkerPool":
+        if self.front_mode == "door":
+            self.door = FrontDoor(self.board, self.host, self.port).start()
         for i in range(self.world):
             self._spawn(i)
         return self
@@ -250,6 +282,9 @@ class WorkerPool:
                     p.kill()
         for i in range(self.world):
             self.board.worker_gone(i)
+        if self.door is not None:
+            self.door.stop()
+            self.door = None
 
     def close(self):
         self.board.close()

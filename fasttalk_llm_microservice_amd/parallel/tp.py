@@ -118,11 +118,18 @@ def worker_loop(cfg, comm: TPComm, bcast: ShmBroadcast):
         bcast.close()
 
 
+def tp_device_index(device_base: int, rank: int, share_device: bool = False) -> int:
+    """GPU of TP rank ``rank`` in a group whose first GPU is ``device_base`` (a DP
+    service worker i with TP size t owns GPUs [i*t, (i+1)*t): app/server/workers.py).
+    ``share_device``: every rank on ``device_base`` (tests / rehearsals)."""
+    return int(device_base) + (0 if share_device else int(rank))
+
+
 def _spawned_worker(rank: int, world: int, port: int, bcast_name: str, cfg, device: str,
                     device_base: int):
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     _exit_with_parent(f"TP worker {rank}")
-    dev_index = device_base + (0 if cfg.tp_share_device else rank)
+    dev_index = tp_device_index(device_base, rank, cfg.tp_share_device)
     _set_device(device, dev_index)
     kw = {}
     if device == "cuda" and not cfg.tp_share_device:
@@ -158,10 +165,11 @@ class TPGroup:
                                   device_base))
             p.start()
             self.procs.append(p)
-        _set_device(self.device, device_base)
+        dev0 = tp_device_index(device_base, 0, cfg.tp_share_device)
+        _set_device(self.device, dev0)
         kw = {}
         if self.device == "cuda" and not cfg.tp_share_device:
-            kw["device_id"] = torch.device(f"cuda:{device_base}")
+            kw["device_id"] = torch.device(f"cuda:{dev0}")
         dist.init_process_group(_backend(self.device, cfg),
                                 init_method=f"tcp://127.0.0.1:{self.port}",
                                 rank=0, world_size=self.world, **kw)

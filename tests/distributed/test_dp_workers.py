@@ -1,7 +1,8 @@
 """DP serving as N service worker processes on one port (app/server/workers.py,
-ENGINE_DP_MODE=workers): sessions over SO_REUSEPORT reach every worker, each
-streams from its own engine, and a killed worker is restarted and serves again.
-CPU only: the engines use the synthetic runner (ENGINE_SYNTHETIC_STEP_MS)."""
+ENGINE_DP_MODE=workers): the parent's front door (app/server/front_door.py) places
+every session on the least-loaded worker, each streams from its own engine, and a
+killed worker is restarted and serves again.  CPU only: the engines use the
+synthetic runner (ENGINE_SYNTHETIC_STEP_MS)."""
 import asyncio
 import os
 import socket
@@ -68,8 +69,9 @@ def test_dp_workers_share_one_port_and_restart(monkeypatch):
                     for p in pool.procs]
         r = _sessions(port, 16, probe=per_worker)
         assert r["turns"] == 16 and r["tokens"] == 16 * 6
-        # SO_REUSEPORT spread the connections over both workers
-        assert sum(r["probe"]) == 16 and min(r["probe"]) >= 1, r["probe"]
+        # the front door balanced the sessions: 8 + 8, every run
+        assert r["probe"] == [8, 8], r["probe"]
+        assert pool.door is not None and pool.door.stats["per_worker"][0] >= 8
         victim = pool.procs[0]
         victim.kill()
         victim.join(10)
@@ -168,7 +170,8 @@ def test_dp_workers_behave_as_one_service(monkeypatch):
         m = ms.get("/metrics").get_json()
         assert m["generations"] == 8 and m["total_tokens_generated"] == 8 * 6, m
         per = [w["generations"] for w in m["workers"]]
-        assert sum(per) == 8 and min(per) >= 1, per
+        # 4 sessions x 2 turns placed by the front door: 2 sessions per worker
+        assert per == [4, 4], per
         st, stats = _http_json(port, "/stats")
         assert stats["connections"]["total_generations_completed"] == 8
         assert b"fasttalk_worker_ready" in ms.get("/metrics/prometheus").data
@@ -209,3 +212,91 @@ def test_dp_worker_startup_check_fails_before_serving(monkeypatch):
     finally:
         pool.stop()
         pool.close()
+
+
+def test_dp_tp_workers_own_disjoint_gpu_ranges():
+    """DP x TP: worker i's TP group starts at GPU i*tp (ENGINE_DEVICE_BASE, read by
+    AsyncEngine.from_config) and its ranks take the next tp GPUs; the workers of an
+    8-GPU node partition it."""
+    from app.server.workers import worker_env
+    from fasttalk_llm_microservice_amd.parallel.tp import tp_device_index
+
+    for dp, tp in ((8, 1), (4, 2), (2, 4), (1, 8)):
+        owned = []
+        for i in range(dp):
+            env = worker_env(i, dp, tp)
+            assert env["ENGINE_DP_SIZE"] == "1"
+            base = int(env["ENGINE_DEVICE_BASE"])
+            assert base == i * tp
+            devs = [tp_device_index(base, r) for r in range(tp)]
+            assert devs == list(range(i * tp, (i + 1) * tp))
+            owned += devs
+        assert sorted(owned) == list(range(8))
+    # ranks that share one device (rehearsals) all sit on the base
+    assert {tp_device_index(4, r, share_device=True) for r in range(4)} == {4}
+
+
+def test_front_door_balances_refuses_and_reroutes(tmp_path):
+    """The door alone, with fake workers on its control socket: least-loaded placement
+    (pending hand-offs count before a worker reports), 503 with no worker ready, and a
+    worker whose control socket died is routed around."""
+    import json
+    import socket as _s
+    import urllib.request
+
+    from app.server.front_door import FrontDoor
+    from app.server.node_state import NodeBoard
+
+    board = NodeBoard(3, 100)
+    door = FrontDoor(board, "127.0.0.1", 0).start()
+    ctl = []
+    try:
+        for i in range(3):
+            c = _s.socket(_s.AF_UNIX, _s.SOCK_SEQPACKET)
+            c.connect(door.ctl_path)
+            c.sendall(f"W{i}\n".encode())
+            ctl.append(c)
+            board.worker_started(i, 1000 + i, 0)
+        assert door.listening.wait(10)
+        port = door.port
+        # not ready yet: the door answers 503
+        with pytest.raises(urllib.error.HTTPError) as e:
+            urllib.request.urlopen(f"http://127.0.0.1:{port}/health", timeout=5)
+        assert e.value.code == 503 and json.loads(e.value.read())["status"] == "unavailable"
+        for i in range(3):
+            board.set(i, "ready", 1)
+        board.set(0, "conns", 5)          # worker 0 already busy
+        clients = [_s.create_connection(("127.0.0.1", port)) for _ in range(6)]
+        got = [[] for _ in range(3)]
+        deadline = time.time() + 10
+        while sum(map(len, got)) < 6 and time.time() < deadline:
+            for i, c in enumerate(ctl):
+                c.settimeout(0.05)
+                try:
+                    msg, fds, _, _ = _s.recv_fds(c, 16, 4)
+                except (TimeoutError, _s.timeout, BlockingIOError):
+                    continue
+                got[i] += fds
+        counts = [len(g) for g in got]
+        # nothing reported back yet: the six hand-offs split 0 / 3 / 3 (worker 0 had 5)
+        assert counts == [0, 3, 3], counts
+        for g in got:
+            for fd in g:
+                os.close(fd)
+        # worker 1 (the least loaded) loses its control socket: the door tries it, fails
+        # and routes the connection to worker 2 instead
+        board.set(2, "conns", 1)
+        ctl[1].close()
+        extra = _s.create_connection(("127.0.0.1", port))
+        time.sleep(0.5)
+        ctl[2].settimeout(2)
+        msg, fds, _, _ = _s.recv_fds(ctl[2], 16, 4)
+        assert len(fds) == 1 and door.stats["rerouted"] >= 1
+        os.close(fds[0])
+        for c in clients + [extra]:
+            c.close()
+    finally:
+        door.stop()
+        for c in ctl:
+            c.close()
+        board.close()
