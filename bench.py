@@ -163,6 +163,12 @@ def main():
     ap.add_argument("--device", default="cuda", help="cpu runs the same path over gloo (tests)")
     ap.add_argument("--quant", default="", choices=["", "w4", "awq"],
                     help="W4A16 layer weights (the reference's AWQ-INT4 model); default bf16")
+    ap.add_argument("--serve", choices=["door", "rank"], default="door",
+                    help="DP topology: 'door' (default) = the shipping ENGINE_DP_SIZE service: every "
+                         "rank is a service worker behind ONE port whose front door (rank 0, "
+                         "app/server/front_door.py) places each new session on the least-loaded "
+                         "worker, and every rank's load generator connects to that port; 'rank' = "
+                         "each rank serves its own port to its own load generator")
     ap.add_argument("--agent-tools", type=float, default=-1.0, metavar="FRAC",
                     help="BASELINE config 5: agent with JSON-guided tool calls, FRAC of the turns "
                          "ask for a web search (stub backend); e.g. 0.2")
@@ -208,7 +214,10 @@ def main():
     os.environ["LLM_PROVIDER"] = "native"
     os.environ["ENGINE_MODEL"] = a.model
     os.environ["ENABLE_PYDANTIC_AI"] = "false" if a.no_agent else "true"
-    os.environ.setdefault("LLM_MAX_CONNECTIONS", str(max(64, a.sessions + 8)))
+    door = a.serve == "door"
+    # door: one node-wide cap on the board (sessions may land on any worker)
+    os.environ.setdefault("LLM_MAX_CONNECTIONS",
+                          str(max(64, a.sessions + 8) * (world if door else 1)))
     cpu = a.device == "cpu"
     if cpu:
         os.environ["COMPUTE_DEVICE"] = "cpu"
@@ -248,6 +257,26 @@ def main():
     asgi = AiohttpASGIServer(server.app, "127.0.0.1", port)
     loop = asyncio.new_event_loop()
     ready = threading.Event()
+    board = front = None
+    if door:
+        # the shipping DP service (app/server/workers.py + front_door.py): rank 0 owns the
+        # node board and the front door; every rank is one worker row on the board
+        from app.server.front_door import DoorWorker, FrontDoor
+        from app.server.node_state import NodeBoard
+        from app.server.workers import _Gate
+
+        spec = [None]
+        if rank == 0:
+            board = NodeBoard(world, int(os.environ["LLM_MAX_CONNECTIONS"]))
+            front = FrontDoor(board, "127.0.0.1", a.port or 0).start()
+            spec = [board.spec()]
+        if world > 1:
+            dist.broadcast_object_list(spec, src=0)
+        if board is None:
+            board = NodeBoard.attach(spec[0])
+        board.worker_started(rank, os.getpid(), 0)
+        server.connection_manager.admission = _Gate(board, rank)
+        server.node, server.node_index = board, rank
 
     # FT_BENCH_LOOP_PROFILE=<path>: cProfile of the service event-loop thread (the asyncio
     # loop that runs the WebSocket handlers and the voice agent), dumped after the timed turns
@@ -262,7 +291,13 @@ def main():
 
             loop_prof = cProfile.Profile()
             loop_prof.enable()
-        loop.run_until_complete(asgi.start())
+        if door:
+            loop.run_until_complete(asgi.start(listen=False))
+            loop.run_until_complete(DoorWorker(asgi, board, rank).start())
+            board.set(rank, "ready", 1)
+            board.beat(rank, True)
+        else:
+            loop.run_until_complete(asgi.start())
         ready.set()
         loop.run_forever()
 
@@ -270,6 +305,15 @@ def main():
     th.start()
     if not ready.wait(120):
         raise RuntimeError("server did not start")
+    if door:
+        url = [None]
+        if rank == 0:
+            if not front.listening.wait(60):
+                raise RuntimeError("front door did not open")
+            url = [f"ws://127.0.0.1:{front.port}/ws/llm"]
+        if world > 1:
+            dist.barrier()   # every worker registered with the door
+            dist.broadcast_object_list(url, src=0)
     init_s = time.time() - t_init
 
     def cmd(c):
@@ -279,7 +323,11 @@ def main():
             raise RuntimeError(f"load client failed: {r.get('error')}")
         return r.get("result")
 
+    if door:
+        cmd(("url", url[0]))
     cmd("open")
+    if door and world > 1:
+        dist.barrier()   # every rank's sessions are placed before any turn starts
     hb["phase"] = "warmup turns"
     if a.warmup > 0:
         cmd(("run", a.warmup))
@@ -298,6 +346,8 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     hb["done"] = True
+    # sessions this worker (rank) holds: the front door's placement
+    placed = int(board.get(rank, "active")) if door else a.sessions
     if loop_prof is not None:
         dumped = threading.Event()
 
@@ -313,6 +363,7 @@ def main():
 
     summ = summarize(res)
     local = {"tokens": res["tokens"], "frames": res.get("frames", 0), "elapsed": elapsed,
+             "placed": placed,
              "ttft": res["ttft_s"], "tool_ttft": res.get("tool_ttft_s", []),
              "server_ttft": res.get("server_ttft_ms", []),
              "engine_ttft": res.get("engine_ttft_ms", []),
@@ -351,6 +402,9 @@ def main():
             "dtype": ("w4a16 (bf16 compute)" if a.quant else "bf16") if not cpu else "fp32",
             "data": f"synthetic (random-init {mlabel} weights, synthetic English prompts, "
                     "synthetic Llama-3 tokenizer)",
+            "serve": ({"mode": "front door (one port, least-loaded placement)",
+                       "sessions_per_worker": [r["placed"] for r in allr]}
+                      if door else {"mode": "one port per rank"}),
             "config": {"model": mlabel, "global_batch": a.sessions * world,
                        # measured context: mean tokens a decode row attended over in the
                        # timed turns (max_model_len is the engine's cap, not the workload)
@@ -407,6 +461,10 @@ def main():
     except Exception:
         pass
     loop.call_soon_threadsafe(loop.stop)
+    if front is not None:
+        front.stop()
+    if board is not None:
+        board.close()
     engine.shutdown()
 
 

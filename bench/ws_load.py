@@ -168,6 +168,9 @@ def client_process(conn, url: str, sessions: int, cfg: Dict[str, Any], words: in
                 if cmd == "open":
                     loop.run_until_complete(lc.open())
                     conn.send({"ok": True})
+                elif isinstance(cmd, tuple) and cmd[0] == "url":   # before "open"
+                    lc.url = cmd[1]
+                    conn.send({"ok": True})
                 elif isinstance(cmd, tuple) and cmd[0] == "run":
                     conn.send({"ok": True, "result": loop.run_until_complete(lc.run_turns(cmd[1]))})
                 elif cmd == "close":

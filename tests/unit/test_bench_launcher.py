@@ -38,6 +38,9 @@ def test_gpus_flag_launches_ranks(mode):
     assert out["config"]["parallelism"] == ("tp2" if mode == "tp" else "dp2")
     if mode == "dp":
         assert out["config"]["global_batch"] == 4  # weak scaling: sessions per rank
+        # default DP topology: the shipping front door placed 2 sessions on each worker
+        assert out["serve"]["sessions_per_worker"] == [2, 2], out["serve"]
+    assert out["config"]["ctx_mean"] and out["config"]["ctx_max"] >= out["config"]["ctx_mean"]
 
 
 def test_world_size_mismatch_is_refused():
