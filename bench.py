@@ -80,8 +80,11 @@ def _launch_ranks(n: int, argv) -> int:
     env = dict(os.environ)
     shared = env.get("FT_BENCH_SHARED_GPU", "0") == "1"
     if shared and not env.get("ENGINE_GPU_MEMORY_UTILIZATION"):
-        # every rank's engine sizes its KV cache from the same device
+        # every rank's engine sizes its KV cache from the same device: a 1/n share each,
+        # counted against its own allocations only (the others may or may not have sized
+        # theirs yet)
         env["ENGINE_GPU_MEMORY_UTILIZATION"] = f"{0.85 / n:.3f}"
+        env.setdefault("ENGINE_KV_SIZING", "own")
     port = _free_port(29500 + (os.getpid() % 400))
     procs = []
     for r in range(n):
@@ -433,6 +436,7 @@ def main():
             "engine_decode_step_ms": _timed_decode_ms(m_before, metrics),
             "engine_decode_step_ms_last512": round(metrics.get("decode_step_ms_avg", 0.0), 3),
             "engine_decode_batch_avg": round(metrics.get("decode_batch_avg", 0.0), 2),
+            "kv_blocks": metrics.get("kv_blocks_total"),
             "engine_steps": {k: v for k, v in metrics.items() if k in
                              ("decode_steps", "pipelined_steps", "mixed_steps", "mixed_ahead", "pipeline_shrinks",
                               "mixed_ahead_drain")

@@ -377,7 +377,13 @@ class ModelRunner:
         elif self.is_gpu:
             free, total = torch.cuda.mem_get_info(self.device)
             reserve = 6 << 30  # activations (8k-token prefill), graphs, sampler workspace
-            budget = int(total * cfg.gpu_memory_utilization) - (total - free) - reserve
+            used = total - free
+            if os.environ.get("ENGINE_KV_SIZING", "device") == "own":
+                # several engines time-share this device (FT_BENCH_SHARED_GPU rehearsals):
+                # count only this process's allocations, so the pool does not depend on
+                # whether the other engines have sized theirs yet
+                used = torch.cuda.memory_reserved(self.device)
+            budget = int(total * cfg.gpu_memory_utilization) - used - reserve
             n = max(budget // per_block, 64)
         else:
             n = max(1024, (self.max_model_len // self.bs) * 4)
