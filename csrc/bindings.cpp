@@ -799,10 +799,45 @@ void slab_rope_kv(at::Tensor ws, int64_t splits, int64_t rows, int64_t cols, at:
                            cur_stream()), "slab_rope_kv");
 }
 
+#if defined(FT_KERNEL_CHECKS) && FT_KERNEL_CHECKS
+// checked build: every instrumented kernel unit's hook (ft_common.h FT_CHECK_HOOK)
+extern "C" {
+#define FT_HOOK_DECL(NAME) int ft_check_hook_##NAME(uint32_t*, int, int, int, int);
+FT_HOOK_DECL(attn_decode)
+FT_HOOK_DECL(attn_prefill)
+FT_HOOK_DECL(rope_kv)
+FT_HOOK_DECL(fused_epilogue)
+FT_HOOK_DECL(norm_act)
+FT_HOOK_DECL(sampling)
+FT_HOOK_DECL(kv_copy)
+#undef FT_HOOK_DECL
+}
+
+// word: int32 [4] device tensor (violations, first code, context, value)
+void set_kernel_checks(torch::Tensor word, int64_t num_blocks, int64_t block_size,
+                       int64_t cos_rows, int64_t vocab) {
+  TORCH_CHECK(word.is_cuda() && word.scalar_type() == at::kInt && word.numel() >= 4, "check word");
+  uint32_t* w = reinterpret_cast<uint32_t*>(word.data_ptr<int>());
+  const int nb = (int)num_blocks, bs = (int)block_size, cr = (int)cos_rows, v = (int)vocab;
+  using Hook = int (*)(uint32_t*, int, int, int, int);
+  const Hook hooks[] = {ft_check_hook_attn_decode, ft_check_hook_attn_prefill,
+                        ft_check_hook_rope_kv,     ft_check_hook_fused_epilogue,
+                        ft_check_hook_norm_act,    ft_check_hook_sampling,
+                        ft_check_hook_kv_copy};
+  for (Hook h : hooks) check_rc(h(w, nb, bs, cr, v), "set_kernel_checks");
+}
+#endif
+
 }  // namespace
 
-PYBIND11_MODULE(_C, m) {
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "FastTalk MI355X (gfx950) HIP kernels";
+#if defined(FT_KERNEL_CHECKS) && FT_KERNEL_CHECKS
+  m.attr("kernel_checks") = true;
+  m.def("set_kernel_checks", &set_kernel_checks);
+#else
+  m.attr("kernel_checks") = false;
+#endif
   m.def("rmsnorm", &rmsnorm);
   m.def("fused_add_rmsnorm", &fused_add_rmsnorm);
   m.def("silu_mul", &silu_mul);

@@ -122,3 +122,79 @@ inline int ceil_div(int a, int b) { return (a + b - 1) / b; }
     hipError_t _e = (expr);                                                  \
     if (_e != hipSuccess) return static_cast<int>(_e);                       \
   } while (0)
+
+// ---------------------------------------------------------------------------------
+// Checked kernel build (SURVEY §5 "bounds checks in debug builds"): ops/build.py
+// --checked compiles every kernel with -DFT_KERNEL_CHECKS=1 into _C_checked.so,
+// loaded when FT_KERNEL_CHECKS=1.  Index-taking kernels route block-table entries,
+// KV slots, rotary positions and token ids through ft_check_idx: an out-of-range
+// value is counted in a device error word (first violation: code + context + value,
+// and one printf per wave), then clamped to 0 so the kernel does not fault -- no
+// trap; the runner reads the word after every step and fails it loudly
+// (engine/runner.py, KernelCheckError).  Each translation unit holds its own copy of
+// the word pointer and the limits (kernels are not compiled -fgpu-rdc); the host sets
+// them through ft_check_hook_<unit> (FT_CHECK_HOOK at the end of each unit).  In the
+// release build all of this compiles to nothing.
+// ---------------------------------------------------------------------------------
+namespace ft {
+enum FtCheckCode : int {
+  kCkBlockTable = 1,   // paged attention: block-table entry >= num_blocks
+  kCkSlot = 2,         // KV write: slot >= num_blocks * block_size
+  kCkPosition = 3,     // RoPE: position >= rows of the cos/sin table
+  kCkTokenId = 4,      // embedding: input id >= vocab
+  kCkSampled = 5,      // sampler: sampled id >= vocab
+  kCkCopyBlock = 6,    // KV copy / swap: block id >= num_blocks
+};
+}  // namespace ft
+
+#if defined(FT_KERNEL_CHECKS) && FT_KERNEL_CHECKS
+namespace ft {
+struct FtCheckLimits {
+  int num_blocks;   // KV pool blocks (0: unknown, not checked)
+  int block_size;
+  int cos_rows;     // rows of the rotary cos/sin table
+  int vocab;
+};
+// [0] violations, [1] code of the first, [2] its context (row / token), [3] its value
+static __device__ uint32_t* ft_check_word;
+static __device__ FtCheckLimits ft_check_lim;
+
+__device__ __noinline__ static void ft_check_fail(int code, int ctx, int value) {
+  uint32_t* w = ft_check_word;
+  if (w == nullptr) return;
+  if (atomicAdd(w, 1u) == 0u) {
+    w[1] = static_cast<uint32_t>(code);
+    w[2] = static_cast<uint32_t>(ctx);
+    w[3] = static_cast<uint32_t>(value);
+    printf("[ft-check] kernel bounds violation: code %d ctx %d value %d (block %d thread %d)\n",
+           code, ctx, value, (int)blockIdx.x, (int)threadIdx.x);
+  }
+}
+
+// value if 0 <= value < limit (or the limit is unknown), else report and return 0
+__device__ __forceinline__ int ft_check_idx(int value, long limit, int code, int ctx) {
+  if (limit > 0 && (value < 0 || (long)value >= limit)) {
+    ft_check_fail(code, ctx, value);
+    return 0;
+  }
+  return value;
+}
+}  // namespace ft
+#define FT_LIM_BLOCKS ((long)::ft::ft_check_lim.num_blocks)
+#define FT_LIM_SLOTS ((long)::ft::ft_check_lim.num_blocks * (long)::ft::ft_check_lim.block_size)
+#define FT_LIM_COS ((long)::ft::ft_check_lim.cos_rows)
+#define FT_LIM_VOCAB ((long)::ft::ft_check_lim.vocab)
+#define FT_CHECK_IDX(v, lim, code, ctx) ::ft::ft_check_idx((v), (lim), (code), (ctx))
+#define FT_CHECK_HOOK(NAME)                                                                  \
+  extern "C" int ft_check_hook_##NAME(uint32_t* word, int num_blocks, int block_size,       \
+                                      int cos_rows, int vocab) {                            \
+    const ::ft::FtCheckLimits lim{num_blocks, block_size, cos_rows, vocab};                 \
+    hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(::ft::ft_check_word), &word, sizeof(word)); \
+    if (e == hipSuccess)                                                                    \
+      e = hipMemcpyToSymbol(HIP_SYMBOL(::ft::ft_check_lim), &lim, sizeof(lim));             \
+    return static_cast<int>(e);                                                             \
+  }
+#else
+#define FT_CHECK_IDX(v, lim, code, ctx) (v)
+#define FT_CHECK_HOOK(NAME)
+#endif

@@ -321,7 +321,7 @@ __global__ __launch_bounds__(256, WPC) void paged_decode_kernel(
       int my_blk = 0, my_off = 0;
       if (lane < cc) {
         const int tok = (t0 + c0 + lane) << 4;
-        my_blk = bt[tok >> bs_shift];
+        my_blk = FT_CHECK_IDX(bt[tok >> bs_shift], FT_LIM_BLOCKS, kCkBlockTable, b);
         my_off = tok & bmask;
       }
       auto ld = [&](MTile<D>& t, int i) {
@@ -621,3 +621,6 @@ extern "C" int ft_paged_decode_attention(void* out, int out_stride, float* tmp_o
 #undef FT_DEC_ARGS
   return -2;
 }
+
+// checked build: this unit's error-word / limits hook (ft_common.h)
+FT_CHECK_HOOK(attn_decode)

@@ -337,7 +337,8 @@ __global__ __launch_bounds__(512, 1) void prefill_attn_kernel(
   };
 
   // block-table entries of the KV range (LDS reads never wait on the DMA's vmcnt)
-  for (int i = threadIdx.x; i < nblk; i += blockDim.x) s_bt[i] = bt[i];
+  for (int i = threadIdx.x; i < nblk; i += blockDim.x)
+    s_bt[i] = FT_CHECK_IDX(bt[i], FT_LIM_BLOCKS, kCkBlockTable, b);
   __syncthreads();
 
 #pragma unroll
@@ -490,3 +491,6 @@ extern "C" int ft_prefill_attention(void* out, int out_stride, const void* q, in
 #undef FT_PF_CASE
   return -2;
 }
+
+// checked build: this unit's error-word / limits hook (ft_common.h)
+FT_CHECK_HOOK(attn_prefill)

@@ -151,8 +151,9 @@ __global__ __launch_bounds__(256) void slab_rope_kv_kernel(
   constexpr int HALF = D / 2;
   constexpr int CPH = HALF / 8;
   const int t = blockIdx.x;
-  const int pos = positions[t];
-  const int slot = slot_mapping[t];
+  const int pos = FT_CHECK_IDX(positions[t], FT_LIM_COS, kCkPosition, t);
+  int slot = slot_mapping[t];
+  if (slot >= 0) slot = FT_CHECK_IDX(slot, FT_LIM_SLOTS, kCkSlot, t);
   const float* cs = cos_sin + (size_t)pos * D;
   const int blk = slot >= 0 ? slot / block_size : 0;
   const int off = slot >= 0 ? slot - blk * block_size : 0;
@@ -311,3 +312,6 @@ extern "C" int ft_slab_rope_kv(const float* ws, int splits, int rows, int cols, 
   }
   return static_cast<int>(hipGetLastError());
 }
+
+// checked build: this unit's error-word / limits hook (ft_common.h)
+FT_CHECK_HOOK(fused_epilogue)

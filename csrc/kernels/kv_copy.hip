@@ -11,7 +11,8 @@ __global__ __launch_bounds__(256) void kv_block_copy_kernel(uint4* __restrict__ 
                                                             const int* __restrict__ pairs,
                                                             long vec_per_block) {
   const int p = blockIdx.y;
-  const long src = pairs[2 * p], dst = pairs[2 * p + 1];
+  const long src = FT_CHECK_IDX(pairs[2 * p], FT_LIM_BLOCKS, kCkCopyBlock, p);
+  const long dst = FT_CHECK_IDX(pairs[2 * p + 1], FT_LIM_BLOCKS, kCkCopyBlock, p);
   for (long i = blockIdx.x * 256L + threadIdx.x; i < vec_per_block; i += gridDim.x * 256L) {
     k_cache[dst * vec_per_block + i] = k_cache[src * vec_per_block + i];
     v_cache[dst * vec_per_block + i] = v_cache[src * vec_per_block + i];
@@ -44,7 +45,8 @@ __global__ __launch_bounds__(256) void kv_swap_kernel(const uint64_t* __restrict
                                                       long vec_per_block, int ncache,
                                                       int to_staging) {
   const int c = blockIdx.y, p = blockIdx.z;
-  uint4* cache = reinterpret_cast<uint4*>(ptrs[c]) + (long)ids[p] * vec_per_block;
+  uint4* cache = reinterpret_cast<uint4*>(ptrs[c]) +
+                 (long)FT_CHECK_IDX(ids[p], FT_LIM_BLOCKS, kCkCopyBlock, p) * vec_per_block;
   uint4* st = staging + ((long)p * ncache + c) * vec_per_block;
   if (to_staging) {
     for (long i = blockIdx.x * 256L + threadIdx.x; i < vec_per_block; i += gridDim.x * 256L)
@@ -68,3 +70,6 @@ extern "C" int ft_kv_swap(const uint64_t* ptrs_dev, int ncache, const int* ids_d
                      ids_dev, (uint4*)staging, vec, ncache, to_staging);
   return static_cast<int>(hipGetLastError());
 }
+
+// checked build: this unit's error-word / limits hook (ft_common.h)
+FT_CHECK_HOOK(kv_copy)

@@ -123,7 +123,7 @@ __global__ __launch_bounds__(256) void embed_rmsnorm_kernel(uint16_t* __restrict
   const int row = blockIdx.x * 4 + wave_id();
   if (row >= rows) return;
   const int lane = lane_id();
-  const int tok = min(max(ids[row], 0), vocab - 1);
+  const int tok = min(max(FT_CHECK_IDX(ids[row], vocab, kCkTokenId, row), 0), vocab - 1);
   const uint4* xr = reinterpret_cast<const uint4*>(table + (size_t)tok * hidden);
   uint4* rr = reinterpret_cast<uint4*>(residual + (size_t)row * hidden);
   uint4 v[NCHUNK];
@@ -233,3 +233,6 @@ extern "C" int ft_embed_rmsnorm(void* out, void* residual, const int* ids, const
 #undef FT_EMB_CASE
   return static_cast<int>(hipGetLastError());
 }
+
+// checked build: this unit's error-word / limits hook (ft_common.h)
+FT_CHECK_HOOK(norm_act)

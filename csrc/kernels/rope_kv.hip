@@ -29,8 +29,9 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(uint16_t* __restrict__ qkv
   constexpr int HALF = D / 2;
   constexpr int CPH = HALF / 8;  // 8-pair chunks per head
   const int t = blockIdx.x;
-  const int pos = positions[t];
-  const int slot = slot_mapping[t];
+  const int pos = FT_CHECK_IDX(positions[t], FT_LIM_COS, kCkPosition, t);
+  int slot = slot_mapping[t];
+  if (slot >= 0) slot = FT_CHECK_IDX(slot, FT_LIM_SLOTS, kCkSlot, t);
   uint16_t* row = qkv + (size_t)t * qkv_stride;
   const float* cs = cos_sin + (size_t)pos * D;
 
@@ -109,3 +110,6 @@ extern "C" int ft_rope_kv_write(void* qkv, int qkv_stride, const int* positions,
   }
   return static_cast<int>(hipGetLastError());
 }
+
+// checked build: this unit's error-word / limits hook (ft_common.h)
+FT_CHECK_HOOK(rope_kv)

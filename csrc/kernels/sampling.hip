@@ -217,7 +217,7 @@ __global__ __launch_bounds__(kSampThreads) void sample_kernel(
 #pragma unroll
       for (int c = 0; c < kCand; ++c) {
         if (res && a[c] < lim) {   // the first accepted candidate is the sample
-          out_tokens[row] = __float_as_int(wr[kWsCand + 2 * c + 1]);
+          out_tokens[row] = FT_CHECK_IDX(__float_as_int(wr[kWsCand + 2 * c + 1]), vocab, kCkSampled, row);
           res = 0;
         }
       }
@@ -273,7 +273,7 @@ __global__ __launch_bounds__(kSampThreads) void sample_kernel(
   }
   const float temp = temperature[row];
   if (temp <= 0.f || besti == 0x7fffffff || bestk <= kNegInfKey) {
-    if (tid == 0) out_tokens[row] = (besti == 0x7fffffff) ? 0 : besti;
+    if (tid == 0) out_tokens[row] = FT_CHECK_IDX((besti == 0x7fffffff) ? 0 : besti, vocab, kCkSampled, row);
     return;
   }
   const float M = key_to_f32(bestk);
@@ -458,7 +458,7 @@ __global__ __launch_bounds__(kSampThreads) void sample_kernel(
     const uint64_t h = splitmix64(s0 + (uint64_t)(8 + r0) * 0xD1B54A32D192ED03ull);
     chosen = draw(tstar > thr ? tstar : thr, ((float)(h >> 40) + 0.5f) * (1.0f / 16777216.0f));
   }
-  if (tid == 0) out_tokens[row] = chosen;
+  if (tid == 0) out_tokens[row] = FT_CHECK_IDX(chosen, vocab, kCkSampled, row);
 }
 
 // ---------------------------------------------------------------------------
@@ -765,7 +765,7 @@ __global__ __launch_bounds__(kSampThreads) void samp_draw_kernel(
     const bool done = temp <= 0.f || besti == 0x7fffffff || bestk <= kNegInfKey;
     if (done) {
       if (lane == 0) {
-        out_tokens[row] = (besti == 0x7fffffff) ? 0 : besti;
+        out_tokens[row] = FT_CHECK_IDX((besti == 0x7fffffff) ? 0 : besti, vocab, kCkSampled, row);
         *flag = 0;
         s_done = 1;
       }
@@ -893,7 +893,7 @@ __global__ __launch_bounds__(kSampThreads) void samp_draw_kernel(
   __syncthreads();
   if (tid == 0) {
     if (tp >= 1.f) {   // no nucleus: the first draw is the sample
-      out_tokens[row] = __float_as_int(wr[kWsCand + 1]);
+      out_tokens[row] = FT_CHECK_IDX(__float_as_int(wr[kWsCand + 1]), vocab, kCkSampled, row);
       *flag = 0;
     } else {
       *flag = 3;   // samp_above_kernel + the accept step decide
@@ -1002,7 +1002,7 @@ __global__ __launch_bounds__(kSlThreads) void samp_topk_kernel(
   const int kk = min(top_k[row], C);
   if (kk == 0) {   // everything masked
     if (tid == 0) {
-      out_tokens[row] = 0;
+      out_tokens[row] = FT_CHECK_IDX(0, vocab, kCkSampled, row);
       *flag = 0;
     }
     return;
@@ -1078,7 +1078,7 @@ __global__ __launch_bounds__(kSlThreads) void samp_topk_kernel(
   if (s_pick < 0 && member && rank == s_last) s_pick = mi;
   __syncthreads();
   if (tid == 0) {
-    out_tokens[row] = s_pick;
+    out_tokens[row] = FT_CHECK_IDX(s_pick, vocab, kCkSampled, row);
     *flag = 0;
   }
 }
@@ -1129,3 +1129,6 @@ extern "C" int ft_sample(int* out_tokens, const void* logits, int logits_is_bf16
   }
   return static_cast<int>(hipGetLastError());
 }
+
+// checked build: this unit's error-word / limits hook (ft_common.h)
+FT_CHECK_HOOK(sampling)

@@ -29,6 +29,21 @@ from .scheduler import ScheduledBatch
 log = logging.getLogger("fasttalk.engine.runner")
 
 
+class KernelCheckError(RuntimeError):
+    """The bounds-checked kernel build (FT_KERNEL_CHECKS=1) caught an out-of-range
+    index (block-table entry, KV slot, rotary position, token id) in a step."""
+
+    CODES = {1: "block-table entry >= num_blocks", 2: "KV slot >= pool capacity",
+             3: "position >= rotary table rows", 4: "input token id >= vocab",
+             5: "sampled token id >= vocab", 6: "KV copy/swap block id >= num_blocks"}
+
+    def __init__(self, word):
+        count, code, ctx, value = (int(x) for x in word[:4])
+        self.count, self.code, self.ctx, self.value = count, code, ctx, value
+        super().__init__(f"kernel bounds check: {self.CODES.get(code, f'code {code}')} "
+                         f"(row/token {ctx}, value {value}; {count} violation(s))")
+
+
 class CommFault(RuntimeError):
     """A tensor-parallel collective of this step timed out (custom all-reduce spin
     budget): the step's tokens are discarded and the group now runs on RCCL."""
@@ -186,6 +201,16 @@ class ModelRunner:
                                            + cfg.max_num_seqs)
         self.num_blocks = self._decide_num_blocks()
         self.kv = self.model.allocate_kv_cache(self.num_blocks, self.bs)
+        # FT_KERNEL_CHECKS=1: the bounds-checked kernel build validates every index it
+        # is handed against these limits; the word is read after each step (_wait)
+        self.d_check: Optional[torch.Tensor] = None
+        if self.is_gpu and getattr(ops.native(), "kernel_checks", False):
+            self.d_check = torch.zeros(4, dtype=torch.int32, device=self.device)
+            ops.native().set_kernel_checks(self.d_check, self.num_blocks, self.bs,
+                                           int(self.model.cos_sin.shape[0]), int(self.mcfg.vocab_size))
+            log.warning("FT_KERNEL_CHECKS: bounds-checked kernels (num_blocks=%d, block_size=%d, "
+                        "rotary rows=%d, vocab=%d)", self.num_blocks, self.bs,
+                        self.model.cos_sin.shape[0], self.mcfg.vocab_size)
         # E6 host swap pool (--swap-space): capped at 2x the device pool, allocated
         # (pinned) on the first swap-out so an idle server does not pin host memory
         k0 = self.kv[0][0]
@@ -577,6 +602,21 @@ class ModelRunner:
         while not ev.query():
             time.sleep(0.0001)
         self.stats["wait_ms"] = self.stats.get("wait_ms", 0.0) + 1e3 * (time.perf_counter() - t0)
+        if self.d_check is not None:
+            self.kernel_check()
+
+    def kernel_check(self):
+        """Checked build: raise KernelCheckError if a kernel has reported an out-of-range
+        index since the last reset (the word is sticky until kernel_check_reset)."""
+        if self.d_check is None:
+            return
+        w = self.d_check.cpu()
+        if int(w[0]):
+            raise KernelCheckError(w.tolist())
+
+    def kernel_check_reset(self):
+        if self.d_check is not None:
+            self.d_check.zero_()
 
     def _sample(self, h, sampling, masks, dev_sampling=None, dev_mask=None) -> List[int]:
         logits = self.model.compute_logits(h)

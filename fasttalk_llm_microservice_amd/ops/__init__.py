@@ -21,26 +21,37 @@ _C = None
 _C_err: Optional[BaseException] = None
 
 
+def kernel_checks_requested() -> bool:
+    """``FT_KERNEL_CHECKS=1``: load the bounds-checked kernel build ``_C_checked``
+    (csrc/include/ft_common.h; the runner reads its error word after every step)."""
+    return os.environ.get("FT_KERNEL_CHECKS", "0").strip().lower() in ("1", "true", "yes", "on")
+
+
 def native():
-    """Return the loaded ``_C`` extension (building it in-tree if allowed)."""
+    """Return the loaded ``_C`` extension (``_C_checked`` under FT_KERNEL_CHECKS=1),
+    building it in-tree if allowed."""
     global _C, _C_err
     if _C is not None:
         return _C
     with _lock:
         if _C is not None:
             return _C
+        checked = kernel_checks_requested()
+        name = "_C_checked" if checked else "_C"
+        import importlib
+
         try:
-            from .. import _C as mod  # type: ignore
+            mod = importlib.import_module(f"..{name}", __package__)
         except ImportError as e:  # pragma: no cover - depends on build state
             if os.environ.get("FT_AUTOBUILD", "1") != "0":
                 from .build import build_kernels
 
-                build_kernels(verbose=True)
-                from .. import _C as mod  # type: ignore
+                build_kernels(verbose=True, checked=checked)
+                mod = importlib.import_module(f"..{name}", __package__)
             else:
                 _C_err = e
                 raise RuntimeError(
-                    "fasttalk native extension _C is not built; run "
+                    f"fasttalk native extension {name} is not built; run "
                     "`python -m fasttalk_llm_microservice_amd.ops.build`") from e
         _C = mod
         return _C

@@ -69,7 +69,7 @@ def _torch_flags():
         f"-I{sysconfig.get_paths()['include']}",
         f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
         "-DTORCH_API_INCLUDE_EXTENSION_H",
-        "-DTORCH_EXTENSION_NAME=_C",
+        "-DTORCH_EXTENSION_NAME=_C",   # _C_checked for the checked build (build_kernels)
         "-D__HIP_PLATFORM_AMD__=1",
         "-DUSE_ROCM=1",
         "-fPIC",
@@ -105,16 +105,25 @@ KERNEL_FLAGS = {
 }
 
 
-def build_kernels(force: bool = False, jobs: int = 8, verbose: bool = True) -> Path:
+def build_kernels(force: bool = False, jobs: int = 8, verbose: bool = True,
+                  checked: bool = False) -> Path:
+    """``checked``: the bounds-checked debug build (``-DFT_KERNEL_CHECKS=1``,
+    csrc/include/ft_common.h) as a separate extension ``_C_checked.so``, loaded by
+    ``ops.native()`` when ``FT_KERNEL_CHECKS=1``."""
     headers = sorted((CSRC / "include").glob("*.h")) + sorted((CSRC / "kernels").glob("*.h"))
     kernels = sorted((CSRC / "kernels").glob("*.hip"))
+    name = "_C_checked" if checked else "_C"
+    extra = ["-DFT_KERNEL_CHECKS=1"] if checked else []
+    bdir = BUILD / ("checked" if checked else "")
     kflags = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
-              f"-I{CSRC / 'include'}", "-munsafe-fp-atomics"]
+              f"-I{CSRC / 'include'}", "-munsafe-fp-atomics"] + extra
     tflags, ldflags = _torch_flags()
-    bflags = [HIPCC, f"--offload-arch={ARCH}"] + tflags + [f"-I{CSRC / 'include'}"]
-    jobs_list = [(k, BUILD / "kernels" / (k.stem + ".o"), kflags + KERNEL_FLAGS.get(k.stem, []), headers)
+    tflags = [f for f in tflags if not f.startswith("-DTORCH_EXTENSION_NAME=")] + \
+        [f"-DTORCH_EXTENSION_NAME={name}"]
+    bflags = [HIPCC, f"--offload-arch={ARCH}"] + tflags + [f"-I{CSRC / 'include'}"] + extra
+    jobs_list = [(k, bdir / "kernels" / (k.stem + ".o"), kflags + KERNEL_FLAGS.get(k.stem, []), headers)
                  for k in kernels]
-    jobs_list.append((CSRC / "bindings.cpp", BUILD / "bindings.o", bflags + ["-x", "hip"], headers))
+    jobs_list.append((CSRC / "bindings.cpp", bdir / "bindings.o", bflags + ["-x", "hip"], headers))
     changed = False
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
         futs = {ex.submit(_compile, s, o, c, d, force): s for s, o, c, d in jobs_list}
@@ -123,7 +132,7 @@ def build_kernels(force: bool = False, jobs: int = 8, verbose: bool = True) -> P
                 changed = True
                 if verbose:
                     print(f"[build] compiled {futs[f].name}", flush=True)
-    out = PKG_DIR / ("_C" + _ext_suffix())
+    out = PKG_DIR / (name + _ext_suffix())
     objs = [str(o) for _, o, _, _ in jobs_list]
     if changed or force or not out.exists():
         _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", str(out), *ldflags])
@@ -157,9 +166,12 @@ def build_runtime(force: bool = False, jobs: int = 8, verbose: bool = True) -> P
     return out
 
 
-def build_all(force: bool = False, jobs: int = 8, verbose: bool = True):
+def build_all(force: bool = False, jobs: int = 8, verbose: bool = True, checked: bool = True):
+    """Runtime, release kernels and (``checked``) the bounds-checked kernel build."""
     rt = build_runtime(force=force, jobs=jobs, verbose=verbose)
     k = build_kernels(force=force, jobs=jobs, verbose=verbose)
+    if checked:
+        build_kernels(force=force, jobs=jobs, verbose=verbose, checked=True)
     return k, rt
 
 
@@ -167,10 +179,12 @@ def main(argv=None):
     ap = argparse.ArgumentParser(description=__doc__)
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-j", "--jobs", type=int, default=min(8, os.cpu_count() or 4))
-    ap.add_argument("--only", choices=["kernels", "runtime"], default=None)
+    ap.add_argument("--only", choices=["kernels", "checked", "runtime"], default=None)
     a = ap.parse_args(argv)
     if a.only == "kernels":
         build_kernels(a.force, a.jobs)
+    elif a.only == "checked":
+        build_kernels(a.force, a.jobs, checked=True)
     elif a.only == "runtime":
         build_runtime(a.force, a.jobs)
     else:
