@@ -68,8 +68,9 @@ def main():
                         cands.append((f"xc{nt}/{sp}", lambda nt=nt, sp=sp: ops.native().skinny_gemm(
                             x, wp, out, ws, sp, nt, -4), sp))
             for cfg in [int(c) for c in a.cfgs.split(",")]:
-                bm, bn = [(256, 256), (128, 256), (256, 128), (256, 256), (256, 256),
-                          (192, 256), (192, 128)][cfg]
+                bm, bn = {0: (256, 256), 1: (128, 256), 2: (256, 128), 3: (256, 256), 4: (256, 256),
+                          5: (192, 256), 6: (192, 128), 10: (256, 256), 11: (192, 256),
+                          12: (128, 256), 13: (256, 128), 14: (64, 256)}[cfg]
                 tiles = -(-m // bm) * -(-n // bn)
                 for sp in [int(v) for v in a.splits.split(",")]:
                     if k % (64 * sp) or (sp > 1 and tiles * sp > 2048) or (sp > 1 and tiles >= 512):
@@ -109,7 +110,7 @@ def main():
     w = torch.randn(n, k, device="cuda").bfloat16() * 0.05
     x = torch.randn(300, k, device="cuda").bfloat16()
     g, u = F.linear(x, w).float().chunk(2, dim=-1)
-    for cfg in (0, 1, 3):
+    for cfg in (0, 1, 3, 10, 11, 12, 13, 14):
         h = ops.packed_gemm(x, ops.pack_weight(ops.interleave_gate_up(w, 1)), epi="silu", cfg=cfg)
         print(f"silu epilogue cfg{cfg} max err",
               (h.float() - torch.nn.functional.silu(g) * u).abs().max().item())

@@ -16,7 +16,8 @@ int ft_fused_add_rmsnorm(void* out, const void* x, void* residual, const void* w
 int ft_silu_mul(void* out, const void* gu, int rows, int inter, int il, hipStream_t stream);
 int ft_rope_kv_write(void* qkv, int qkv_stride, const int* positions, const float* cos_sin,
                      const int* slot_mapping, void* k_cache, void* v_cache, int tokens, int nq,
-                     int nkv, int head_dim, int block_size, hipStream_t stream);
+                     int nkv, int head_dim, int block_size, int cos_rows, int num_slots,
+                     hipStream_t stream);
 int ft_decode_waves();
 int ft_decode_max_batch();
 int ft_paged_decode_attention(void* out, int out_stride, float* tmp_out, float* tmp_ml,
@@ -24,21 +25,22 @@ int ft_paged_decode_attention(void* out, int out_stride, float* tmp_out, float* 
                               const void* v_cache, const int* block_tables, int bt_stride,
                               const int* seq_lens, int batch, int nq, int nkv, int head_dim,
                               int block_size, float scale, int* counters, int piece,
-                              int slot_cap, hipStream_t stream);
+                              int slot_cap, int num_blocks, hipStream_t stream);
 int ft_prefill_tile_tokens(int nq, int nkv);
 int ft_prefill_attention(void* out, int out_stride, const void* q, int q_stride,
                          const void* k_cache, const void* v_cache, const int* block_tables,
                          int bt_stride, const int* seq_lens, const int* q_start_loc,
                          const int* tile_info, int num_tiles, int nq, int nkv, int head_dim,
                          int block_size, float scale, float* part_o, float* part_ml,
-                         const int* combine, int num_combine, int invariant, hipStream_t stream);
+                         const int* combine, int num_combine, int invariant, int num_blocks,
+                         hipStream_t stream);
 int ft_sample(int* out_tokens, const void* logits, int logits_is_bf16, long logit_stride,
               int batch, int vocab, const float* temperature, const float* top_p,
               const int* top_k, const long long* seeds, const int* steps,
               const uint32_t* allow_mask, int mask_words, float* ws, hipStream_t stream);
 int ft_sample_ws_floats();
 int ft_kv_block_copy(void* k_cache, void* v_cache, const int* src_dst, int num_pairs,
-                     long block_elems, hipStream_t stream);
+                     long block_elems, int num_blocks, hipStream_t stream);
 int ft_w4_gemm(const void* x, int x_stride, int M, const uint32_t* wq, const void* sz, int N, int K,
                float* ws, void* out, int out_stride, int splits, int nt, hipStream_t stream);
 int ft_w4_dequant(const uint32_t* wq, const void* sz, void* out, int N, int K, hipStream_t stream);
@@ -46,7 +48,7 @@ int ft_w4_gemm_xr(const void* x, int x_stride, int M, const uint32_t* wq, const 
                   float* ws, void* out, int out_stride, int splits, int nt, int silu,
                   hipStream_t stream);
 int ft_kv_swap(const uint64_t* ptrs_dev, int ncache, const int* ids_dev, int n, void* staging,
-               long block_elems, int to_staging, hipStream_t stream);
+               long block_elems, int to_staging, int num_blocks, hipStream_t stream);
 int ft_skinny_gemm_xc(const void* x, int x_stride, int M, const void* w, int N, int K, float* ws,
                       void* out, int out_stride, int splits, int nt, hipStream_t stream);
 int ft_embed_rmsnorm(void* out, void* residual, const int* ids, const void* table, const void* w,
@@ -90,7 +92,8 @@ int ft_slab_store(const float* ws, int splits, int rows, int cols, void* out, in
 int ft_slab_rope_kv(const float* ws, int splits, int rows, int cols, void* q_out, int q_stride,
                     const int* positions, const float* cos_sin, const int* slot_mapping,
                     void* k_cache, void* v_cache, int nq, int nkv, int head_dim, int block_size,
-                    const void* residual, int hidden, float eps, hipStream_t stream);
+                    const void* residual, int hidden, float eps, int cos_rows, int num_slots,
+                    hipStream_t stream);
 }
 
 namespace {
@@ -193,7 +196,8 @@ void rope_kv_write(at::Tensor qkv, at::Tensor positions, at::Tensor cos_sin,
   check_rc(ft_rope_kv_write(qkv.data_ptr(), (int)qkv.stride(0), positions.data_ptr<int>(),
                             cos_sin.data_ptr<float>(), slot_mapping.data_ptr<int>(),
                             k_cache.data_ptr(), v_cache.data_ptr(), tokens, (int)nq, (int)nkv,
-                            (int)head_dim, (int)k_cache.size(2), cur_stream()),
+                            (int)head_dim, (int)k_cache.size(2), (int)cos_sin.size(0),
+                            (int)(k_cache.size(0) * k_cache.size(2)), cur_stream()),
            "rope_kv_write");
 }
 
@@ -240,6 +244,7 @@ void paged_decode_attention(at::Tensor out, at::Tensor q, at::Tensor k_cache, at
                                      seq_lens.data_ptr<int>(), batch, (int)nq, (int)nkv,
                                      (int)head_dim, (int)k_cache.size(2), (float)scale, cnt,
                                      (int)piece, (int)std::min<int64_t>(slot_cap, INT32_MAX),
+                                     (int)k_cache.size(0),
                                      cur_stream()),
            "paged_decode_attention");
 }
@@ -288,7 +293,7 @@ void prefill_attention(at::Tensor out, at::Tensor q, at::Tensor k_cache, at::Ten
                                 seq_lens.data_ptr<int>(), q_start_loc.data_ptr<int>(),
                                 tile_info.data_ptr<int>(), (int)num_tiles, (int)nq, (int)nkv,
                                 (int)head_dim, (int)k_cache.size(2), (float)scale, po, pml, cb,
-                                (int)num_combine, (int)invariant, cur_stream()),
+                                (int)num_combine, (int)invariant, (int)k_cache.size(0), cur_stream()),
            "prefill_attention");
 }
 
@@ -343,7 +348,8 @@ void kv_block_copy(at::Tensor k_cache, at::Tensor v_cache, at::Tensor src_dst) {
   const long block_elems = (long)(k_cache.numel() / k_cache.size(0));
   TORCH_CHECK(block_elems % 8 == 0, "block size");
   check_rc(ft_kv_block_copy(k_cache.data_ptr(), v_cache.data_ptr(), src_dst.data_ptr<int>(),
-                            (int)(src_dst.numel() / 2), block_elems, cur_stream()),
+                            (int)(src_dst.numel() / 2), block_elems, (int)k_cache.size(0),
+                            cur_stream()),
            "kv_block_copy");
 }
 
@@ -351,7 +357,7 @@ void kv_block_copy(at::Tensor k_cache, at::Tensor v_cache, at::Tensor src_dst) {
 // block_elems elements per block); ids: int32 device [n]; staging: bf16 device
 // [n, 2L, block_elems].  The caller bounds-checks ids against the pool size.
 void kv_swap(at::Tensor ptrs, at::Tensor ids, at::Tensor staging, int64_t block_elems,
-             bool to_staging) {
+             bool to_staging, int64_t num_blocks) {
   check_dev(ptrs, "ptrs");
   TORCH_CHECK(ptrs.scalar_type() == at::kLong && ptrs.is_contiguous(), "ptrs int64");
   check_i32(ids, "ids");
@@ -361,7 +367,7 @@ void kv_swap(at::Tensor ptrs, at::Tensor ids, at::Tensor staging, int64_t block_
   TORCH_CHECK(staging.numel() >= (int64_t)n * ptrs.numel() * block_elems, "staging too small");
   check_rc(ft_kv_swap(reinterpret_cast<const uint64_t*>(ptrs.data_ptr<int64_t>()),
                       (int)ptrs.numel(), ids.data_ptr<int>(), n, staging.data_ptr(), block_elems,
-                      to_staging ? 1 : 0, cur_stream()),
+                      to_staging ? 1 : 0, (int)num_blocks, cur_stream()),
            "kv_swap");
 }
 
@@ -796,13 +802,14 @@ void slab_rope_kv(at::Tensor ws, int64_t splits, int64_t rows, int64_t cols, at:
                            cos_sin.data_ptr<float>(), slot_mapping.data_ptr<int>(),
                            k_cache.data_ptr(), v_cache.data_ptr(), (int)nq, (int)nkv,
                            (int)head_dim, (int)k_cache.size(2), rp, hidden, (float)eps,
+                           (int)cos_sin.size(0), (int)(k_cache.size(0) * k_cache.size(2)),
                            cur_stream()), "slab_rope_kv");
 }
 
 #if defined(FT_KERNEL_CHECKS) && FT_KERNEL_CHECKS
 // checked build: every instrumented kernel unit's hook (ft_common.h FT_CHECK_HOOK)
 extern "C" {
-#define FT_HOOK_DECL(NAME) int ft_check_hook_##NAME(uint32_t*, int, int, int, int);
+#define FT_HOOK_DECL(NAME) int ft_check_hook_##NAME(uint32_t*);
 FT_HOOK_DECL(attn_decode)
 FT_HOOK_DECL(attn_prefill)
 FT_HOOK_DECL(rope_kv)
@@ -813,18 +820,17 @@ FT_HOOK_DECL(kv_copy)
 #undef FT_HOOK_DECL
 }
 
-// word: int32 [4] device tensor (violations, first code, context, value)
-void set_kernel_checks(torch::Tensor word, int64_t num_blocks, int64_t block_size,
-                       int64_t cos_rows, int64_t vocab) {
+// word: int32 [4] device tensor (violations, first code, context, value); the process's
+// checked kernels report into it until it is replaced
+void set_kernel_checks(torch::Tensor word) {
   TORCH_CHECK(word.is_cuda() && word.scalar_type() == at::kInt && word.numel() >= 4, "check word");
   uint32_t* w = reinterpret_cast<uint32_t*>(word.data_ptr<int>());
-  const int nb = (int)num_blocks, bs = (int)block_size, cr = (int)cos_rows, v = (int)vocab;
-  using Hook = int (*)(uint32_t*, int, int, int, int);
+  using Hook = int (*)(uint32_t*);
   const Hook hooks[] = {ft_check_hook_attn_decode, ft_check_hook_attn_prefill,
                         ft_check_hook_rope_kv,     ft_check_hook_fused_epilogue,
                         ft_check_hook_norm_act,    ft_check_hook_sampling,
                         ft_check_hook_kv_copy};
-  for (Hook h : hooks) check_rc(h(w, nb, bs, cr, v), "set_kernel_checks");
+  for (Hook h : hooks) check_rc(h(w), "set_kernel_checks");
 }
 #endif
 
@@ -859,7 +865,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("top_p"), py::arg("top_k"), py::arg("seeds"), py::arg("steps"),
         py::arg("mask") = py::none());
   m.def("kv_block_copy", &kv_block_copy);
-  m.def("kv_swap", &kv_swap);
+  m.def("kv_swap", &kv_swap, py::arg("ptrs"), py::arg("ids"), py::arg("staging"),
+        py::arg("block_elems"), py::arg("to_staging"), py::arg("num_blocks") = 0);
   m.def("w4_gemm", &w4_gemm, py::arg("x"), py::arg("wq"), py::arg("sz"), py::arg("N"),
         py::arg("out") = py::none(), py::arg("ws") = py::none(), py::arg("splits") = 1,
         py::arg("nt") = 1, py::arg("xr") = false, py::arg("silu") = false);

@@ -149,15 +149,8 @@ enum FtCheckCode : int {
 
 #if defined(FT_KERNEL_CHECKS) && FT_KERNEL_CHECKS
 namespace ft {
-struct FtCheckLimits {
-  int num_blocks;   // KV pool blocks (0: unknown, not checked)
-  int block_size;
-  int cos_rows;     // rows of the rotary cos/sin table
-  int vocab;
-};
 // [0] violations, [1] code of the first, [2] its context (row / token), [3] its value
 static __device__ uint32_t* ft_check_word;
-static __device__ FtCheckLimits ft_check_lim;
 
 __device__ __noinline__ static void ft_check_fail(int code, int ctx, int value) {
   uint32_t* w = ft_check_word;
@@ -171,7 +164,7 @@ __device__ __noinline__ static void ft_check_fail(int code, int ctx, int value) 
   }
 }
 
-// value if 0 <= value < limit (or the limit is unknown), else report and return 0
+// value if 0 <= value < limit (a limit <= 0 is unknown: unchecked), else report and 0
 __device__ __forceinline__ int ft_check_idx(int value, long limit, int code, int ctx) {
   if (limit > 0 && (value < 0 || (long)value >= limit)) {
     ft_check_fail(code, ctx, value);
@@ -180,19 +173,11 @@ __device__ __forceinline__ int ft_check_idx(int value, long limit, int code, int
   return value;
 }
 }  // namespace ft
-#define FT_LIM_BLOCKS ((long)::ft::ft_check_lim.num_blocks)
-#define FT_LIM_SLOTS ((long)::ft::ft_check_lim.num_blocks * (long)::ft::ft_check_lim.block_size)
-#define FT_LIM_COS ((long)::ft::ft_check_lim.cos_rows)
-#define FT_LIM_VOCAB ((long)::ft::ft_check_lim.vocab)
 #define FT_CHECK_IDX(v, lim, code, ctx) ::ft::ft_check_idx((v), (lim), (code), (ctx))
 #define FT_CHECK_HOOK(NAME)                                                                  \
-  extern "C" int ft_check_hook_##NAME(uint32_t* word, int num_blocks, int block_size,       \
-                                      int cos_rows, int vocab) {                            \
-    const ::ft::FtCheckLimits lim{num_blocks, block_size, cos_rows, vocab};                 \
-    hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(::ft::ft_check_word), &word, sizeof(word)); \
-    if (e == hipSuccess)                                                                    \
-      e = hipMemcpyToSymbol(HIP_SYMBOL(::ft::ft_check_lim), &lim, sizeof(lim));             \
-    return static_cast<int>(e);                                                             \
+  extern "C" int ft_check_hook_##NAME(uint32_t* word) {                                     \
+    return static_cast<int>(                                                                \
+        hipMemcpyToSymbol(HIP_SYMBOL(::ft::ft_check_word), &word, sizeof(word)));           \
   }
 #else
 #define FT_CHECK_IDX(v, lim, code, ctx) (v)

@@ -258,7 +258,7 @@ __global__ __launch_bounds__(256, WPC) void paged_decode_kernel(
     uint16_t* __restrict__ k_cache, uint16_t* __restrict__ v_cache,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ seq_lens,
     int batch, int nkv, int bs_shift, float scale_log2, int* __restrict__ counters,
-    int min_tiles, int piece, int slot_cap) {
+    int min_tiles, int piece, int slot_cap, int num_blocks) {
   static_assert(G >= 1 && G <= 16, "GQA group must fit the 16 MFMA columns");
   constexpr int KC = D / 32, ND = D / 16;
   // s_pre: tile prefix; s_pre + kDecMaxBatch + 1: piece prefix (piece mode)
@@ -321,7 +321,7 @@ __global__ __launch_bounds__(256, WPC) void paged_decode_kernel(
       int my_blk = 0, my_off = 0;
       if (lane < cc) {
         const int tok = (t0 + c0 + lane) << 4;
-        my_blk = FT_CHECK_IDX(bt[tok >> bs_shift], FT_LIM_BLOCKS, kCkBlockTable, b);
+        my_blk = FT_CHECK_IDX(bt[tok >> bs_shift], num_blocks, kCkBlockTable, b);
         my_off = tok & bmask;
       }
       auto ld = [&](MTile<D>& t, int i) {
@@ -541,7 +541,7 @@ extern "C" int ft_paged_decode_attention(void* out, int out_stride, float* tmp_o
                                          int bt_stride, const int* seq_lens, int batch, int nq,
                                          int nkv, int head_dim, int block_size, float scale,
                                          int* counters, int piece, int slot_cap,
-                                         hipStream_t stream) {
+                                         int num_blocks, hipStream_t stream) {
   if (batch <= 0) return 0;
   if (nq % nkv != 0) return -1;
   if (piece < 0 || (piece > 0 && counters == nullptr)) return -6;  // pieces merge in-launch
@@ -578,7 +578,7 @@ extern "C" int ft_paged_decode_attention(void* out, int out_stride, float* tmp_o
 #define FT_DEC_ARGS                                                                             \
   (uint16_t*)out, out_stride, tmp_out, tmp_ml, (const uint16_t*)q, q_stride, (uint16_t*)k_cache, \
       (uint16_t*)v_cache, block_tables, bt_stride, seq_lens, batch, nkv, bs_shift, scale_log2,   \
-      counters, min_tiles, piece, slot_cap
+      counters, min_tiles, piece, slot_cap, num_blocks
 #define FT_DEC_LAUNCH(DD, GG, RR, FCC)                                                  \
   if (wpc == 1)                                                                                \
     hipLaunchKernelGGL((ft::paged_decode_kernel<DD, GG, RR, FCC, 1>), dim3(nwg), dim3(64 * nwv), \

@@ -68,7 +68,8 @@ __global__ __launch_bounds__(512, 1) void prefill_attn_kernel(
     const uint16_t* __restrict__ k_cache, const uint16_t* __restrict__ v_cache,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ seq_lens,
     const int* __restrict__ q_start_loc, const int* __restrict__ tile_info, int nkv,
-    int block_size, float scale_log2, float* __restrict__ part_o, float* __restrict__ part_ml) {
+    int block_size, float scale_log2, float* __restrict__ part_o, float* __restrict__ part_ml,
+    int num_blocks) {
   constexpr int NCH = D / 8;          // 16-B chunks per K row
   constexpr int KC = D / 32;          // k-steps of S^T = K Q^T
   constexpr int ND = D / 16;          // 16-row dim tiles of O^T
@@ -338,7 +339,7 @@ __global__ __launch_bounds__(512, 1) void prefill_attn_kernel(
 
   // block-table entries of the KV range (LDS reads never wait on the DMA's vmcnt)
   for (int i = threadIdx.x; i < nblk; i += blockDim.x)
-    s_bt[i] = FT_CHECK_IDX(bt[i], FT_LIM_BLOCKS, kCkBlockTable, b);
+    s_bt[i] = FT_CHECK_IDX(bt[i], num_blocks, kCkBlockTable, b);
   __syncthreads();
 
 #pragma unroll
@@ -451,7 +452,8 @@ extern "C" int ft_prefill_attention(void* out, int out_stride, const void* q, in
                                     const int* q_start_loc, const int* tile_info, int num_tiles,
                                     int nq, int nkv, int head_dim, int block_size, float scale,
                                     float* part_o, float* part_ml, const int* combine,
-                                    int num_combine, int invariant, hipStream_t stream) {
+                                    int num_combine, int invariant, int num_blocks,
+                                    hipStream_t stream) {
   if (num_tiles <= 0) return 0;
   if (nq % nkv != 0) return -1;
   if (num_combine > 0 && (part_o == nullptr || part_ml == nullptr || combine == nullptr)) return -3;
@@ -465,13 +467,13 @@ extern "C" int ft_prefill_attention(void* out, int out_stride, const void* q, in
                          (uint16_t*)out, out_stride, (const uint16_t*)q, q_stride,           \
                          (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables,   \
                          bt_stride, seq_lens, q_start_loc, tile_info, nkv, block_size,       \
-                         scale_log2, part_o, part_ml);                                       \
+                         scale_log2, part_o, part_ml, num_blocks);                           \
     else                                                                                     \
       hipLaunchKernelGGL((ft::prefill_attn_kernel<DD, GG, false>), grid, block, 0, stream,   \
                          (uint16_t*)out, out_stride, (const uint16_t*)q, q_stride,           \
                          (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables,   \
                          bt_stride, seq_lens, q_start_loc, tile_info, nkv, block_size,       \
-                         scale_log2, part_o, part_ml);                                       \
+                         scale_log2, part_o, part_ml, num_blocks);                           \
     if (num_combine > 0)                                                                     \
       hipLaunchKernelGGL((ft::prefill_combine_kernel<DD, GG>),                               \
                          dim3(num_combine, nkv, ft::kPrefillRows / (256 / (DD / 4))),         \

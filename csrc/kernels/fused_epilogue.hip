@@ -147,13 +147,14 @@ __global__ __launch_bounds__(256) void slab_rope_kv_kernel(
     SrcSlab src, uint16_t* __restrict__ q_out, int q_stride, const int* __restrict__ positions,
     const float* __restrict__ cos_sin, const int* __restrict__ slot_mapping,
     uint16_t* __restrict__ k_cache, uint16_t* __restrict__ v_cache, int nq, int nkv,
-    int block_size, const uint16_t* __restrict__ residual, int hidden, float eps) {
+    int block_size, const uint16_t* __restrict__ residual, int hidden, float eps, int cos_rows,
+    int num_slots) {
   constexpr int HALF = D / 2;
   constexpr int CPH = HALF / 8;
   const int t = blockIdx.x;
-  const int pos = FT_CHECK_IDX(positions[t], FT_LIM_COS, kCkPosition, t);
+  const int pos = FT_CHECK_IDX(positions[t], cos_rows, kCkPosition, t);
   int slot = slot_mapping[t];
-  if (slot >= 0) slot = FT_CHECK_IDX(slot, FT_LIM_SLOTS, kCkSlot, t);
+  if (slot >= 0) slot = FT_CHECK_IDX(slot, num_slots, kCkSlot, t);
   const float* cs = cos_sin + (size_t)pos * D;
   const int blk = slot >= 0 ? slot / block_size : 0;
   const int off = slot >= 0 ? slot - blk * block_size : 0;
@@ -293,7 +294,8 @@ extern "C" int ft_slab_rope_kv(const float* ws, int splits, int rows, int cols, 
                                int q_stride, const int* positions, const float* cos_sin,
                                const int* slot_mapping, void* k_cache, void* v_cache, int nq,
                                int nkv, int head_dim, int block_size, const void* residual,
-                               int hidden, float eps, hipStream_t stream) {
+                               int hidden, float eps, int cos_rows, int num_slots,
+                               hipStream_t stream) {
   if (rows <= 0) return 0;
   if (residual != nullptr && hidden % 8 != 0) return -2;
   ft::SrcSlab src{ws, splits, rows, cols};
@@ -301,12 +303,12 @@ extern "C" int ft_slab_rope_kv(const float* ws, int splits, int rows, int cols, 
     hipLaunchKernelGGL(ft::slab_rope_kv_kernel<128>, dim3(rows, 2), dim3(256), 0, stream, src,
                        (uint16_t*)q_out, q_stride, positions, cos_sin, slot_mapping,
                        (uint16_t*)k_cache, (uint16_t*)v_cache, nq, nkv, block_size,
-                       (const uint16_t*)residual, hidden, eps);
+                       (const uint16_t*)residual, hidden, eps, cos_rows, num_slots);
   } else if (head_dim == 64) {
     hipLaunchKernelGGL(ft::slab_rope_kv_kernel<64>, dim3(rows, 2), dim3(256), 0, stream, src,
                        (uint16_t*)q_out, q_stride, positions, cos_sin, slot_mapping,
                        (uint16_t*)k_cache, (uint16_t*)v_cache, nq, nkv, block_size,
-                       (const uint16_t*)residual, hidden, eps);
+                       (const uint16_t*)residual, hidden, eps, cos_rows, num_slots);
   } else {
     return -1;
   }

@@ -9,10 +9,10 @@ namespace ft {
 __global__ __launch_bounds__(256) void kv_block_copy_kernel(uint4* __restrict__ k_cache,
                                                             uint4* __restrict__ v_cache,
                                                             const int* __restrict__ pairs,
-                                                            long vec_per_block) {
+                                                            long vec_per_block, int num_blocks) {
   const int p = blockIdx.y;
-  const long src = FT_CHECK_IDX(pairs[2 * p], FT_LIM_BLOCKS, kCkCopyBlock, p);
-  const long dst = FT_CHECK_IDX(pairs[2 * p + 1], FT_LIM_BLOCKS, kCkCopyBlock, p);
+  const long src = FT_CHECK_IDX(pairs[2 * p], num_blocks, kCkCopyBlock, p);
+  const long dst = FT_CHECK_IDX(pairs[2 * p + 1], num_blocks, kCkCopyBlock, p);
   for (long i = blockIdx.x * 256L + threadIdx.x; i < vec_per_block; i += gridDim.x * 256L) {
     k_cache[dst * vec_per_block + i] = k_cache[src * vec_per_block + i];
     v_cache[dst * vec_per_block + i] = v_cache[src * vec_per_block + i];
@@ -22,13 +22,13 @@ __global__ __launch_bounds__(256) void kv_block_copy_kernel(uint4* __restrict__ 
 }  // namespace ft
 
 extern "C" int ft_kv_block_copy(void* k_cache, void* v_cache, const int* src_dst, int num_pairs,
-                                long block_elems, hipStream_t stream) {
+                                long block_elems, int num_blocks, hipStream_t stream) {
   if (num_pairs <= 0) return 0;
   const long vec = block_elems / 8;
   int gx = (int)((vec + 255) / 256);
   if (gx > 64) gx = 64;
   hipLaunchKernelGGL(ft::kv_block_copy_kernel, dim3(gx, num_pairs), dim3(256), 0, stream,
-                     (uint4*)k_cache, (uint4*)v_cache, src_dst, vec);
+                     (uint4*)k_cache, (uint4*)v_cache, src_dst, vec, num_blocks);
   return static_cast<int>(hipGetLastError());
 }
 
@@ -43,10 +43,10 @@ __global__ __launch_bounds__(256) void kv_swap_kernel(const uint64_t* __restrict
                                                       const int* __restrict__ ids,
                                                       uint4* __restrict__ staging,
                                                       long vec_per_block, int ncache,
-                                                      int to_staging) {
+                                                      int to_staging, int num_blocks) {
   const int c = blockIdx.y, p = blockIdx.z;
   uint4* cache = reinterpret_cast<uint4*>(ptrs[c]) +
-                 (long)FT_CHECK_IDX(ids[p], FT_LIM_BLOCKS, kCkCopyBlock, p) * vec_per_block;
+                 (long)FT_CHECK_IDX(ids[p], num_blocks, kCkCopyBlock, p) * vec_per_block;
   uint4* st = staging + ((long)p * ncache + c) * vec_per_block;
   if (to_staging) {
     for (long i = blockIdx.x * 256L + threadIdx.x; i < vec_per_block; i += gridDim.x * 256L)
@@ -60,14 +60,15 @@ __global__ __launch_bounds__(256) void kv_swap_kernel(const uint64_t* __restrict
 }  // namespace ft
 
 extern "C" int ft_kv_swap(const uint64_t* ptrs_dev, int ncache, const int* ids_dev, int n,
-                          void* staging, long block_elems, int to_staging, hipStream_t stream) {
+                          void* staging, long block_elems, int to_staging, int num_blocks,
+                          hipStream_t stream) {
   if (n <= 0) return 0;
   if (block_elems % 8 != 0 || ncache <= 0 || ncache > 65535 || n > 65535) return -1;
   const long vec = block_elems / 8;
   int gx = (int)((vec + 255) / 256);
   if (gx > 16) gx = 16;
   hipLaunchKernelGGL(ft::kv_swap_kernel, dim3(gx, ncache, n), dim3(256), 0, stream, ptrs_dev,
-                     ids_dev, (uint4*)staging, vec, ncache, to_staging);
+                     ids_dev, (uint4*)staging, vec, ncache, to_staging, num_blocks);
   return static_cast<int>(hipGetLastError());
 }
 

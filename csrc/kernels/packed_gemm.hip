@@ -479,6 +479,214 @@ __global__ __launch_bounds__(256) void unpack_weight_kernel(uint16_t* __restrict
   }
 }
 
+// ---------------------------------------------------------------------------
+// "pg32": the tile of packed_gemm_kernel with 32-deep stages in an S-slot LDS ring
+// (BM x BN x 32 per slot, S = 5 for 256 x 256: the whole 160 KiB), so S - 1 stages
+// (4 x 32 KiB for 256 x 256) are in flight while one computes -- packed_gemm_kernel's
+// 64-deep stages fit two slots and keep ONE stage in flight, which at one workgroup
+// per CU leaves the DMA latency exposed at every k-step (0.44-1.1 PF/s at 129-512
+// rows, profiles/pg_probe_192_r04.log).  One raw s_barrier per stage; the slot a
+// stage is loaded into was last read one stage earlier, and every wave consumed
+// those reads in its MFMAs before it reached the barrier.
+//   * A (x rows): 16 rows x 64 B per DMA instruction, the 16-B chunk c of local row
+//     r at slot c ^ f[(r >> 2) & 3], f = {0, 2, 3, 1}: the four ds_read_b128 lane
+//     groups of an A fragment (lane (g, r) reads row r, chunk g) then hit 16
+//     distinct 16-B bank slots (conflict-free); the swizzle is applied on the
+//     per-lane SOURCE address (the DMA destination is lane-linear).
+//   * B (packed W): the two 32-deep halves of a 64-deep fragment block are
+//     contiguous, so stage t of a column tile is 1 KiB at element offset 512 t;
+//     the LDS image is in fragment order (lane l reads 16 B at 16 l).
+//   * 8 waves as 2 (M) x 4 (N), each MT x NT 16 x 16 tiles, v_mfma_f32_16x16x32_bf16.
+//   * bf16 / SiLU epilogues go through LDS (rows padded to 144 / 80 B, conflict
+//     free) and leave as 16-B row stores; fp32 slabs are stored directly.
+__device__ __forceinline__ int pg32_swz(int rq) { return (0x1320 >> (4 * (rq & 3))) & 3; }
+
+template <int PW, int D>
+__device__ __forceinline__ void pg32_wait(int ahead) {
+  // retire everything but `ahead` stages (PW DMA instructions each) of this wave
+  if constexpr (D >= 4) {
+    if (ahead >= 3) { vm_wait<3 * PW>(); return; }
+  }
+  if constexpr (D >= 3) {
+    if (ahead >= 2) { vm_wait<2 * PW>(); return; }
+  }
+  if constexpr (D >= 2) {
+    if (ahead >= 1) { vm_wait<PW>(); return; }
+  }
+  vm_wait<0>();
+}
+
+template <int MT, int NT, int S, int EPI>
+__global__ __launch_bounds__(512, 1) void pg32_kernel(
+    const uint16_t* __restrict__ x, int x_stride, int M, const uint16_t* __restrict__ wpk, int N,
+    int K, int k_slice, uint16_t* __restrict__ out, int out_stride, float* __restrict__ ws) {
+  constexpr int BM = 32 * MT, BN = 64 * NT;
+  constexpr int A_BYTES = BM * 64, B_BYTES = BN * 64, SLOT = A_BYTES + B_BYTES;
+  constexpr int A_INST = BM / 16, B_INST = BN / 16;   // 1 KiB DMA instructions per stage
+  constexpr int A_PW = (A_INST + 7) / 8, B_PW = (B_INST + 7) / 8;
+  constexpr int PW = A_PW + B_PW;
+  constexpr int D = S - 1;   // stages in flight ahead of the computing one
+  static_assert(S * SLOT <= 160 * 1024, "LDS");
+  static_assert(D >= 1 && D <= 5, "ring depth");
+  static_assert(EPI != kPgSilu || NT % 2 == 0, "SiLU pairs need an even NT");
+  __shared__ __attribute__((aligned(16))) uint8_t smem[S * SLOT];
+
+  const int lane = lane_id(), w = wave_id();
+  const int wm = w >> 2, wn = w & 3;
+  const int l15 = lane & 15, g = lane >> 4;
+
+  // tile id: XCD-aware bijective remap, m fastest inside an n-block (the m-tiles that
+  // read one weight slice run together on one XCD and share it through its L2)
+  const int mt_tiles = (M + BM - 1) / BM;
+  const int total = gridDim.x;
+  const int orig = blockIdx.x;
+  const int q = total / 8, r8 = total % 8, xcd = orig % 8;
+  const int wgid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + orig / 8;
+  const int tn = wgid / mt_tiles, tm = wgid % mt_tiles;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int s = blockIdx.y;
+  const int kbeg = s * k_slice;
+  const int ns = k_slice >> 5;
+  const int ksteps = K >> 6;
+  const int ntiles_all = N >> 4;
+  const uint32_t lds0 = lds_off(smem);
+
+  // per-wave DMA instructions (every wave issues A_PW + B_PW per stage; a wave
+  // without its own instruction re-issues its previous one: identical bytes)
+  const uint16_t* a_src[A_PW];
+  uint32_t a_dst[A_PW];
+#pragma unroll
+  for (int i = 0; i < A_PW; ++i) {
+    int inst = w + 8 * i;
+    if (inst >= A_INST) inst -= 8;
+    const int rl = inst * 16 + (lane >> 2);
+    const int c = (lane & 3) ^ pg32_swz(g);   // (rl & 15) >> 2 == lane >> 4
+    const int row = min(m0 + rl, M - 1);
+    a_src[i] = x + (size_t)row * x_stride + kbeg + c * 8;
+    a_dst[i] = inst * 1024;
+  }
+  const uint16_t* b_src[B_PW];
+  uint32_t b_dst[B_PW];
+#pragma unroll
+  for (int i = 0; i < B_PW; ++i) {
+    int inst = w + 8 * i;
+    if (inst >= B_INST) inst -= 8;
+    const int nt = min((n0 >> 4) + inst, ntiles_all - 1);
+    b_src[i] = wpk + ((size_t)nt * ksteps + (kbeg >> 6)) * 1024 + lane * 8;
+    b_dst[i] = A_BYTES + inst * 1024;
+  }
+  auto issue = [&](int t, uint32_t base) {
+#pragma unroll
+    for (int i = 0; i < A_PW; ++i) glds16(a_src[i] + t * 32, base + a_dst[i]);
+#pragma unroll
+    for (int i = 0; i < B_PW; ++i) glds16(b_src[i] + (size_t)t * 512, base + b_dst[i]);
+  };
+
+  pg_floatx4 acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = pg_floatx4{0.f, 0.f, 0.f, 0.f};
+
+  const uint32_t a_off = (wm * MT) * 1024 + l15 * 64 + ((g ^ pg32_swz(l15 >> 2)) * 16);
+  const uint32_t b_off = A_BYTES + (wn * NT) * 1024 + lane * 16;
+
+#pragma unroll
+  for (int t = 0; t < D; ++t)
+    if (t < ns) issue(t, lds0 + t * SLOT);
+
+  int slot = 0;        // slot of stage t
+  int islot = D % S;   // slot of stage t + D
+  for (int t = 0; t < ns; ++t) {
+    pg32_wait<PW, D>(min(D - 1, ns - 1 - t));
+    __builtin_amdgcn_s_barrier();
+    if (t + D < ns) issue(t + D, lds0 + islot * SLOT);
+    const uint32_t base = lds0 + slot * SLOT;
+    uint4 bf[NT];
+#pragma unroll
+    for (int j = 0; j < NT; ++j) bf[j] = ds_read16(base + b_off + j * 1024);
+    uint4 af[MT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i) af[i] = ds_read16(base + a_off + i * 1024);
+    static_for<0, MT>([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      lgkm_wait<MT - 1 - i>();
+      dep(af[i]);
+      if constexpr (i == 0) {
+#pragma unroll
+        for (int j = 0; j < NT; ++j) dep(bf[j]);
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pg_frag(af[i]), pg_frag(bf[j]),
+                                                            acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    });
+    slot = slot + 1 == S ? 0 : slot + 1;
+    islot = islot + 1 == S ? 0 : islot + 1;
+  }
+
+  // epilogue: C layout, lane (g, l15) holds rows 4g..4g+3 of column l15 of each tile
+  const int mw = m0 + wm * MT * 16;
+  const int nw = n0 + wn * NT * 16;
+  if constexpr (EPI == kPgSlab) {
+    float* slab = ws + (size_t)s * M * N;
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const int n = nw + 16 * j + l15;
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          const int m = mw + 16 * i + 4 * g + rr;
+          if (m < M && n < N) slab[(size_t)m * N + n] = acc[i][j][rr];
+        }
+      }
+    return;
+  }
+  // bf16 rows through LDS: this wave's (16 MT) x OC tile, rows padded to RS bytes
+  constexpr int OC = EPI == kPgSilu ? 8 * NT : 16 * NT;   // output columns per wave
+  constexpr int RS = OC * 2 + 16;
+  static_assert(8 * 16 * MT * RS <= S * SLOT, "epilogue staging");
+  __syncthreads();   // every wave is past its last fragment read; no DMA in flight
+  uint8_t* sw = smem + w * (16 * MT * RS);
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int row = 16 * i + 4 * g + rr;
+      if constexpr (EPI == kPgSilu) {
+#pragma unroll
+        for (int j = 0; j < NT; j += 2) {
+          const float gv = acc[i][j][rr], uv = acc[i][j + 1][rr];
+          *reinterpret_cast<uint16_t*>(sw + row * RS + ((j >> 1) * 16 + l15) * 2) =
+              f32_to_bf16(gv / (1.f + __expf(-gv)) * uv);
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+          *reinterpret_cast<uint16_t*>(sw + row * RS + (16 * j + l15) * 2) =
+              f32_to_bf16(acc[i][j][rr]);
+      }
+    }
+  // the wave reads back only its own staging rows (no other wave touches them)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  constexpr int CPR = OC / 8;             // 16-B chunks per output row
+  constexpr int RPI = 64 / CPR;           // rows per wave instruction
+  const int out_cols = EPI == kPgSilu ? (N >> 1) : N;
+  const int oc0 = EPI == kPgSilu ? (nw >> 1) : nw;
+#pragma unroll
+  for (int r0 = 0; r0 < 16 * MT; r0 += RPI) {
+    const int row = r0 + lane / CPR, ch = lane % CPR;
+    const uint4 v = *reinterpret_cast<const uint4*>(sw + row * RS + ch * 16);
+    const int m = mw + row, c = oc0 + ch * 8;
+    if (m < M && c < out_cols)
+      *reinterpret_cast<uint4*>(out + (size_t)m * out_stride + c) = v;
+  }
+}
+
 }  // namespace ft
 
 // cfg: 0 = 256x256 tile (2x4 waves of 128x64, 2 LDS slots), 1 = 128x256 (2x4 waves
@@ -504,10 +712,19 @@ extern "C" int ft_packed_gemm(const void* x, int x_stride, int M, const void* wp
     case 4: bm = 256; bn = 256; break;
     case 5: bm = 192; bn = 256; break;
     case 6: bm = 192; bn = 128; break;
+    case 10: bm = 256; bn = 256; break;
+    case 11: bm = 192; bn = 256; break;
+    case 12: bm = 128; bn = 256; break;
+    case 13: bm = 256; bn = 128; break;
+    case 14: bm = 64; bn = 256; break;
     default: return -5;
   }
   const int tiles = ((M + bm - 1) / bm) * ((N + bn - 1) / bn);
   dim3 grid(tiles, splits), block(cfg == 4 ? 256 : 512);
+  if (cfg >= 10) {
+    // pg32 (BK 32 ring): bf16 / SiLU epilogues store 16-B row chunks
+    if (epi != 1 && (out_stride % 8 != 0 || (reinterpret_cast<uintptr_t>(out) & 15) != 0)) return -6;
+  }
 #define FT_PG(CFG, WM, WN, MT, NT, S)                                                          \
   if (cfg == CFG) {                                                                            \
     if (epi == 0)                                                                              \
@@ -548,6 +765,28 @@ extern "C" int ft_packed_gemm(const void* x, int x_stride, int M, const void* wp
   FT_PG(5, 2, 4, 6, 4, 2)
   FT_PG(6, 4, 2, 3, 4, 3)
 #undef FT_PG
+#define FT_PG32(CFG, MT, NT, S)                                                              \
+  if (cfg == CFG) {                                                                          \
+    if (epi == 0)                                                                            \
+      hipLaunchKernelGGL((ft::pg32_kernel<MT, NT, S, ft::kPgStore>), grid, block, 0, stream, \
+                         (const uint16_t*)x, x_stride, M, (const uint16_t*)wpk, N, K,        \
+                         k_slice, (uint16_t*)out, out_stride, ws);                           \
+    else if (epi == 1)                                                                       \
+      hipLaunchKernelGGL((ft::pg32_kernel<MT, NT, S, ft::kPgSlab>), grid, block, 0, stream,  \
+                         (const uint16_t*)x, x_stride, M, (const uint16_t*)wpk, N, K,        \
+                         k_slice, (uint16_t*)out, out_stride, ws);                           \
+    else                                                                                     \
+      hipLaunchKernelGGL((ft::pg32_kernel<MT, NT, S, ft::kPgSilu>), grid, block, 0, stream,  \
+                         (const uint16_t*)x, x_stride, M, (const uint16_t*)wpk, N, K,        \
+                         k_slice, (uint16_t*)out, out_stride, ws);                           \
+    return static_cast<int>(hipGetLastError());                                              \
+  }
+  FT_PG32(10, 8, 4, 5)
+  FT_PG32(11, 6, 4, 5)
+  FT_PG32(12, 4, 4, 6)
+  FT_PG32(13, 8, 2, 6)
+  FT_PG32(14, 2, 4, 6)
+#undef FT_PG32
   return -5;
 }
 

@@ -25,13 +25,14 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(uint16_t* __restrict__ qkv
                                                       const int* __restrict__ slot_mapping,
                                                       uint16_t* __restrict__ k_cache,
                                                       uint16_t* __restrict__ v_cache, int nq,
-                                                      int nkv, int block_size) {
+                                                      int nkv, int block_size, int cos_rows,
+                                                      int num_slots) {
   constexpr int HALF = D / 2;
   constexpr int CPH = HALF / 8;  // 8-pair chunks per head
   const int t = blockIdx.x;
-  const int pos = FT_CHECK_IDX(positions[t], FT_LIM_COS, kCkPosition, t);
+  const int pos = FT_CHECK_IDX(positions[t], cos_rows, kCkPosition, t);
   int slot = slot_mapping[t];
-  if (slot >= 0) slot = FT_CHECK_IDX(slot, FT_LIM_SLOTS, kCkSlot, t);
+  if (slot >= 0) slot = FT_CHECK_IDX(slot, num_slots, kCkSlot, t);
   uint16_t* row = qkv + (size_t)t * qkv_stride;
   const float* cs = cos_sin + (size_t)pos * D;
 
@@ -94,17 +95,18 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(uint16_t* __restrict__ qkv
 extern "C" int ft_rope_kv_write(void* qkv, int qkv_stride, const int* positions,
                                 const float* cos_sin, const int* slot_mapping, void* k_cache,
                                 void* v_cache, int tokens, int nq, int nkv, int head_dim,
-                                int block_size, hipStream_t stream) {
+                                int block_size, int cos_rows, int num_slots,
+                                hipStream_t stream) {
   if (tokens <= 0) return 0;
   dim3 grid(tokens), block(256);
   if (head_dim == 128) {
     hipLaunchKernelGGL(ft::rope_kv_kernel<128>, grid, block, 0, stream, (uint16_t*)qkv,
                        qkv_stride, positions, cos_sin, slot_mapping, (uint16_t*)k_cache,
-                       (uint16_t*)v_cache, nq, nkv, block_size);
+                       (uint16_t*)v_cache, nq, nkv, block_size, cos_rows, num_slots);
   } else if (head_dim == 64) {
     hipLaunchKernelGGL(ft::rope_kv_kernel<64>, grid, block, 0, stream, (uint16_t*)qkv,
                        qkv_stride, positions, cos_sin, slot_mapping, (uint16_t*)k_cache,
-                       (uint16_t*)v_cache, nq, nkv, block_size);
+                       (uint16_t*)v_cache, nq, nkv, block_size, cos_rows, num_slots);
   } else {
     return -1;
   }

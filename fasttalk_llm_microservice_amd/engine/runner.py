@@ -202,14 +202,14 @@ class ModelRunner:
         self.num_blocks = self._decide_num_blocks()
         self.kv = self.model.allocate_kv_cache(self.num_blocks, self.bs)
         # FT_KERNEL_CHECKS=1: the bounds-checked kernel build validates every index it
-        # is handed against these limits; the word is read after each step (_wait)
+        # is handed against the tensors of the launch (this pool's blocks, the rotary
+        # table's rows, the vocab) and reports into this word, read after each step
         self.d_check: Optional[torch.Tensor] = None
         if self.is_gpu and getattr(ops.native(), "kernel_checks", False):
             self.d_check = torch.zeros(4, dtype=torch.int32, device=self.device)
-            ops.native().set_kernel_checks(self.d_check, self.num_blocks, self.bs,
-                                           int(self.model.cos_sin.shape[0]), int(self.mcfg.vocab_size))
-            log.warning("FT_KERNEL_CHECKS: bounds-checked kernels (num_blocks=%d, block_size=%d, "
-                        "rotary rows=%d, vocab=%d)", self.num_blocks, self.bs,
+            ops.native().set_kernel_checks(self.d_check)
+            log.warning("FT_KERNEL_CHECKS: bounds-checked kernels (KV pool %d blocks x %d, "
+                        "rotary rows %d, vocab %d)", self.num_blocks, self.bs,
                         self.model.cos_sin.shape[0], self.mcfg.vocab_size)
         # E6 host swap pool (--swap-space): capped at 2x the device pool, allocated
         # (pinned) on the first swap-out so an idle server does not pin host memory

@@ -363,7 +363,7 @@ def kv_swap(caches, ptrs, ids: torch.Tensor, staging: torch.Tensor, to_staging: 
     flat = [c for kv in caches for c in kv]
     if staging.is_cuda:
         nblk = flat[0].shape[0]
-        native().kv_swap(ptrs, ids, staging, flat[0].numel() // nblk, to_staging)
+        native().kv_swap(ptrs, ids, staging, flat[0].numel() // nblk, to_staging, nblk)
         return
     st = staging.view(n, len(flat), -1)
     idx = ids.long()

@@ -30,7 +30,7 @@ CHILD = textwrap.dedent(r"""
     torch.manual_seed(0)
     nq, nkv, d, bs, nb = 8, 2, 128, 16, 8
     word = torch.zeros(4, dtype=torch.int32, device=dev)
-    C.set_kernel_checks(word, nb, bs, 64, 1000)
+    C.set_kernel_checks(word)
 
     def take():
         torch.cuda.synchronize()

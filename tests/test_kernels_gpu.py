@@ -735,7 +735,7 @@ def test_slab_rope_kv_residual_norm():
 
 
 @pytest.mark.parametrize("m", [65, 80, 200, 256, 300, 700])
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 5, 6])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 5, 6, 10, 11, 12, 13, 14])
 def test_packed_gemm_matches_fp32(m, cfg):
     """packed_gemm.hip (any M, on the decode kernels' packed image) vs fp32
     x W^T: bf16 store, split-K slabs (+ slab_store), odd N tails (N % 256 != 0)."""
@@ -753,7 +753,7 @@ def test_packed_gemm_matches_fp32(m, cfg):
         _close(out, ref, atol=3e-2, rtol=2e-2, msg=f"pg cfg{cfg} split-K")
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 3, 5, 6])
+@pytest.mark.parametrize("cfg", [0, 1, 3, 5, 6, 10, 11, 12, 13, 14])
 def test_packed_gemm_silu_epilogue_and_interleaved_silu(cfg):
     """gate_up in the single-image layout (interleave_gate_up(w, 1)): the GEMM's
     SiLU epilogue, silu_mul(interleaved) on its dense output and slab_silu on
