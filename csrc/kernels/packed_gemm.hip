@@ -488,6 +488,11 @@ __global__ __launch_bounds__(256) void unpack_weight_kernel(uint16_t* __restrict
 // rows, profiles/pg_probe_192_r04.log).  One raw s_barrier per stage; the slot a
 // stage is loaded into was last read one stage earlier, and every wave consumed
 // those reads in its MFMAs before it reached the barrier.
+//   * stage t is half h = t & 1 of 64-deep k-step t >> 1, and in the packed image
+//     half h of lane (g, r) holds k = 16 g + 8 h + [0, 8) of that k-step
+//     (ops.pack_weight), so the A chunk c of a stage row is x[row][64 (t >> 1) +
+//     16 c + 8 h + [0, 8)]: four 16-B pieces at a 32-B stride (the other half's
+//     pieces fill the gaps one stage later, from the same L2 lines).
 //   * A (x rows): 16 rows x 64 B per DMA instruction, the 16-B chunk c of local row
 //     r at slot c ^ f[(r >> 2) & 3], f = {0, 2, 3, 1}: the four ds_read_b128 lane
 //     groups of an A fragment (lane (g, r) reads row r, chunk g) then hit 16
@@ -562,7 +567,7 @@ __global__ __launch_bounds__(512, 1) void pg32_kernel(
     const int rl = inst * 16 + (lane >> 2);
     const int c = (lane & 3) ^ pg32_swz(g);   // (rl & 15) >> 2 == lane >> 4
     const int row = min(m0 + rl, M - 1);
-    a_src[i] = x + (size_t)row * x_stride + kbeg + c * 8;
+    a_src[i] = x + (size_t)row * x_stride + kbeg + c * 16;
     a_dst[i] = inst * 1024;
   }
   const uint16_t* b_src[B_PW];
@@ -577,7 +582,7 @@ __global__ __launch_bounds__(512, 1) void pg32_kernel(
   }
   auto issue = [&](int t, uint32_t base) {
 #pragma unroll
-    for (int i = 0; i < A_PW; ++i) glds16(a_src[i] + t * 32, base + a_dst[i]);
+    for (int i = 0; i < A_PW; ++i) glds16(a_src[i] + (t >> 1) * 64 + (t & 1) * 8, base + a_dst[i]);
 #pragma unroll
     for (int i = 0; i < B_PW; ++i) glds16(b_src[i] + (size_t)t * 512, base + b_dst[i]);
   };
