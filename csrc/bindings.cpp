@@ -47,6 +47,9 @@ int ft_w4_dequant(const uint32_t* wq, const void* sz, void* out, int N, int K, h
 int ft_w4_gemm_xr(const void* x, int x_stride, int M, const uint32_t* wq, const void* sz, int N, int K,
                   float* ws, void* out, int out_stride, int splits, int nt, int silu,
                   hipStream_t stream);
+int ft_w4_gemm_xr8(const void* x, int x_stride, int M, const uint32_t* wq, const void* sz, int N,
+                   int K, float* ws, void* out, int out_stride, int splits, int nt, int silu,
+                   hipStream_t stream);
 int ft_kv_swap(const uint64_t* ptrs_dev, int ncache, const int* ids_dev, int n, void* staging,
                long block_elems, int to_staging, int num_blocks, hipStream_t stream);
 int ft_skinny_gemm_xc(const void* x, int x_stride, int M, const void* w, int N, int K, float* ws,
@@ -391,7 +394,7 @@ void check_w4(const at::Tensor& wq, const at::Tensor& sz, int64_t N, int64_t K) 
 }
 
 void w4_gemm(at::Tensor x, at::Tensor wq, at::Tensor sz, int64_t N, c10::optional<at::Tensor> out,
-             c10::optional<at::Tensor> ws, int64_t splits, int64_t nt, bool xr, bool silu) {
+             c10::optional<at::Tensor> ws, int64_t splits, int64_t nt, int64_t xr, bool silu) {
   check_bf16(x, "x");
   check_rows(x, "x");
   const int M = (int)x.size(0), K = (int)x.size(1);
@@ -414,6 +417,14 @@ void w4_gemm(at::Tensor x, at::Tensor wq, at::Tensor sz, int64_t N, c10::optiona
     ostride = (int)out->stride(0);
   }
   TORCH_CHECK(!silu || (xr && !ws.has_value()), "the SiLU epilogue is an xr bf16-output variant");
+  if (xr == 2) {   // 8-wave x-in-LDS variant
+    check_rc(ft_w4_gemm_xr8(x.data_ptr(), (int)x.stride(0), M,
+                            reinterpret_cast<const uint32_t*>(wq.data_ptr<int>()), sz.data_ptr(),
+                            (int)N, K, wsp, op, ostride, (int)splits, (int)nt, silu ? 1 : 0,
+                            cur_stream()),
+             "w4_gemm_xr8");
+    return;
+  }
   if (xr) {
     check_rc(ft_w4_gemm_xr(x.data_ptr(), (int)x.stride(0), M,
                            reinterpret_cast<const uint32_t*>(wq.data_ptr<int>()), sz.data_ptr(),

@@ -556,14 +556,15 @@ __global__ __launch_bounds__(512, 1) void pg32_kernel(
   const int ntiles_all = N >> 4;
   const uint32_t lds0 = lds_off(smem);
 
-  // per-wave DMA instructions (every wave issues A_PW + B_PW per stage; a wave
-  // without its own instruction re-issues its previous one: identical bytes)
+  // per-wave DMA instructions (every wave issues A_PW + B_PW per stage, so the
+  // counted vmcnt waits are uniform; a wave without an instruction of its own
+  // re-issues one of another wave: the same bytes to the same place)
   const uint16_t* a_src[A_PW];
   uint32_t a_dst[A_PW];
 #pragma unroll
   for (int i = 0; i < A_PW; ++i) {
     int inst = w + 8 * i;
-    if (inst >= A_INST) inst -= 8;
+    if (inst >= A_INST) inst %= A_INST;
     const int rl = inst * 16 + (lane >> 2);
     const int c = (lane & 3) ^ pg32_swz(g);   // (rl & 15) >> 2 == lane >> 4
     const int row = min(m0 + rl, M - 1);
@@ -575,7 +576,7 @@ __global__ __launch_bounds__(512, 1) void pg32_kernel(
 #pragma unroll
   for (int i = 0; i < B_PW; ++i) {
     int inst = w + 8 * i;
-    if (inst >= B_INST) inst -= 8;
+    if (inst >= B_INST) inst %= B_INST;
     const int nt = min((n0 >> 4) + inst, ntiles_all - 1);
     b_src[i] = wpk + ((size_t)nt * ksteps + (kbeg >> 6)) * 1024 + lane * 8;
     b_dst[i] = A_BYTES + inst * 1024;

@@ -154,7 +154,7 @@ def w4_gemm(x: torch.Tensor, w: W4Weight, out=None, ws=None, splits: int = 1, nt
             xr: bool = False, silu: bool = False):
     """y = x dequant(w)^T for M <= 64 rows.  With ``ws`` the kernel leaves fp32
     slabs ([splits, M, N]) for a fused epilogue; otherwise returns bf16 ``out``.
-    ``xr``: the x-in-LDS variant (17..64 rows); ``silu``: its SiLU epilogue on a
+    ``xr``: the x-in-LDS variant (17..64 rows; 2 = its 8-wave form); ``silu``: its SiLU epilogue on a
     gate/up image interleaved in 16-row groups (returns h = silu(gate) * up)."""
     if not x.is_cuda:
         y = x @ w4_dequant(w, dtype=x.dtype).t()
@@ -166,5 +166,5 @@ def w4_gemm(x: torch.Tensor, w: W4Weight, out=None, ws=None, splits: int = 1, nt
 
     if ws is None and out is None:
         out = torch.empty(x.shape[0], w.n // 2 if silu else w.n, dtype=x.dtype, device=x.device)
-    native().w4_gemm(x, w.wq, w.sz, w.n, out, ws, splits, nt, xr, silu)
+    native().w4_gemm(x, w.wq, w.sz, w.n, out, ws, splits, nt, int(xr), silu)
     return out if ws is None else ws
