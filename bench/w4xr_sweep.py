@@ -41,7 +41,7 @@ def main():
             rows = []
             cfgs = [("reg", nt, sp) for nt in (2, 4) for sp in (1, 2, 4, 8)] + \
                    [("xr", nt, sp) for nt in (1, 2, 4) for sp in (1, 2, 4, 7, 8, 14)] + \
-                   [("xr8", nt, sp) for nt in (1, 2) for sp in (1, 2, 4, 7, 8)]
+                   [("xr8", 1, sp) for sp in (1, 2, 4, 7, 8)]
             for kind, nt, sp in cfgs:
                 xr = {"reg": 0, "xr": 1, "xr8": 2}[kind]
                 kq = 512 if xr else 128
@@ -66,7 +66,7 @@ def main():
                 hout = torch.empty(m, n // 2, device=dev).bfloat16()
                 fn = lambda W: (lambda: Q.w4_gemm(x, W, out=hout, nt=2, xr=True, silu=True))
                 rows.append((graph_time([fn(W) for W in seq]), "xr-silu", 2, 1, 0.0))
-                fn = lambda W: (lambda: Q.w4_gemm(x, W, out=hout, nt=2, xr=2, silu=True))
+                fn = lambda W: (lambda: Q.w4_gemm(x, W, out=hout, nt=1, xr=2, silu=True))
                 rows.append((graph_time([fn(W) for W in seq]), "xr8-silu", 2, 1, 0.0))
             rows.sort()
             best = "  ".join(f"{kd}{nt}/{sp}={t:.1f}" + (f"(err {e:.0e})" if e > 2e-2 else "")

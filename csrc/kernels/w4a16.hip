@@ -25,6 +25,7 @@
 // Prefill (M > 64) dequantizes one projection into a bf16 scratch with
 // w4_dequant_kernel and runs the library GEMM.
 #include "ft_common.h"
+#include "ft_lds.h"
 
 #include <type_traits>
 
@@ -349,35 +350,34 @@ __global__ __launch_bounds__(256, 1) void w4_xr_kernel(
 
 
 // ---------------------------------------------------------------------------
-// "xr8": the xr kernel on 8-wave workgroups (two waves per SIMD) with the K range
-// split inside the workgroup, for 33..64 rows.  Profile of xr at 50 rows
-// (profiles/w4_pmc_r05.txt): one wave per SIMD, each holding one 512-wide chunk of
-// its weight fragments in flight (32 KiB per CU), streams 1.0-1.6 TB/s of int4 --
-// the MFMA + dequant work (~10 us for gate_up) waits on the weight stream.  Here:
-//   * waves w and w + 4 share column group w & 3 (16 NT columns) and split each
-//     chunk's 4 groups between them (kh = w >> 2 takes groups 2 kh, 2 kh + 1), so a
-//     SIMD interleaves two waves' MFMA / dequant / loads;
-//   * each wave keeps TWO chunks of its weight fragments in flight (register ring
-//     depth 2: 64 KiB of int4 per CU in flight);
-//   * x staging is shared by all 512 threads (half a 128-k run each, the run's sum
-//     combined across the lane pair);
-//   * at the end the kh = 1 waves hand their accumulators to their kh = 0 partners
-//     through LDS, which apply the epilogue (bf16 / fp32 slab / SiLU pairs).
+// "xr8": the x-in-LDS W4 GEMM rebuilt from its PMC profile (gate_up at 50 rows,
+// profiles/w4_pmc_r05.txt: 8.1k VALU per wave against 1k MFMAs -- the MFMA pipe 18%
+// busy -- and 38% of the wave cycles waiting on memory / barriers, one wave per SIMD):
+//   * x chunks go global -> LDS by LDS-DMA (global_load_lds, swizzle on the source
+//     address): no staging registers and no staging VALU;
+//   * the zero-point term needs x . 1 per (row, group): computed by MFMAs against a
+//     ones operand (the MFMA pipe has the room) instead of VALU sums at staging;
+//   * 8 waves (two per SIMD): waves w and w + 4 share column group w & 3 (16 NT
+//     columns) and split each 512-wide chunk's four groups (kh = w >> 2 takes groups
+//     2 kh, 2 kh + 1); the kh = 1 sums reach their partners through LDS at the end;
+//   * each wave keeps two chunks of its weight fragments in flight (register ring of
+//     depth 2), 64 KiB of int4 per CU.
+// Epilogues as xr: bf16 / fp32 slabs ws[s][m][n] / SiLU of interleaved gate-up pairs.
 template <int MT, int NT, int EPI>
 __global__ __launch_bounds__(512, 1) void w4_xr8_kernel(
     const uint16_t* __restrict__ x, int x_stride, int M, const uint32_t* __restrict__ wq,
     const float2* __restrict__ sz, int K, float* __restrict__ ws, uint16_t* __restrict__ out,
     int out_stride, int N, int k_slice) {
   constexpr bool SILU = EPI == 1;
-  static_assert(!SILU || NT % 2 == 0, "SiLU pairs a gate tile with its up tile");
+  // SiLU pairs a gate tile with its up tile: inside a wave (NT even) or, with NT 1,
+  // across the column groups cg (gate, even) and cg + 1 (up) of the workgroup
+  static_assert(!SILU || NT % 2 == 0 || NT == 1, "SiLU pairing");
   constexpr int KC = 512, NG = KC / 128;     // k per chunk, groups per chunk
   constexpr int GW = NG / 2;                 // groups per wave per chunk
   constexpr int ROWS = 16 * MT;
-  constexpr int XR = 8;                      // 16-B loads per staging thread (half a group run)
-  static_assert(ROWS * NG * 2 <= 512, "staging threads");
-  __shared__ __attribute__((aligned(16))) uint16_t s_x[2][ROWS * KC];
-  __shared__ __attribute__((aligned(16))) float s_xs[2][NG][ROWS];
-  const int tid = threadIdx.x;
+  constexpr int XI = ROWS / 8;               // x DMA instructions (1 KiB = one row) per wave
+  constexpr int SLOT_BYTES = ROWS * KC * 2;
+  __shared__ __attribute__((aligned(16))) uint8_t s_x[2 * SLOT_BYTES];
   const int lane = lane_id(), wave = wave_id();
   const int l15 = lane & 15, g = lane >> 4;
   const int cg = wave & 3, kh = wave >> 2;
@@ -387,12 +387,22 @@ __global__ __launch_bounds__(512, 1) void w4_xr8_kernel(
   const int nch = k_slice / KC;
   const int groups_total = K >> 7;
   const int grp0 = kbeg >> 7;
+  const uint32_t lds0 = lds_off(s_x);
 
-  // staging: thread -> (row, group, half) of a chunk; pairs of lanes share a run
-  const bool stager = tid < ROWS * NG * 2;
-  const int run = tid >> 1, part = tid & 1;
-  const int srow = run / NG, sgrp = run % NG;
-  const uint16_t* xsrc = x + (size_t)min(srow, M - 1) * x_stride + kbeg + sgrp * 128 + part * 64;
+  // x DMA: wave w moves rows w + 8 i; lane L fills LDS slot L of the row, which holds
+  // 16-B chunk (L & ~7) | ((L & 7) ^ (row & 7)) (the xr swizzle)
+  const uint16_t* xsrc[XI];
+#pragma unroll
+  for (int i = 0; i < XI; ++i) {
+    const int row = wave + 8 * i;
+    const int ch = (lane & ~7) | ((lane & 7) ^ (row & 7));
+    xsrc[i] = x + (size_t)min(row, M - 1) * x_stride + kbeg + ch * 8;
+  }
+  auto issue_x = [&](int c) {
+    const uint32_t base = lds0 + (c & 1) * SLOT_BYTES;
+#pragma unroll
+    for (int i = 0; i < XI; ++i) glds16(xsrc[i] + (size_t)c * KC, base + (wave + 8 * i) * (KC * 2));
+  };
 
   const uint32_t* wp[NT];
   const float2* sp[NT];
@@ -409,15 +419,8 @@ __global__ __launch_bounds__(512, 1) void w4_xr8_kernel(
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[i][j] = w4_floatx4{0.f, 0.f, 0.f, 0.f};
 
-  w4_u32x4 xr[XR];
   w4_u32x4 wr[2][GW][NT];     // ring: chunk c's fragments in slot c & 1
   float2 szr[2][GW][NT];
-  auto load_x = [&](int c) {
-    if (stager) {
-#pragma unroll
-      for (int p = 0; p < XR; ++p) xr[p] = *reinterpret_cast<const w4_u32x4*>(xsrc + (size_t)c * KC + p * 8);
-    }
-  };
   auto load_w = [&](int c, int sl) {
 #pragma unroll
     for (int q = 0; q < GW; ++q)
@@ -428,31 +431,28 @@ __global__ __launch_bounds__(512, 1) void w4_xr8_kernel(
         szr[sl][q][j] = sp[j][(size_t)gi * 16];
       }
   };
-  load_x(0);
+  const uint4 ones4 = make_uint4(0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u);
+  const w4_bf16x8 ones = __builtin_bit_cast(w4_bf16x8, ones4);
+
+  issue_x(0);
   load_w(0, 0);
   if (nch > 1) load_w(1, 1);
 
-  // chunk c from ring slot SL; MORE: chunk c + 2 exists (refill the slot after use)
+  // chunk c: weights from ring slot SL; MORE: chunk c + 2 exists (refill the slot)
   auto chunk = [&](int c, auto sl_tag, auto more_tag) {
     constexpr int SL = decltype(sl_tag)::value;
     constexpr bool MORE = decltype(more_tag)::value;
-    uint16_t* sx = s_x[c & 1];
-    if (stager) {
-      float sum = 0.f;
-#pragma unroll
-      for (int p = 0; p < XR; ++p) {
-        const int ch = sgrp * 16 + part * 8 + p;
-        const int slot = (ch & ~7) | ((ch & 7) ^ (srow & 7));
-        *reinterpret_cast<w4_u32x4*>(&sx[srow * KC + slot * 8]) = xr[p];
-        float f[8];
-        load8(__builtin_bit_cast(uint4, xr[p]), f);
-        sum += ((f[0] + f[1]) + (f[2] + f[3])) + ((f[4] + f[5]) + (f[6] + f[7]));
-      }
-      sum += __shfl_xor(sum, 1, 64);
-      if (part == 0) s_xs[c & 1][sgrp][srow] = sum;
-    }
-    if (c + 1 < nch) load_x(c + 1);
+    // this wave's x DMAs of chunk c landed: vmcnt counts in issue order, and only the
+    // weight loads of the ring refill (W_OPS per chunk) were issued after them --
+    // chunk 0: the prologue's two chunks; chunk c: the refill of chunk c + 1
+    constexpr int W_OPS = GW * NT * 2;   // a dwordx4 + a dwordx2 per (group, tile)
+    const int after = c == 0 ? (nch > 1 ? 2 : 1) : (c + 1 < nch ? 1 : 0);
+    if (after == 2) vm_wait<2 * W_OPS>();
+    else if (after == 1) vm_wait<W_OPS>();
+    else vm_wait<0>();
     __syncthreads();   // chunk c visible; every wave is past chunk c-1's reads of the other buffer
+    if (c + 1 < nch) issue_x(c + 1);
+    const uint8_t* sx = s_x + (c & 1) * SLOT_BYTES;
 #pragma unroll
     for (int q = 0; q < GW; ++q) {
       const int gq = kh * GW + q;
@@ -464,10 +464,14 @@ __global__ __launch_bounds__(512, 1) void w4_xr8_kernel(
         for (int h = 0; h < 4; ++h) {
           const int ch = gq * 16 + 8 * (h >> 1) + 2 * g + (h & 1);
           const int slot = (ch & ~7) | ((ch & 7) ^ (row & 7));
-          xf[h] = *reinterpret_cast<const w4_u32x4*>(&sx[row * KC + slot * 8]);
+          xf[h] = *reinterpret_cast<const w4_u32x4*>(sx + row * (KC * 2) + slot * 16);
         }
-        const float4 xs4 = *reinterpret_cast<const float4*>(&s_xs[c & 1][gq][16 * i + 4 * g]);
-        const float xs[4] = {xs4.x, xs4.y, xs4.z, xs4.w};
+        // x . 1 over the group for rows 4 g + r (C layout; every column equal)
+        w4_floatx4 xs = w4_floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int h = 0; h < 4; ++h)
+          xs = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(w4_bf16x8, xf[h]), ones, xs,
+                                                       0, 0, 0);
 #pragma unroll
         for (int j = 0; j < NT; ++j) {
           w4_floatx4 a = w4_floatx4{0.f, 0.f, 0.f, 0.f};
@@ -478,10 +482,8 @@ __global__ __launch_bounds__(512, 1) void w4_xr8_kernel(
           const float sc = szr[SL][q][j].x, zz = szr[SL][q][j].y;
 #pragma unroll
           for (int r = 0; r < 4; ++r) acc[i][j][r] = fmaf(sc, fmaf(-zz, xs[r], a[r]), acc[i][j][r]);
-          // one (row tile, column tile) block at a time: hoisting the dequantized
-          // fragments and x fragments of several blocks spilled at 2 waves / SIMD
-          __builtin_amdgcn_sched_barrier(0);
         }
+        __builtin_amdgcn_sched_barrier(0);   // one row tile's fragments live at a time
       }
     }
     if constexpr (MORE) load_w(c + 2, SL);   // two chunks ahead
@@ -491,23 +493,22 @@ __global__ __launch_bounds__(512, 1) void w4_xr8_kernel(
     chunk(c, std::integral_constant<int, 0>{}, std::true_type{});
     chunk(c + 1, std::integral_constant<int, 1>{}, std::true_type{});
   }
-  // tail: 1..3 chunks left (c even)
-  if (c + 2 < nch) {   // 3 left: c refills c + 2
+  if (c + 2 < nch) {          // three chunks left
     chunk(c, std::integral_constant<int, 0>{}, std::true_type{});
     chunk(c + 1, std::integral_constant<int, 1>{}, std::false_type{});
     chunk(c + 2, std::integral_constant<int, 0>{}, std::false_type{});
-  } else if (c + 1 < nch) {
+  } else if (c + 1 < nch) {   // two
     chunk(c, std::integral_constant<int, 0>{}, std::false_type{});
     chunk(c + 1, std::integral_constant<int, 1>{}, std::false_type{});
-  } else {
+  } else {                    // one
     chunk(c, std::integral_constant<int, 0>{}, std::false_type{});
   }
 
   // K halves: the kh = 1 waves pass their sums to the kh = 0 partners through LDS
-  __syncthreads();   // every wave is past its last x reads
-  float* red = reinterpret_cast<float*>(&s_x[0][0]);   // [4 cg][MT * NT * 4][64]
+  __syncthreads();   // every wave is past its last x reads; no DMA in flight
+  float* red = reinterpret_cast<float*>(s_x);   // [4 cg][MT * NT * 4][64]
   constexpr int NREG = MT * NT * 4;
-  static_assert(4 * NREG * 64 * 4 <= (int)sizeof(s_x), "reduction buffer");
+  static_assert(4 * NREG * 64 * 4 <= 2 * SLOT_BYTES, "reduction buffer");
   if (kh == 1) {
 #pragma unroll
     for (int i = 0; i < MT; ++i)
@@ -517,13 +518,39 @@ __global__ __launch_bounds__(512, 1) void w4_xr8_kernel(
         for (int r = 0; r < 4; ++r) red[((cg * NREG) + (i * NT + j) * 4 + r) * 64 + lane] = acc[i][j][r];
   }
   __syncthreads();
+  if (kh == 0) {
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[i][j][r] += red[((cg * NREG) + (i * NT + j) * 4 + r) * 64 + lane];
+  }
+  if constexpr (SILU && NT == 1) {
+    // the up-tile waves (odd cg) hand their sums to the gate-tile waves (cg - 1)
+    __syncthreads();   // every kh = 0 wave is done reading the partials
+    if (kh == 0 && (cg & 1)) {
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) red[((cg >> 1) * MT * 4 + i * 4 + r) * 64 + lane] = acc[i][0][r];
+    }
+    __syncthreads();
+    if (kh == 1 || (cg & 1) || n0 >= N) return;
+    const int col = (n0 >> 1) + l15;
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = 16 * i + g * 4 + r;
+        if (m < M) {
+          const float gt = acc[i][0][r], up = red[((cg >> 1) * MT * 4 + i * 4 + r) * 64 + lane];
+          out[(size_t)m * out_stride + col] = f32_to_bf16(gt / (1.f + __expf(-gt)) * up);
+        }
+      }
+    return;
+  }
   if (kh == 1 || n0 >= N) return;
-#pragma unroll
-  for (int i = 0; i < MT; ++i)
-#pragma unroll
-    for (int j = 0; j < NT; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) acc[i][j][r] += red[((cg * NREG) + (i * NT + j) * 4 + r) * 64 + lane];
   if constexpr (SILU) {
 #pragma unroll
     for (int j = 0; j < NT; j += 2) {
@@ -655,7 +682,7 @@ extern "C" int ft_w4_gemm_xr(const void* x, int x_stride, int M, const uint32_t*
 }
 
 // "xr8" variant (33..64 rows): as ft_w4_gemm_xr (N % (64 * nt) == 0, K % (512 * splits)
-// == 0, silu: nt even, one split), 8-wave workgroups.
+// == 0, silu: one split, nt 1 or even), 8-wave workgroups.
 extern "C" int ft_w4_gemm_xr8(const void* x, int x_stride, int M, const uint32_t* wq,
                               const void* sz, int N, int K, float* ws, void* out, int out_stride,
                               int splits, int nt, int silu, hipStream_t stream) {
@@ -665,7 +692,7 @@ extern "C" int ft_w4_gemm_xr8(const void* x, int x_stride, int M, const uint32_t
   if (K % (512 * splits) != 0) return -3;
   if (splits > 1 && (ws == nullptr || silu)) return -4;
   if (ws == nullptr && out == nullptr) return -6;
-  if (silu && nt % 2) return -7;
+  if (silu && nt % 2 && nt != 1) return -7;
   const int mt = (M + 15) / 16;
   dim3 grid(N / (64 * nt), splits), block(512);
   const int k_slice = K / splits;
@@ -676,10 +703,11 @@ extern "C" int ft_w4_gemm_xr8(const void* x, int x_stride, int M, const uint32_t
                        (uint16_t*)out, out_stride, N, k_slice);                              \
     return static_cast<int>(hipGetLastError());                                              \
   }
+  // nt 1 only: with two column tiles per wave the 48-64-row forms need more than the
+  // 256 registers of a two-waves-per-SIMD kernel (the compiler spilled 100-270)
 #define FT_W4X8_M(NT_, E_) FT_W4X8(2, NT_, E_) FT_W4X8(3, NT_, E_) FT_W4X8(4, NT_, E_)
   FT_W4X8_M(1, 0)
-  FT_W4X8_M(2, 0)
-  FT_W4X8_M(2, 1)
+  FT_W4X8_M(1, 1)
 #undef FT_W4X8_M
 #undef FT_W4X8
   return -5;
