@@ -363,6 +363,27 @@ __global__ __launch_bounds__(256, 1) void w4_xr_kernel(
 //   * each wave keeps two chunks of its weight fragments in flight (register ring of
 //     depth 2), 64 KiB of int4 per CU.
 // Epilogues as xr: bf16 / fp32 slabs ws[s][m][n] / SiLU of interleaved gate-up pairs.
+// weight-ring loads in inline asm: hidden from hipcc's waitcnt pass, which would
+// otherwise wait for the NEXT chunk's fragments (it cannot see the x DMAs issued
+// after them and counts vmcnt as if they were not there); the kernel waits with
+// counted vmcnt itself and ties the values to those waits with dep()
+__device__ __forceinline__ w4_u32x4 w4_gload16nt(const void* p) {
+  w4_u32x4 v;
+  asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+__device__ __forceinline__ float2 w4_gload8(const void* p) {
+  u32x2_t v;
+  asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+  return __builtin_bit_cast(float2, v);
+}
+__device__ __forceinline__ void w4_dep(w4_u32x4& v) { asm volatile("" : "+v"(v)); }
+__device__ __forceinline__ void w4_dep(float2& v) {
+  u32x2_t t = __builtin_bit_cast(u32x2_t, v);
+  asm volatile("" : "+v"(t));
+  v = __builtin_bit_cast(float2, t);
+}
+
 template <int MT, int NT, int EPI>
 __global__ __launch_bounds__(512, 1) void w4_xr8_kernel(
     const uint16_t* __restrict__ x, int x_stride, int M, const uint32_t* __restrict__ wq,
@@ -427,8 +448,8 @@ __global__ __launch_bounds__(512, 1) void w4_xr8_kernel(
 #pragma unroll
       for (int j = 0; j < NT; ++j) {
         const int gi = c * NG + kh * GW + q;
-        wr[sl][q][j] = __builtin_nontemporal_load(reinterpret_cast<const w4_u32x4*>(wp[j] + (size_t)gi * 256));
-        szr[sl][q][j] = sp[j][(size_t)gi * 16];
+        wr[sl][q][j] = w4_gload16nt(wp[j] + (size_t)gi * 256);
+        szr[sl][q][j] = w4_gload8(sp[j] + (size_t)gi * 16);
       }
   };
   const uint4 ones4 = make_uint4(0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u);
@@ -450,7 +471,18 @@ __global__ __launch_bounds__(512, 1) void w4_xr8_kernel(
     if (after == 2) vm_wait<2 * W_OPS>();
     else if (after == 1) vm_wait<W_OPS>();
     else vm_wait<0>();
-    __syncthreads();   // chunk c visible; every wave is past chunk c-1's reads of the other buffer
+    // (the weight fragments of chunk c are older than its x DMAs: landed too)
+#pragma unroll
+    for (int q = 0; q < GW; ++q)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        w4_dep(wr[SL][q][j]);
+        w4_dep(szr[SL][q][j]);
+      }
+    lgkm_wait<0>();
+    // raw barrier: chunk c visible to every wave, every wave past chunk c-1's reads of
+    // the other buffer (consumed by its MFMAs); __syncthreads could drain the ring
+    __builtin_amdgcn_s_barrier();
     if (c + 1 < nch) issue_x(c + 1);
     const uint8_t* sx = s_x + (c & 1) * SLOT_BYTES;
 #pragma unroll
@@ -505,6 +537,7 @@ __global__ __launch_bounds__(512, 1) void w4_xr8_kernel(
   }
 
   // K halves: the kh = 1 waves pass their sums to the kh = 0 partners through LDS
+  vm_wait<0>();
   __syncthreads();   // every wave is past its last x reads; no DMA in flight
   float* red = reinterpret_cast<float*>(s_x);   // [4 cg][MT * NT * 4][64]
   constexpr int NREG = MT * NT * 4;
