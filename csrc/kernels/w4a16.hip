@@ -483,6 +483,8 @@ __global__ __launch_bounds__(512, 1) void w4_xr8_kernel(
     // raw barrier: chunk c visible to every wave, every wave past chunk c-1's reads of
     // the other buffer (consumed by its MFMAs); __syncthreads could drain the ring
     __builtin_amdgcn_s_barrier();
+    // s_barrier orders no memory for the compiler: keep this chunk's LDS reads below it
+    asm volatile("" ::: "memory");
     if (c + 1 < nch) issue_x(c + 1);
     const uint8_t* sx = s_x + (c & 1) * SLOT_BYTES;
 #pragma unroll

@@ -469,7 +469,8 @@ def test_w4_gemm_matches_fp32(m, n, k, nt, splits):
 @pytest.mark.parametrize("xr", [1, 2])
 @pytest.mark.parametrize("m", [17, 33, 50, 64])
 @pytest.mark.parametrize("n,k,nt,splits", [(1024, 4096, 1, 1), (2048, 4096, 2, 2), (2048, 4096, 4, 1),
-                                           (1024, 14336, 1, 4), (2048, 14336, 2, 7)])
+                                           (1024, 14336, 1, 4), (2048, 14336, 2, 7),
+                                           (1024, 4096, 1, 4), (1024, 4096, 1, 8)])
 def test_w4_xr_gemm_matches_fp32(m, n, k, nt, splits, xr):
     """The x-in-LDS W4A16 variants (17..64 rows; xr 2 = 8-wave workgroups with the
     K range split between wave pairs): bf16 out and split-K fp32 slabs."""
