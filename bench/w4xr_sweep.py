@@ -41,9 +41,10 @@ def main():
             rows = []
             cfgs = [("reg", nt, sp) for nt in (2, 4) for sp in (1, 2, 4, 8)] + \
                    [("xr", nt, sp) for nt in (1, 2, 4) for sp in (1, 2, 4, 7, 8, 14)] + \
-                   [("xr8", 1, sp) for sp in (1, 2, 4, 7, 8)]
+                   [("xr8", 1, sp) for sp in (1, 2, 4, 7, 8)] + \
+                   [("xrm", nt, sp) for nt in (1, 2) for sp in (1, 2, 4, 7, 8)]
             for kind, nt, sp in cfgs:
-                xr = {"reg": 0, "xr": 1, "xr8": 2}[kind]
+                xr = {"reg": 0, "xr": 1, "xr8": 2, "xrm": 3}[kind]
                 kq = 512 if xr else 128
                 if n % ((64 if xr else 16) * nt) or k % (kq * sp) or sp * m * n > ws.numel():
                     continue
@@ -68,6 +69,8 @@ def main():
                 rows.append((graph_time([fn(W) for W in seq]), "xr-silu", 2, 1, 0.0))
                 fn = lambda W: (lambda: Q.w4_gemm(x, W, out=hout, nt=1, xr=2, silu=True))
                 rows.append((graph_time([fn(W) for W in seq]), "xr8-silu", 2, 1, 0.0))
+                fn = lambda W: (lambda: Q.w4_gemm(x, W, out=hout, nt=2, xr=3, silu=True))
+                rows.append((graph_time([fn(W) for W in seq]), "xrm-silu", 2, 1, 0.0))
             rows.sort()
             best = "  ".join(f"{kd}{nt}/{sp}={t:.1f}" + (f"(err {e:.0e})" if e > 2e-2 else "")
                              for t, kd, nt, sp, e in rows)

@@ -45,7 +45,7 @@ int ft_w4_gemm(const void* x, int x_stride, int M, const uint32_t* wq, const voi
                float* ws, void* out, int out_stride, int splits, int nt, hipStream_t stream);
 int ft_w4_dequant(const uint32_t* wq, const void* sz, void* out, int N, int K, hipStream_t stream);
 int ft_w4_gemm_xr(const void* x, int x_stride, int M, const uint32_t* wq, const void* sz, int N, int K,
-                  float* ws, void* out, int out_stride, int splits, int nt, int silu,
+                  float* ws, void* out, int out_stride, int splits, int nt, int silu, int xsm,
                   hipStream_t stream);
 int ft_w4_gemm_xr8(const void* x, int x_stride, int M, const uint32_t* wq, const void* sz, int N,
                    int K, float* ws, void* out, int out_stride, int splits, int nt, int silu,
@@ -426,10 +426,11 @@ void w4_gemm(at::Tensor x, at::Tensor wq, at::Tensor sz, int64_t N, c10::optiona
     return;
   }
   if (xr) {
+    // xr 1: sums by VALU while staging; 3: sums by MFMA against ones
     check_rc(ft_w4_gemm_xr(x.data_ptr(), (int)x.stride(0), M,
                            reinterpret_cast<const uint32_t*>(wq.data_ptr<int>()), sz.data_ptr(),
                            (int)N, K, wsp, op, ostride, (int)splits, (int)nt, silu ? 1 : 0,
-                           cur_stream()),
+                           xr == 3 ? 1 : 0, cur_stream()),
              "w4_gemm_xr");
     return;
   }

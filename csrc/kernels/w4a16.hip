@@ -199,7 +199,9 @@ __global__ __launch_bounds__(256) void w4_skinny_kernel(
 // EPI 1: SiLU epilogue on a gate/up image interleaved in 16-row groups
 // (ops.quant.pack_w4 of interleave_gate_up(w, 1)): with NT = 2 a wave holds a gate
 // tile and its up tile and writes h = silu(g) * u (N/2 columns, bf16).
-template <int MT, int NT, int EPI>
+// XSM: the per-(row, group) sums x . 1 by MFMAs against a ones operand instead of
+// VALU adds while staging (PMC: the staging sums were ~30% of the kernel's VALU)
+template <int MT, int NT, int EPI, bool XSM = false>
 __global__ __launch_bounds__(256, 1) void w4_xr_kernel(
     const uint16_t* __restrict__ x, int x_stride, int M, const uint32_t* __restrict__ wq,
     const float2* __restrict__ sz, int K, float* __restrict__ ws, uint16_t* __restrict__ out,
@@ -272,11 +274,13 @@ __global__ __launch_bounds__(256, 1) void w4_xr_kernel(
         const int ch = sgrp * 16 + p;
         const int slot = (ch & ~7) | ((ch & 7) ^ (srow & 7));
         *reinterpret_cast<w4_u32x4*>(&sx[srow * KC + slot * 8]) = xr[p];
-        float f[8];
-        load8(__builtin_bit_cast(uint4, xr[p]), f);
-        sum += ((f[0] + f[1]) + (f[2] + f[3])) + ((f[4] + f[5]) + (f[6] + f[7]));
+        if constexpr (!XSM) {
+          float f[8];
+          load8(__builtin_bit_cast(uint4, xr[p]), f);
+          sum += ((f[0] + f[1]) + (f[2] + f[3])) + ((f[4] + f[5]) + (f[6] + f[7]));
+        }
       }
-      s_xs[c & 1][sgrp][srow] = sum;
+      if constexpr (!XSM) s_xs[c & 1][sgrp][srow] = sum;
     }
     if constexpr (MORE) load_x(c + 1);
     __syncthreads();   // chunk c visible; every wave is past chunk c-1's reads of the other buffer
@@ -292,8 +296,21 @@ __global__ __launch_bounds__(256, 1) void w4_xr_kernel(
           const int slot = (ch & ~7) | ((ch & 7) ^ (row & 7));
           xf[h] = *reinterpret_cast<const w4_u32x4*>(&sx[row * KC + slot * 8]);
         }
-        const float4 xs4 = *reinterpret_cast<const float4*>(&s_xs[c & 1][gq][16 * i + 4 * g]);
-        const float xs[4] = {xs4.x, xs4.y, xs4.z, xs4.w};
+        float xs[4];
+        if constexpr (XSM) {
+          const uint4 ones4 = make_uint4(0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u);
+          w4_floatx4 xm = w4_floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int h = 0; h < 4; ++h)
+            xm = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(w4_bf16x8, xf[h]),
+                                                         __builtin_bit_cast(w4_bf16x8, ones4), xm,
+                                                         0, 0, 0);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) xs[r] = xm[r];
+        } else {
+          const float4 xs4 = *reinterpret_cast<const float4*>(&s_xs[c & 1][gq][16 * i + 4 * g]);
+          xs[0] = xs4.x; xs[1] = xs4.y; xs[2] = xs4.z; xs[3] = xs4.w;
+        }
 #pragma unroll
         for (int j = 0; j < NT; ++j) {
           w4_floatx4 a = w4_floatx4{0.f, 0.f, 0.f, 0.f};
@@ -353,143 +370,98 @@ __global__ __launch_bounds__(256, 1) void w4_xr_kernel(
 // "xr8": the x-in-LDS W4 GEMM rebuilt from its PMC profile (gate_up at 50 rows,
 // profiles/w4_pmc_r05.txt: 8.1k VALU per wave against 1k MFMAs -- the MFMA pipe 18%
 // busy -- and 38% of the wave cycles waiting on memory / barriers, one wave per SIMD):
-//   * x chunks go global -> LDS by LDS-DMA (global_load_lds, swizzle on the source
-//     address): no staging registers and no staging VALU;
 //   * the zero-point term needs x . 1 per (row, group): computed by MFMAs against a
-//     ones operand (the MFMA pipe has the room) instead of VALU sums at staging;
-//   * 8 waves (two per SIMD): waves w and w + 4 share column group w & 3 (16 NT
+//     ones operand (the MFMA pipe has the room) instead of VALU sums while staging,
+//     so staging x is a plain copy (global -> registers -> LDS, 16 B per load);
+//   * 8 waves (two per SIMD): waves w and w + 4 share column group w & 3 (16
 //     columns) and split each 512-wide chunk's four groups (kh = w >> 2 takes groups
 //     2 kh, 2 kh + 1); the kh = 1 sums reach their partners through LDS at the end;
 //   * each wave keeps two chunks of its weight fragments in flight (register ring of
 //     depth 2), 64 KiB of int4 per CU.
-// Epilogues as xr: bf16 / fp32 slabs ws[s][m][n] / SiLU of interleaved gate-up pairs.
-// weight-ring loads in inline asm: hidden from hipcc's waitcnt pass, which would
-// otherwise wait for the NEXT chunk's fragments (it cannot see the x DMAs issued
-// after them and counts vmcnt as if they were not there); the kernel waits with
-// counted vmcnt itself and ties the values to those waits with dep()
-__device__ __forceinline__ w4_u32x4 w4_gload16nt(const void* p) {
-  w4_u32x4 v;
-  asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(v) : "v"(p) : "memory");
-  return v;
-}
-__device__ __forceinline__ float2 w4_gload8(const void* p) {
-  u32x2_t v;
-  asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
-  return __builtin_bit_cast(float2, v);
-}
-__device__ __forceinline__ void w4_dep(w4_u32x4& v) { asm volatile("" : "+v"(v)); }
-__device__ __forceinline__ void w4_dep(float2& v) {
-  u32x2_t t = __builtin_bit_cast(u32x2_t, v);
-  asm volatile("" : "+v"(t));
-  v = __builtin_bit_cast(float2, t);
-}
-
-template <int MT, int NT, int EPI>
+// Every load is an ordinary (compiler-visible) load, so hipcc's counted waits are
+// exact: an LDS-DMA x stage or asm weight loads (measured variants) either made the
+// compiler's waits drain the ring or let it move the asm-loaded registers before
+// they had landed.  Epilogues as xr: bf16 / fp32 slabs / SiLU, the gate / up tile
+// pair of a SiLU image on the column groups cg (gate, even) and cg + 1 (up).
+template <int MT, int EPI>
 __global__ __launch_bounds__(512, 1) void w4_xr8_kernel(
     const uint16_t* __restrict__ x, int x_stride, int M, const uint32_t* __restrict__ wq,
     const float2* __restrict__ sz, int K, float* __restrict__ ws, uint16_t* __restrict__ out,
     int out_stride, int N, int k_slice) {
   constexpr bool SILU = EPI == 1;
-  // SiLU pairs a gate tile with its up tile: inside a wave (NT even) or, with NT 1,
-  // across the column groups cg (gate, even) and cg + 1 (up) of the workgroup
-  static_assert(!SILU || NT % 2 == 0 || NT == 1, "SiLU pairing");
   constexpr int KC = 512, NG = KC / 128;     // k per chunk, groups per chunk
   constexpr int GW = NG / 2;                 // groups per wave per chunk
   constexpr int ROWS = 16 * MT;
-  constexpr int XI = ROWS / 8;               // x DMA instructions (1 KiB = one row) per wave
-  constexpr int SLOT_BYTES = ROWS * KC * 2;
-  __shared__ __attribute__((aligned(16))) uint8_t s_x[2 * SLOT_BYTES];
+  constexpr int CPR = KC / 8;                // 16-B chunks per x row per chunk
+  constexpr int XL = ROWS * CPR / 512;       // x loads per thread per chunk
+  __shared__ __attribute__((aligned(16))) uint16_t s_x[2][ROWS * KC];
+  const int tid = threadIdx.x;
   const int lane = lane_id(), wave = wave_id();
   const int l15 = lane & 15, g = lane >> 4;
   const int cg = wave & 3, kh = wave >> 2;
-  const int n0 = (blockIdx.x * 4 + cg) * (16 * NT);
+  const int n0 = (blockIdx.x * 4 + cg) * 16;
   const int s = blockIdx.y;
   const int kbeg = s * k_slice;
   const int nch = k_slice / KC;
   const int groups_total = K >> 7;
   const int grp0 = kbeg >> 7;
-  const uint32_t lds0 = lds_off(s_x);
 
-  // x DMA: wave w moves rows w + 8 i; lane L fills LDS slot L of the row, which holds
-  // 16-B chunk (L & ~7) | ((L & 7) ^ (row & 7)) (the xr swizzle)
-  const uint16_t* xsrc[XI];
+  int xoff[XL];   // 32-bit element offsets (half the registers of pointers)
 #pragma unroll
-  for (int i = 0; i < XI; ++i) {
-    const int row = wave + 8 * i;
-    const int ch = (lane & ~7) | ((lane & 7) ^ (row & 7));
-    xsrc[i] = x + (size_t)min(row, M - 1) * x_stride + kbeg + ch * 8;
+  for (int p = 0; p < XL; ++p) {
+    const int e = tid + 512 * p;
+    xoff[p] = min(e / CPR, M - 1) * x_stride + kbeg + (e % CPR) * 8;
   }
-  auto issue_x = [&](int c) {
-    const uint32_t base = lds0 + (c & 1) * SLOT_BYTES;
-#pragma unroll
-    for (int i = 0; i < XI; ++i) glds16(xsrc[i] + (size_t)c * KC, base + (wave + 8 * i) * (KC * 2));
-  };
+  const size_t tile = (size_t)(min(n0, N - 16) / 16) * groups_total + grp0;
+  const uint32_t* wp = wq + tile * 256 + lane * 4;
+  const float2* sp = sz + tile * 16 + l15;
 
-  const uint32_t* wp[NT];
-  const float2* sp[NT];
+  w4_floatx4 acc[MT];
 #pragma unroll
-  for (int j = 0; j < NT; ++j) {
-    const size_t tile = (size_t)(min(n0 + 16 * j, N - 16) / 16) * groups_total + grp0;
-    wp[j] = wq + tile * 256 + lane * 4;
-    sp[j] = sz + tile * 16 + l15;
-  }
+  for (int i = 0; i < MT; ++i) acc[i] = w4_floatx4{0.f, 0.f, 0.f, 0.f};
 
-  w4_floatx4 acc[MT][NT];
-#pragma unroll
-  for (int i = 0; i < MT; ++i)
-#pragma unroll
-    for (int j = 0; j < NT; ++j) acc[i][j] = w4_floatx4{0.f, 0.f, 0.f, 0.f};
-
-  w4_u32x4 wr[2][GW][NT];     // ring: chunk c's fragments in slot c & 1
-  float2 szr[2][GW][NT];
+  w4_u32x4 xr[XL];
+  w4_u32x4 wr[2][GW];         // ring: chunk c's fragments in slot c & 1
+  float2 szr[2][GW];
   auto load_w = [&](int c, int sl) {
 #pragma unroll
-    for (int q = 0; q < GW; ++q)
-#pragma unroll
-      for (int j = 0; j < NT; ++j) {
-        const int gi = c * NG + kh * GW + q;
-        wr[sl][q][j] = w4_gload16nt(wp[j] + (size_t)gi * 256);
-        szr[sl][q][j] = w4_gload8(sp[j] + (size_t)gi * 16);
-      }
+    for (int q = 0; q < GW; ++q) {
+      const int gi = c * NG + kh * GW + q;
+      wr[sl][q] = __builtin_nontemporal_load(reinterpret_cast<const w4_u32x4*>(wp + (size_t)gi * 256));
+      szr[sl][q] = sp[(size_t)gi * 16];
+    }
   };
   const uint4 ones4 = make_uint4(0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u);
   const w4_bf16x8 ones = __builtin_bit_cast(w4_bf16x8, ones4);
 
-  issue_x(0);
+#pragma unroll
+  for (int p = 0; p < XL; ++p) xr[p] = *reinterpret_cast<const w4_u32x4*>(x + xoff[p]);
   load_w(0, 0);
   if (nch > 1) load_w(1, 1);
 
-  // chunk c: weights from ring slot SL; MORE: chunk c + 2 exists (refill the slot)
+  // chunk c: x registers -> LDS buffer c & 1, next chunk's x loads, barrier, MFMAs;
+  // weights from ring slot SL, refilled with chunk c + 2 (MORE) after use
   auto chunk = [&](int c, auto sl_tag, auto more_tag) {
     constexpr int SL = decltype(sl_tag)::value;
     constexpr bool MORE = decltype(more_tag)::value;
-    // this wave's x DMAs of chunk c landed: vmcnt counts in issue order, and only the
-    // weight loads of the ring refill (W_OPS per chunk) were issued after them --
-    // chunk 0: the prologue's two chunks; chunk c: the refill of chunk c + 1
-    constexpr int W_OPS = GW * NT * 2;   // a dwordx4 + a dwordx2 per (group, tile)
-    const int after = c == 0 ? (nch > 1 ? 2 : 1) : (c + 1 < nch ? 1 : 0);
-    if (after == 2) vm_wait<2 * W_OPS>();
-    else if (after == 1) vm_wait<W_OPS>();
-    else vm_wait<0>();
-    // (the weight fragments of chunk c are older than its x DMAs: landed too)
+    uint16_t* sx = s_x[c & 1];
 #pragma unroll
-    for (int q = 0; q < GW; ++q)
+    for (int p = 0; p < XL; ++p) {
+      const int e = tid + 512 * p;
+      const int row = e / CPR, ch = e % CPR;
+      const int slot = (ch & ~7) | ((ch & 7) ^ (row & 7));
+      *reinterpret_cast<w4_u32x4*>(&sx[row * KC + slot * 8]) = xr[p];
+    }
+    if (c + 1 < nch) {
 #pragma unroll
-      for (int j = 0; j < NT; ++j) {
-        w4_dep(wr[SL][q][j]);
-        w4_dep(szr[SL][q][j]);
-      }
-    lgkm_wait<0>();
-    // raw barrier: chunk c visible to every wave, every wave past chunk c-1's reads of
-    // the other buffer (consumed by its MFMAs); __syncthreads could drain the ring
-    __builtin_amdgcn_s_barrier();
-    // s_barrier orders no memory for the compiler: keep this chunk's LDS reads below it
-    asm volatile("" ::: "memory");
-    if (c + 1 < nch) issue_x(c + 1);
-    const uint8_t* sx = s_x + (c & 1) * SLOT_BYTES;
+      for (int p = 0; p < XL; ++p) xr[p] = *reinterpret_cast<const w4_u32x4*>(x + xoff[p] + (c + 1) * KC);
+    }
+    __syncthreads();   // chunk c visible; every wave is past chunk c-1's reads of the other buffer
 #pragma unroll
     for (int q = 0; q < GW; ++q) {
       const int gq = kh * GW + q;
+      const uint32_t wd[4] = {wr[SL][q][0], wr[SL][q][1], wr[SL][q][2], wr[SL][q][3]};
+      const float sc = szr[SL][q].x, zz = szr[SL][q].y;
 #pragma unroll
       for (int i = 0; i < MT; ++i) {
         const int row = 16 * i + l15;
@@ -498,77 +470,62 @@ __global__ __launch_bounds__(512, 1) void w4_xr8_kernel(
         for (int h = 0; h < 4; ++h) {
           const int ch = gq * 16 + 8 * (h >> 1) + 2 * g + (h & 1);
           const int slot = (ch & ~7) | ((ch & 7) ^ (row & 7));
-          xf[h] = *reinterpret_cast<const w4_u32x4*>(sx + row * (KC * 2) + slot * 16);
+          xf[h] = *reinterpret_cast<const w4_u32x4*>(&sx[row * KC + slot * 8]);
         }
         // x . 1 over the group for rows 4 g + r (C layout; every column equal)
         w4_floatx4 xs = w4_floatx4{0.f, 0.f, 0.f, 0.f};
+        w4_floatx4 a = w4_floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int h = 0; h < 4; ++h)
+        for (int h = 0; h < 4; ++h) {
           xs = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(w4_bf16x8, xf[h]), ones, xs,
                                                        0, 0, 0);
-#pragma unroll
-        for (int j = 0; j < NT; ++j) {
-          w4_floatx4 a = w4_floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-          for (int h = 0; h < 4; ++h)
-            a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(w4_bf16x8, xf[h]),
-                                                        w4_frag(wr[SL][q][j][h]), a, 0, 0, 0);
-          const float sc = szr[SL][q][j].x, zz = szr[SL][q][j].y;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) acc[i][j][r] = fmaf(sc, fmaf(-zz, xs[r], a[r]), acc[i][j][r]);
+          a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(w4_bf16x8, xf[h]),
+                                                      w4_frag(wd[h]), a, 0, 0, 0);
         }
-        __builtin_amdgcn_sched_barrier(0);   // one row tile's fragments live at a time
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[i][r] = fmaf(sc, fmaf(-zz, xs[r], a[r]), acc[i][r]);
+        if constexpr (MT == 4) __builtin_amdgcn_sched_barrier(0);   // (one row tile's x live: no spills)
       }
     }
     if constexpr (MORE) load_w(c + 2, SL);   // two chunks ahead
   };
-  int c = 0;
-  for (; c + 3 < nch; c += 2) {
-    chunk(c, std::integral_constant<int, 0>{}, std::true_type{});
-    chunk(c + 1, std::integral_constant<int, 1>{}, std::true_type{});
-  }
-  if (c + 2 < nch) {          // three chunks left
-    chunk(c, std::integral_constant<int, 0>{}, std::true_type{});
-    chunk(c + 1, std::integral_constant<int, 1>{}, std::false_type{});
-    chunk(c + 2, std::integral_constant<int, 0>{}, std::false_type{});
-  } else if (c + 1 < nch) {   // two
-    chunk(c, std::integral_constant<int, 0>{}, std::false_type{});
-    chunk(c + 1, std::integral_constant<int, 1>{}, std::false_type{});
-  } else {                    // one
-    chunk(c, std::integral_constant<int, 0>{}, std::false_type{});
+  for (int c = 0; c < nch; ++c) {   // ring slot c & 1; refill while chunk c + 2 exists
+    const bool more = c + 2 < nch;
+    if (c & 1) {
+      if (more) chunk(c, std::integral_constant<int, 1>{}, std::true_type{});
+      else chunk(c, std::integral_constant<int, 1>{}, std::false_type{});
+    } else {
+      if (more) chunk(c, std::integral_constant<int, 0>{}, std::true_type{});
+      else chunk(c, std::integral_constant<int, 0>{}, std::false_type{});
+    }
   }
 
   // K halves: the kh = 1 waves pass their sums to the kh = 0 partners through LDS
-  vm_wait<0>();
-  __syncthreads();   // every wave is past its last x reads; no DMA in flight
-  float* red = reinterpret_cast<float*>(s_x);   // [4 cg][MT * NT * 4][64]
-  constexpr int NREG = MT * NT * 4;
-  static_assert(4 * NREG * 64 * 4 <= 2 * SLOT_BYTES, "reduction buffer");
+  __syncthreads();   // every wave is past its last x reads
+  float* red = reinterpret_cast<float*>(&s_x[0][0]);   // [4 cg][MT * 4][64]
+  constexpr int NREG = MT * 4;
+  static_assert(4 * NREG * 64 * 4 <= (int)sizeof(s_x), "reduction buffer");
   if (kh == 1) {
 #pragma unroll
     for (int i = 0; i < MT; ++i)
 #pragma unroll
-      for (int j = 0; j < NT; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) red[((cg * NREG) + (i * NT + j) * 4 + r) * 64 + lane] = acc[i][j][r];
+      for (int r = 0; r < 4; ++r) red[((cg * NREG) + i * 4 + r) * 64 + lane] = acc[i][r];
   }
   __syncthreads();
   if (kh == 0) {
 #pragma unroll
     for (int i = 0; i < MT; ++i)
 #pragma unroll
-      for (int j = 0; j < NT; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) acc[i][j][r] += red[((cg * NREG) + (i * NT + j) * 4 + r) * 64 + lane];
+      for (int r = 0; r < 4; ++r) acc[i][r] += red[((cg * NREG) + i * 4 + r) * 64 + lane];
   }
-  if constexpr (SILU && NT == 1) {
+  if constexpr (SILU) {
     // the up-tile waves (odd cg) hand their sums to the gate-tile waves (cg - 1)
     __syncthreads();   // every kh = 0 wave is done reading the partials
     if (kh == 0 && (cg & 1)) {
 #pragma unroll
       for (int i = 0; i < MT; ++i)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) red[((cg >> 1) * MT * 4 + i * 4 + r) * 64 + lane] = acc[i][0][r];
+        for (int r = 0; r < 4; ++r) red[((cg >> 1) * MT * 4 + i * 4 + r) * 64 + lane] = acc[i][r];
     }
     __syncthreads();
     if (kh == 1 || (cg & 1) || n0 >= N) return;
@@ -579,30 +536,13 @@ __global__ __launch_bounds__(512, 1) void w4_xr8_kernel(
       for (int r = 0; r < 4; ++r) {
         const int m = 16 * i + g * 4 + r;
         if (m < M) {
-          const float gt = acc[i][0][r], up = red[((cg >> 1) * MT * 4 + i * 4 + r) * 64 + lane];
+          const float gt = acc[i][r], up = red[((cg >> 1) * MT * 4 + i * 4 + r) * 64 + lane];
           out[(size_t)m * out_stride + col] = f32_to_bf16(gt / (1.f + __expf(-gt)) * up);
         }
       }
     return;
   }
   if (kh == 1 || n0 >= N) return;
-  if constexpr (SILU) {
-#pragma unroll
-    for (int j = 0; j < NT; j += 2) {
-      const int col = ((n0 + 16 * j) >> 1) + l15;   // (gate tile, up tile) -> 16 h columns
-#pragma unroll
-      for (int i = 0; i < MT; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int m = 16 * i + g * 4 + r;
-          if (m < M) {
-            const float gt = acc[i][j][r], up = acc[i][j + 1][r];
-            out[(size_t)m * out_stride + col] = f32_to_bf16(gt / (1.f + __expf(-gt)) * up);
-          }
-        }
-    }
-    return;
-  }
   float* slab = ws + (size_t)s * M * N;
 #pragma unroll
   for (int i = 0; i < MT; ++i)
@@ -610,14 +550,11 @@ __global__ __launch_bounds__(512, 1) void w4_xr8_kernel(
     for (int r = 0; r < 4; ++r) {
       const int m = 16 * i + g * 4 + r;
       if (m < M) {
-#pragma unroll
-        for (int j = 0; j < NT; ++j) {
-          const int n = n0 + 16 * j + l15;
-          if (ws == nullptr)
-            out[(size_t)m * out_stride + n] = f32_to_bf16(acc[i][j][r]);
-          else
-            slab[(size_t)m * N + n] = acc[i][j][r];
-        }
+        const int n = n0 + l15;
+        if (ws == nullptr)
+          out[(size_t)m * out_stride + n] = f32_to_bf16(acc[i][r]);
+        else
+          slab[(size_t)m * N + n] = acc[i][r];
       }
     }
 }
@@ -688,7 +625,7 @@ extern "C" int ft_w4_gemm(const void* x, int x_stride, int M, const uint32_t* wq
 // out [M, N/2]; splits > 1 needs ws (slab output), silu needs splits == 1.
 extern "C" int ft_w4_gemm_xr(const void* x, int x_stride, int M, const uint32_t* wq, const void* sz,
                              int N, int K, float* ws, void* out, int out_stride, int splits, int nt,
-                             int silu, hipStream_t stream) {
+                             int silu, int xsm, hipStream_t stream) {
   if (M <= 0) return 0;
   if (M > 64 || splits < 1) return -1;
   if (N % (64 * nt) != 0) return -2;
@@ -701,6 +638,11 @@ extern "C" int ft_w4_gemm_xr(const void* x, int x_stride, int M, const uint32_t*
   const int k_slice = K / splits;
 #define FT_W4X(MT_, NT_, E_)                                                                 \
   if (mt == MT_ && nt == NT_ && silu == E_) {                                                \
+    if (xsm) /* nt 4: the VALU sums (hipcc's AGPR-copy rewrite crashes on that form) */     \
+      hipLaunchKernelGGL((ft::w4_xr_kernel<MT_, NT_, E_, (NT_ <= 2)>), grid, block, 0, stream,\
+                         (const uint16_t*)x, x_stride, M, wq, (const float2*)sz, K, ws,      \
+                         (uint16_t*)out, out_stride, N, k_slice);                            \
+    else                                                                                     \
     hipLaunchKernelGGL((ft::w4_xr_kernel<MT_, NT_, E_>), grid, block, 0, stream,             \
                        (const uint16_t*)x, x_stride, M, wq, (const float2*)sz, K, ws,        \
                        (uint16_t*)out, out_stride, N, k_slice);                              \
@@ -716,34 +658,30 @@ extern "C" int ft_w4_gemm_xr(const void* x, int x_stride, int M, const uint32_t*
   return -5;
 }
 
-// "xr8" variant (33..64 rows): as ft_w4_gemm_xr (N % (64 * nt) == 0, K % (512 * splits)
-// == 0, silu: one split, nt 1 or even), 8-wave workgroups.
+// "xr8" variant (33..64 rows): nt must be 1 (16 columns per wave), N % 64 == 0,
+// K % (512 * splits) == 0; silu: one split, gate / up tile pairs across waves.
 extern "C" int ft_w4_gemm_xr8(const void* x, int x_stride, int M, const uint32_t* wq,
                               const void* sz, int N, int K, float* ws, void* out, int out_stride,
                               int splits, int nt, int silu, hipStream_t stream) {
   if (M <= 0) return 0;
   if (M > 64 || splits < 1) return -1;
-  if (N % (64 * nt) != 0) return -2;
+  if (nt != 1) return -7;
+  if (N % 64 != 0) return -2;
   if (K % (512 * splits) != 0) return -3;
   if (splits > 1 && (ws == nullptr || silu)) return -4;
   if (ws == nullptr && out == nullptr) return -6;
-  if (silu && nt % 2 && nt != 1) return -7;
   const int mt = (M + 15) / 16;
-  dim3 grid(N / (64 * nt), splits), block(512);
+  dim3 grid(N / 64, splits), block(512);
   const int k_slice = K / splits;
-#define FT_W4X8(MT_, NT_, E_)                                                                \
-  if (mt == MT_ && nt == NT_ && silu == E_) {                                                \
-    hipLaunchKernelGGL((ft::w4_xr8_kernel<MT_, NT_, E_>), grid, block, 0, stream,            \
+#define FT_W4X8(MT_, E_)                                                                     \
+  if (mt == MT_ && silu == E_) {                                                             \
+    hipLaunchKernelGGL((ft::w4_xr8_kernel<MT_, E_>), grid, block, 0, stream,                 \
                        (const uint16_t*)x, x_stride, M, wq, (const float2*)sz, K, ws,        \
                        (uint16_t*)out, out_stride, N, k_slice);                              \
     return static_cast<int>(hipGetLastError());                                              \
   }
-  // nt 1 only: with two column tiles per wave the 48-64-row forms need more than the
-  // 256 registers of a two-waves-per-SIMD kernel (the compiler spilled 100-270)
-#define FT_W4X8_M(NT_, E_) FT_W4X8(2, NT_, E_) FT_W4X8(3, NT_, E_) FT_W4X8(4, NT_, E_)
-  FT_W4X8_M(1, 0)
-  FT_W4X8_M(1, 1)
-#undef FT_W4X8_M
+  FT_W4X8(2, 0) FT_W4X8(3, 0) FT_W4X8(4, 0)
+  FT_W4X8(2, 1) FT_W4X8(3, 1) FT_W4X8(4, 1)
 #undef FT_W4X8
   return -5;
 }

@@ -466,7 +466,7 @@ def test_w4_gemm_matches_fp32(m, n, k, nt, splits):
     assert (y - ref_y).abs().max().item() < 1e-3 * ref_y.abs().max().item() + 1e-3
 
 
-@pytest.mark.parametrize("xr", [1, 2])
+@pytest.mark.parametrize("xr", [1, 2, 3])
 @pytest.mark.parametrize("m", [17, 33, 50, 64])
 @pytest.mark.parametrize("n,k,nt,splits", [(1024, 4096, 1, 1), (2048, 4096, 2, 2), (2048, 4096, 4, 1),
                                            (1024, 14336, 1, 4), (2048, 14336, 2, 7),
@@ -489,7 +489,7 @@ def test_w4_xr_gemm_matches_fp32(m, n, k, nt, splits, xr):
     assert (y - ref_y).abs().max().item() < 1e-3 * ref_y.abs().max().item() + 1e-3
 
 
-@pytest.mark.parametrize("xr", [1, 2])
+@pytest.mark.parametrize("xr", [1, 2, 3])
 @pytest.mark.parametrize("m", [20, 64])
 def test_w4_xr_silu_epilogue(m, xr):
     """gate_up quantized with its rows interleaved in 16-row groups: the W4 xr
@@ -508,7 +508,7 @@ def test_w4_xr_silu_epilogue(m, xr):
     y = x.float() @ wdq.t()
     gt, up = y.view(m, -1, 2, 16).unbind(2)
     ref = (torch.nn.functional.silu(gt) * up).reshape(m, inter)
-    h = Q.w4_gemm(x.to(DEV), W, nt=2 if xr == 1 else 1, xr=xr, silu=True).float().cpu()
+    h = Q.w4_gemm(x.to(DEV), W, nt=1 if xr == 2 else 2, xr=xr, silu=True).float().cpu()
     assert h.shape == (m, inter)
     assert (h - ref).abs().max().item() < 2e-2 * ref.abs().max().item() + 1e-2
 
