@@ -111,6 +111,12 @@ class LLMEngine:
         # at equal tok/s, profiles/ab_pipeline_shrink_r03.log).  Workloads with think
         # time between turns keep the GPU busy with it on.
         self.pipeline_shrink = os.environ.get("ENGINE_PIPELINE_SHRINK", "0") == "1"
+        # ENGINE_MIXED_CHAIN: mixed steps are queued like decode steps -- a drained
+        # queue launches its mixed step without waiting for it, and the next mixed
+        # step (more prompts, the next chunk of a long or background prompt) is
+        # queued behind a running one -- instead of running each synchronously with
+        # the GPU idle while the host collects it and builds the next
+        self.mixed_chain = self.mixed_ahead and os.environ.get("ENGINE_MIXED_CHAIN", "1") != "0"
         self._last_complete = 0.0
         from .debug import FaultInjector, StepProfiler
 
@@ -234,11 +240,27 @@ class LLMEngine:
         if sched.waiting or warm:
             return self._speculate_mixed(last) if self.mixed_ahead else None
         seqs = [q for q in last if q.status != SeqStatus.FINISHED]
+        # every row ends with the queued steps' tokens (length limits): nothing to
+        # speculate -- a lone request would otherwise queue a decode step whose only
+        # row is discarded, and the next prompt would wait behind it
+        if all(self._at_length(q) for q in seqs):
+            return None
         rowmap = None
         if len(seqs) != len(last):
             if not self.pipeline_shrink or not seqs or not self.runner.can_pipeline(len(seqs)):
                 return None
             rowmap = [i for i, q in enumerate(last) if q.status != SeqStatus.FINISHED]
+        if self.mixed_chain:
+            # running sequences that are not rows of the last queued step joined after
+            # it was built (a prompt completed by an earlier, collected mixed step):
+            # with nothing queued for them their ids come from the host (rowmap -1)
+            rows = {id(q) for q in last}
+            extra = [q for q in sched.running if id(q) not in rows]
+            if extra:
+                if any(q.inflight or q.grammar is not None or q.drop_next for q in extra):
+                    return None
+                rowmap = (rowmap if rowmap is not None else list(range(len(seqs)))) + [-1] * len(extra)
+                seqs = seqs + extra
         if not self.runner.can_pipeline(len(seqs)):
             return None
         if any(q.grammar is not None for q in seqs) and not self._guided_pipeline():
@@ -249,9 +271,15 @@ class LLMEngine:
             return None
         if not self._grow_for_next(seqs):
             return None
-        if rowmap is not None:
+        if rowmap is not None and len(seqs) < len(last):
             self.stats["pipeline_shrinks"] += 1
         return self._launch_decode(seqs, True, rowmap)
+
+    def _at_length(self, q: Sequence) -> bool:
+        """The tokens of the steps queued for ``q`` reach its max_tokens / the model
+        length, so it finishes when they are processed."""
+        return q.num_output + q.inflight >= q.params.max_tokens or \
+            q.n_tokens + q.inflight >= self.max_model_len
 
     def _grow_for_next(self, seqs) -> bool:
         """KV blocks for one more token past everything queued (no preemption: a
@@ -283,8 +311,10 @@ class LLMEngine:
             self.stats["mixed_ahead_skip_" + why] += 1
             return None
 
-        if any(e.mixed for e in self._inflight) or sched.swapped:
-            return skip("queued_mixed" if not sched.swapped else "swapped")
+        if sched.swapped:
+            return skip("swapped")
+        if not self.mixed_chain and any(e.mixed for e in self._inflight):
+            return skip("queued_mixed")
         if not hasattr(self.runner, "mixed_launch") or getattr(self.runner, "bcast", None) is not None:
             return None
         if any(q.grammar is not None or q.lazy or q.jf_ids for q in sched.waiting) or \
@@ -298,7 +328,11 @@ class LLMEngine:
         # until their masks were known was built and measured in round 4 -- more, smaller
         # mixed steps and a worse tool-turn tail, p99 462 / 541 vs 408 / 398 ms on one
         # box, profiles/ab_guided_mixed_ahead_r04.log -- and removed)
-        if any(id(q) not in pos or q.grammar is not None or q.drop_next for q in running):
+        # a running sequence that is not a row of the last queued step joined after it
+        # was built (its prompt completed in an earlier, collected step): with nothing
+        # queued for it, its id is its last token (rowmap -1)
+        if any((id(q) not in pos and q.inflight) or q.grammar is not None or q.drop_next
+               for q in running):
             return skip("rows")
         if not self._grow_for_next(running):
             return skip("blocks")
@@ -309,12 +343,51 @@ class LLMEngine:
             self._finalize(q, "abort", emit=False)
         if not pseqs:
             return skip("no_prefill")
-        mb = ScheduledBatch(running, pseqs, ptok, psamp)
-        h = self.runner.mixed_launch(mb, [pos[id(q)] for q in running])
+        mb = sched.stamp(ScheduledBatch(running, pseqs, ptok, psamp))
+        h = self.runner.mixed_launch(mb, [pos.get(id(q), -1) for q in running])
         for q in mb.sampled_seqs():
             q.inflight += 1
         self.stats["mixed_ahead"] += 1
+        if self._inflight[-1].mixed:
+            self.stats["mixed_chain"] += 1
         return _Inflight(mb, h, True)
+
+    def _launch_mixed_drained(self, batch: ScheduledBatch, masks) -> bool:
+        """Mixed chain: the drained path's mixed step is launched and queued (ids
+        from the host) instead of run synchronously, so the steps behind it can be
+        queued while it runs.  False where only the synchronous path applies: TP
+        broadcast, allow-masks, jump-forward chunks, swaps."""
+        if not self.mixed_chain or masks is not None or batch.swap_out or batch.swap_in \
+                or not hasattr(self.runner, "mixed_launch") \
+                or getattr(self.runner, "bcast", None) is not None \
+                or self.runner.__class__.__name__ != "ModelRunner" or not self.cfg.async_output:
+            return False
+        if any(q.status == SeqStatus.RUNNING or q.grammar is not None or q.lazy
+               for q in batch.prefill_seqs) or any(q.grammar is not None for q in batch.decode_seqs):
+            return False
+        h = self.runner.mixed_launch(batch, None)
+        for q in batch.sampled_seqs():
+            q.inflight += 1
+        e = _Inflight(batch, h, True)
+        e.t_launch = time.perf_counter()
+        self._inflight = [e]
+        self.stats["mixed_drained_launch"] += 1
+        return True
+
+    def _wait_mark(self, e: "_Inflight"):
+        """A step is about to be queued behind the mixed step ``e``: wait (admitting
+        new requests) until the GPU has passed ``e``'s mark, three quarters into its
+        layers by default (runner ENGINE_MIXED_CHAIN_AT), so prompts that arrive
+        meanwhile still make the next step -- built at once, the next step would
+        leave them a step behind (+9 ms p50 engine TTFT at the driver config) --
+        while the host has the rest of ``e`` to build and queue it."""
+        mark = getattr(e.handle, "mark", None)
+        poll = self.poll_hook
+        if mark is None or poll is None or not self.mixed_chain:
+            return
+        while not mark.query() and not self.runner.step_done(e.handle):
+            poll()
+            time.sleep(0.0002)
 
     def _drain_wait(self, e: "_Inflight"):
         """The queue is draining (nothing could be queued behind ``e``: a stop, or no
@@ -340,6 +413,8 @@ class LLMEngine:
         t0 = time.perf_counter()
         # top the queue up to depth + 1 steps before waiting on the oldest
         while len(self._inflight) <= self.pipeline_depth:
+            if self._inflight[-1].mixed:
+                self._wait_mark(self._inflight[-1])
             nxt = self._speculate()
             if nxt is None:
                 break
@@ -428,6 +503,8 @@ class LLMEngine:
             for q in e.batch.sampled_seqs():
                 q.inflight = 0
                 q.drop_next = 0
+            for q in e.batch.prefill_seqs:
+                q.pf_sched = 0
         self._inflight = []
         discard = getattr(self.runner, "discard_pending", None)
         if discard is not None:
@@ -492,6 +569,8 @@ class LLMEngine:
             return self._step_pipelined()
         sampled_seqs = batch.sampled_seqs()
         masks = self._masks_for(sampled_seqs)
+        if not outs and batch.has_prefill and self._launch_mixed_drained(batch, masks):
+            return self._step_pipelined()
         self._executing = batch
         toks = self.runner.execute(batch, masks)
         self._executing = None

@@ -134,7 +134,8 @@ class _Staging:
         self.h_small, self.h_f32, self.h_seeds, self.h_bt = _input_views(self.h_in, mb, max_blocks)
         self.h_out = torch.zeros(mb, dtype=i32, pin_memory=pin)
         self.h_err = torch.zeros(1, dtype=i32, pin_memory=pin)  # TP collective error flag
-        self.h_map = torch.zeros(mb, dtype=torch.int64, pin_memory=pin)  # pipelined row gather
+        # pipelined row gather: [source rows | destination rows] (partial gathers)
+        self.h_map = torch.zeros(2 * mb, dtype=torch.int64, pin_memory=pin)
         self.err_armed = False
         self.hs = self.h_small.numpy()
         self.hbt = self.h_bt.numpy()
@@ -144,14 +145,21 @@ class _Staging:
 
 
 class MixedHandle:
-    """A queued mixed step's sampled ids (pinned host copy) and completion event;
-    two alternate (at most one mixed step is queued at a time)."""
-    __slots__ = ("host", "event", "n")
+    """A queued mixed step's sampled ids (pinned host copy), completion event and
+    ``mark``: an event recorded after MIXED_MARK_FRAC of its layers (the engine
+    builds the step queued behind it once the GPU passes it).  They rotate; a
+    handle is reused only after MIXED_HANDLES - 1 later mixed launches, more than
+    the steps the engine keeps queued (ENGINE_PIPELINE_DEPTH + 1)."""
+    __slots__ = ("host", "event", "mark", "n")
 
     def __init__(self, rows: int, pin: bool, gpu: bool):
         self.host = torch.zeros(rows, dtype=torch.int32, pin_memory=pin)
         self.event = torch.cuda.Event() if gpu else None
+        self.mark = torch.cuda.Event() if gpu else None
         self.n = 0
+
+
+MIXED_HANDLES = 4
 
 
 class DecodeHandle:
@@ -249,12 +257,15 @@ class ModelRunner:
         self.d_temp = self.d_f32[0:mb]
         self.d_top_p = self.d_f32[mb:2 * mb]
         self.d_out = torch.zeros(mb, dtype=i32, device=dv)
-        self.d_map = torch.zeros(mb, dtype=torch.int64, device=dv)
+        self.d_map = torch.zeros(2 * mb, dtype=torch.int64, device=dv)
         # pinned staging sets: while decode step n runs, steps n+1 .. n+depth are
         # filled and queued behind it from the other sets (pipelined decode)
         nstg = max(2, int(getattr(cfg, "pipeline_depth", 1)) + 1)
         self.stg = [_Staging(mb, self.max_blocks_per_seq, pin, self.is_gpu) for _ in range(nstg)]
-        self._mx_handles = [MixedHandle(mb, pin, self.is_gpu) for _ in range(2)]
+        self._mx_handles = [MixedHandle(mb, pin, self.is_gpu) for _ in range(MIXED_HANDLES)]
+        # ENGINE_MIXED_CHAIN_AT: fraction of a queued mixed step's layers after which
+        # its mark event is recorded (0: no mark, the next step is built at once)
+        self.mixed_mark_frac = float(os.environ.get("ENGINE_MIXED_CHAIN_AT", "0.75"))
         self._mx_next = 0
         self._stg_next = 0
         self._upload = _Uploader(dv, pin) if self.is_gpu else None
@@ -434,7 +445,7 @@ class ModelRunner:
         self._assert_no_pending_split("execute")
         if batch.has_prefill:
             if self._gaps is not None:
-                self._gaps.append([None, None])
+                self._gap_mark(True, "m")   # closed by _wait, right after the last launch
             return self._mixed(batch, masks)
         if not batch.decode_seqs:
             return []
@@ -468,6 +479,10 @@ class ModelRunner:
         dseqs = batch.decode_seqs
         pseqs = [s for s, n in zip(batch.prefill_seqs, batch.prefill_tokens) if n > 0]
         ntoks = [n for n in batch.prefill_tokens if n > 0]
+        # chunk starts as scheduled (a chunk queued behind an in-flight chunk of the
+        # same prompt starts after it; num_computed only moves in post_step)
+        starts = [a for a, n in zip(batch.prefill_start or [None] * len(batch.prefill_seqs),
+                                    batch.prefill_tokens) if n > 0]
         psamp = [sm for sm, n in zip(batch.prefill_sample, batch.prefill_tokens) if n > 0]
         bs = self.bs
         nd = len(dseqs)
@@ -495,8 +510,9 @@ class ModelRunner:
         qsl = np.zeros(len(pseqs) + 1, np.int32)
         maxb = max([len(s.block_ids) for s in pseqs] or [1])
         bt = np.zeros((max(1, len(pseqs)), maxb), np.int32)
-        for i, (s, n) in enumerate(zip(pseqs, ntoks)):
-            a = s.num_computed
+        for i, (s, n, a) in enumerate(zip(pseqs, ntoks, starts)):
+            if a is None:
+                a = s.num_computed
             ids.append(s.tokens[a:a + n])
             p = np.arange(a, a + n, dtype=np.int32)
             pos.append(p)
@@ -596,6 +612,8 @@ class ModelRunner:
         holding the GIL: a plain ``.cpu()`` / ``synchronize`` keeps the GIL for the
         whole step and starves the asyncio thread that streams to the WebSockets."""
         if ev is None:
+            if self._gaps and self._gaps[-1][1] is None:
+                self._gap_mark(False)
             ev = self._done_event
             ev.record()
         t0 = time.perf_counter()
@@ -727,7 +745,7 @@ class ModelRunner:
         gather = None
         if ahead and rowmap is not None:
             gather = np.zeros(nb, dtype=np.int64)   # padding rows read row 0 (ignored)
-            gather[:n] = rowmap
+            gather[:n] = rowmap   # -1: no queued step has the row, its id comes from the host
         self._assert_no_pending_split("decode_launch")
         if defer_sample:
             assert self.can_defer_sample()
@@ -808,15 +826,18 @@ class ModelRunner:
         return ev is None or ev.query()
 
     @torch.inference_mode()
-    def mixed_launch(self, batch: ScheduledBatch, rowmap: List[int]) -> "MixedHandle":
-        """Queues a mixed (decode + prefill) step behind the queued decode step(s)
-        without waiting (engine ``_speculate_mixed``): decode row i's input id is
-        row ``rowmap[i]`` of the last queued step's sampled ids (``d_out``),
-        gathered on the device; its position is ``inflight`` tokens ahead.  The
+    def mixed_launch(self, batch: ScheduledBatch, rowmap: Optional[List[int]]) -> "MixedHandle":
+        """Queues a mixed (decode + prefill) step behind the queued step(s) without
+        waiting (engine ``_speculate_mixed``): decode row i's input id is row
+        ``rowmap[i]`` of the last queued step's sampled ids (``d_out``), gathered on
+        the device; its position is ``inflight`` tokens ahead.  ``rowmap`` None:
+        nothing is queued, the ids are the sequences' last tokens (host).  The
         sampled ids land in ``d_out`` (rows = ``batch.sampled_seqs()``) for the
         decode step queued next, and in a pinned host buffer for the collect.
         Single process only (no TP broadcast), no allow-masks."""
         self._assert_no_pending_split("mixed_launch")
+        if self._gaps is not None:
+            self._gap_mark(True, "a")
         host = self._mixed_host(batch)
         nd = host["nd"]
         self.stats["prefill_steps"] += 1
@@ -825,16 +846,24 @@ class ModelRunner:
         if nd:
             names += ["d_bt", "d_sl"]
         arrays = [host[k] for k in names] + list(host["sampling"])
-        gather = np.asarray(rowmap, dtype=np.int64)
-        arrays.append(gather if nd else np.zeros(1, np.int64))
+        # rowmap[i] < 0: row i's sequence has no queued step (it joined after the last
+        # queued step was built); its id is its last token, already in host["ids"]
+        rm = np.asarray(rowmap if rowmap is not None else [], dtype=np.int64)
+        dst = np.nonzero(rm >= 0)[0].astype(np.int64)
+        partial = nd and rowmap is not None and len(dst) < nd
+        arrays.append(rm[dst] if nd and len(dst) else np.zeros(1, np.int64))
+        arrays.append(dst if partial and len(dst) else np.zeros(1, np.int64))
         if self.is_gpu:
             dev = self._upload(arrays)
         else:
             dev = [torch.from_numpy(np.ascontiguousarray(a)) for a in arrays]
         d = dict(zip(names, dev))
-        if nd:
-            idx = dev[len(names) + 5]
-            torch.index_select(self.d_out, 0, idx, out=d["ids"][:nd])
+        if nd and len(dst):
+            src_t, dst_t = dev[len(names) + 5], dev[len(names) + 6]
+            if partial:
+                d["ids"].index_copy_(0, dst_t, self.d_out.index_select(0, src_t))
+            else:
+                torch.index_select(self.d_out, 0, src_t, out=d["ids"][:nd])
         meta = AttnMeta(
             positions=d["pos"], slot_mapping=d["slots"], logits_indices=d["lrows"], num_decode=nd,
             block_tables=d["bt"], seq_lens=d["seq_lens"],
@@ -849,21 +878,29 @@ class ModelRunner:
             meta.dec_seq_lens = d["d_sl"]
             meta.tmp_out, meta.tmp_ml = self.tmp_out, self.tmp_ml
             meta.dec_counters = self.dec_counters
-        h = self.model.forward(d["ids"], meta, self.kv)
+        mh = self._mx_handles[self._mx_next]
+        self._mx_next = (self._mx_next + 1) % len(self._mx_handles)
+        nl = len(getattr(self.model, "layers", ()))
+        if mh.mark is not None and nl and self.mixed_mark_frac > 0:
+            self.model.mark_at = (min(nl - 1, int(self.mixed_mark_frac * nl)), mh.mark)
+        try:
+            h = self.model.forward(d["ids"], meta, self.kv)
+        finally:
+            self.model.mark_at = None
         logits = self.model.compute_logits(h)
         if self.logits_tap is not None:
-            self._tap(logits.float().clone())
+            self._tap(logits.float().cpu())   # taps are host tensors (tests)
         n = logits.shape[0]
         temp, topp, topk, seeds, steps = dev[len(names):len(names) + 5]
         ops.sample(logits, temp, topp, topk, seeds, steps, out=self.d_out[:n])
-        mh = self._mx_handles[self._mx_next]
-        self._mx_next ^= 1
         if mh.host.shape[0] < n:
             mh.host = torch.zeros(2 * n, dtype=torch.int32, pin_memory=self.is_gpu)
         mh.n = n
         mh.host[:n].copy_(self.d_out[:n], non_blocking=self.is_gpu)
         if mh.event is not None:
             mh.event.record()
+        if self._gaps is not None:
+            self._gap_mark(False)
         return mh
 
     def mixed_collect(self, h: "MixedHandle") -> List[int]:
@@ -910,34 +947,50 @@ class ModelRunner:
             st.hf[mb + n:mb + nb] = 1.0
         return maxblk
 
-    def _gap_mark(self, start: bool):
+    def _gap_mark(self, start: bool, kind: str = "d"):
         ev = torch.cuda.Event(enable_timing=True)
         ev.record()
         if start:
-            self._gaps.append([ev, None])
-        else:
+            if self._gaps and self._gaps[-1][1] is None:   # an unclosed step: drop it
+                self._gaps.pop()
+            self._gaps.append([ev, None, kind])
+        elif self._gaps and self._gaps[-1][1] is None:
             self._gaps[-1][1] = ev
 
     def gap_summary(self) -> Dict[str, float]:
-        """FT_GPU_GAPS: idle GPU time between consecutive graph-replayed decode
-        steps (ms total / per step / max) and their mean on-GPU time."""
+        """FT_GPU_GAPS: idle GPU time between consecutive steps, by transition
+        (d = graph-replayed decode, m = synchronous mixed step, a = mixed step
+        queued ahead), and each kind's mean span from its first to its last
+        launch (a mixed step's span includes any wait for the host's launches)."""
         if not self._gaps:
             return {}
         torch.cuda.synchronize(self.device)
-        gaps, busy, prev = [], [], None
-        for e0, e1 in self._gaps:
-            if e0 is None:   # an eager (mixed) step ran in between: chain broken
+        out: Dict[str, float] = {}
+        busy: Dict[str, List[float]] = {}
+        trans: Dict[str, List[float]] = {}
+        prev = None
+        for e0, e1, kind in self._gaps:
+            if e1 is None:
                 prev = None
                 continue
-            busy.append(e0.elapsed_time(e1))
+            busy.setdefault(kind, []).append(e0.elapsed_time(e1))
             if prev is not None:
-                gaps.append(max(0.0, prev.elapsed_time(e0)))
-            prev = e1
-        if not gaps:
+                trans.setdefault(prev[1] + kind, []).append(max(0.0, prev[0].elapsed_time(e0)))
+            prev = (e1, kind)
+        if not trans:
             return {}
-        return {"idle_ms_total": round(sum(gaps), 1), "idle_ms_per_step": round(sum(gaps) / len(gaps), 3),
-                "idle_ms_max": round(max(gaps), 2), "gpu_ms_per_step": round(sum(busy) / len(busy), 3),
-                "steps": len(busy)}
+        gaps = [g for v in trans.values() for g in v]
+        out.update(idle_ms_total=round(sum(gaps), 1), idle_ms_per_step=round(sum(gaps) / len(gaps), 3),
+                   idle_ms_max=round(max(gaps), 2), steps=sum(len(v) for v in busy.values()))
+        for k, v in sorted(busy.items()):
+            out[f"span_ms_{k}"] = round(sum(v) / len(v), 3)
+            out[f"n_{k}"] = len(v)
+        if "d" in busy:
+            out["gpu_ms_per_step"] = out["span_ms_d"]
+        for k, v in sorted(trans.items()):
+            out[f"idle_ms_{k}"] = round(sum(v), 1)
+            out[f"n_{k}"] = len(v)
+        return out
 
     def _decode_enqueue(self, st: "_Staging", nb: int, n: int, from_device: bool = False,
                         gather: Optional[np.ndarray] = None, fwd_only: bool = False):
@@ -948,10 +1001,20 @@ class ModelRunner:
         if from_device:  # the previous step's sampled ids feed this step
             if gather is None:
                 self.d_input_ids[:nb].copy_(self.d_out[:nb])
-            else:   # rows of the previous step, survivors only (pinned per staging set)
+            elif (gather >= 0).all():   # rows of the previous step, survivors only
                 st.h_map[:nb].numpy()[:] = gather
                 self.d_map[:nb].copy_(st.h_map[:nb], non_blocking=True)
                 torch.index_select(self.d_out, 0, self.d_map[:nb], out=self.d_input_ids[:nb])
+            else:   # gather < 0: a sequence with no queued step keeps its host id
+                dst = np.nonzero(gather >= 0)[0]
+                k = len(dst)
+                if k:
+                    hm = st.h_map.numpy()
+                    hm[:k] = gather[dst]
+                    hm[k:2 * k] = dst
+                    self.d_map[:2 * k].copy_(st.h_map[:2 * k], non_blocking=True)
+                    self.d_input_ids.index_copy_(0, self.d_map[k:2 * k],
+                                                 self.d_out.index_select(0, self.d_map[:k]))
         if fwd_only:
             pair = self.graphs_split.get(nb)
             if pair is None:

@@ -41,6 +41,10 @@ class ScheduledBatch:
     # swap-outs first: a block freed by a swap-out may be reused by this step
     swap_out: List[Tuple[int, int]] = dataclasses.field(default_factory=list)
     swap_in: List[Tuple[int, int]] = dataclasses.field(default_factory=list)
+    # per prefill chunk: first prompt position and the sequence's epoch when it was
+    # scheduled (Scheduler.stamp); empty for batches built outside the scheduler
+    prefill_start: List[int] = dataclasses.field(default_factory=list)
+    prefill_epoch: List[int] = dataclasses.field(default_factory=list)
 
     @property
     def is_prefill(self) -> bool:
@@ -211,7 +215,19 @@ class Scheduler:
         swap_out, self._swap_out = self._swap_out, []
         if not decode and not pseqs and not rejected and not swap_out and not swap_in:
             return None
-        return ScheduledBatch(decode, pseqs, ptok, psamp, rejected, swap_out, swap_in)
+        return self.stamp(ScheduledBatch(decode, pseqs, ptok, psamp, rejected, swap_out, swap_in))
+
+    @staticmethod
+    def stamp(batch: ScheduledBatch) -> ScheduledBatch:
+        """Records where each prefill chunk starts and counts it as scheduled
+        (``pf_sched``) until its step's post_step, so a step queued behind this one
+        before it completes (engine mixed chain) continues a chunked prompt after it
+        instead of repeating it."""
+        batch.prefill_start = [s.num_computed + s.pf_sched for s in batch.prefill_seqs]
+        batch.prefill_epoch = [s.epoch for s in batch.prefill_seqs]
+        for s, n in zip(batch.prefill_seqs, batch.prefill_tokens):
+            s.pf_sched += n
+        return batch
 
     def _swap_out_seq(self, seq: Sequence) -> bool:
         """Parks a running sequence's KV blocks in host memory (False if there is no
@@ -268,6 +284,8 @@ class Scheduler:
         seq.num_computed = 0
         seq.num_committed_blocks = 0
         seq.num_cached_tokens = 0
+        seq.pf_sched = 0
+        seq.epoch += 1
 
     def _schedule_prefill(self, budget: int, n_decode: int):
         seqs, ntok, samp, rejected = [], [], [], []
@@ -296,12 +314,13 @@ class Scheduler:
                         seq.num_computed = len(hit) * self.bs
                         seq.num_committed_blocks = len(hit)
                         seq.num_cached_tokens = seq.num_computed
-            remaining = seq.n_tokens - seq.num_computed
+            start = seq.num_computed + seq.pf_sched   # chunks already queued come first
+            remaining = seq.n_tokens - start
             if not seqs and remaining >= soft:
                 soft = 0
             limit = budget if not seqs or not soft else min(budget, soft - used)
             chunk = min(remaining, limit)
-            need = self._blocks_needed(seq, seq.num_computed + chunk)
+            need = self._blocks_needed(seq, start + chunk)
             if need and not self.bm.can_allocate(need) and self._release_background():
                 pass  # a warm-up's blocks went back to the pool first (optional work)
             if need and not self.bm.can_allocate(need):
@@ -368,9 +387,10 @@ class Scheduler:
                 seq.num_computed = len(hit) * self.bs
                 seq.num_committed_blocks = len(hit)
                 seq.num_cached_tokens = seq.num_computed
-        remaining = seq.n_tokens - seq.num_computed
+        start = seq.num_computed + seq.pf_sched
+        remaining = seq.n_tokens - start
         chunk = min(remaining, room)
-        need = self._blocks_needed(seq, seq.num_computed + chunk)
+        need = self._blocks_needed(seq, start + chunk)
         if need and not self.bm.can_allocate(need):
             self.background.popleft()
             self.release(seq)
@@ -435,9 +455,14 @@ class Scheduler:
         return list(self.running)
 
     def post_step(self, batch: ScheduledBatch):
-        items = [(s, 1, False) for s in batch.decode_seqs] + \
-            list(zip(batch.prefill_seqs, batch.prefill_tokens, batch.prefill_sample))
-        for seq, n, smp in items:
+        items = [(s, 1, False, None) for s in batch.decode_seqs] + \
+            list(zip(batch.prefill_seqs, batch.prefill_tokens, batch.prefill_sample,
+                     batch.prefill_epoch or [None] * len(batch.prefill_seqs)))
+        for seq, n, smp, ep in items:
+            if ep is not None:
+                if ep != seq.epoch:   # its KV was dropped after this chunk was queued
+                    continue
+                seq.pf_sched = max(0, seq.pf_sched - n)
             if seq.status == SeqStatus.FINISHED:
                 continue
             seq.num_computed += n

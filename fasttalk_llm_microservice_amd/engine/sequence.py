@@ -39,7 +39,7 @@ class Sequence:
                  "first_token_time", "finish_reason", "detok_stream", "on_output", "grammar",
                  "grammar_state", "stop_buf", "text_len", "aborted", "preemptions", "admit_order",
                  "meta", "host_slots", "background", "jf_text", "jf_ids", "lazy", "inflight",
-                 "drop_next")
+                 "drop_next", "pf_sched", "epoch")
 
     def __init__(self, request_id: str, prompt_ids: List[int], params: SamplingParams,
                  on_output: Optional[Callable[[RequestOutput], None]] = None, meta: Any = None):
@@ -81,6 +81,12 @@ class Sequence:
         # samples of queued steps to discard: a jump-forward (pipelined guided decoding)
         # appended forced tokens after the step behind it was already queued
         self.drop_next = 0
+        # prompt tokens of prefill chunks in queued (launched, not yet post-stepped)
+        # steps: the next chunk starts at num_computed + pf_sched
+        self.pf_sched = 0
+        # bumped when the sequence's KV is dropped (_reset_to_waiting): a queued
+        # chunk scheduled before that is not counted when its step completes
+        self.epoch = 0
 
     # ---------------------------------------------------------------- tokens
     @property

@@ -376,6 +376,7 @@ class LlamaModel:
         self._w4_scratch: Optional[torch.Tensor] = None
         self.w4_gu_il = False     # W4 gate_up image interleaved in 16-row groups
         self.fused = False
+        self.mark_at = None   # (layer, event): recorded as the forward reaches that layer
         self.gu_nt = 2
         self.gu_il = False        # gate_up image interleaved in groups of 16 (packed bf16)
         self.w4_slab: dict = {}   # W4 projections that leave split-K slabs
@@ -905,7 +906,10 @@ class LlamaModel:
         tps = self._tp_slabs(t)
         tpf = tps and self._tp_fused(t)
         pend = None
+        mark = self.mark_at
         for li, L in enumerate(self.layers):
+            if mark is not None and li == mark[0]:   # progress event (engine mixed chain)
+                mark[1].record()
             if residual is None:
                 x, residual = ops.embed_rmsnorm(input_ids, self.embed, L.ln1, eps)  # K1 + K2
             elif pend is not None:   # residual += all-reduce(down partial); x = rmsnorm * ln1

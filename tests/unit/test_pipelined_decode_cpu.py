@@ -59,13 +59,14 @@ class ModelRunner:
         self.launches.append((len(seqs), ahead, None if rowmap is None else list(rowmap)))
         if ahead:
             rows = rowmap if rowmap is not None else range(len(seqs))
-            ids = [self.d_out[r] for r in rows]
+            ids = [self.d_out[r] if r >= 0 else int(s.tokens[-1]) for r, s in zip(rows, seqs)]
         else:
             ids = [int(s.tokens[-1]) for s in seqs]
         out = []
-        for s, tok in zip(seqs, ids):
+        for i, (s, tok) in enumerate(zip(seqs, ids)):
             pos = s.n_tokens - 1 + s.inflight
             assert ahead or s.inflight == 0
+            assert not ahead or rowmap is None or rowmap[i] >= 0 or s.inflight == 0
             assert pos // self.bs < len(s.block_ids), "KV slot of a queued step has no block"
             out.append(_next(tok, pos))
         self.d_out = out
@@ -75,17 +76,31 @@ class ModelRunner:
         return list(h.out)
 
     def mixed_launch(self, batch, rowmap):
-        self.mixed.append((len(batch.decode_seqs), list(batch.prefill_tokens), list(rowmap)))
+        """``rowmap`` None: launched from a drained queue, ids from the host."""
+        self.mixed.append((len(batch.decode_seqs), list(batch.prefill_tokens),
+                           None if rowmap is None else list(rowmap)))
         out = []
-        for s, r in zip(batch.decode_seqs, rowmap):
+        for i, s in enumerate(batch.decode_seqs):
             pos = s.n_tokens - 1 + s.inflight
-            assert s.inflight >= 1 and pos // self.bs < len(s.block_ids)
-            out.append(_next(self.d_out[r], pos))
-        for s, n, smp in zip(batch.prefill_seqs, batch.prefill_tokens, batch.prefill_sample):
+            if rowmap is None or rowmap[i] < 0:
+                assert s.inflight == 0
+                tok = int(s.tokens[-1])
+            else:
+                assert s.inflight >= 1
+                tok = self.d_out[rowmap[i]]
+            assert pos // self.bs < len(s.block_ids)
+            out.append(_next(tok, pos))
+        starts = batch.prefill_start or [s.num_computed for s in batch.prefill_seqs]
+        chunks = self.__dict__.setdefault("chunks", {})
+        for s, n, smp, a in zip(batch.prefill_seqs, batch.prefill_tokens, batch.prefill_sample, starts):
             assert s.inflight == 0
-            assert (s.num_computed + n + self.bs - 1) // self.bs <= len(s.block_ids)
+            assert (a + n + self.bs - 1) // self.bs <= len(s.block_ids)
+            # a prompt's chunks are contiguous, also when queued behind each other
+            prev = chunks.get(id(s))
+            assert prev is None or prev == a or a == s.num_computed, (prev, a, s.num_computed)
+            chunks[id(s)] = a + n
             if smp:
-                assert s.num_computed + n == s.n_tokens
+                assert a + n == s.n_tokens
                 out.append(_next(int(s.tokens[-1]), s.n_tokens - 1))
         self.d_out = out
         return _Handle(out)
@@ -95,14 +110,17 @@ class ModelRunner:
 
 
 def _run(async_output: bool, depth: int, n_req: int = 9, shrink: bool = True, late: int = 0,
-         mixed_ahead: bool = False):
+         mixed_ahead: bool = False, chain: bool = False, prefill_chunk: int = 512,
+         max_batched: int = 8192):
     """``late`` requests arrive one every third engine step after the first ``n_req``."""
     import os
 
     os.environ["ENGINE_PIPELINE_SHRINK"] = "1" if shrink else "0"
     os.environ["ENGINE_MIXED_AHEAD"] = "1" if mixed_ahead else "0"
+    os.environ["ENGINE_MIXED_CHAIN"] = "1" if chain else "0"
     cfg = EngineConfig(model="tiny", device="cpu", block_size=4, async_output=async_output,
-                       pipeline_depth=depth, max_num_seqs=32)
+                       pipeline_depth=depth, max_num_seqs=32, prefill_chunk=prefill_chunk,
+                       max_num_batched_tokens=max_batched)
     runner = ModelRunner()
     eng = LLMEngine(cfg, runner=runner)
     res = {}
@@ -124,8 +142,9 @@ def _run(async_output: bool, depth: int, n_req: int = 9, shrink: bool = True, la
         step += 1
     os.environ.pop("ENGINE_PIPELINE_SHRINK", None)
     os.environ.pop("ENGINE_MIXED_AHEAD", None)
+    os.environ.pop("ENGINE_MIXED_CHAIN", None)
     assert eng.bm.num_free() == eng.bm.num_blocks
-    assert all(q.inflight == 0 for q in eng.scheduler.by_id.values())
+    assert all(q.inflight == 0 and q.pf_sched == 0 for q in eng.scheduler.by_id.values())
     return [res.get(i, []) for i in range(n_req + late)], eng, runner
 
 
@@ -171,8 +190,29 @@ def test_mixed_ahead_matches_synchronous(depth):
     assert eng.stats["mixed_ahead"] > 0 and runner.mixed
     # decode steps were queued behind mixed ones (ids from the mixed step's rows)
     assert eng.stats["pipelined_steps"] > 0
-    # the drained path handled the rest: no mixed step ran while another was queued
-    assert all(d > 0 for d, _, _ in runner.mixed)
+    # without the chain the drained path ran the rest synchronously: every queued
+    # mixed step sat behind a decode step
+    assert all(d > 0 and rm is not None for d, _, rm in runner.mixed)
+
+
+@pytest.mark.parametrize("depth", [1, 2])
+@pytest.mark.parametrize("budget", [8192, 20])
+def test_mixed_chain_matches_synchronous(depth, budget):
+    """Mixed chain: a drained queue launches its mixed step (ids from the host) and
+    further mixed steps queue behind running ones, continuing chunked prompts after
+    their queued chunks (``budget`` 20 tokens per step: long prompts are split over
+    several chained steps).  Tokens equal the synchronous engine's, chunks are
+    contiguous, every block comes back and no chunk stays counted as scheduled."""
+    ref, _, _ = _run(False, 1, n_req=6, late=12, max_batched=budget)
+    got, eng, runner = _run(True, depth, n_req=6, late=12, mixed_ahead=True, chain=True,
+                            max_batched=budget)
+    assert got == ref
+    assert eng.stats["mixed_drained_launch"] > 0
+    assert any(rm is None for _, _, rm in runner.mixed)
+    if budget == 20:
+        assert eng.stats["mixed_chain"] > 0
+        # rows that joined after the last queued step was built take their host id
+        assert any(rm and min(rm) < 0 for _, _, rm in runner.mixed)
 
 
 def test_mixed_ahead_with_background_warmups():
@@ -268,8 +308,9 @@ def test_prompt_arriving_during_drain_is_queued_behind_running_step():
 
 
 def _failing_collect(self, h):
-    """decode_collect fails once a mixed step has been queued behind the step."""
-    if self.mixed and not self.__dict__.get("failed"):
+    """decode_collect fails once a mixed step has been queued behind the step (one
+    launched from a drained queue, rowmap None, does not count)."""
+    if any(rm is not None for _, _, rm in self.mixed) and not self.__dict__.get("failed"):
         self.failed = True
         raise RuntimeError("injected device error")
     return list(h.out)
