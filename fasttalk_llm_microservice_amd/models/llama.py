@@ -168,9 +168,12 @@ PG_MAX_SLAB_ROWS = 2048
 # At prefill-burst sizes hipBLASLt's tiles beat packed_gemm (1.35-1.66 vs 1.1-1.2
 # PF/s at M = 4096, profiles/packed_gemm_*_r02.log) by more than it costs to unpack
 # the layer's weight into a transient row-major copy (one read + one write of the
-# weight, ~0.17 ms per 8B layer): from this many rows up the projection unpacks and
-# calls the library.  The resident weights stay single-image.  0 disables.
-PG_BLAS_ROWS = int(os.environ.get("FT_PG_BLAS_ROWS", "2048"))
+# weight, ~0.17 ms per 8B layer).  FT_PG_BLAS_ROWS=N: from N rows up the projection
+# unpacks and calls the library.  Default 0 (off, round 5): end to end the library
+# path gained nothing -- config 5 4,854 / 4,757 with it vs 4,844 / 4,797 without,
+# driver config 5,672 vs 5,700 (profiles/ab_pg_blas_rows_r05.log) -- so every GEMM of
+# the serving path runs the hand-written kernels.
+PG_BLAS_ROWS = int(os.environ.get("FT_PG_BLAS_ROWS", "0"))
 # With memory to spare (an 8B model is 16 GB of a 288 GB MI355X) qkv / o / gate_up
 # also stay resident row-major and run hipBLASLt from this many rows up: at the
 # soft-budgeted mixed-step sizes (300-512 rows) the library beats packed_gemm on
