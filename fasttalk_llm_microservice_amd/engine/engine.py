@@ -91,6 +91,8 @@ class LLMEngine:
         # request arrivals, written at shutdown -- what the GPU waits on between turns
         self._trace_path = os.environ.get("FT_STEP_TRACE") or None
         self._trace: List[tuple] = []
+        if self._trace_path:
+            self.scheduler.admit_trace = self._trace
         self.host_prof = collections.Counter()
         # queued decode steps, oldest first: [(batch, DecodeHandle)], at most
         # cfg.pipeline_depth + 1 of them (ENGINE_PIPELINE_DEPTH)

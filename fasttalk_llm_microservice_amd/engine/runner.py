@@ -782,6 +782,8 @@ class ModelRunner:
         st.err_armed = False
         st.event.record()
         h.pending = False
+        if self._gaps is not None:
+            self._gap_mark(False)
 
     def discard_pending(self):
         """Forget a deferred-sample step whose sampler will never be queued (the
@@ -995,8 +997,8 @@ class ModelRunner:
     def _decode_enqueue(self, st: "_Staging", nb: int, n: int, from_device: bool = False,
                         gather: Optional[np.ndarray] = None, fwd_only: bool = False):
         nw = 10 * self.max_decode_batch + nb * self.max_blocks_per_seq
-        if self._gaps is not None and not fwd_only:
-            self._gap_mark(True)
+        if self._gaps is not None:   # g: a split step, closed by its sampler (sample_launch)
+            self._gap_mark(True, "g" if fwd_only else "d")
         self.d_in[:nw].copy_(st.h_in[:nw], non_blocking=True)
         if from_device:  # the previous step's sampled ids feed this step
             if gather is None:

@@ -25,6 +25,8 @@ from __future__ import annotations
 
 import collections
 import dataclasses
+import os
+import time
 from typing import Deque, Dict, List, Optional, Tuple
 
 from .sequence import SeqStatus, Sequence
@@ -94,6 +96,7 @@ class Scheduler:
         self.bs = block_size
         self.max_num_seqs = max_num_seqs
         self.max_tokens = max_num_batched_tokens
+        self.admit_trace: Optional[list] = None   # the engine's step trace list, when on
         # Soft prefill budget (0 = off): the first waiting prompt may fill the whole
         # step budget (a lone long prompt prefills in one step), further prompts join
         # only up to this many prefill tokens per step.  A burst of many short turns
@@ -295,7 +298,9 @@ class Scheduler:
         # every session: short new messages on a cached history); when the head
         # itself needs more than the soft budget (a long first prompt, or every
         # session re-rendering its history window at once) the step is filled to the
-        # hard budget instead, for throughput
+        # hard budget instead, for throughput.  (Prefilling such a head alone was
+        # measured neutral in round 5 -- config 5 4,811 / 4,679 vs 4,793 / 4,799 tok/s,
+        # tool-turn p99 396 / 364 vs 363 / 382 ms, profiles/ab_prefill_flood_r05.log.)
         soft = self.prefill_chunk
         if soft and self.chunk_counts_decode:
             # the soft budget bounds the step's GEMM rows (decode rows + prefill
@@ -314,6 +319,9 @@ class Scheduler:
                         seq.num_computed = len(hit) * self.bs
                         seq.num_committed_blocks = len(hit)
                         seq.num_cached_tokens = seq.num_computed
+                if self.admit_trace is not None:   # FT_STEP_TRACE: what each admission costs
+                    self.admit_trace.append(("admit", time.perf_counter(), seq.request_id, seq.n_tokens,
+                                             seq.num_computed, seq.grammar is not None, seq.background))
             start = seq.num_computed + seq.pf_sched   # chunks already queued come first
             remaining = seq.n_tokens - start
             if not seqs and remaining >= soft:
