@@ -25,7 +25,6 @@ from __future__ import annotations
 
 import collections
 import dataclasses
-import os
 import time
 from typing import Deque, Dict, List, Optional, Tuple
 
