@@ -525,6 +525,30 @@ class LlamaModel:
             self._w4_scratch = torch.empty(max(need, big), dtype=self.dtype, device=self.device)
         return Q.w4_dequant(w, out=self._w4_scratch[:need].view(w.n, w.k))
 
+    def _prepare_w4_prefill(self):
+        """W4A16 prefill image: every W4 projection dequantized ONCE into the packed
+        bf16 layout (gate_up keeps the W4 image's 16-row interleave, which is the
+        SiLU epilogue's), so steps above W4_ROWS rows run packed_gemm.hip on it
+        instead of dequantizing every layer's weight into a scratch and calling
+        hipBLASLt on every mixed step (15 GB written and read again per step for an
+        8B model).  Decode steps keep streaming the int4 image.  FT_W4_PREFILL_IMAGE:
+        auto (default: when the bf16 image is <= 15% of device memory -- 8B: 14 GB of
+        288; 70B at TP=1 is not), 1, 0."""
+        mode = os.environ.get("FT_W4_PREFILL_IMAGE", "auto")
+        if self.quant is None or mode == "0" or self.device.type != "cuda" or not self.layers:
+            return
+        qs = [(L, p, L.q4[p]) for L in self.layers for p in _ATTR if L.q4 and p in L.q4]
+        if not qs:
+            return
+        nbytes = sum(q.n * q.k * 2 for _, _, q in qs)
+        if mode != "1":
+            _, total = torch.cuda.mem_get_info(self.device)
+            if nbytes > 0.15 * total:
+                return
+        for L, p, q in qs:
+            setattr(L, _ATTR[p] + "_pk", ops.pack_weight(Q.w4_dequant(q)))
+        log.info("W4A16 prefill image (dequantized, packed bf16): %.1f GB", nbytes / 1e9)
+
     def _prepare_rowmajor(self):
         """Resident row-major copies of the RM_PROJS images (hipBLASLt from PG_RM_ROWS
         rows, see there) when they fit the memory policy."""
@@ -572,6 +596,7 @@ class LlamaModel:
                 L.wd_pk, L.wd = ops.pack_weight(L.wd), None
             if fold:
                 L.ln1 = L.ln2 = one
+        self._prepare_w4_prefill()
         self.gu_il = self.layers[0].wgu_pk is not None
         self._unpack_need = max((w.numel() for w in (self.layers[0].wqkv_pk, self.layers[0].wo_pk,
                                                       self.layers[0].wgu_pk, self.layers[0].wd_pk)
@@ -760,6 +785,9 @@ class LlamaModel:
                     return sp, None
                 y = Q.w4_gemm(x, q, nt=nt, xr=bool(xr))
             else:
+                wp = getattr(L, _ATTR[proj] + "_pk")
+                if wp is not None:   # the dequantized prefill image (_prepare_w4_prefill)
+                    return self._packed(x, wp, proj)
                 y = F.linear(x, self._w4_dense(q))
             return 0, (ops.silu_mul(y, interleaved=il) if proj == "gu" else y)
         attr = _ATTR[proj]

@@ -4,6 +4,7 @@ import pytest
 import torch
 
 from fasttalk_llm_microservice_amd import ops
+from fasttalk_llm_microservice_amd.ops import quant as Q
 from fasttalk_llm_microservice_amd.engine.config import EngineConfig
 from fasttalk_llm_microservice_amd.engine.engine import LLMEngine
 from fasttalk_llm_microservice_amd.engine.sampling_params import SamplingParams
@@ -366,7 +367,7 @@ def test_single_weight_image_llama3_8b():
 @pytest.mark.parametrize("model,rows,quant", [
     ("llama3-8b", 1, None), ("llama3-8b", 20, None), ("llama3-8b", 50, None), ("llama3-8b", 100, None),
     ("llama3-70b", 1, None), ("llama3-70b", 72, None),
-    ("llama3-8b", 50, "w4"), ("llama3-8b", 64, "w4"), ("llama3-8b", 8, "w4")])
+    ("llama3-8b", 50, "w4"), ("llama3-8b", 64, "w4"), ("llama3-8b", 8, "w4"), ("llama3-8b", 100, "w4")])
 def test_llama3_shape_decode_matches_cpu_fp32(model, rows, quant):
     """a 2-layer Llama-3-8B-shaped model (H 4096, I 14336, GQA 4) -- and
     a 70B-shaped one (H 8192, I 28672, GQA 8) -- decoding `rows` sequences with ragged
@@ -384,7 +385,11 @@ def test_llama3_shape_decode_matches_cpu_fp32(model, rows, quant):
     c = LlamaModel(cfg, torch.device("cpu"), torch.float32, max_model_len=8192, quantization=quant)
     c.init_random(5, consistent=True)
     if quant:
-        assert g.layers[0].q4 and g.layers[0].wqkv is None and g.layers[0].wqkv_pk is None
+        # the int4 image streams the <= 64-row steps; above, packed_gemm runs on the
+        # dequantized prefill image (models/llama.py _prepare_w4_prefill, rows 100)
+        L0 = g.layers[0]
+        assert L0.q4 and L0.wqkv is None and L0.wqkv_pk is not None
+        assert torch.equal(L0.wqkv_pk, ops.pack_weight(Q.w4_dequant(L0.q4["qkv"])))
     rng = np.random.default_rng(rows)
     lens = rng.integers(64, 6000, rows)
     lens[0] = 6000
