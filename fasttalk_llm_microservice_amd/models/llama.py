@@ -79,8 +79,6 @@ class LayerWeights:
     wgu_pk: Optional[torch.Tensor] = None
     wd_pk: Optional[torch.Tensor] = None
     # resident row-major copies of some packed projections for hipBLASLt at mixed /
-    # prefill step sizes (LlamaModel._prepare_rowmajor): proj -> [N, K]
-    rm: Optional[Dict[str, torch.Tensor]] = None
     # fused decode layer (skinny_pkr.hip): QKV / gate_up packed with the input norms
     # folded in (W diag(ln)), gate_up rows interleaved for the SiLU epilogue; o / down
     # share the packed images above when present
@@ -165,26 +163,12 @@ PG_PLAN = {
     "lm": ((128, 1, 1), (192, 5, 1), (256, 3, 1), (384, 5, 1), (1 << 30, 0, 1)),
 }
 PG_MAX_SLAB_ROWS = 2048
-# At prefill-burst sizes hipBLASLt's tiles beat packed_gemm (1.35-1.66 vs 1.1-1.2
-# PF/s at M = 4096, profiles/packed_gemm_*_r02.log) by more than it costs to unpack
-# the layer's weight into a transient row-major copy (one read + one write of the
-# weight, ~0.17 ms per 8B layer).  FT_PG_BLAS_ROWS=N: from N rows up the projection
-# unpacks and calls the library.  Default 0 (off, round 5): end to end the library
-# path gained nothing -- config 5 4,854 / 4,757 with it vs 4,844 / 4,797 without,
-# driver config 5,672 vs 5,700 (profiles/ab_pg_blas_rows_r05.log) -- so every GEMM of
-# the serving path runs the hand-written kernels.
-PG_BLAS_ROWS = int(os.environ.get("FT_PG_BLAS_ROWS", "0"))
-# With memory to spare (an 8B model is 16 GB of a 288 GB MI355X) qkv / o / gate_up
-# also stay resident row-major and run hipBLASLt from this many rows up: at the
-# soft-budgeted mixed-step sizes (300-512 rows) the library beats packed_gemm on
-# them (qkv 32.8 vs 43.4 us, o 26.5 vs 33.0, gate_up 91.7 vs 113 at 512 rows,
-# profiles/pg_probe_300_512_r02.log) while down stays packed (71.9 vs 78.7).
-# FT_ROWMAJOR_COPIES: 0 (default: one weight image) / auto (copies <= 15% of device
-# memory) / 1.  At the driver config the copies were worth +1.2% tok/s, within the
-# run-to-run spread (profiles/ab_rowmajor_copies_r03.log), for 10 GB more resident
-# weights, so the single packed image stays the default.
-PG_RM_ROWS = int(os.environ.get("FT_PG_RM_ROWS", "257"))
-RM_PROJS = ("qkv", "o", "gu")
+# hipBLASLt detours removed in round 5: unpacking the packed image into a row-major
+# copy for the library from 2048 rows (FT_PG_BLAS_ROWS) measured neutral end to end
+# (config 5 4,806 vs 4,820 tok/s, driver 5,672 vs 5,700: profiles/ab_pg_blas_rows_r05.log),
+# and resident row-major copies for 257+ rows (FT_ROWMAJOR_COPIES) +1.2%, within the
+# spread, for 10 GB (profiles/ab_rowmajor_copies_r03.log).  Every GEMM of the model
+# runs the hand-written kernels on the packed image.
 
 
 def pg_cfg(proj: str, rows: int, k: int) -> Tuple[int, int]:
@@ -383,8 +367,6 @@ class LlamaModel:
         self.gu_nt = 2
         self.gu_il = False        # gate_up image interleaved in groups of 16 (packed bf16)
         self.w4_slab: dict = {}   # W4 projections that leave split-K slabs
-        self._unpack_buf: Optional[torch.Tensor] = None  # transient row-major weight (prefill)
-        self._unpack_need = 0
         self.tickets: Optional[torch.Tensor] = None
         # TP: all-reduce + residual add + RMSNorm in one launch (FT_TP_FUSED_NORM=0: the
         # separate slab_store -> all-reduce -> add+RMSNorm launches, for A/B runs)
@@ -517,13 +499,19 @@ class LlamaModel:
                 self._install_w4(L, proj, *sh[attr])
             self.layers.append(L)
 
-    def _w4_dense(self, w: "Q.W4Weight") -> torch.Tensor:
-        """bf16 copy of a W4 projection in a shared scratch (prefill-size GEMMs)."""
+    def _w4_packed(self, w: "Q.W4Weight") -> torch.Tensor:
+        """A W4 projection dequantized and re-laid out into the packed image, in two
+        shared scratches (prefill-size steps when the resident prefill image is off)."""
         need = w.n * w.k
-        if self._w4_scratch is None or self._w4_scratch.numel() < need:
+        if self._w4_scratch is None or self._w4_scratch.shape[1] < need:
             big = max(q.n * q.k for L in self.layers for q in (L.q4 or {}).values())
-            self._w4_scratch = torch.empty(max(need, big), dtype=self.dtype, device=self.device)
-        return Q.w4_dequant(w, out=self._w4_scratch[:need].view(w.n, w.k))
+            self._w4_scratch = torch.empty(2, max(need, big), dtype=self.dtype, device=self.device)
+        dense = Q.w4_dequant(w, out=self._w4_scratch[0, :need].view(w.n, w.k))
+        out = self._w4_scratch[1, :need]
+        n, k = w.n, w.k
+        out.view(n // 16, k // 64, 2, 4, 16, 8).copy_(
+            dense.view(n // 16, 16, k // 64, 4, 2, 8).permute(0, 2, 4, 3, 1, 5))
+        return out.view(n, k)
 
     def _prepare_w4_prefill(self):
         """W4A16 prefill image: every W4 projection dequantized ONCE into the packed
@@ -548,25 +536,6 @@ class LlamaModel:
         for L, p, q in qs:
             setattr(L, _ATTR[p] + "_pk", ops.pack_weight(Q.w4_dequant(q)))
         log.info("W4A16 prefill image (dequantized, packed bf16): %.1f GB", nbytes / 1e9)
-
-    def _prepare_rowmajor(self):
-        """Resident row-major copies of the RM_PROJS images (hipBLASLt from PG_RM_ROWS
-        rows, see there) when they fit the memory policy."""
-        mode = os.environ.get("FT_ROWMAJOR_COPIES", "0")
-        if mode == "0" or not self.device.type == "cuda" or not self.layers:
-            return
-        pk = [getattr(L, _ATTR[p] + "_pk") for L in self.layers for p in RM_PROJS]
-        if any(w is None for w in pk):
-            return
-        nbytes = sum(w.numel() * w.element_size() for w in pk)
-        if mode != "1":
-            _, total = torch.cuda.mem_get_info(self.device)
-            if nbytes > 0.15 * total:
-                return
-        for L in self.layers:
-            L.rm = {p: ops.unpack_weight(getattr(L, _ATTR[p] + "_pk")) for p in RM_PROJS}
-        log.info("row-major copies of %s for hipBLASLt at >= %d rows: %.1f GB", "/".join(RM_PROJS),
-                 PG_RM_ROWS, nbytes / 1e9)
 
     def _prepare_packed(self):
         """ONE weight image on the GPU (bf16): every layer projection and the LM head
@@ -597,11 +566,9 @@ class LlamaModel:
             if fold:
                 L.ln1 = L.ln2 = one
         self._prepare_w4_prefill()
-        self.gu_il = self.layers[0].wgu_pk is not None
-        self._unpack_need = max((w.numel() for w in (self.layers[0].wqkv_pk, self.layers[0].wo_pk,
-                                                      self.layers[0].wgu_pk, self.layers[0].wd_pk)
-                                 if w is not None), default=0)
-        self._prepare_rowmajor()
+        # gate_up split-K slabs come from a 16-row-interleaved image: the packed bf16 one,
+        # or (W4) the int4 image dequantized into a scratch above 64 rows
+        self.gu_il = self.layers[0].wgu_pk is not None or self.w4_gu_il
         if self.lm_head is not None:
             self.lm_head_pk = ops.pack_weight(self.lm_head)
             self.lm_head = None
@@ -785,31 +752,26 @@ class LlamaModel:
                     return sp, None
                 y = Q.w4_gemm(x, q, nt=nt, xr=bool(xr))
             else:
+                # the dequantized prefill image (_prepare_w4_prefill), or this
+                # projection dequantized and packed into a scratch when it is off
                 wp = getattr(L, _ATTR[proj] + "_pk")
-                if wp is not None:   # the dequantized prefill image (_prepare_w4_prefill)
-                    return self._packed(x, wp, proj)
-                y = F.linear(x, self._w4_dense(q))
+                return self._packed(x, wp if wp is not None else self._w4_packed(q), proj)
             return 0, (ops.silu_mul(y, interleaved=il) if proj == "gu" else y)
         attr = _ATTR[proj]
         wp = getattr(L, attr + "_pk")
         if wp is None:  # row-major weights: CPU backend, or FT_PACKED_GEMM=0
             y = F.linear(x, getattr(L, attr))
             return 0, (ops.silu_mul(y) if proj == "gu" else y)
-        return self._packed(x, wp, proj, L.rm.get(proj) if L.rm else None)
+        return self._packed(x, wp, proj)
 
-    def _packed(self, x: torch.Tensor, wp: torch.Tensor, proj: str,
-                rm: Optional[torch.Tensor] = None) -> Tuple[int, Optional[torch.Tensor]]:
+    def _packed(self, x: torch.Tensor, wp: torch.Tensor, proj: str) -> Tuple[int, Optional[torch.Tensor]]:
         """y = x W^T on the packed image: the decode kernels up to PACKED_ROWS rows
-        (skinny_gemm.hip), the tiled MFMA GEMM above (packed_gemm.hip); hipBLASLt on
-        the resident row-major copy ``rm`` from PG_RM_ROWS rows."""
+        (skinny_gemm.hip), the tiled MFMA GEMM above (packed_gemm.hip)."""
         if self.invariant:
             return self._packed_invariant(x, wp, proj)
         rows = x.shape[0]
         n, k = wp.shape
         gu = proj == "gu"
-        if rm is not None and rows >= PG_RM_ROWS:
-            y = F.linear(x, rm)
-            return 0, (ops.silu_mul(y, interleaved=True) if gu else y)
         slab_ok = self._slab_ok(proj, rows) and self.ws is not None
         c = packed_cfg(proj, rows) if proj in PACKED_PLAN else None
         while c is not None and c[2] > 1 and not _cfg_fits(c, n, k):
@@ -824,12 +786,6 @@ class LlamaModel:
             y = ops.skinny_gemm(x, wp, splits=1, nt=nt, u=u)
             if u in (-6, -8):  # the xr kernel's own SiLU epilogue: y is already h
                 return 0, y
-            return 0, (ops.silu_mul(y, interleaved=True) if gu else y)
-        if PG_BLAS_ROWS and rows >= PG_BLAS_ROWS and proj != "lm":
-            if self._unpack_buf is None or self._unpack_buf.numel() < n * k:
-                self._unpack_buf = torch.empty(max(n * k, self._unpack_need), dtype=wp.dtype,
-                                               device=wp.device)
-            y = F.linear(x, ops.unpack_weight(wp, out=self._unpack_buf))
             return 0, (ops.silu_mul(y, interleaved=True) if gu else y)
         cfg, sp = pg_cfg(proj, rows, k)
         if sp > 1 and (self.ws is None or sp * rows * n > self.ws.numel()):

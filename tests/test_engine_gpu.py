@@ -29,20 +29,21 @@ def _prompts(n, lens, seed=0):
 @pytest.mark.parametrize("model,quant,T,fused_rows", [
     ("tiny-gqa4", None, 40, None), ("tiny-2k", None, 40, None), ("tiny-2k", None, 7, None),
     ("tiny-2k", None, 40, 64), ("tiny-2k", "w4", 40, None), ("tiny-2k", "w4", 100, None),
-    ("tiny", "w4", 40, None), ("tiny-2k", None, 300, None)])
+    ("tiny-2k", "w4", 101, None), ("tiny", "w4", 40, None), ("tiny-2k", None, 300, None)])
 def test_gpu_logits_match_cpu_reference(model, quant, T, fused_rows, monkeypatch):
     """Full forward on GPU (bf16 HIP kernels; at hidden 2048 the down projection
     and LM head run on the packed-weight skinny GEMMs) vs CPU fp32 reference ops.
     bf16 <= FUSED_ROWS rows: the fused decode layer (fused_rows=64 at 40 rows runs
     the 48-row bucket, wave-split-N GEMMs).  W4: <= 64 rows run the W4A16 kernels
-    (o / down into split-K slabs), 100 rows the dequantize + hipBLASLt path; the CPU
-    side holds the dequantized weights.  bf16 at 300 rows with FT_ROWMAJOR_COPIES=1:
-    qkv / o / gate_up on hipBLASLt over resident row-major copies, down on packed_gemm."""
+    (o / down into split-K slabs), 100 rows packed_gemm on the resident dequantized
+    prefill image, 101 rows the same with the image off (each projection dequantized
+    and packed into a scratch); the CPU side holds the dequantized weights.  bf16 at
+    300 rows: packed_gemm's split-K plan."""
     if fused_rows is not None:
         from fasttalk_llm_microservice_amd.models import llama
         monkeypatch.setattr(llama, "FUSED_ROWS", fused_rows)
-    if T >= 257 and quant is None:
-        monkeypatch.setenv("FT_ROWMAJOR_COPIES", "1")
+    if quant and T == 101:
+        monkeypatch.setenv("FT_W4_PREFILL_IMAGE", "0")
     cfg = MODELS[model]
     # consistent=True: both draw the same unsharded weights on the host from one seed
     g = LlamaModel(cfg, torch.device("cuda"), torch.bfloat16, max_model_len=512,
@@ -51,8 +52,7 @@ def test_gpu_logits_match_cpu_reference(model, quant, T, fused_rows, monkeypatch
     c.init_random(3, consistent=True)
     if quant:
         assert g.layers[0].q4 and g.layers[0].wgu is None and c.layers[0].q4 is None
-    elif T >= 257:   # qkv / o / gate_up on hipBLASLt over the resident row-major copies
-        assert g.layers[0].rm is not None and set(g.layers[0].rm) == {"qkv", "o", "gu"}
+        assert (g.layers[0].wgu_pk is None) == (T == 101)
     bs = 16
     nblk = max(8, -(-T // bs))
     for m in (g, c):
