@@ -190,6 +190,12 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and os.environ.get("FT_BENCH_SHARED_GPU", "0") == "1" and \
+            not os.environ.get("ENGINE_GPU_MEMORY_UTILIZATION"):
+        # ranks started by torch.distributed.run (not _launch_ranks) sharing one device:
+        # the same 1/n KV share each, sized against their own allocations
+        os.environ["ENGINE_GPU_MEMORY_UTILIZATION"] = f"{0.85 / world:.3f}"
+        os.environ.setdefault("ENGINE_KV_SIZING", "own")
     if a.tp > 1:
         return bench_tp(a, rank, world, local_rank)
 

@@ -16,18 +16,28 @@ from gemm_sweep import graph_time  # noqa: E402
 
 
 def main():
+    import argparse
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="8b", choices=["8b", "70b"])
+    ap.add_argument("--rows", default="50,64")
+    a = ap.parse_args()
     torch.manual_seed(0)
     dev = "cuda"
-    ws = torch.empty(16 * 64 * 28672, device=dev)
-    shapes = [("qkv", 6144, 4096, False), ("o", 4096, 4096, False), ("gu", 28672, 4096, True),
-              ("down", 4096, 14336, False)]
+    if a.model == "70b":   # Llama-3-70B at TP=1: H 8192, I 28672, 64 q / 8 kv heads
+        shapes = [("qkv", 10240, 8192, False), ("o", 8192, 8192, False), ("gu", 57344, 8192, True),
+                  ("down", 8192, 28672, False)]
+    else:
+        shapes = [("qkv", 6144, 4096, False), ("o", 4096, 4096, False), ("gu", 28672, 4096, True),
+                  ("down", 4096, 14336, False)]
+    ws = torch.empty(8 * 64 * max(n for _, n, _, _ in shapes), device=dev)
     for name, n, k, gu in shapes:
         ncopy = max(2, min(32, (640 << 20) // (n * k * 2)))
         Wr = [(torch.randn(n, k, device=dev) * 0.02).bfloat16() for _ in range(ncopy)]
         if gu:
             Wr = [ops.interleave_gate_up(w, 1) for w in Wr]
         Wp = [ops.pack_weight(w) for w in Wr]
-        for M in (50, 64):
+        for M in [int(r) for r in a.rows.split(",")]:
             x = torch.randn(M, k, device=dev).bfloat16()
             ref = (x.float() @ Wr[0].float().t())
             if gu:

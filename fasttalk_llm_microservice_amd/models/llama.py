@@ -312,10 +312,24 @@ def w4_cfg(proj: str, rows: int):
     return W4_PLAN[proj][b]
 
 
-def packed_cfg(proj: str, rows: int):
+# Projections of >= 64 M weights (Llama-3-70B at TP=1: qkv 10240 x 8192, o 8192 x 8192,
+# down 8192 x 28672) at 33-64 rows: two column tiles per wave (qkv, down) or 8-wave
+# workgroups (o), same splits -- cold-cache us at 50 rows, round 5
+# (profiles/xr_sweep_70b_r05.log): qkv 35.3 vs 44.6, o 25.2 vs 28.3, down 77.9 vs 85.3.
+# FT_WIDE_DECODE_PLAN=0 keeps the default plan for them.
+PACKED_PLAN_WIDE = {"qkv": {64: (2, -5, 2)}, "o": {64: (1, -7, 4)}, "down": {64: (2, -5, 4)}}
+WIDE_ELEMS = 64 << 20
+WIDE_PLAN = os.environ.get("FT_WIDE_DECODE_PLAN", "1") != "0"
+
+
+def packed_cfg(proj: str, rows: int, n: int = 0, k: int = 0):
     if rows > PACKED_ROWS:
         return None
     b = next(m for m in _M_BUCKETS if m >= rows)
+    if WIDE_PLAN and n * k >= WIDE_ELEMS:
+        c = PACKED_PLAN_WIDE.get(proj, {}).get(b)
+        if c is not None:
+            return c
     return PACKED_PLAN[proj].get(b)
 
 
@@ -773,7 +787,7 @@ class LlamaModel:
         n, k = wp.shape
         gu = proj == "gu"
         slab_ok = self._slab_ok(proj, rows) and self.ws is not None
-        c = packed_cfg(proj, rows) if proj in PACKED_PLAN else None
+        c = packed_cfg(proj, rows, n, k) if proj in PACKED_PLAN else None
         while c is not None and c[2] > 1 and not _cfg_fits(c, n, k):
             c = (c[0], c[1], c[2] // 2)   # a K the plan's split does not divide (TP shards)
         if c is not None and _cfg_fits(c, n, k):
