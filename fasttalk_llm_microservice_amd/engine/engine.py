@@ -378,8 +378,8 @@ class LLMEngine:
 
     def _wait_mark(self, e: "_Inflight"):
         """A step is about to be queued behind the mixed step ``e``: wait (admitting
-        new requests) until the GPU has passed ``e``'s mark, three quarters into its
-        layers by default (runner ENGINE_MIXED_CHAIN_AT), so prompts that arrive
+        new requests) until the GPU has passed ``e``'s mark, 60% into its layers by
+        default (runner ENGINE_MIXED_CHAIN_AT), so prompts that arrive
         meanwhile still make the next step -- built at once, the next step would
         leave them a step behind (+9 ms p50 engine TTFT at the driver config) --
         while the host has the rest of ``e`` to build and queue it."""

@@ -264,8 +264,10 @@ class ModelRunner:
         self.stg = [_Staging(mb, self.max_blocks_per_seq, pin, self.is_gpu) for _ in range(nstg)]
         self._mx_handles = [MixedHandle(mb, pin, self.is_gpu) for _ in range(MIXED_HANDLES)]
         # ENGINE_MIXED_CHAIN_AT: fraction of a queued mixed step's layers after which
-        # its mark event is recorded (0: no mark, the next step is built at once)
-        self.mixed_mark_frac = float(os.environ.get("ENGINE_MIXED_CHAIN_AT", "0.75"))
+        # its mark event is recorded (0: no mark, the next step is built at once).
+        # 0.6: 5,751 / 5,782 / 5,694 vs 5,701-5,711 tok/s at 0.75, same p50 TTFT
+        # (profiles/ab_sched_screen_r05.log)
+        self.mixed_mark_frac = float(os.environ.get("ENGINE_MIXED_CHAIN_AT", "0.6"))
         self._mx_next = 0
         self._stg_next = 0
         self._upload = _Uploader(dv, pin) if self.is_gpu else None
