@@ -842,7 +842,9 @@ class ModelRunner:
         self._assert_no_pending_split("mixed_launch")
         if self._gaps is not None:
             self._gap_mark(True, "a")
+        tp0 = time.perf_counter()
         host = self._mixed_host(batch)
+        tp1 = time.perf_counter()
         nd = host["nd"]
         self.stats["prefill_steps"] += 1
         self.stats["mixed_ahead"] = self.stats.get("mixed_ahead", 0) + 1
@@ -862,12 +864,14 @@ class ModelRunner:
         else:
             dev = [torch.from_numpy(np.ascontiguousarray(a)) for a in arrays]
         d = dict(zip(names, dev))
+        tp2 = time.perf_counter()
         if nd and len(dst):
             src_t, dst_t = dev[len(names) + 5], dev[len(names) + 6]
             if partial:
                 d["ids"].index_copy_(0, dst_t, self.d_out.index_select(0, src_t))
             else:
                 torch.index_select(self.d_out, 0, src_t, out=d["ids"][:nd])
+        tp3 = time.perf_counter()
         meta = AttnMeta(
             positions=d["pos"], slot_mapping=d["slots"], logits_indices=d["lrows"], num_decode=nd,
             block_tables=d["bt"], seq_lens=d["seq_lens"],
@@ -905,6 +909,14 @@ class ModelRunner:
             mh.event.record()
         if self._gaps is not None:
             self._gap_mark(False)
+        tp4 = time.perf_counter()
+        ml = self.stats.setdefault("mixed_launch_ms", {"host": 0.0, "upload": 0.0, "gather": 0.0,
+                                                        "forward": 0.0, "n": 0})
+        ml["host"] += 1e3 * (tp1 - tp0)
+        ml["upload"] += 1e3 * (tp2 - tp1)
+        ml["gather"] += 1e3 * (tp3 - tp2)
+        ml["forward"] += 1e3 * (tp4 - tp3)
+        ml["n"] += 1
         return mh
 
     def mixed_collect(self, h: "MixedHandle") -> List[int]:
