@@ -119,6 +119,12 @@ class LLMEngine:
         # queued behind a running one -- instead of running each synchronously with
         # the GPU idle while the host collects it and builds the next
         self.mixed_chain = self.mixed_ahead and os.environ.get("ENGINE_MIXED_CHAIN", "1") != "0"
+        # ENGINE_MIXED_CHAIN_GUIDED: the chain also covers guided (grammar-masked) rows
+        # and prompts -- a mixed step queued behind guided decode rows defers its
+        # sampler until their masks are known (runner.sample_launch), like the split
+        # decode graphs do
+        self.mixed_chain_guided = self.mixed_chain and \
+            os.environ.get("ENGINE_MIXED_CHAIN_GUIDED", "1") != "0"
         self._last_complete = 0.0
         from .debug import FaultInjector, StepProfiler
 
@@ -319,8 +325,11 @@ class LLMEngine:
             return skip("queued_mixed")
         if not hasattr(self.runner, "mixed_launch") or getattr(self.runner, "bcast", None) is not None:
             return None
-        if any(q.grammar is not None or q.lazy or q.jf_ids for q in sched.waiting) or \
-                any(q.grammar is not None for q in sched.background):
+        guided = self.mixed_chain_guided and self.pipeline_depth == 1 and self._guided_pipeline()
+        # (a guided prompt's jump-forward head, jf_ids, is part of its prompt: prefilled
+        # like the rest, reported with its first sampled token)
+        if any(not guided and (q.grammar is not None or q.lazy or q.jf_ids) for q in sched.waiting) \
+                or any(q.grammar is not None for q in sched.background):
             return skip("grammar")
         running = list(sched.running)
         if not running:   # nothing to overlap: the drained path schedules it
@@ -333,8 +342,8 @@ class LLMEngine:
         # a running sequence that is not a row of the last queued step joined after it
         # was built (its prompt completed in an earlier, collected step): with nothing
         # queued for it, its id is its last token (rowmap -1)
-        if any((id(q) not in pos and q.inflight) or q.grammar is not None or q.drop_next
-               for q in running):
+        if any((id(q) not in pos and q.inflight) or (q.grammar is not None and not guided)
+               or q.drop_next for q in running):
             return skip("rows")
         if not self._grow_for_next(running):
             return skip("blocks")
@@ -346,10 +355,19 @@ class LLMEngine:
         if not pseqs:
             return skip("no_prefill")
         mb = sched.stamp(ScheduledBatch(running, pseqs, ptok, psamp))
-        h = self.runner.mixed_launch(mb, [pos.get(id(q), -1) for q in running])
+        rowmap = [pos.get(id(q), -1) for q in running]
+        # guided decode rows: their masks wait for the tokens of the step queued ahead,
+        # so the sampler is queued once those are processed (_step_pipelined); guided
+        # prompts alone (initial grammar states) have their masks now
+        defer = any(q.grammar is not None for q in running)
+        masks = None if defer else self._masks_for(mb.sampled_seqs())
+        h = self.runner.mixed_launch(mb, rowmap, masks=masks, defer_sample=defer) \
+            if (defer or masks is not None) else self.runner.mixed_launch(mb, rowmap)
         for q in mb.sampled_seqs():
             q.inflight += 1
         self.stats["mixed_ahead"] += 1
+        if defer:
+            self.stats["mixed_deferred_sample"] += 1
         if self._inflight[-1].mixed:
             self.stats["mixed_chain"] += 1
         return _Inflight(mb, h, True)
@@ -359,15 +377,19 @@ class LLMEngine:
         from the host) instead of run synchronously, so the steps behind it can be
         queued while it runs.  False where only the synchronous path applies: TP
         broadcast, allow-masks, jump-forward chunks, swaps."""
-        if not self.mixed_chain or masks is not None or batch.swap_out or batch.swap_in \
+        if not self.mixed_chain or (masks is not None and not self.mixed_chain_guided) \
+                or batch.swap_out or batch.swap_in \
                 or not hasattr(self.runner, "mixed_launch") \
                 or getattr(self.runner, "bcast", None) is not None \
                 or self.runner.__class__.__name__ != "ModelRunner" or not self.cfg.async_output:
             return False
-        if any(q.status == SeqStatus.RUNNING or q.grammar is not None or q.lazy
-               for q in batch.prefill_seqs) or any(q.grammar is not None for q in batch.decode_seqs):
+        guided = self.mixed_chain_guided
+        if any(q.status == SeqStatus.RUNNING or (not guided and (q.grammar is not None or q.lazy or q.jf_ids))
+               for q in batch.prefill_seqs) or \
+                (not guided and any(q.grammar is not None for q in batch.decode_seqs)):
             return False
-        h = self.runner.mixed_launch(batch, None)
+        h = self.runner.mixed_launch(batch, None, masks=masks) if masks is not None \
+            else self.runner.mixed_launch(batch, None)
         for q in batch.sampled_seqs():
             q.inflight += 1
         e = _Inflight(batch, h, True)
@@ -437,7 +459,7 @@ class LLMEngine:
         if self._inflight and getattr(self._inflight[0].handle, "pending", False):
             nxt = self._inflight[0]
             self.runner.sample_launch(nxt.handle, self._masks_for(nxt.batch.sampled_seqs()))
-            self.stats["guided_pipelined_steps"] += 1
+            self.stats["guided_pipelined_mixed" if nxt.mixed else "guided_pipelined_steps"] += 1
         t2 = time.perf_counter()
         dt = t2 - self._last_complete if self._last_complete else t2 - t0
         self._last_complete = t2

@@ -150,13 +150,18 @@ class MixedHandle:
     builds the step queued behind it once the GPU passes it).  They rotate; a
     handle is reused only after MIXED_HANDLES - 1 later mixed launches, more than
     the steps the engine keeps queued (ENGINE_PIPELINE_DEPTH + 1)."""
-    __slots__ = ("host", "event", "mark", "n")
+    __slots__ = ("host", "event", "mark", "n", "pending", "logits", "samp")
 
     def __init__(self, rows: int, pin: bool, gpu: bool):
         self.host = torch.zeros(rows, dtype=torch.int32, pin_memory=pin)
         self.event = torch.cuda.Event() if gpu else None
         self.mark = torch.cuda.Event() if gpu else None
         self.n = 0
+        # deferred sampler (guided rows behind a queued step): the logits and the
+        # device sampling arrays wait here for sample_launch
+        self.pending = False
+        self.logits = None
+        self.samp = None
 
 
 MIXED_HANDLES = 4
@@ -770,11 +775,19 @@ class ModelRunner:
         return DecodeHandle(st, n, nb)
 
     @torch.inference_mode()
-    def sample_launch(self, h: DecodeHandle, masks: Optional[np.ndarray]):
+    def sample_launch(self, h, masks: Optional[np.ndarray]):
         """Queues the sampler of a step whose forward pass ``decode_launch(...,
         defer_sample=True)`` queued: its allow-masks go up, the sampler graph reads
         the forward graph's logits, the ids land in ``d_out`` (the next step's
-        inputs) and in the staging set's pinned copy."""
+        inputs) and in the staging set's pinned copy.  A mixed step's
+        (``mixed_launch(..., defer_sample=True)``) eager sampler reads its held logits."""
+        if isinstance(h, MixedHandle):
+            assert h.pending
+            dmask = None
+            if masks is not None:
+                dmask = self._upload([masks])[0] if self.is_gpu else torch.from_numpy(masks)
+            self._mixed_sample(h, h.logits, h.samp, dmask)
+            return
         assert h.pending and self._pending_split is h
         self._set_masks(masks, h.n)
         self.graphs_split[h.nb][1].replay()
@@ -830,7 +843,8 @@ class ModelRunner:
         return ev is None or ev.query()
 
     @torch.inference_mode()
-    def mixed_launch(self, batch: ScheduledBatch, rowmap: Optional[List[int]]) -> "MixedHandle":
+    def mixed_launch(self, batch: ScheduledBatch, rowmap: Optional[List[int]],
+                     masks: Optional[np.ndarray] = None, defer_sample: bool = False) -> "MixedHandle":
         """Queues a mixed (decode + prefill) step behind the queued step(s) without
         waiting (engine ``_speculate_mixed``): decode row i's input id is row
         ``rowmap[i]`` of the last queued step's sampled ids (``d_out``), gathered on
@@ -838,7 +852,11 @@ class ModelRunner:
         nothing is queued, the ids are the sequences' last tokens (host).  The
         sampled ids land in ``d_out`` (rows = ``batch.sampled_seqs()``) for the
         decode step queued next, and in a pinned host buffer for the collect.
-        Single process only (no TP broadcast), no allow-masks."""
+        ``masks``: the sampled rows' allow-masks when they are known at launch;
+        ``defer_sample``: they are not (guided rows whose grammar waits for the step
+        queued ahead) -- the forward pass is queued now, the sampler by
+        :meth:`sample_launch` once the engine has the masks.  Single process only
+        (no TP broadcast)."""
         self._assert_no_pending_split("mixed_launch")
         if self._gaps is not None:
             self._gap_mark(True, "a")
@@ -859,6 +877,8 @@ class ModelRunner:
         partial = nd and rowmap is not None and len(dst) < nd
         arrays.append(rm[dst] if nd and len(dst) else np.zeros(1, np.int64))
         arrays.append(dst if partial and len(dst) else np.zeros(1, np.int64))
+        if masks is not None and not defer_sample:
+            arrays.append(masks)
         if self.is_gpu:
             dev = self._upload(arrays)
         else:
@@ -899,14 +919,18 @@ class ModelRunner:
         if self.logits_tap is not None:
             self._tap(logits.float().cpu())   # taps are host tensors (tests)
         n = logits.shape[0]
-        temp, topp, topk, seeds, steps = dev[len(names):len(names) + 5]
-        ops.sample(logits, temp, topp, topk, seeds, steps, out=self.d_out[:n])
+        samp = dev[len(names):len(names) + 5]
         if mh.host.shape[0] < n:
             mh.host = torch.zeros(2 * n, dtype=torch.int32, pin_memory=self.is_gpu)
         mh.n = n
-        mh.host[:n].copy_(self.d_out[:n], non_blocking=self.is_gpu)
-        if mh.event is not None:
-            mh.event.record()
+        if defer_sample:
+            # the sampling arrays are views into the shared upload buffer, which the
+            # masks' upload (sample_launch) overwrites first: keep copies
+            mh.pending, mh.logits, mh.samp = True, logits, [t.clone() for t in samp]
+            self.stats["deferred_mixed"] = self.stats.get("deferred_mixed", 0) + 1
+        else:
+            dmask = dev[len(names) + 7] if masks is not None else None
+            self._mixed_sample(mh, logits, samp, dmask)
         if self._gaps is not None:
             self._gap_mark(False)
         tp4 = time.perf_counter()
@@ -918,6 +942,14 @@ class ModelRunner:
         ml["forward"] += 1e3 * (tp4 - tp3)
         ml["n"] += 1
         return mh
+
+    def _mixed_sample(self, mh: "MixedHandle", logits, samp, dmask):
+        temp, topp, topk, seeds, steps = samp
+        ops.sample(logits, temp, topp, topk, seeds, steps, out=self.d_out[:mh.n], mask=dmask)
+        mh.host[:mh.n].copy_(self.d_out[:mh.n], non_blocking=self.is_gpu)
+        if mh.event is not None:
+            mh.event.record()
+        mh.pending, mh.logits, mh.samp = False, None, None
 
     def mixed_collect(self, h: "MixedHandle") -> List[int]:
         if h.event is not None:

@@ -454,13 +454,23 @@ def test_jump_forward_prefills_forced_grammar_runs(tiny_engine, monkeypatch):
     eng = tiny_engine
     steps = []
     orig = eng.runner.execute
+    orig_launch = eng.runner.mixed_launch
+
+    def record(batch):
+        starts = batch.prefill_start or [s.num_computed for s in batch.prefill_seqs]
+        steps.append([(a, n, s.status.name) for s, n, a in
+                      zip(batch.prefill_seqs, batch.prefill_tokens, starts)] + [("d", len(batch.decode_seqs))])
 
     def spy(batch, masks):
-        steps.append([(s.num_computed, n, s.status.name) for s, n in
-                      zip(batch.prefill_seqs, batch.prefill_tokens)] + [("d", len(batch.decode_seqs))])
+        record(batch)
         return orig(batch, masks)
 
+    def spy_launch(batch, rowmap, *args, **kw):   # mixed steps queued by the mixed chain
+        record(batch)
+        return orig_launch(batch, rowmap, *args, **kw)
+
     monkeypatch.setattr(eng.runner, "execute", spy)
+    monkeypatch.setattr(eng.runner, "mixed_launch", spy_launch)
     before = eng.stats["jump_forward_tokens"]
     outs = []
     for seed in range(4):

@@ -426,6 +426,41 @@ class _GuidedRunner(ModelRunner):
         assert not h.pending, "collected a step whose sampler never ran"
         return list(h.out)
 
+    def mixed_launch(self, batch, rowmap, masks=None, defer_sample=False):
+        """Mixed step: decode rows' ids from the last queued step (rowmap) or the host
+        (None / -1), completed prompts sample at their last position; a deferred
+        sampler waits for sample_launch (guided rows behind a queued step)."""
+        self.mixed.append((len(batch.decode_seqs), list(batch.prefill_tokens),
+                           None if rowmap is None else list(rowmap)))
+        ids, pos = [], []
+        for i, s in enumerate(batch.decode_seqs):
+            if rowmap is None or rowmap[i] < 0:
+                assert s.inflight == 0
+                ids.append(int(s.tokens[-1]))
+            else:
+                assert s.inflight >= 1 and self.d_out is not None
+                ids.append(self.d_out[rowmap[i]])
+            pos.append(s.n_tokens - 1 + s.inflight)
+            assert pos[-1] // self.bs < len(s.block_ids)
+        starts = batch.prefill_start or [s.num_computed for s in batch.prefill_seqs]
+        for s, n, smp, a in zip(batch.prefill_seqs, batch.prefill_tokens, batch.prefill_sample, starts):
+            assert (a + n + self.bs - 1) // self.bs <= len(s.block_ids)
+            if smp:
+                assert a + n == s.n_tokens
+                ids.append(int(s.tokens[-1]))
+                pos.append(s.n_tokens - 1)
+        h = _GHandle(ids, pos, defer_sample)
+        if defer_sample:
+            self.d_out = None
+            self.stats["deferred_mixed"] = self.stats.get("deferred_mixed", 0) + 1
+        else:
+            self._sample(h, masks)
+        return h
+
+    def mixed_collect(self, h):
+        assert not h.pending, "collected a mixed step whose sampler never ran"
+        return list(h.out)
+
 _GuidedRunner.__name__ = "ModelRunner"
 
 
@@ -475,3 +510,60 @@ def test_guided_batches_pipeline_with_deferred_sampler():
     assert eng.stats["guided_pipelined_steps"] > 0 and runner.stats.get("deferred", 0) > 0
     assert eng.stats["jump_forward_tokens"] > 0 and eng.stats["pipelined_jump_drops"] > 0
 
+
+
+def test_guided_rows_chain_mixed_steps_with_deferred_sampler():
+    """Mixed chain with guided rows: prompts arriving while guided tool calls decode
+    are prefilled in mixed steps queued behind them, whose sampler waits for the
+    guided rows' masks (ENGINE_MIXED_CHAIN_GUIDED).  Tokens equal the synchronous
+    engine's; every block and in-flight count comes back."""
+    import json
+    import os
+
+    from fasttalk_llm_microservice_amd.engine.guided import GuidedSpec, tool_call_ast
+
+    tools = [{"type": "function", "function": {"name": "duckduckgo_search", "parameters": {
+        "type": "object", "properties": {"query": {"type": "string", "maxLength": 24},
+                                         "max_results": {"type": "integer"}},
+        "required": ["query", "max_results"]}}}]
+    spec = GuidedSpec(tool_call_ast(tools))
+
+    def run(async_output):
+        os.environ["ENGINE_MIXED_AHEAD"] = "1"
+        os.environ["ENGINE_MIXED_CHAIN"] = "1"
+        cfg = EngineConfig(model="tiny", device="cpu", block_size=4, async_output=async_output,
+                           pipeline_depth=1, max_num_seqs=32, max_num_batched_tokens=24)
+        runner = _GuidedRunner()
+        eng = LLMEngine(cfg, runner=runner)
+        res = {}
+
+        def add(i):
+            guided = i % 3 == 0
+            sp = SamplingParams(temperature=0.0, max_tokens=60 if guided else 8 + 3 * (i % 4),
+                                stop_token_ids=None if guided else [EOS],
+                                guided=spec if guided else None)
+            eng.add_request(f"r{i}", [20 + 3 * i + j for j in range(5 + (i % 5) * 4)], sp,
+                            on_output=lambda o, i=i: res.setdefault(i, []).extend(o.token_ids))
+
+        for i in range(4):
+            add(i)
+        k, step = 4, 0
+        while eng.has_work() or k < 14:
+            if k < 14 and step % 2 == 1:
+                add(k)
+                k += 1
+            eng.step()
+            step += 1
+        for v in ("ENGINE_MIXED_AHEAD", "ENGINE_MIXED_CHAIN"):
+            os.environ.pop(v, None)
+        assert eng.bm.num_free() == eng.bm.num_blocks
+        assert all(q.inflight == 0 and q.drop_next == 0 and q.pf_sched == 0
+                   for q in eng.scheduler.by_id.values())
+        return [res.get(i, []) for i in range(14)], eng, runner
+
+    ref, _, _ = run(False)
+    got, eng, runner = run(True)
+    assert got == ref
+    for i in range(0, 14, 3):   # the guided ones are valid calls
+        assert json.loads(eng.tokenizer.decode(got[i]))["name"] == "duckduckgo_search"
+    assert eng.stats["mixed_deferred_sample"] > 0 and eng.stats["guided_pipelined_mixed"] > 0
