@@ -89,6 +89,11 @@ class AgentConfig(BaseModel):
     # so a real checkpoint picks tools itself and its calls are always valid JSON (the
     # keyword router behind guided_tool_calls exists for random weights)
     model_tool_choice: bool = False
+    # scheduling priority of a tool round's follow-up request (AGENT_TOOL_ROUND_PRIORITY):
+    # the user has already waited through the call and the tool, so the re-prompt is
+    # prefilled ahead of waiting prompts that have not started (engine
+    # Scheduler.add); 0 queues it in arrival order like any new turn
+    tool_round_priority: int = 1
 
 
 @dataclass(slots=True)
@@ -127,6 +132,7 @@ class VoiceAgent:
             guided_tool_calls=e("AGENT_GUIDED_TOOL_CALLS", "false").lower() == "true",
             prefill_tool_head=e("AGENT_PREFILL_TOOL_HEAD", "true").lower() == "true",
             model_tool_choice=e("AGENT_MODEL_TOOL_CHOICE", "false").lower() == "true",
+            tool_round_priority=int(e("AGENT_TOOL_ROUND_PRIORITY", "1")),
         )
 
     # ------------------------------------------------------------------ backend
@@ -256,7 +262,8 @@ class VoiceAgent:
                     request_id=sid, session_id=sid if (rnd == 0 and (guided is None or lazy)) else None,
                     prefix_session=sid, assistant_prefix=head, tools=schemas or None, guided=guided,
                     seed=seed, guided_lazy=lazy,
-                    ignore_eos=ignore_eos and (guided is None or lazy), min_tokens=min_tokens):
+                    ignore_eos=ignore_eos and (guided is None or lazy), min_tokens=min_tokens,
+                    priority=self.config.tool_round_priority if rnd > 0 else 0):
                 if out.finished:
                     finish = out.finish_reason
                 n = len(out.token_ids)

@@ -49,15 +49,28 @@ def test_agent_guided_tool_call_round_trip(engine):
     assert agent.is_native and set(agent.tools()) == {"duckduckgo_search", "get_current_time",
                                                        "get_session_info"}
 
+    prios = []
+    orig = engine.generate
+
+    def spy(prompt_ids, params, request_id=None):
+        prios.append((params.guided is not None, params.priority))
+        return orig(prompt_ids, params, request_id=request_id)
+
     async def run():
         return [ev async for ev in agent.generate_events("Search the web for the weather news",
                                                          _ctx(), seed=5, max_tokens=24)]
 
-    events = asyncio.run(run())
+    engine.generate = spy
+    try:
+        events = asyncio.run(run())
+    finally:
+        engine.generate = orig
     calls = [e for e in events if e.tool_call]
     assert calls, "guided decoding must produce a valid tool call"
     assert calls[0].tool_call["name"] in agent.tools() and calls[0].tool_result
     assert events[-1].finish_reason in ("stop", "length")
+    # the forced call keeps arrival order; the re-prompt after the tool jumps the queue
+    assert prios[0] == (True, 0) and len(prios) >= 2 and prios[1][1] == 1, prios
 
 
 @pytest.mark.parametrize("head", [True, False])
