@@ -89,11 +89,11 @@ class AgentConfig(BaseModel):
     # so a real checkpoint picks tools itself and its calls are always valid JSON (the
     # keyword router behind guided_tool_calls exists for random weights)
     model_tool_choice: bool = False
-    # scheduling priority of a tool round's follow-up request (AGENT_TOOL_ROUND_PRIORITY):
-    # the user has already waited through the call and the tool, so the re-prompt is
-    # prefilled ahead of waiting prompts that have not started (engine
-    # Scheduler.add); 0 queues it in arrival order like any new turn
-    tool_round_priority: int = 1
+    # scheduling priority of a tool round's follow-up request (AGENT_TOOL_ROUND_PRIORITY,
+    # opt-in): > 0 prefills the re-prompt ahead of waiting prompts that have not started
+    # (engine Scheduler.add); 0 queues it in arrival order like any new turn.  Measured
+    # neutral at config 5 with the mixed chain (profiles/ab_tool_round_priority_r05.log)
+    tool_round_priority: int = 0
 
 
 @dataclass(slots=True)
@@ -132,7 +132,7 @@ class VoiceAgent:
             guided_tool_calls=e("AGENT_GUIDED_TOOL_CALLS", "false").lower() == "true",
             prefill_tool_head=e("AGENT_PREFILL_TOOL_HEAD", "true").lower() == "true",
             model_tool_choice=e("AGENT_MODEL_TOOL_CHOICE", "false").lower() == "true",
-            tool_round_priority=int(e("AGENT_TOOL_ROUND_PRIORITY", "1")),
+            tool_round_priority=int(e("AGENT_TOOL_ROUND_PRIORITY", "0")),
         )
 
     # ------------------------------------------------------------------ backend

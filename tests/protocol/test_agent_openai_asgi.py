@@ -44,8 +44,8 @@ def test_tools_offline():
 # ----------------------------------------------------------------------------- agent
 def test_agent_guided_tool_call_round_trip(engine):
     handler = NativeHandler(engine=engine)
-    agent = VoiceAgent(AgentConfig(guided_tool_calls=True, max_tokens=24, temperature=0.7),
-                       backend=handler)
+    agent = VoiceAgent(AgentConfig(guided_tool_calls=True, max_tokens=24, temperature=0.7,
+                                   tool_round_priority=1), backend=handler)
     assert agent.is_native and set(agent.tools()) == {"duckduckgo_search", "get_current_time",
                                                        "get_session_info"}
 
@@ -70,6 +70,7 @@ def test_agent_guided_tool_call_round_trip(engine):
     assert calls[0].tool_call["name"] in agent.tools() and calls[0].tool_result
     assert events[-1].finish_reason in ("stop", "length")
     # the forced call keeps arrival order; the re-prompt after the tool jumps the queue
+    # (AGENT_TOOL_ROUND_PRIORITY, opt-in)
     assert prios[0] == (True, 0) and len(prios) >= 2 and prios[1][1] == 1, prios
 
 
