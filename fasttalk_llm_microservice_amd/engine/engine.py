@@ -335,10 +335,11 @@ class LLMEngine:
         if not running:   # nothing to overlap: the drained path schedules it
             return skip("no_running")
         pos = {id(q): i for i, q in enumerate(last)}
-        # (guided decode rows: a mixed step queued behind them with its sampler deferred
-        # until their masks were known was built and measured in round 4 -- more, smaller
-        # mixed steps and a worse tool-turn tail, p99 462 / 541 vs 408 / 398 ms on one
-        # box, profiles/ab_guided_mixed_ahead_r04.log -- and removed)
+        # (guided decode rows: round 4 queued a mixed step behind them, sampler deferred
+        # until their masks were known, without the chain -- more, smaller mixed steps
+        # and a worse tool-turn tail, profiles/ab_guided_mixed_ahead_r04.log.  With the
+        # round-5 chain the same deferral measured +5.2% tok/s at config 5 and a lower
+        # p99 TTFT, profiles/ab_mixed_chain_guided_r05.log: ENGINE_MIXED_CHAIN_GUIDED)
         # a running sequence that is not a row of the last queued step joined after it
         # was built (its prompt completed in an earlier, collected step): with nothing
         # queued for it, its id is its last token (rowmap -1)
