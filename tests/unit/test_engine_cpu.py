@@ -647,3 +647,47 @@ def test_priority_does_not_jump_preempted_sequences():
     sch.add(fresh)
     sch.add(mk("t", 1))
     assert [q.request_id for q in sch.waiting] == ["victim", "t", "fresh"]
+
+
+def test_chained_prefill_chunks_and_epoch_guard():
+    """Mixed chain bookkeeping (Scheduler.stamp / post_step): a second chunk of a
+    chunked prompt scheduled before the first one's step completed continues after
+    it (Sequence.pf_sched), and a chunk whose KV was dropped while it was queued
+    (recompute preemption: epoch bump) is ignored when its step completes."""
+    from fasttalk_llm_microservice_amd.engine.scheduler import Scheduler
+    from fasttalk_llm_microservice_amd.engine.sequence import Sequence
+    from fasttalk_llm_microservice_amd.runtime import rt
+
+    bm = rt().BlockManager(64, 4, False)
+    sch = Scheduler(bm, 4, 8, 8, 512)          # 8-token steps: a 20-token prompt takes 3 chunks
+    seq = Sequence("p", list(range(1, 21)), SamplingParams(max_tokens=4))
+    sch.add(seq)
+    b1 = sch.schedule()                        # chunk 1, not yet completed
+    assert b1.prefill_seqs == [seq] and b1.prefill_start == [0] and b1.prefill_tokens == [8]
+    assert seq.pf_sched == 8 and seq.num_computed == 0
+    b2 = sch.schedule()                        # chunk 2 queued behind it (chained)
+    assert b2.prefill_start == [8] and b2.prefill_tokens == [8] and seq.pf_sched == 16
+    sch.post_step(b1)
+    assert seq.num_computed == 8 and seq.pf_sched == 8
+    sch.post_step(b2)
+    assert seq.num_computed == 16 and seq.pf_sched == 0
+    b3 = sch.schedule()                        # the last chunk: sampled, then running
+    assert b3.prefill_start == [16] and b3.prefill_tokens == [4] and b3.prefill_sample == [True]
+    sch.post_step(b3)
+    assert seq.num_computed == 20 and seq in sch.running and seq.pf_sched == 0
+    # a second prompt's first chunk is queued, then the prompt loses its KV while the
+    # chunk is in flight (a waiting sequence mid-prefill is the first to give its
+    # blocks up: Scheduler._preempt_one); the stale chunk must not count
+    other = Sequence("q", list(range(1, 21)), SamplingParams(max_tokens=4))
+    sch.add(other)
+    c1 = sch.schedule()
+    assert other in c1.prefill_seqs and other.pf_sched > 0 and other.block_ids
+    ep = other.epoch
+    sch._reset_to_waiting(other)
+    assert other.epoch == ep + 1 and other.pf_sched == 0 and not other.block_ids
+    sch.post_step(c1)
+    assert other.num_computed == 0 and other.pf_sched == 0 and other not in sch.running
+    assert seq.num_computed == 21                 # the decode row of that step still counts
+    c2 = sch.schedule()                           # the prompt restarts from its first token
+    i = c2.prefill_seqs.index(other)
+    assert c2.prefill_start[i] == 0 and c2.prefill_epoch[i] == ep + 1
