@@ -85,6 +85,13 @@ int ft_pkr_gemm(const void* x, int x_stride, int M, const void* wpk, int N, int 
                 void* out, int out_stride, void* residual, int res_stride, int* tickets,
                 int splits, int nt, int depth, int epi, int norm, int wn, float eps,
                 hipStream_t stream);
+int ft_decode_block_plan(int H, int Ko, int I, int* so, int* sd, int* tpw, int* grid);
+size_t ft_decode_block_ws_floats(int H, int M);
+int ft_decode_block_ctl_words();
+int ft_decode_block(const void* attn, int attn_stride, void* residual, int res_stride, void* h,
+                    int h_stride, const void* wo, const void* wgu, const void* wd, float* ws,
+                    long ws_floats, float* xg, long xg_floats, int* ctl, long long* stamps, int M,
+                    int H, int Ko, int I, float eps, hipStream_t stream);
 int ft_row_rmsnorm(const void* x, int x_stride, const float* ws, int splits, void* out,
                    int out_stride, void* residual, const void* w, int rows, int hidden, float eps,
                    hipStream_t stream);
@@ -624,6 +631,48 @@ void pkr_gemm(at::Tensor x, at::Tensor w, c10::optional<at::Tensor> out,
            "pkr_gemm");
 }
 
+// Persistent post-attention decode block (csrc/kernels/decode_block.hip):
+// residual += attn Wo^T; h = silu . rms-scaled (residual Wgu^T); residual += h Wd^T.
+void decode_block(at::Tensor attn, at::Tensor residual, at::Tensor h, at::Tensor wo, at::Tensor wgu,
+                  at::Tensor wd, at::Tensor ws, at::Tensor xg, at::Tensor ctl, double eps,
+                  c10::optional<at::Tensor> stamps) {
+  long long* sp = nullptr;
+  if (stamps.has_value()) {
+    check_dev(*stamps, "stamps");
+    TORCH_CHECK(stamps->scalar_type() == at::kLong && stamps->numel() >= 16 * 1024, "stamps int64 [>= 16K]");
+    sp = reinterpret_cast<long long*>(stamps->data_ptr<int64_t>());
+  }
+  for (auto* t : {&attn, &residual, &h, &wo, &wgu, &wd}) {
+    check_bf16(*t, "decode_block operand");
+    TORCH_CHECK(t->dim() == 2 && t->is_contiguous(), "decode_block operands must be contiguous 2-D");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "decode_block alignment");
+  }
+  check_dev(ws, "ws");
+  check_dev(xg, "xg");
+  TORCH_CHECK(ws.scalar_type() == at::kFloat && xg.scalar_type() == at::kFloat, "ws / xg float32");
+  TORCH_CHECK(ws.is_contiguous() && xg.is_contiguous(), "ws / xg contiguous");
+  check_i32(ctl, "ctl");
+  TORCH_CHECK(ctl.numel() >= ft_decode_block_ctl_words(), "ctl too small");
+  const int M = (int)attn.size(0), Ko = (int)attn.size(1), H = (int)residual.size(1);
+  const int I = (int)h.size(1);
+  TORCH_CHECK(M >= 1 && M <= 64, "decode_block: 1..64 rows");
+  TORCH_CHECK(residual.size(0) == M && h.size(0) >= M, "decode_block rows");
+  TORCH_CHECK(wo.size(0) == H && wo.size(1) == Ko, "wo shape");
+  TORCH_CHECK(wgu.size(0) == 2 * I && wgu.size(1) == H, "wgu shape");
+  TORCH_CHECK(wd.size(0) == H && wd.size(1) == I, "wd shape");
+  check_rc(ft_decode_block(attn.data_ptr(), Ko, residual.data_ptr(), H, h.data_ptr(), I,
+                           wo.data_ptr(), wgu.data_ptr(), wd.data_ptr(), ws.data_ptr<float>(),
+                           (long)ws.numel(), xg.data_ptr<float>(), (long)xg.numel(),
+                           ctl.data_ptr<int>(), sp, M, H, Ko, I, (float)eps, cur_stream()),
+           "decode_block");
+}
+
+py::object decode_block_plan(int64_t H, int64_t Ko, int64_t I) {
+  int so = 0, sd = 0, tpw = 0, grid = 0;
+  if (ft_decode_block_plan((int)H, (int)Ko, (int)I, &so, &sd, &tpw, &grid) != 0) return py::none();
+  return py::make_tuple(so, sd, tpw, grid);
+}
+
 // ---- custom one-shot all-reduce (csrc/kernels/custom_ar.hip) ----------------------
 int64_t custom_ar_alloc(int64_t bytes) {
   void* p = nullptr;
@@ -893,6 +942,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("tickets") = py::none(), py::arg("splits") = 1, py::arg("nt") = 2,
         py::arg("depth") = 3, py::arg("epi") = 0, py::arg("norm") = false, py::arg("eps") = 0.0,
         py::arg("wn") = false);
+  m.def("decode_block", &decode_block, py::arg("attn"), py::arg("residual"), py::arg("h"),
+        py::arg("wo"), py::arg("wgu"), py::arg("wd"), py::arg("ws"), py::arg("xg"), py::arg("ctl"),
+        py::arg("eps"), py::arg("stamps") = py::none());
+  m.def("decode_block_plan", &decode_block_plan);
+  m.def("decode_block_ws_floats",
+        [](int64_t H, int64_t M) { return (int64_t)ft_decode_block_ws_floats((int)H, (int)M); });
+  m.def("decode_block_ctl_words", []() { return (int64_t)ft_decode_block_ctl_words(); });
   m.def("row_rmsnorm", &row_rmsnorm, py::arg("out"), py::arg("x") = py::none(),
         py::arg("ws") = py::none(), py::arg("splits") = 1, py::arg("residual") = py::none(),
         py::arg("w"), py::arg("rows"), py::arg("eps"));

@@ -1000,9 +1000,12 @@ class AsyncEngine:
                 fatal = not self._recoverable(e) or self._fail_streak >= self.max_fail_streak
                 if fatal:  # set before the error outputs go out: no new request slips in
                     self.error = e
-                from .runner import CommFault
+                from .runner import CommFault, DecodeBlockFault, KernelCheckError
 
-                eng.fail_unfinished(str(e), reset_cache=isinstance(e, CommFault))
+                # KV written from un-reduced partials, clamped indices or a timed-out
+                # decode block must not be re-attached from the prefix cache
+                eng.fail_unfinished(str(e), reset_cache=isinstance(
+                    e, (CommFault, DecodeBlockFault, KernelCheckError)))
                 self._flush()
                 continue
             self._fail_streak = 0

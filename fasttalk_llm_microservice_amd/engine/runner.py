@@ -29,6 +29,11 @@ from .scheduler import ScheduledBatch
 log = logging.getLogger("fasttalk.engine.runner")
 
 
+class DecodeBlockFault(RuntimeError):
+    """A persistent decode-block launch gave up at a grid barrier: the step's rows
+    (and the K/V they wrote) are garbage."""
+
+
 class KernelCheckError(RuntimeError):
     """The bounds-checked kernel build (FT_KERNEL_CHECKS=1) caught an out-of-range
     index (block-table entry, KV slot, rotary position, token id) in a step."""
@@ -322,6 +327,13 @@ class ModelRunner:
             if self.is_gpu and (self.invariant or os.environ.get("FT_DECODE_FUSED_COMBINE", "1") == "1") \
             else None
         self._done_event = torch.cuda.Event() if self.is_gpu else None
+        # persistent decode block: its sticky give-up word (ctl[2]) is copied to pinned
+        # memory every BLOCK_CHECK_EVERY waits and read at the next check (never a sync)
+        self._blk_host = torch.zeros(1, dtype=torch.int32, pin_memory=True) \
+            if self.is_gpu and self.model.block else None
+        self._blk_event = torch.cuda.Event() if self._blk_host is not None else None
+        self._blk_armed = False
+        self._blk_waits = 0
         self.graphs: Dict[int, torch.cuda.CUDAGraph] = {}
         # guided decoding, pipelined: per bucket a forward graph (-> logits) and a
         # sampler graph, so the next step's forward is queued before this step's
@@ -629,6 +641,31 @@ class ModelRunner:
         self.stats["wait_ms"] = self.stats.get("wait_ms", 0.0) + 1e3 * (time.perf_counter() - t0)
         if self.d_check is not None:
             self.kernel_check()
+        if self._blk_host is not None:
+            self._block_check()
+
+    BLOCK_CHECK_EVERY = 64
+
+    def _block_check(self):
+        """Decode block give-up word: a grid barrier that timed out (a grid that was
+        not fully resident) leaves garbage rows; the step fails loudly and the model
+        falls back to the unfused layer (graphs recaptured on demand)."""
+        self._blk_waits += 1
+        if self._blk_armed and self._blk_event.query():
+            self._blk_armed = False
+            if int(self._blk_host[0]) and self.model.block_fault():
+                self._blk_host = None
+                self.graphs.clear()
+                self._graph_logits.clear()
+                self.graphs_split.clear()
+                self._fwd_logits.clear()
+                self._pending_split = None
+                raise DecodeBlockFault("decode block grid barrier timed out; step discarded, "
+                                       "unfused decode layer from now on")
+        if not self._blk_armed and self._blk_waits % self.BLOCK_CHECK_EVERY == 0:
+            self._blk_host.copy_(self.model.db_ctl[2:3], non_blocking=True)
+            self._blk_event.record()
+            self._blk_armed = True
 
     def kernel_check(self):
         """Checked build: raise KernelCheckError if a kernel has reported an out-of-range
@@ -637,6 +674,9 @@ class ModelRunner:
             return
         w = self.d_check.cpu()
         if int(w[0]):
+            # clear the sticky word as the error is raised: the serving loop fails the
+            # affected requests and carries on, and later steps must not re-raise it
+            self.d_check.zero_()
             raise KernelCheckError(w.tolist())
 
     def kernel_check_reset(self):

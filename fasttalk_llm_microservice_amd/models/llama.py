@@ -233,6 +233,25 @@ FUSED_PLAN = {
              48: (4, 2, 4, 0), 64: (4, 2, 4, 0)},
 }
 _SILU_CONFIGS = ((2, 2), (2, 3), (2, 4), (4, 2), (4, 3))
+# Persistent post-attention decode block (csrc/kernels/decode_block.hip), bf16, TP=1,
+# BLOCK_MIN_ROWS..64 rows, OPT-IN (FT_DECODE_BLOCK=1): per layer the QKV xr GEMM on the
+# raw residual (ln1 folded in), slab_rope_kv (applies the input RMS), the decode
+# attention and ONE launch for o -> add -> RMSNorm -> gate_up+SiLU -> down -> add.
+# Measured 96-98 us per layer against 86 us for the five launches it replaces at 50
+# rows (profiles/decode_block_r06.log): each in-launch hand-off costs 5-10 us once the
+# weight streams saturate HBM, kernel boundaries 1.2-1.9 us.  Never enabled where
+# several processes share the device (its grid must be resident: one workgroup per CU).
+BLOCK_ROWS = 64
+BLOCK_MIN_ROWS = int(os.environ.get("FT_DECODE_BLOCK_MIN_ROWS", str(FUSED_ROWS + 1)))
+
+
+def _decode_block_enabled() -> bool:
+    if os.environ.get("FT_DECODE_BLOCK", "0").lower() not in ("1", "true", "on"):
+        return False
+    shared = (os.environ.get("FT_BENCH_SHARED_GPU", "0") == "1"
+              or os.environ.get("ENGINE_KV_SIZING", "") == "own"
+              or os.environ.get("ENGINE_TP_SHARE_DEVICE", "0").lower() in ("1", "true"))
+    return not shared
 # (Measured negatives, removed: the QKV projection with RoPE + the paged K/V write
 # in its own epilogue -- 3.52 vs 3.25 ms per single-session decode step, the
 # in-launch split-K seam costs more than the launch it saves
@@ -382,6 +401,8 @@ class LlamaModel:
         self.gu_il = False        # gate_up image interleaved in groups of 16 (packed bf16)
         self.w4_slab: dict = {}   # W4 projections that leave split-K slabs
         self.tickets: Optional[torch.Tensor] = None
+        self.block = False        # persistent post-attention decode block (_prepare_block)
+        self.db_h = self.db_xg = self.db_ctl = None
         # TP: all-reduce + residual add + RMSNorm in one launch (FT_TP_FUSED_NORM=0: the
         # separate slab_store -> all-reduce -> add+RMSNorm launches, for A/B runs)
         self.tp_fused_norm = os.environ.get("FT_TP_FUSED_NORM", "1") != "0"
@@ -611,6 +632,7 @@ class LlamaModel:
         self.tickets = torch.zeros(max(4096, H // 16), dtype=torch.int32, device=self.device)
         torch.cuda.empty_cache()
         self._prepare_fused()
+        self._prepare_block()
 
     def _prepare_fused(self):
         """The fused decode layer (<= FUSED_ROWS rows) streams the same images: QKV /
@@ -632,6 +654,46 @@ class LlamaModel:
         if self.tickets is None:
             self.tickets = torch.zeros(max(4096, H // 16), dtype=torch.int32, device=self.device)
         self.fused = True
+
+    def _prepare_block(self):
+        """Scratch and plan of the persistent decode block: it streams the same packed
+        images (o, gate_up with ln2 folded and 16-row interleave, down)."""
+        self.block = False
+        cfg = self.cfg
+        H, I = cfg.hidden_size, cfg.intermediate_size
+        L0 = self.layers[0]
+        if (self.quant or self.tp != 1 or not _decode_block_enabled() or L0.wo_pk is None
+                or L0.wgu_pk is None or L0.wd_pk is None or L0.wqkv_pk is None):
+            return
+        plan = ops.decode_block_plan(H, self.nq * self.d, I)
+        if plan is None:
+            return
+        so, sd, tpw, grid = plan
+        need = ops.decode_block_ws_floats(H, BLOCK_ROWS)
+        nqkv = (self.nq + 2 * self.nkv) * self.d
+        need = max(need, MAX_SPLITS * BLOCK_ROWS * nqkv)
+        if self.ws is None or self.ws.numel() < need:
+            self.ws = torch.empty(need, dtype=torch.float32, device=self.device)
+        self.db_h = torch.empty(BLOCK_ROWS, I, dtype=self.dtype, device=self.device)
+        self.db_xg = torch.empty((grid // 2) * 2 * 4 * 256, dtype=torch.float32, device=self.device)
+        self.db_ctl = torch.zeros(ops.decode_block_ctl_words(), dtype=torch.int32, device=self.device)
+        self.block = True
+        log.info("decode block: down splits %d, <= %d gate/up pairs per workgroup, grid %d",
+                 sd, tpw, grid)
+
+    def block_fault(self) -> bool:
+        """True (and the block path switched off, its counters re-armed) if a decode
+        block launch gave up waiting at a grid barrier (sticky word ctl[2])."""
+        if self.db_ctl is None:
+            return False
+        if int(self.db_ctl[2].item()) == 0:
+            return False
+        log.error("decode block gave up at a grid barrier (error word %d): falling back "
+                  "to the unfused decode layer", int(self.db_ctl[2].item()))
+        torch.cuda.synchronize(self.device)
+        self.db_ctl.zero_()
+        self.block = False
+        return True
 
     def resident_weight_bytes(self) -> int:
         """Bytes of weights held on the device (every layer tensor, embedding, head)."""
@@ -890,8 +952,46 @@ class LlamaModel:
             return rows
         return ops.rmsnorm(rows, self.norm, eps)
 
+    def _forward_block(self, input_ids: torch.Tensor, meta: AttnMeta, kv_caches) -> torch.Tensor:
+        """Decode rows through the persistent post-attention block: per layer the QKV
+        GEMM on the raw residual (split-K slabs), slab_rope_kv (input RMS from the
+        residual row, RoPE, paged K/V write), the decode attention, and ONE
+        decode_block launch that leaves the next layer's residual."""
+        cfg = self.cfg
+        eps = cfg.rms_norm_eps
+        nq, nkv, d = self.nq, self.nkv, self.d
+        t = input_ids.shape[0]
+        H = cfg.hidden_size
+        nqkv = (nq + 2 * nkv) * d
+        nt, u, sp = packed_cfg("qkv", t, nqkv, H)
+        if sp == 1:
+            sp = 2   # slab_rope_kv reduces split-K slabs
+        while sp > 1 and not _cfg_fits((nt, u, sp), nqkv, H):
+            sp //= 2
+        residual = self.embed.index_select(0, input_ids)
+        mark = self.mark_at
+        for li, L in enumerate(self.layers):
+            if mark is not None and li == mark[0]:   # progress event (engine mixed chain)
+                mark[1].record()
+            kc, vc = kv_caches[li]
+            qkv = torch.empty(t, nqkv, dtype=self.dtype, device=self.device)
+            ops.skinny_gemm(residual, L.wqkv_pk, ws=self.ws, splits=sp, nt=nt, u=u)
+            ops.slab_rope_kv(self.ws, sp, t, nqkv, qkv, meta.positions, self.cos_sin,
+                             meta.slot_mapping, kc, vc, nq, nkv, d, residual=residual, eps=eps)
+            attn = self._attention(qkv, meta, kc, vc)
+            ops.decode_block(attn, residual, self.db_h, L.wo_pk, L.wgu_pk, L.wd_pk, self.ws,
+                             self.db_xg, self.db_ctl, eps)
+        idx = meta.logits_indices
+        rows = residual.index_select(0, idx) if idx.numel() != t else residual
+        if rows.shape[0] == 0:
+            return rows
+        return ops.rmsnorm(rows, self.norm, eps)
+
     def forward(self, input_ids: torch.Tensor, meta: AttnMeta, kv_caches) -> torch.Tensor:
         """Returns the final-normed hidden rows at ``meta.logits_indices``."""
+        t = input_ids.shape[0]
+        if self.block and not self.invariant and BLOCK_MIN_ROWS <= t <= BLOCK_ROWS:
+            return self._forward_block(input_ids, meta, kv_caches)
         if self.fused and input_ids.shape[0] <= FUSED_ROWS:
             return self._forward_fused(input_ids, meta, kv_caches)
         cfg = self.cfg

@@ -524,3 +524,34 @@ def pkr_gemm(x, w_pk, epi: str = "store", out=None, ws=None, residual=None, tick
     native().pkr_gemm(x, w_pk, out, ws, residual, tickets, splits, nt, depth, _PKR_EPI[epi],
                       norm, eps, wn)
     return out
+
+
+# ---------------------------------------------------------------------------------
+# persistent post-attention decode block (csrc/kernels/decode_block.hip)
+# ---------------------------------------------------------------------------------
+
+def decode_block_plan(hidden: int, attn_dim: int, inter: int):
+    """(o splits, down splits, gate_up tiles per workgroup, grid) when the block
+    kernel covers this layer shape on the current device, else None."""
+    if not native_available():
+        return None
+    return native().decode_block_plan(hidden, attn_dim, inter)
+
+
+def decode_block_ws_floats(hidden: int, rows: int) -> int:
+    """fp32 split-K slab floats the block kernel needs at ``rows`` rows."""
+    return int(native().decode_block_ws_floats(hidden, rows))
+
+
+def decode_block_ctl_words() -> int:
+    return int(native().decode_block_ctl_words())
+
+
+def decode_block(attn, residual, h, wo_pk, wgu_pk, wd_pk, ws, xg, ctl, eps: float, stamps=None):
+    """One launch per layer after the attention: residual += attn Wo^T; h = silu(g) * u
+    of rmsnorm(residual) Wgu^T (the norm weight folded into the interleaved packed
+    gate_up image, the 1/rms applied in the epilogue); residual += h Wd^T.  ``h``
+    [>= rows, I] bf16 scratch; ``ws`` / ``xg`` fp32 scratch; ``ctl`` int32 counters
+    (zeroed, left zeroed; word 2 is a sticky give-up flag)."""
+    native().decode_block(attn, residual, h, wo_pk, wgu_pk, wd_pk, ws, xg, ctl, eps, stamps)
+    return residual

@@ -364,11 +364,12 @@ def test_single_weight_image_llama3_8b():
     torch.cuda.empty_cache()
 
 
-@pytest.mark.parametrize("model,rows,quant", [
-    ("llama3-8b", 1, None), ("llama3-8b", 20, None), ("llama3-8b", 50, None), ("llama3-8b", 100, None),
-    ("llama3-70b", 1, None), ("llama3-70b", 72, None),
-    ("llama3-8b", 50, "w4"), ("llama3-8b", 64, "w4"), ("llama3-8b", 8, "w4"), ("llama3-8b", 100, "w4")])
-def test_llama3_shape_decode_matches_cpu_fp32(model, rows, quant):
+@pytest.mark.parametrize("model,rows,quant,block", [
+    ("llama3-8b", 1, None, False), ("llama3-8b", 20, None, False), ("llama3-8b", 50, None, False),
+    ("llama3-8b", 100, None, False), ("llama3-70b", 1, None, False), ("llama3-70b", 72, None, False),
+    ("llama3-8b", 50, "w4", False), ("llama3-8b", 64, "w4", False), ("llama3-8b", 8, "w4", False),
+    ("llama3-8b", 100, "w4", False), ("llama3-8b", 40, None, True), ("llama3-8b", 64, None, True)])
+def test_llama3_shape_decode_matches_cpu_fp32(model, rows, quant, block, monkeypatch):
     """a 2-layer Llama-3-8B-shaped model (H 4096, I 14336, GQA 4) -- and
     a 70B-shaped one (H 8192, I 28672, GQA 8) -- decoding `rows` sequences with ragged
     contexts up to 6k over random KV caches: the fused layer (1 / 20 rows), the
@@ -376,12 +377,15 @@ def test_llama3_shape_decode_matches_cpu_fp32(model, rows, quant):
     100 rows), eager and replayed from a hipGraph, against the fp32 CPU model on the
     same weights and cache contents.  ``quant="w4"``: the W4A16 (AWQ-format, group 128)
     decode GEMMs of the 8 / 64 row buckets -- the reference's default deployment
-    precision (VERDICT r2 #7) -- against the fp32 model on the dequantized weights."""
+    precision -- against the fp32 model on the dequantized weights.
+    ``block``: the opt-in persistent post-attention block (FT_DECODE_BLOCK=1)."""
     import dataclasses as dc
 
+    monkeypatch.setenv("FT_DECODE_BLOCK", "1" if block else "0")
     cfg = dc.replace(MODELS[model], name=f"{model}-2l", num_layers=2)
     g = LlamaModel(cfg, torch.device("cuda"), torch.bfloat16, max_model_len=8192, quantization=quant)
     g.init_random(5, consistent=True)
+    assert g.block == block
     c = LlamaModel(cfg, torch.device("cpu"), torch.float32, max_model_len=8192, quantization=quant)
     c.init_random(5, consistent=True)
     if quant:

@@ -108,6 +108,13 @@ CHILD = textwrap.dedent(r"""
         res["engine_raised"] = None
     except KernelCheckError as e:
         res["engine_raised"] = [e.code, e.value]
+    # the word is cleared as the error is raised: the next clean request succeeds
+    r._decode_fill = orig
+    eng.fail_unfinished("kernel check", reset_cache=True)   # what the serving loop does
+    eng.runner.kernel_check()
+    outs = eng.generate([[3, 1, 4, 1, 5]], SamplingParams(temperature=0.0, max_tokens=4, ignore_eos=True))
+    res["engine_after"] = [len(o) for o in outs]
+    res["engine_after_word"] = r.d_check.cpu().tolist()
     print("RESULT " + json.dumps(res), flush=True)
 """)
 
@@ -134,3 +141,4 @@ def test_checked_build_catches_out_of_range_indices():
     # engine: clean run leaves the word at zero; a corrupted step raises KernelCheckError
     assert res["engine_clean"] == [4] and res["engine_clean_word"][0] == 0, res
     assert res["engine_raised"] == [1, 10 ** 6], res
+    assert res["engine_after"] == [4] and res["engine_after_word"][0] == 0, res
