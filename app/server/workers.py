@@ -123,6 +123,9 @@ def _worker_main(index: int, world: int, host: str, port: int, tp: int, board_sp
         import torch
 
         torch.cuda.set_device(index * tp)
+        from fasttalk_llm_microservice_amd.parallel.affinity import pin_to_device
+
+        pin_to_device(index * tp)   # this worker's threads on its GPU's NUMA-local cores
     monitor = ServiceMonitor()
     server = WebSocketLLMServer(cfg, monitor=monitor)
     monitor.attach_server(server)

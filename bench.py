@@ -241,10 +241,23 @@ def main():
     import torch
     import torch.distributed as dist
 
+    placement = {"rank": rank, "device": dev_idx, "pci": None, "numa_node": None, "pinned": False}
     if not cpu:
         torch.cuda.set_device(dev_idx)
+        from fasttalk_llm_microservice_amd.parallel.affinity import pin_to_device
+
+        # this rank's threads AND its load generator on the GPU's NUMA-local cores
+        # (shared-GPU rehearsals leave the mask alone: the ranks would pile on one node)
+        if not shared:
+            placement.update(pin_to_device(dev_idx, pids=[client.pid]))
+        else:
+            from fasttalk_llm_microservice_amd.parallel.affinity import device_pci_address
+
+            placement["pci"] = device_pci_address(dev_idx)
+    backend = None
     if world > 1:
-        if shared or cpu:
+        backend = "gloo" if shared or cpu else "nccl"
+        if backend == "gloo":
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=torch.device(f"cuda:{dev_idx}"))
@@ -376,7 +389,8 @@ def main():
              "ttft": res["ttft_s"], "tool_ttft": res.get("tool_ttft_s", []),
              "server_ttft": res.get("server_ttft_ms", []),
              "engine_ttft": res.get("engine_ttft_ms", []),
-             "cached": res["cached_prompt_tokens"], "prompt": res["prompt_tokens"]}
+             "cached": res["cached_prompt_tokens"], "prompt": res["prompt_tokens"],
+             "placement": {k: placement.get(k) for k in ("rank", "device", "pci", "numa_node", "pinned")}}
     if world > 1:
         allr = [None] * world
         dist.all_gather_object(allr, local)
@@ -411,6 +425,12 @@ def main():
             "dtype": ("w4a16 (bf16 compute)" if a.quant else "bf16") if not cpu else "fp32",
             "data": f"synthetic (random-init {mlabel} weights, synthetic English prompts, "
                     "synthetic Llama-3 tokenizer)",
+            # which GPUs the ranks ran on and over what: an N-GPU record shows by itself
+            # that the collectives saw N distinct devices
+            "dist_backend": ("nccl (RCCL)" if backend == "nccl" else backend) if world > 1 else None,
+            "world_size": world,
+            "rank_devices": [r["placement"] for r in allr],
+            "distinct_gpus": len({r["placement"]["pci"] or r["placement"]["device"] for r in allr}),
             "serve": ({"mode": "front door (one port, least-loaded placement)",
                        "sessions_per_worker": [r["placed"] for r in allr]}
                       if door else {"mode": "one port per rank"}),

@@ -80,7 +80,6 @@ int ft_skinny_gemm_xr(const void* x, int x_stride, int M, const void* w, int N, 
                       hipStream_t stream);
 int ft_packed_gemm(const void* x, int x_stride, int M, const void* wpk, int N, int K, int splits,
                    int epi, int cfg, void* out, int out_stride, float* ws, hipStream_t stream);
-int ft_unpack_weight(void* out, const void* wpk, int N, int K, hipStream_t stream);
 int ft_pkr_gemm(const void* x, int x_stride, int M, const void* wpk, int N, int K, float* ws,
                 void* out, int out_stride, void* residual, int res_stride, int* tickets,
                 int splits, int nt, int depth, int epi, int norm, int wn, float eps,
@@ -572,15 +571,6 @@ void packed_gemm(at::Tensor x, at::Tensor w, c10::optional<at::Tensor> out,
            "packed_gemm");
 }
 
-void unpack_weight(at::Tensor out, at::Tensor wpk) {
-  check_bf16(out, "out");
-  check_bf16(wpk, "wpk");
-  TORCH_CHECK(wpk.dim() == 2 && wpk.is_contiguous() && out.is_contiguous(), "contiguous 2-D");
-  TORCH_CHECK(out.numel() >= wpk.numel(), "out too small");
-  check_rc(ft_unpack_weight(out.data_ptr(), wpk.data_ptr(), (int)wpk.size(0), (int)wpk.size(1),
-                            cur_stream()),
-           "unpack_weight");
-}
 
 // Ring-pipelined packed decode GEMM with fused epilogues (csrc/kernels/skinny_pkr.hip).
 // epi: 0 store (out or slabs), 1 silu (gate/up interleaved, out [M, N/2]), 2 resid.
@@ -964,7 +954,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("custom_ar_allreduce", &custom_ar_allreduce);
   m.def("custom_ar_add_rmsnorm", &custom_ar_add_rmsnorm);
   m.def("packed_gemm", &packed_gemm);
-  m.def("unpack_weight", &unpack_weight);
   m.def("custom_ar_allgather", &custom_ar_allgather);
   m.def("custom_ar_export_error", &custom_ar_export_error);
   m.def("slab_silu", &slab_silu);

@@ -453,31 +453,6 @@ __global__ __launch_bounds__(512, 1) void packed_gemm8_kernel(
   }
 }
 
-// ---------------------------------------------------------------------------
-// Packed image -> row-major W[N][K] (a transient copy for hipBLASLt at prefill
-// sizes, where the library's tiles are faster than packed_gemm; the resident
-// weights stay single-image).  One thread moves the two 16-B halves of one
-// (column, 16-k group) of a fragment block: a contiguous 32-B row segment.
-__global__ __launch_bounds__(256) void unpack_weight_kernel(uint16_t* __restrict__ out,
-                                                            const uint16_t* __restrict__ wpk,
-                                                            int N, int K) {
-  const long nunits = (long)(N / 16) * (K / 64) * 64;   // (tile, k-step, lane)
-  for (long u = (long)blockIdx.x * blockDim.x + threadIdx.x; u < nunits;
-       u += (long)gridDim.x * blockDim.x) {
-    const long blk = u >> 6;                  // t * (K/64) + s
-    const int lane = (int)(u & 63);
-    const int ks = K >> 6;
-    const long t = blk / ks;
-    const int st = (int)(blk - t * ks);
-    const uint16_t* src = wpk + blk * 1024 + lane * 8;
-    const uint4 lo = *reinterpret_cast<const uint4*>(src);
-    const uint4 hi = *reinterpret_cast<const uint4*>(src + 512);
-    const int r = lane & 15, g = lane >> 4;
-    uint4* dst = reinterpret_cast<uint4*>(out + (size_t)(t * 16 + r) * K + st * 64 + g * 16);
-    dst[0] = lo;
-    dst[1] = hi;
-  }
-}
 
 // ---------------------------------------------------------------------------
 // "pg32": the tile of packed_gemm_kernel with 32-deep stages in an S-slot LDS ring
@@ -796,11 +771,3 @@ extern "C" int ft_packed_gemm(const void* x, int x_stride, int M, const void* wp
   return -5;
 }
 
-extern "C" int ft_unpack_weight(void* out, const void* wpk, int N, int K, hipStream_t stream) {
-  if (N % 16 != 0 || K % 64 != 0) return -1;
-  const long units = (long)(N / 16) * (K / 64) * 64;
-  const int grid = (int)std::min<long>((units + 255) / 256, 256 * 32);
-  hipLaunchKernelGGL(ft::unpack_weight_kernel, dim3(grid), dim3(256), 0, stream, (uint16_t*)out,
-                     (const uint16_t*)wpk, N, K);
-  return static_cast<int>(hipGetLastError());
-}

@@ -22,8 +22,9 @@
 //     gridDim.y (1 split included) writes fp32 slabs reduced by the row
 //     epilogues (fused_epilogue.hip), exactly as the bf16 packed path; without
 //     one (1 split) it stores bf16.
-// Prefill (M > 64) dequantizes one projection into a bf16 scratch with
-// w4_dequant_kernel and runs the library GEMM.
+// Above 64 rows the model runs packed_gemm.hip on a resident dequantized prefill
+// image (models/llama.py _prepare_w4_prefill), or on one projection dequantized by
+// w4_dequant_kernel into a packed scratch when that image is off.
 #include "ft_common.h"
 #include "ft_lds.h"
 

@@ -1,8 +1,8 @@
 """Llama-3 decoder for the in-process engine (replaces the vLLM container the
 reference talks to over HTTP: ``app/core/vllm_handler.py:53-62``).
 
-Per layer:  fused add+RMSNorm (K2, HIP) -> QKV GEMM (K3,
-hipBLASLt) -> RoPE + paged KV write (K4, HIP) -> prefill flash attention (K5,
+Per layer:  fused add+RMSNorm (K2, HIP) -> QKV GEMM (K3, HIP
+packed MFMA) -> RoPE + paged KV write (K4, HIP) -> prefill flash attention (K5,
 HIP/MFMA) or paged MFMA decode attention (K6, HIP) -> O GEMM (K7) [+ RCCL
 all-reduce under TP] -> fused add+RMSNorm -> gate_up GEMM (K8) -> SiLU-mul
 (K9, HIP) -> down GEMM (K10) [+ all-reduce].  Only the last-token rows reach the
@@ -78,7 +78,6 @@ class LayerWeights:
     wo_pk: Optional[torch.Tensor] = None
     wgu_pk: Optional[torch.Tensor] = None
     wd_pk: Optional[torch.Tensor] = None
-    # resident row-major copies of some packed projections for hipBLASLt at mixed /
     # fused decode layer (skinny_pkr.hip): QKV / gate_up packed with the input norms
     # folded in (W diag(ln)), gate_up rows interleaved for the SiLU epilogue; o / down
     # share the packed images above when present
@@ -94,12 +93,12 @@ _ATTR = {"qkv": "wqkv", "o": "wo", "gu": "wgu", "down": "wd"}
 
 
 # Decode GEMMs (<= 64 rows) on pre-packed weights (csrc/kernels/skinny_gemm.hip,
-# "pk"/"xcp").  Per projection and row bucket: (nt, u, splits), or None for
-# hipBLASLt.  Chosen from cold-cache sweeps on MI355X (bench/gemm_sweep.py,
-# us at M = 1 / 8 / 16 / 32 / 64 vs hipBLASLt):
-#   qkv     9.8 / 10.3 / 11.1  vs 14-15   (M >= 32: hipBLASLt; its epilogue is RoPE)
+# "pk"/"xcp").  Per projection and row bucket: (nt, u, splits).  Chosen from
+# cold-cache sweeps on MI355X (bench/gemm_sweep.py, us at M = 1 / 8 / 16 / 32 / 64;
+# hipBLASLt on row-major weights, measured for reference in round 2, after "vs"):
+#   qkv     9.8 / 10.3 / 11.1  vs 14-15
 #   o       7.3 / 7.5 / 7.7 / 9.0 / 13.1 vs 14-15   split 2 -> slabs -> add+RMSNorm
-#   gate_up 35 / 38 / 41 / 45            vs 55-66   (M = 64: hipBLASLt)
+#   gate_up 35 / 38 / 41 / 45            vs 55-66
 #   down    18.6 / 19.3 / 20 / 22 / 28   vs 26-40   split 2-4 -> slabs -> add+RMSNorm
 #   lm_head 148 / 161 / 174 / 184 / 197  vs 188-212
 # Split-K partial sums stay fp32 in one workspace and are reduced inside the

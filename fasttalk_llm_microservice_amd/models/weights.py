@@ -1,7 +1,9 @@
 """Weights: deterministic random init and (TP-sharded) safetensors loading.
 
-Layout held by :class:`LlamaModel` (all ``[out_features, in_features]`` for
-``F.linear``, i.e. the hipBLASLt "NT" GEMM):
+Layout produced here and handed to :class:`LlamaModel` (all
+``[out_features, in_features]``; on the GPU the model re-lays every projection out
+into the MFMA-fragment image the hand-written GEMMs stream, ``ops.pack_weight``, and
+drops these row-major tensors; the CPU backend keeps them for ``F.linear``):
 
 * ``wqkv``  [ (nq + 2 nkv)/tp * D, H ]   column parallel, q|k|v fused
 * ``wo``    [ H, nq/tp * D ]             row parallel (all-reduce after)

@@ -434,19 +434,6 @@ def packed_gemm(x, w, out=None, ws=None, splits: int = 1, epi: str = "store", cf
     return ws if code == 1 else out
 
 
-def unpack_weight(wp: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Inverse of pack_weight(): a row-major [N, K] copy (transient, for library
-    GEMMs at prefill sizes)."""
-    n, k = wp.shape
-    if not wp.is_cuda:
-        return wp.reshape(n // 16, k // 64, 2, 4, 16, 8).permute(0, 4, 1, 3, 2, 5).reshape(n, k)
-    if out is None:
-        out = torch.empty(n, k, dtype=wp.dtype, device=wp.device)
-    out = out.view(-1)[: n * k].view(n, k)
-    native().unpack_weight(out, wp)
-    return out
-
-
 def embed_rmsnorm(ids: torch.Tensor, table: torch.Tensor, w: torch.Tensor, eps: float):
     """(rmsnorm(table[ids]) * w, table[ids]): the embedding gather fused with the
     first layer's input norm; the second tensor starts the residual stream."""

@@ -82,6 +82,9 @@ def _replica_main(index: int, cfg, conn, device_base: int = 0):
             import torch
 
             torch.cuda.set_device(base)
+            from .affinity import pin_to_device
+
+            pin_to_device(base)
         if cfg.tp_size > 1:
             from .tp import spawn_tp_engine
 

@@ -131,6 +131,10 @@ def _spawned_worker(rank: int, world: int, port: int, bcast_name: str, cfg, devi
     _exit_with_parent(f"TP worker {rank}")
     dev_index = tp_device_index(device_base, rank, cfg.tp_share_device)
     _set_device(device, dev_index)
+    if device == "cuda" and not cfg.tp_share_device:
+        from .affinity import pin_to_device
+
+        pin_to_device(dev_index)   # each TP rank on its own GPU's NUMA-local cores
     kw = {}
     if device == "cuda" and not cfg.tp_share_device:
         kw["device_id"] = torch.device(f"cuda:{dev_index}")

@@ -781,9 +781,3 @@ def test_packed_gemm_silu_epilogue_and_interleaved_silu(cfg):
     _close(h, ref, atol=3e-2, rtol=2e-2, msg="slab_silu il")
 
 
-def test_unpack_weight_roundtrip():
-    """unpack_weight(pack_weight(w)) == w bit for bit (the transient row-major copy
-    the prefill-size GEMMs hand to hipBLASLt)."""
-    for n, k in [(768, 512), (6144, 4096), (48, 192)]:
-        w = torch.randn(n, k, device="cuda").bfloat16()
-        assert torch.equal(ops.unpack_weight(ops.pack_weight(w)), w)

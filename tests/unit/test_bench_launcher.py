@@ -56,3 +56,22 @@ def test_missing_gpus_fail_loudly():
              env_extra={"HIP_VISIBLE_DEVICES": "", "CUDA_VISIBLE_DEVICES": ""}, timeout=180)
     assert r.returncode != 0
     assert not _json_lines(r.stdout)
+
+
+def test_eight_ranks_through_the_front_door():
+    """the 8-rank data-parallel path of ``bench.py --gpus 8`` end to
+    end on the CPU (gloo): 8 ranks, the shipping front door spreading the 24 sessions
+    evenly (spread <= 1), and the record names its backend, world size and every
+    rank's device placement."""
+    r = _run(["--gpus", "8", "--device", "cpu", "--model", "tiny", "--serve", "door",
+              "--sessions", "3", "--steps", "1", "--warmup", "1", "--gen", "4", "--words", "6"],
+             timeout=900)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1, r.stdout
+    out = lines[0]
+    assert out["ranks"] == 8 and out["world_size"] == 8 and out["dist_backend"] == "gloo"
+    assert out["config"]["parallelism"] == "dp8" and out["config"]["global_batch"] == 24
+    spw = out["serve"]["sessions_per_worker"]
+    assert len(spw) == 8 and sum(spw) == 24 and max(spw) - min(spw) <= 1, spw
+    assert sorted(d["rank"] for d in out["rank_devices"]) == list(range(8))

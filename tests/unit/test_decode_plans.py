@@ -24,7 +24,7 @@ def test_buckets_round_up():
     assert llama.fused_bucket(9) == 16
     assert llama.fused_bucket(33) == 48
     assert llama.fused_bucket(50) == 64
-    assert llama.packed_cfg("o", 65) is None  # above PACKED_ROWS: the library GEMM
+    assert llama.packed_cfg("o", 65) is None  # above PACKED_ROWS: packed_gemm.hip
 
 
 def test_packed_overlay_sets_and_removes(plans):
