@@ -167,7 +167,9 @@ class FrontDoor:
             if i in exclude or i not in self._ctl:
                 continue
             w = ws[i]
-            if not (w["alive"] and w["ready"]):
+            # a worker whose event loop stopped beating (alive but stalled) gets no new
+            # sessions: it would not read its control socket either
+            if not (w["alive"] and w["ready"] and w["heartbeat_fresh"]):
                 continue
             ld = self.load(i)
             if best is None or ld < best_load:
@@ -185,7 +187,15 @@ class FrontDoor:
                     break
                 ctl = self._ctl[i]
                 try:
-                    socket.send_fds(ctl, [b"c"], [conn.fileno()])
+                    # never block the accept thread (and, under the lock, every other
+                    # placement) on one worker whose socket buffer is full: MSG_DONTWAIT,
+                    # and a full buffer (EAGAIN) reroutes like an unreachable worker
+                    socket.send_fds(ctl, [b"c"], [conn.fileno()], socket.MSG_DONTWAIT)
+                except BlockingIOError:
+                    log.warning("front door: worker %d not reading its hand-offs; rerouting", i)
+                    tried.add(i)
+                    self.stats["rerouted"] += 1
+                    continue
                 except OSError as e:
                     log.warning("front door: worker %d unreachable (%s); rerouting", i, e)
                     self._ctl.pop(i, None)

@@ -116,6 +116,7 @@ class Scheduler:
         self.by_id: Dict[str, Sequence] = {}
         self._admit_counter = 0
         self.num_preemptions = 0
+        self.stale_chunks = 0   # chained prefill chunks whose sequence was reset in flight
         self.swapped: Deque[Sequence] = collections.deque()
         # background (prefix-cache warm-up) prompts: prefilled only into the room a
         # step has left after every waiting prompt, within the soft budget
@@ -468,6 +469,7 @@ class Scheduler:
         for seq, n, smp, ep in items:
             if ep is not None:
                 if ep != seq.epoch:   # its KV was dropped after this chunk was queued
+                    self.stale_chunks += 1
                     continue
                 seq.pf_sched = max(0, seq.pf_sched - n)
             if seq.status == SeqStatus.FINISHED:

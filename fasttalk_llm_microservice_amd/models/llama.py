@@ -533,14 +533,31 @@ class LlamaModel:
                 self._install_w4(L, proj, *sh[attr])
             self.layers.append(L)
 
-    def _w4_packed(self, w: "Q.W4Weight") -> torch.Tensor:
+    def _w4_prefill_dense(self, proj: str, dense: torch.Tensor) -> Optional[torch.Tensor]:
+        """The dequantized weight as packed_gemm.hip wants it: gate_up in the 16-row
+        interleave its SiLU epilogue pairs (the int4 image has it only when its row
+        count allowed: _install_w4), None when the shape cannot be packed."""
+        n, k = dense.shape
+        if proj == "gu" and not self.w4_gu_il:
+            if (n // 2) % 16:
+                return None
+            dense = ops.interleave_gate_up(dense, 1)
+        if n % 16 or k % 64:
+            return None
+        return dense
+
+    def _w4_packed(self, w: "Q.W4Weight", proj: str) -> Optional[torch.Tensor]:
         """A W4 projection dequantized and re-laid out into the packed image, in two
-        shared scratches (prefill-size steps when the resident prefill image is off)."""
+        shared scratches (prefill-size steps when the resident prefill image is off);
+        None when the shape cannot be packed (the caller runs the dense fallback)."""
         need = w.n * w.k
+        if w.n % 16 or w.k % 64 or (proj == "gu" and not self.w4_gu_il and (w.n // 2) % 16):
+            return None
         if self._w4_scratch is None or self._w4_scratch.shape[1] < need:
             big = max(q.n * q.k for L in self.layers for q in (L.q4 or {}).values())
             self._w4_scratch = torch.empty(2, max(need, big), dtype=self.dtype, device=self.device)
         dense = Q.w4_dequant(w, out=self._w4_scratch[0, :need].view(w.n, w.k))
+        dense = self._w4_prefill_dense(proj, dense)
         out = self._w4_scratch[1, :need]
         n, k = w.n, w.k
         out.view(n // 16, k // 64, 2, 4, 16, 8).copy_(
@@ -568,7 +585,9 @@ class LlamaModel:
             if nbytes > 0.15 * total:
                 return
         for L, p, q in qs:
-            setattr(L, _ATTR[p] + "_pk", ops.pack_weight(Q.w4_dequant(q)))
+            dense = self._w4_prefill_dense(p, Q.w4_dequant(q))
+            if dense is not None:   # else packed per step (_w4_packed) or the dense fallback
+                setattr(L, _ATTR[p] + "_pk", ops.pack_weight(dense))
         log.info("W4A16 prefill image (dequantized, packed bf16): %.1f GB", nbytes / 1e9)
 
     def _prepare_packed(self):
@@ -601,8 +620,9 @@ class LlamaModel:
                 L.ln1 = L.ln2 = one
         self._prepare_w4_prefill()
         # gate_up split-K slabs come from a 16-row-interleaved image: the packed bf16 one,
-        # or (W4) the int4 image dequantized into a scratch above 64 rows
-        self.gu_il = self.layers[0].wgu_pk is not None or self.w4_gu_il
+        # or (W4) the dequantized image, interleaved when the int4 image is not
+        # (_w4_prefill_dense)
+        self.gu_il = True
         if self.lm_head is not None:
             self.lm_head_pk = ops.pack_weight(self.lm_head)
             self.lm_head = None
@@ -830,7 +850,12 @@ class LlamaModel:
                 # the dequantized prefill image (_prepare_w4_prefill), or this
                 # projection dequantized and packed into a scratch when it is off
                 wp = getattr(L, _ATTR[proj] + "_pk")
-                return self._packed(x, wp if wp is not None else self._w4_packed(q), proj)
+                if wp is None:
+                    wp = self._w4_packed(q, proj)
+                if wp is not None:
+                    return self._packed(x, wp, proj)
+                # a shard shape packed_gemm cannot tile: the dequantized weight, dense
+                y = F.linear(x, Q.w4_dequant(q))
             return 0, (ops.silu_mul(y, interleaved=il) if proj == "gu" else y)
         attr = _ATTR[proj]
         wp = getattr(L, attr + "_pk")

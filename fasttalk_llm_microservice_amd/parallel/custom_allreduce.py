@@ -63,14 +63,16 @@ class CustomAllReduce:
         self.max_blocks = int(max_blocks)
         self._C.custom_ar_set_max_blocks(self.max_blocks)
         self.max_bytes = int(max_bytes)
-        # spin budgets: ~0.19 us per spin on a GPU of its own.  Ranks on separate GPUs
-        # declare a missing peer dead after 2^23 spins (~1.6 s) and give the group's
-        # first steps (lazy library / code-object loads, allocator growth on one rank
-        # while the others already wait) 2^26 (~13 s).  Ranks time-sharing ONE device
-        # (tests / rehearsals: 0.36 us per spin at 8 ranks, and a peer may not be
-        # scheduled for seconds) get 2^25 / 2^28.
+        # spin budgets: ~0.19 us per spin on a GPU of its own.  A timeout raises
+        # CommFault and drops the group to RCCL for the rest of the process, so the budget
+        # must cover real host / scheduling stalls of a peer, and no multi-GPU run has
+        # measured those yet (no 8-GPU node in this environment): every group keeps the
+        # conservative 2^25 spins (~6-12 s) and 2^28 for its first steps (lazy library /
+        # code-object loads, allocator growth on one rank while the others already wait).
+        # ENGINE_CUSTOM_AR_SPIN / _SPIN_FIRST tune them once a multi-GPU run has
+        # measured the stalls.
         self.shared_device = bool(shared_device)
-        default_spin, default_first = (1 << 25, 1 << 28) if shared_device else (1 << 23, 1 << 26)
+        default_spin, default_first = 1 << 25, 1 << 28
         if spin_budget is None:
             spin_budget = int(os.environ.get("ENGINE_CUSTOM_AR_SPIN", str(default_spin)))
         self.spin_budget = int(spin_budget)

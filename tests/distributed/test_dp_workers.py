@@ -265,6 +265,7 @@ def test_front_door_balances_refuses_and_reroutes(tmp_path):
         assert e.value.code == 503 and json.loads(e.value.read())["status"] == "unavailable"
         for i in range(3):
             board.set(i, "ready", 1)
+            board.beat(i, True)
         board.set(0, "conns", 5)          # worker 0 already busy
         clients = [_s.create_connection(("127.0.0.1", port)) for _ in range(6)]
         got = [[] for _ in range(3)]
@@ -293,7 +294,19 @@ def test_front_door_balances_refuses_and_reroutes(tmp_path):
         msg, fds, _, _ = _s.recv_fds(ctl[2], 16, 4)
         assert len(fds) == 1 and door.stats["rerouted"] >= 1
         os.close(fds[0])
-        for c in clients + [extra]:
+        # a worker alive and ready but whose heartbeat went stale (event loop stalled)
+        # gets no new sessions: worker 0 is idle now, yet the next one goes to worker 2
+        board.set(0, "conns", 0)
+        board.set(0, "heartbeat", time.time() - 60)
+        late = _s.create_connection(("127.0.0.1", port))
+        time.sleep(0.5)
+        msg, fds, _, _ = _s.recv_fds(ctl[2], 16, 4)
+        assert len(fds) == 1
+        os.close(fds[0])
+        ctl[0].settimeout(0.2)
+        with pytest.raises((TimeoutError, _s.timeout, BlockingIOError)):
+            _s.recv_fds(ctl[0], 16, 4)
+        for c in clients + [extra, late]:
             c.close()
     finally:
         door.stop()

@@ -111,7 +111,7 @@ class ModelRunner:
 
 def _run(async_output: bool, depth: int, n_req: int = 9, shrink: bool = True, late: int = 0,
          mixed_ahead: bool = False, chain: bool = False, prefill_chunk: int = 512,
-         max_batched: int = 8192):
+         max_batched: int = 8192, num_blocks: int = 256):
     """``late`` requests arrive one every third engine step after the first ``n_req``."""
     import os
 
@@ -121,7 +121,7 @@ def _run(async_output: bool, depth: int, n_req: int = 9, shrink: bool = True, la
     cfg = EngineConfig(model="tiny", device="cpu", block_size=4, async_output=async_output,
                        pipeline_depth=depth, max_num_seqs=32, prefill_chunk=prefill_chunk,
                        max_num_batched_tokens=max_batched)
-    runner = ModelRunner()
+    runner = ModelRunner(num_blocks=num_blocks)
     eng = LLMEngine(cfg, runner=runner)
     res = {}
 
@@ -213,6 +213,22 @@ def test_mixed_chain_matches_synchronous(depth, budget):
         assert eng.stats["mixed_chain"] > 0
         # rows that joined after the last queued step was built take their host id
         assert any(rm and min(rm) < 0 for _, _, rm in runner.mixed)
+
+
+@pytest.mark.parametrize("depth", [1, 2])
+def test_mixed_chain_under_kv_pressure(depth):
+    """chained prefill chunks whose sequence is reset while they are in
+    flight (recompute preemption under a tiny KV pool: ``_reset_to_waiting`` drops the
+    blocks and bumps the epoch).  The queued chunk is ignored by its post_step, the
+    prompt re-prefills from the start, tokens still equal the synchronous engine's,
+    every block comes back and nothing stays counted as scheduled or in flight."""
+    ref, eng0, _ = _run(False, 1, n_req=6, late=12, max_batched=20, num_blocks=40)
+    got, eng, runner = _run(True, depth, n_req=6, late=12, mixed_ahead=True, chain=True,
+                            max_batched=20, num_blocks=40)
+    assert got == ref
+    assert eng.scheduler.num_preemptions > 0      # the pool really ran out mid-chain
+    assert eng.scheduler.stale_chunks > 0         # ... and dropped chunks still in flight
+    assert eng.stats["mixed_chain"] > 0
 
 
 def test_mixed_ahead_with_background_warmups():
