@@ -481,7 +481,8 @@ def main():
             out["guided_output_tokens"] = metrics.get("guided_output_tokens", {})
             out["engine_guided"] = {k: v for k, v in metrics.items()
                                     if k in ("jump_forward_tokens", "grammar_complete_stops",
-                                             "guided_pipelined_steps", "pipelined_jump_drops")}
+                                             "guided_pipelined_steps", "pipelined_jump_drops",
+                                             "guided_capped_steps")}
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

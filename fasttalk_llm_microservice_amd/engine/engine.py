@@ -76,7 +76,8 @@ class LLMEngine:
                                    cfg.max_num_batched_tokens, self.max_model_len,
                                    host_blocks=getattr(runner, "num_host_blocks", 0),
                                    prefill_chunk=cfg.prefill_chunk,
-                                   chunk_counts_decode=cfg.prefill_chunk_rows)
+                                   chunk_counts_decode=cfg.prefill_chunk_rows,
+                                   guided_prefill_cap=cfg.guided_prefill_cap)
         self.stop_ids = set(self.tokenizer.stop_ids) | set(self.model_cfg.eos_token_ids)
         self._trie = None
         # jump-forward over grammar-forced runs (ENGINE_JUMP_FORWARD=0 disables)
@@ -845,6 +846,7 @@ class LLMEngine:
             "kv_usage": self.kv_usage(),
             "prefix_cache_hit_rate": (self.bm.hits / self.bm.queries) if self.bm.queries else 0.0,
             "preemptions": self.scheduler.num_preemptions,
+            "guided_capped_steps": self.scheduler.guided_capped,
             "swapped": len(self.scheduler.swapped),
             "swap_outs": self.scheduler.num_swap_out,
             "swap_ins": self.scheduler.num_swap_in,

@@ -90,7 +90,8 @@ class HostSwapPool:
 class Scheduler:
     def __init__(self, block_manager, block_size: int, max_num_seqs: int,
                  max_num_batched_tokens: int, max_model_len: int, host_blocks: int = 0,
-                 prefill_chunk: int = 0, chunk_counts_decode: bool = False):
+                 prefill_chunk: int = 0, chunk_counts_decode: bool = False,
+                 guided_prefill_cap: int = 0):
         self.bm = block_manager
         self.bs = block_size
         self.max_num_seqs = max_num_seqs
@@ -110,6 +111,13 @@ class Scheduler:
         # 1024; 384 / 256 cost 2.5-3.5% tok/s (profiles/ab_prefill_chunk_512_r02.log).
         self.prefill_chunk = int(prefill_chunk)
         self.chunk_counts_decode = bool(chunk_counts_decode)
+        # Prefill tokens a step may carry while it decodes a guided (tool-call) row
+        # (0 = no cap): the free argument string of a call (~14 tokens) is decoded one
+        # token per step, and a step carrying a full prefill chunk takes ~2x a decode
+        # step, so a tool turn's time to its re-prompt grows with every chunk it rides
+        # along (tool-turn p99 406 ms).
+        self.guided_prefill_cap = int(guided_prefill_cap)
+        self.guided_capped = 0
         self.max_model_len = max_model_len
         self.waiting: Deque[Sequence] = collections.deque()
         self.running: List[Sequence] = []
@@ -208,6 +216,10 @@ class Scheduler:
             decode = [s for s in decode if s.n_tokens - s.num_computed <= 1]
         jtok = [s.n_tokens - s.num_computed for s in jumps]
         budget = self.max_tokens - len(decode) - sum(jtok)
+        if self.guided_prefill_cap > 0 and any(
+                s.grammar is not None and not s.lazy for s in decode):
+            budget = min(budget, self.guided_prefill_cap)
+            self.guided_capped += 1
         n_rows = len(decode) + len(jumps)
         if self.swapped:  # swapped sequences go first; only unfinished chunks continue
             pseqs, ptok, psamp, rejected = [], [], [], []

@@ -691,3 +691,50 @@ def test_chained_prefill_chunks_and_epoch_guard():
     c2 = sch.schedule()                           # the prompt restarts from its first token
     i = c2.prefill_seqs.index(other)
     assert c2.prefill_start[i] == 0 and c2.prefill_epoch[i] == ep + 1
+
+
+def test_guided_rows_cap_the_steps_prefill():
+    """ENGINE_GUIDED_PREFILL_CAP: while a guided (tool-call / JSON)
+    row decodes, a step carries at most the cap of prefill tokens, so the call's free
+    argument string is not decoded in steps stretched by full prefill chunks; steps
+    without guided rows keep the normal budget, and every output is unchanged."""
+    schema = {"type": "object", "properties": {"city": {"type": "string", "maxLength": 12},
+                                               "n": {"type": "integer"}}}
+    rng = np.random.default_rng(5)
+    prompts = [rng.integers(0, 120000, 40).tolist() for _ in range(6)]
+    outs = {}
+    for cap in (0, 8):
+        eng = LLMEngine(EngineConfig(model="tiny", device="cpu", num_kv_blocks=512, max_model_len=1024,
+                                     max_num_seqs=8, max_num_batched_tokens=64, prefill_chunk=0,
+                                     guided_prefill_cap=cap))
+        steps = []
+        orig = eng.scheduler.schedule
+
+        def rec(orig=orig, steps=steps, eng=eng):
+            b = orig()
+            if b is not None:
+                guided = any(s.grammar is not None and not s.lazy for s in b.decode_seqs)
+                steps.append((guided, sum(b.prefill_tokens)))
+            return b
+
+        eng.scheduler.schedule = rec
+        sp_json = SamplingParams(temperature=0.8, max_tokens=40, seed=3,
+                                 guided=GuidedSpec.json_schema(schema))
+        sp = SamplingParams(temperature=0, max_tokens=4, ignore_eos=True)
+        eng.add_request("g", [1, 2, 3], sp_json)
+        res = {}
+        for _ in range(2):
+            eng.step()
+        for i, p in enumerate(prompts):
+            eng.add_request(f"p{i}", p, sp, on_output=lambda o, i=i: res.setdefault(i, []).extend(o.token_ids))
+        while eng.has_work():
+            eng.step()
+        outs[cap] = [res[i] for i in range(len(prompts))]
+        g_steps = [n for g, n in steps if g]
+        assert g_steps, steps
+        if cap:
+            assert max(g_steps) <= cap and eng.scheduler.guided_capped > 0, steps
+            assert max(n for g, n in steps if not g) > cap   # the cap applies to guided steps only
+        else:
+            assert max(g_steps) > 8
+    assert outs[0] == outs[8]
