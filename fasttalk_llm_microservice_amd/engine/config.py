@@ -44,7 +44,8 @@ class EngineConfig:
     max_num_batched_tokens: int = 8192
     prefill_chunk: int = 512          # soft per-step prefill budget beyond the first prompt (0 = off)
     prefill_chunk_rows: bool = True    # the soft budget also counts the step's decode rows
-    guided_prefill_cap: int = 0        # prefill tokens of a step that decodes guided rows (0 = off)
+    guided_prefill_cap: int = 96       # prefill tokens of a step that decodes guided rows (0 = off;
+                                       # 96: +0.9 % tok/s on config 5, profiles/ab_guided_cap_r06.txt)
     max_model_len: int = 8192
     gpu_memory_utilization: float = 0.90
     num_kv_blocks: Optional[int] = None
@@ -104,7 +105,7 @@ class EngineConfig:
             max_model_len=_env(["ENGINE_MAX_MODEL_LEN", "VLLM_MAX_MODEL_LEN"], 8192, int),
             prefill_chunk=_env(["ENGINE_PREFILL_CHUNK"], 512, int),
             prefill_chunk_rows=_env(["ENGINE_PREFILL_CHUNK_ROWS"], "1", str).lower() in ("1", "true"),
-            guided_prefill_cap=_env(["ENGINE_GUIDED_PREFILL_CAP"], 0, int),
+            guided_prefill_cap=_env(["ENGINE_GUIDED_PREFILL_CAP"], 96, int),
             gpu_memory_utilization=_env(["ENGINE_GPU_MEMORY_UTILIZATION",
                                          "VLLM_GPU_MEMORY_UTILIZATION"], 0.90, float),
             num_kv_blocks=_env(["ENGINE_NUM_KV_BLOCKS"], None, int),
