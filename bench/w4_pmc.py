@@ -14,9 +14,12 @@ SHAPES = {"qkv": (6144, 4096), "o": (4096, 4096), "gu": (28672, 4096), "down": (
 ap = argparse.ArgumentParser()
 ap.add_argument("--proj", default="gu")
 ap.add_argument("--m", type=int, default=50)
+ap.add_argument("--cfg", default="", help="nt,splits,xr override of the plan entry")
 a = ap.parse_args()
 n, k = SHAPES[a.proj]
 nt, sp, xr = w4_cfg(a.proj, a.m)
+if a.cfg:
+    nt, sp, xr = (int(v) for v in a.cfg.split(","))
 silu = a.proj == "gu"
 ws = torch.empty(16 * 64 * 28672, device="cuda")
 Ws = []
@@ -27,8 +30,8 @@ x = torch.randn(a.m, k, device="cuda").bfloat16()
 out = torch.empty(a.m, n, device="cuda").bfloat16()   # silu writes n / 2 of it
 for i in range(64):
     if sp > 1:
-        Q.w4_gemm(x, Ws[i % 4], ws=ws, splits=sp, nt=nt, xr=bool(xr))
+        Q.w4_gemm(x, Ws[i % 4], ws=ws, splits=sp, nt=nt, xr=xr)
     else:
-        Q.w4_gemm(x, Ws[i % 4], out=out, nt=nt, xr=bool(xr), silu=silu and bool(xr))
+        Q.w4_gemm(x, Ws[i % 4], out=out, nt=nt, xr=xr, silu=silu and bool(xr))
 torch.cuda.synchronize()
 print("done", a.proj, (nt, sp, xr))

@@ -45,11 +45,11 @@ int ft_w4_gemm(const void* x, int x_stride, int M, const uint32_t* wq, const voi
                float* ws, void* out, int out_stride, int splits, int nt, hipStream_t stream);
 int ft_w4_dequant(const uint32_t* wq, const void* sz, void* out, int N, int K, hipStream_t stream);
 int ft_w4_gemm_xr(const void* x, int x_stride, int M, const uint32_t* wq, const void* sz, int N, int K,
-                  float* ws, void* out, int out_stride, int splits, int nt, int silu, int xsm,
+                  float* ws, void* out, int out_stride, int splits, int nt, int silu,
                   hipStream_t stream);
-int ft_w4_gemm_xr8(const void* x, int x_stride, int M, const uint32_t* wq, const void* sz, int N,
-                   int K, float* ws, void* out, int out_stride, int splits, int nt, int silu,
-                   hipStream_t stream);
+int ft_w4_gemm_mh(const void* x, int x_stride, int M, const uint32_t* wq, const void* sz, int N, int K,
+                  float* ws, void* out, int out_stride, int splits, int ring, int silu,
+                  hipStream_t stream);
 int ft_kv_swap(const uint64_t* ptrs_dev, int ncache, const int* ids_dev, int n, void* staging,
                long block_elems, int to_staging, int num_blocks, hipStream_t stream);
 int ft_skinny_gemm_xc(const void* x, int x_stride, int M, const void* w, int N, int K, float* ws,
@@ -423,20 +423,19 @@ void w4_gemm(at::Tensor x, at::Tensor wq, at::Tensor sz, int64_t N, c10::optiona
     ostride = (int)out->stride(0);
   }
   TORCH_CHECK(!silu || (xr && !ws.has_value()), "the SiLU epilogue is an xr bf16-output variant");
-  if (xr == 2) {   // 8-wave x-in-LDS variant
-    check_rc(ft_w4_gemm_xr8(x.data_ptr(), (int)x.stride(0), M,
-                            reinterpret_cast<const uint32_t*>(wq.data_ptr<int>()), sz.data_ptr(),
-                            (int)N, K, wsp, op, ostride, (int)splits, (int)nt, silu ? 1 : 0,
-                            cur_stream()),
-             "w4_gemm_xr8");
+  if (xr == 4 || xr == 5) {   // "mh": two tiles per wave, rows over wave pairs; ring 2 (+2 x chunks) / 3
+    check_rc(ft_w4_gemm_mh(x.data_ptr(), (int)x.stride(0), M,
+                           reinterpret_cast<const uint32_t*>(wq.data_ptr<int>()), sz.data_ptr(),
+                           (int)N, K, wsp, op, ostride, (int)splits, xr == 4 ? 2 : 3, silu ? 1 : 0,
+                           cur_stream()),
+             "w4_gemm_mh");
     return;
   }
-  if (xr) {
-    // xr 1: sums by VALU while staging; 3: sums by MFMA against ones
+  if (xr) {   // "xr": x chunks in LDS, x sums while staging
     check_rc(ft_w4_gemm_xr(x.data_ptr(), (int)x.stride(0), M,
                            reinterpret_cast<const uint32_t*>(wq.data_ptr<int>()), sz.data_ptr(),
                            (int)N, K, wsp, op, ostride, (int)splits, (int)nt, silu ? 1 : 0,
-                           xr == 3 ? 1 : 0, cur_stream()),
+                           cur_stream()),
              "w4_gemm_xr");
     return;
   }

@@ -51,6 +51,19 @@ __device__ __forceinline__ w4_bf16x8 w4_frag(uint32_t w) {
   return __builtin_bit_cast(w4_bf16x8, r);
 }
 
+// the same with the two constants in VGPRs (opaque to the compiler): gfx950's VOP3
+// encoding takes no literal, so with literal masks hipcc emitted v_and + v_or per
+// output word (11 VALU per packed word); with register operands it is one
+// v_and_or_b32 (7 per word)
+__device__ __forceinline__ w4_bf16x8 w4_frag_r(uint32_t w, uint32_t vm, uint32_t vc) {
+  uint4 r;
+  r.x = (w & vm) | vc;
+  r.y = ((w >> 4) & vm) | vc;
+  r.z = ((w >> 8) & vm) | vc;
+  r.w = ((w >> 12) & vm) | vc;
+  return __builtin_bit_cast(w4_bf16x8, r);
+}
+
 __device__ __forceinline__ w4_bf16x8 w4_xfrag(const uint4& v) {
   return __builtin_bit_cast(w4_bf16x8, v);
 }
@@ -200,9 +213,7 @@ __global__ __launch_bounds__(256) void w4_skinny_kernel(
 // EPI 1: SiLU epilogue on a gate/up image interleaved in 16-row groups
 // (ops.quant.pack_w4 of interleave_gate_up(w, 1)): with NT = 2 a wave holds a gate
 // tile and its up tile and writes h = silu(g) * u (N/2 columns, bf16).
-// XSM: the per-(row, group) sums x . 1 by MFMAs against a ones operand instead of
-// VALU adds while staging (PMC: the staging sums were ~30% of the kernel's VALU)
-template <int MT, int NT, int EPI, bool XSM = false>
+template <int MT, int NT, int EPI>
 __global__ __launch_bounds__(256, 1) void w4_xr_kernel(
     const uint16_t* __restrict__ x, int x_stride, int M, const uint32_t* __restrict__ wq,
     const float2* __restrict__ sz, int K, float* __restrict__ ws, uint16_t* __restrict__ out,
@@ -275,13 +286,11 @@ __global__ __launch_bounds__(256, 1) void w4_xr_kernel(
         const int ch = sgrp * 16 + p;
         const int slot = (ch & ~7) | ((ch & 7) ^ (srow & 7));
         *reinterpret_cast<w4_u32x4*>(&sx[srow * KC + slot * 8]) = xr[p];
-        if constexpr (!XSM) {
-          float f[8];
-          load8(__builtin_bit_cast(uint4, xr[p]), f);
-          sum += ((f[0] + f[1]) + (f[2] + f[3])) + ((f[4] + f[5]) + (f[6] + f[7]));
-        }
+        float f[8];
+        load8(__builtin_bit_cast(uint4, xr[p]), f);
+        sum += ((f[0] + f[1]) + (f[2] + f[3])) + ((f[4] + f[5]) + (f[6] + f[7]));
       }
-      if constexpr (!XSM) s_xs[c & 1][sgrp][srow] = sum;
+      s_xs[c & 1][sgrp][srow] = sum;
     }
     if constexpr (MORE) load_x(c + 1);
     __syncthreads();   // chunk c visible; every wave is past chunk c-1's reads of the other buffer
@@ -298,17 +307,7 @@ __global__ __launch_bounds__(256, 1) void w4_xr_kernel(
           xf[h] = *reinterpret_cast<const w4_u32x4*>(&sx[row * KC + slot * 8]);
         }
         float xs[4];
-        if constexpr (XSM) {
-          const uint4 ones4 = make_uint4(0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u);
-          w4_floatx4 xm = w4_floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-          for (int h = 0; h < 4; ++h)
-            xm = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(w4_bf16x8, xf[h]),
-                                                         __builtin_bit_cast(w4_bf16x8, ones4), xm,
-                                                         0, 0, 0);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) xs[r] = xm[r];
-        } else {
+        {
           const float4 xs4 = *reinterpret_cast<const float4*>(&s_xs[c & 1][gq][16 * i + 4 * g]);
           xs[0] = xs4.x; xs[1] = xs4.y; xs[2] = xs4.z; xs[3] = xs4.w;
         }
@@ -368,194 +367,246 @@ __global__ __launch_bounds__(256, 1) void w4_xr_kernel(
 
 
 // ---------------------------------------------------------------------------
-// "xr8": the x-in-LDS W4 GEMM rebuilt from its PMC profile (gate_up at 50 rows,
-// profiles/w4_pmc_r05.txt: 8.1k VALU per wave against 1k MFMAs -- the MFMA pipe 18%
-// busy -- and 38% of the wave cycles waiting on memory / barriers, one wave per SIMD):
-//   * the zero-point term needs x . 1 per (row, group): computed by MFMAs against a
-//     ones operand (the MFMA pipe has the room) instead of VALU sums while staging,
-//     so staging x is a plain copy (global -> registers -> LDS, 16 B per load);
-//   * 8 waves (two per SIMD): waves w and w + 4 share column group w & 3 (16
-//     columns) and split each 512-wide chunk's four groups (kh = w >> 2 takes groups
-//     2 kh, 2 kh + 1); the kh = 1 sums reach their partners through LDS at the end;
-//   * each wave keeps two chunks of its weight fragments in flight (register ring of
-//     depth 2), 64 KiB of int4 per CU.
-// Every load is an ordinary (compiler-visible) load, so hipcc's counted waits are
-// exact: an LDS-DMA x stage or asm weight loads (measured variants) either made the
-// compiler's waits drain the ring or let it move the asm-loaded registers before
-// they had landed.  Epilogues as xr: bf16 / fp32 slabs / SiLU, the gate / up tile
-// pair of a SiLU image on the column groups cg (gate, even) and cg + 1 (up).
-template <int MT, int EPI>
-__global__ __launch_bounds__(512, 1) void w4_xr8_kernel(
+// "mh" W4 variant for 33..64 rows (round 6).  Measured on MI355X at 50 rows
+// (bench/w4mx_sweep.py, profiles/w4_mh_r06.log): qkv 12.2 vs 13.9 us, o 8.8 vs
+// 9.2, gate_up + SiLU 38.5 vs 40.0 against xr / the register kernel; down stays on
+// the register kernel.  Relative to xr:
+//   * the zero-point term leaves the inner loop: y = sum_g s_g a_g - sum_g (s_g z'_g)
+//     xs_g, a_g = x . (128 + q) over group g and xs_g = x . 1; the loop keeps one FMA
+//     per accumulator register and group, the sums xs_g are parked in LDS, and
+//     after the loop one v_mfma_f32_16x16x4_f32 per four groups subtracts
+//     xs . (s z')^T (exact fp32 operands) into the same accumulators;
+//   * the x . 1 sums come from the fragments the main loop already holds: for group
+//     gi the column wave cw == gi % 4 of each row half adds 4 ones-MFMAs per row
+//     tile (no VALU sums, no extra LDS reads, +12.5% MFMA);
+//   * conflict-free x layout: 16-B piece ch of row r at slot ch ^ (r & 15) (each
+//     16-lane group of a ds_read_b128 covers all 64 banks once; PMC: LDS bank
+//     conflict cycles 4.6M -> 57k per 64 gate_up calls);
+//   * two column tiles per wave (each x fragment read feeds two MFMAs), the rows
+//     split over MH halves of two row tiles: waves (cw, mh), cw = column wave 0..3;
+//     the two row halves of a column wave load the same weight bytes (served
+//     on-chip the second time) and dequantize them each, so 8 waves (two per SIMD)
+//     fit in 256 registers without spills;
+//   * dequant with its constants in registers: one v_and_or_b32 per output word;
+//   * weight ring RING chunks deep (KC 256 = 2 groups per chunk); XD = 2 keeps two
+//     x chunks in flight (ring 2).
+// What still bounds it (ablations, profiles/w4_mh_r06.log): the weight stream of
+// this register-ring form alone -- no math, no x loads, no barriers, no scale loads
+// -- takes 22 us for gate_up against 12.2 us for a plain 66 MB read
+// (profiles/bw_blocks_r06.log): 8 KB of loads in flight per wave is what 256
+// registers allow; going past it needs an LDS-DMA weight ring.
+// Epilogues: bf16 out (ws == nullptr) or fp32 slabs ws[s][m][n]; EPI 1 SiLU of the
+// in-wave gate / up tile pair of the 16-row interleaved image.  x rows >= M are
+// never loaded (an MFMA row feeds only its own output row).
+template <int MH, int RING, int EPI, int XD>
+__global__ __launch_bounds__(256 * MH, 2) void w4_mh_kernel(
     const uint16_t* __restrict__ x, int x_stride, int M, const uint32_t* __restrict__ wq,
     const float2* __restrict__ sz, int K, float* __restrict__ ws, uint16_t* __restrict__ out,
     int out_stride, int N, int k_slice) {
   constexpr bool SILU = EPI == 1;
-  constexpr int KC = 512, NG = KC / 128;     // k per chunk, groups per chunk
-  constexpr int GW = NG / 2;                 // groups per wave per chunk
-  constexpr int ROWS = 16 * MT;
-  constexpr int CPR = KC / 8;                // 16-B chunks per x row per chunk
-  constexpr int XL = ROWS * CPR / 512;       // x loads per thread per chunk
+  static_assert(XD == 1 || RING % 2 == 0, "two x register sets ride the ring-slot parity");
+  constexpr int MTW = 2, NT = 2, KC = 256, NG = KC / 128;
+  constexpr int NW = 4 * MH;
+  constexpr int ROWS = 16 * MTW * MH;
+  constexpr int NTH = 64 * NW;
+  constexpr int CPR = KC / 8;                // 16-B x pieces per row per chunk
+  constexpr int XL = (ROWS * CPR + NTH - 1) / NTH;
+  constexpr int XSG = 32;                    // groups per K slice (host-checked)
   __shared__ __attribute__((aligned(16))) uint16_t s_x[2][ROWS * KC];
+  __shared__ float s_xs[ROWS][XSG + 1];
   const int tid = threadIdx.x;
   const int lane = lane_id(), wave = wave_id();
   const int l15 = lane & 15, g = lane >> 4;
-  const int cg = wave & 3, kh = wave >> 2;
-  const int n0 = (blockIdx.x * 4 + cg) * 16;
+  const int cw = wave & 3, mh = wave >> 2;
+  const int t0 = (blockIdx.x * 4 + cw) * NT;          // first 16-column tile of this wave
   const int s = blockIdx.y;
   const int kbeg = s * k_slice;
   const int nch = k_slice / KC;
   const int groups_total = K >> 7;
   const int grp0 = kbeg >> 7;
+  const int ntiles = N >> 4;
 
-  int xoff[XL];   // 32-bit element offsets (half the registers of pointers)
+  int xoff[XL];
+  bool xok[XL];
 #pragma unroll
   for (int p = 0; p < XL; ++p) {
-    const int e = tid + 512 * p;
-    xoff[p] = min(e / CPR, M - 1) * x_stride + kbeg + (e % CPR) * 8;
+    const int e = tid + NTH * p;
+    const int row = e / CPR;
+    xok[p] = e < ROWS * CPR && row < M;
+    xoff[p] = min(row, M - 1) * x_stride + kbeg + (e % CPR) * 8;
   }
-  const size_t tile = (size_t)(min(n0, N - 16) / 16) * groups_total + grp0;
-  const uint32_t* wp = wq + tile * 256 + lane * 4;
-  const float2* sp = sz + tile * 16 + l15;
-
-  w4_floatx4 acc[MT];
+  const uint32_t* wp[NT];
+  const float* sp[NT];
 #pragma unroll
-  for (int i = 0; i < MT; ++i) acc[i] = w4_floatx4{0.f, 0.f, 0.f, 0.f};
+  for (int j = 0; j < NT; ++j) {
+    const size_t tile = (size_t)min(t0 + j, ntiles - 1) * groups_total + grp0;
+    wp[j] = wq + tile * 256 + lane * 4;
+    sp[j] = reinterpret_cast<const float*>(sz + tile * 16 + l15);
+  }
+  // this wave's LDS row base (row tile 2 mh + i, row l15 of it), swizzle key l15
+  const int rbase = (16 * MTW * mh + l15) * KC;
 
-  w4_u32x4 xr[XL];
-  w4_u32x4 wr[2][GW];         // ring: chunk c's fragments in slot c & 1
-  float2 szr[2][GW];
+  w4_floatx4 acc[MTW][NT];
+#pragma unroll
+  for (int i = 0; i < MTW; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = w4_floatx4{0.f, 0.f, 0.f, 0.f};
+
+  w4_u32x4 xr[XD][XL];
+  w4_u32x4 wr[RING][NG][NT];
+  float scr[RING][NG][NT];
   auto load_w = [&](int c, int sl) {
 #pragma unroll
-    for (int q = 0; q < GW; ++q) {
-      const int gi = c * NG + kh * GW + q;
-      wr[sl][q] = __builtin_nontemporal_load(reinterpret_cast<const w4_u32x4*>(wp + (size_t)gi * 256));
-      szr[sl][q] = sp[(size_t)gi * 16];
-    }
+    for (int gq = 0; gq < NG; ++gq)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const int gi = c * NG + gq;
+        wr[sl][gq][j] = *reinterpret_cast<const w4_u32x4*>(wp[j] + (size_t)gi * 256);
+        scr[sl][gq][j] = sp[j][(size_t)gi * 32];   // float2 stride: (tile, group) records of 16 columns
+      }
   };
   const uint4 ones4 = make_uint4(0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u);
   const w4_bf16x8 ones = __builtin_bit_cast(w4_bf16x8, ones4);
+  uint32_t vmask = 0x000F000Fu, vbias = 0x43004300u;
+  asm volatile("" : "+v"(vmask), "+v"(vbias));
 
 #pragma unroll
-  for (int p = 0; p < XL; ++p) xr[p] = *reinterpret_cast<const w4_u32x4*>(x + xoff[p]);
-  load_w(0, 0);
-  if (nch > 1) load_w(1, 1);
+  for (int p = 0; p < XL; ++p)
+    if (xok[p]) xr[0][p] = *reinterpret_cast<const w4_u32x4*>(x + xoff[p]);
+  if (XD == 2 && nch > 1) {
+#pragma unroll
+    for (int p = 0; p < XL; ++p)
+      if (xok[p]) xr[XD - 1][p] = *reinterpret_cast<const w4_u32x4*>(x + xoff[p] + KC);
+  }
+#pragma unroll
+  for (int r = 0; r < RING; ++r)
+    if (r < nch) load_w(r, r);
 
-  // chunk c: x registers -> LDS buffer c & 1, next chunk's x loads, barrier, MFMAs;
-  // weights from ring slot SL, refilled with chunk c + 2 (MORE) after use
   auto chunk = [&](int c, auto sl_tag, auto more_tag) {
     constexpr int SL = decltype(sl_tag)::value;
     constexpr bool MORE = decltype(more_tag)::value;
     uint16_t* sx = s_x[c & 1];
 #pragma unroll
     for (int p = 0; p < XL; ++p) {
-      const int e = tid + 512 * p;
+      const int e = tid + NTH * p;
       const int row = e / CPR, ch = e % CPR;
-      const int slot = (ch & ~7) | ((ch & 7) ^ (row & 7));
-      *reinterpret_cast<w4_u32x4*>(&sx[row * KC + slot * 8]) = xr[p];
+      if (xok[p]) *reinterpret_cast<w4_u32x4*>(&sx[row * KC + (ch ^ (row & 15)) * 8]) = xr[XD == 2 ? (SL & 1) : 0][p];
     }
-    if (c + 1 < nch) {
+    if (c + XD < nch) {   // x of chunk c + XD into the register set just written out
 #pragma unroll
-      for (int p = 0; p < XL; ++p) xr[p] = *reinterpret_cast<const w4_u32x4*>(x + xoff[p] + (c + 1) * KC);
+      for (int p = 0; p < XL; ++p)
+        if (xok[p]) xr[XD == 2 ? (SL & 1) : 0][p] = *reinterpret_cast<const w4_u32x4*>(x + xoff[p] + (c + XD) * KC);
     }
     __syncthreads();   // chunk c visible; every wave is past chunk c-1's reads of the other buffer
 #pragma unroll
-    for (int q = 0; q < GW; ++q) {
-      const int gq = kh * GW + q;
-      const uint32_t wd[4] = {wr[SL][q][0], wr[SL][q][1], wr[SL][q][2], wr[SL][q][3]};
-      const float sc = szr[SL][q].x, zz = szr[SL][q].y;
+    for (int gq = 0; gq < NG; ++gq) {
+      const int gi = c * NG + gq;
+      w4_bf16x8 wf[NT][4];
 #pragma unroll
-      for (int i = 0; i < MT; ++i) {
-        const int row = 16 * i + l15;
+      for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int h = 0; h < 4; ++h) wf[j][h] = w4_frag_r(wr[SL][gq][j][h], vmask, vbias);
+      float sc[NT];
+#pragma unroll
+      for (int j = 0; j < NT; ++j) sc[j] = scr[SL][gq][j];
+      if constexpr (MORE) {   // refill this slot with chunk c + RING right away
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          const int gn = (c + RING) * NG + gq;
+          wr[SL][gq][j] = *reinterpret_cast<const w4_u32x4*>(wp[j] + (size_t)gn * 256);
+          scr[SL][gq][j] = sp[j][(size_t)gn * 32];
+        }
+      }
+      const bool xs_duty = cw == (gi & 3);
+#pragma unroll
+      for (int i = 0; i < MTW; ++i) {
         w4_u32x4 xf[4];
 #pragma unroll
         for (int h = 0; h < 4; ++h) {
           const int ch = gq * 16 + 8 * (h >> 1) + 2 * g + (h & 1);
-          const int slot = (ch & ~7) | ((ch & 7) ^ (row & 7));
-          xf[h] = *reinterpret_cast<const w4_u32x4*>(&sx[row * KC + slot * 8]);
-        }
-        // x . 1 over the group for rows 4 g + r (C layout; every column equal)
-        w4_floatx4 xs = w4_floatx4{0.f, 0.f, 0.f, 0.f};
-        w4_floatx4 a = w4_floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int h = 0; h < 4; ++h) {
-          xs = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(w4_bf16x8, xf[h]), ones, xs,
-                                                       0, 0, 0);
-          a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(w4_bf16x8, xf[h]),
-                                                      w4_frag(wd[h]), a, 0, 0, 0);
+          xf[h] = *reinterpret_cast<const w4_u32x4*>(&sx[rbase + 16 * i * KC + (ch ^ l15) * 8]);
         }
 #pragma unroll
-        for (int r = 0; r < 4; ++r) acc[i][r] = fmaf(sc, fmaf(-zz, xs[r], a[r]), acc[i][r]);
-        if constexpr (MT == 4) __builtin_amdgcn_sched_barrier(0);   // (one row tile's x live: no spills)
+        for (int j = 0; j < NT; ++j) {
+          w4_floatx4 a = w4_floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int h = 0; h < 4; ++h)
+            a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(w4_bf16x8, xf[h]), wf[j][h], a, 0, 0, 0);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[i][j][r] = fmaf(sc[j], a[r], acc[i][j][r]);
+        }
+        if (xs_duty) {   // x . 1 of (row tile 2 mh + i, group gi) from the fragments in hand
+          w4_floatx4 xm = w4_floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int h = 0; h < 4; ++h)
+            xm = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(w4_bf16x8, xf[h]), ones, xm, 0, 0, 0);
+          if (l15 == 0) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) s_xs[16 * (MTW * mh + i) + 4 * g + r][gi] = xm[r];
+          }
+        }
       }
     }
-    if constexpr (MORE) load_w(c + 2, SL);   // two chunks ahead
   };
-  for (int c = 0; c < nch; ++c) {   // ring slot c & 1; refill while chunk c + 2 exists
-    const bool more = c + 2 < nch;
-    if (c & 1) {
-      if (more) chunk(c, std::integral_constant<int, 1>{}, std::true_type{});
-      else chunk(c, std::integral_constant<int, 1>{}, std::false_type{});
-    } else {
-      if (more) chunk(c, std::integral_constant<int, 0>{}, std::true_type{});
-      else chunk(c, std::integral_constant<int, 0>{}, std::false_type{});
+  for (int c = 0; c < nch; ++c) {   // ring slot c % RING; refill while chunk c + RING exists
+    const bool more = c + RING < nch;
+    static_for<0, RING>([&](auto sl) {
+      if (c % RING == decltype(sl)::value) {
+        if (more) chunk(c, sl, std::true_type{});
+        else chunk(c, sl, std::false_type{});
+      }
+    });
+  }
+  __syncthreads();   // every wave's x sums are in s_xs
+  // zero-point term: acc -= xs . (s z')^T, four groups per f32 MFMA
+  const int ng = k_slice >> 7;
+  for (int q = 0; q < ng; q += 4) {
+    const bool gv = q + g < ng;
+    float bz[NT];
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const float2 v = reinterpret_cast<const float2*>(sp[j])[(size_t)min(q + g, ng - 1) * 16];
+      bz[j] = gv ? -v.x * v.y : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < MTW; ++i) {
+      const float xa = gv ? s_xs[16 * (MTW * mh + i) + l15][q + g] : 0.f;
+#pragma unroll
+      for (int j = 0; j < NT; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa, bz[j], acc[i][j], 0, 0, 0);
     }
   }
-
-  // K halves: the kh = 1 waves pass their sums to the kh = 0 partners through LDS
-  __syncthreads();   // every wave is past its last x reads
-  float* red = reinterpret_cast<float*>(&s_x[0][0]);   // [4 cg][MT * 4][64]
-  constexpr int NREG = MT * 4;
-  static_assert(4 * NREG * 64 * 4 <= (int)sizeof(s_x), "reduction buffer");
-  if (kh == 1) {
-#pragma unroll
-    for (int i = 0; i < MT; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) red[((cg * NREG) + i * 4 + r) * 64 + lane] = acc[i][r];
-  }
-  __syncthreads();
-  if (kh == 0) {
-#pragma unroll
-    for (int i = 0; i < MT; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) acc[i][r] += red[((cg * NREG) + i * 4 + r) * 64 + lane];
-  }
+  if (t0 >= ntiles) return;
   if constexpr (SILU) {
-    // the up-tile waves (odd cg) hand their sums to the gate-tile waves (cg - 1)
-    __syncthreads();   // every kh = 0 wave is done reading the partials
-    if (kh == 0 && (cg & 1)) {
+    const int col = ((t0 * 16) >> 1) + l15;   // (gate tile, up tile) -> 16 h columns
 #pragma unroll
-      for (int i = 0; i < MT; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) red[((cg >> 1) * MT * 4 + i * 4 + r) * 64 + lane] = acc[i][r];
-    }
-    __syncthreads();
-    if (kh == 1 || (cg & 1) || n0 >= N) return;
-    const int col = (n0 >> 1) + l15;
-#pragma unroll
-    for (int i = 0; i < MT; ++i)
+    for (int i = 0; i < MTW; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int m = 16 * i + g * 4 + r;
+        const int m = 16 * (MTW * mh + i) + g * 4 + r;
         if (m < M) {
-          const float gt = acc[i][r], up = red[((cg >> 1) * MT * 4 + i * 4 + r) * 64 + lane];
+          const float gt = acc[i][0][r], up = acc[i][1][r];
           out[(size_t)m * out_stride + col] = f32_to_bf16(gt / (1.f + __expf(-gt)) * up);
         }
       }
     return;
   }
-  if (kh == 1 || n0 >= N) return;
   float* slab = ws + (size_t)s * M * N;
 #pragma unroll
-  for (int i = 0; i < MT; ++i)
+  for (int i = 0; i < MTW; ++i)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int m = 16 * i + g * 4 + r;
+      const int m = 16 * (MTW * mh + i) + g * 4 + r;
       if (m < M) {
-        const int n = n0 + l15;
-        if (ws == nullptr)
-          out[(size_t)m * out_stride + n] = f32_to_bf16(acc[i][r]);
-        else
-          slab[(size_t)m * N + n] = acc[i][r];
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          const int n = (t0 + j) * 16 + l15;
+          if (t0 + j < ntiles) {
+            if (ws == nullptr)
+              out[(size_t)m * out_stride + n] = f32_to_bf16(acc[i][j][r]);
+            else
+              slab[(size_t)m * N + n] = acc[i][j][r];
+          }
+        }
       }
     }
 }
@@ -626,7 +677,7 @@ extern "C" int ft_w4_gemm(const void* x, int x_stride, int M, const uint32_t* wq
 // out [M, N/2]; splits > 1 needs ws (slab output), silu needs splits == 1.
 extern "C" int ft_w4_gemm_xr(const void* x, int x_stride, int M, const uint32_t* wq, const void* sz,
                              int N, int K, float* ws, void* out, int out_stride, int splits, int nt,
-                             int silu, int xsm, hipStream_t stream) {
+                             int silu, hipStream_t stream) {
   if (M <= 0) return 0;
   if (M > 64 || splits < 1) return -1;
   if (N % (64 * nt) != 0) return -2;
@@ -639,11 +690,6 @@ extern "C" int ft_w4_gemm_xr(const void* x, int x_stride, int M, const uint32_t*
   const int k_slice = K / splits;
 #define FT_W4X(MT_, NT_, E_)                                                                 \
   if (mt == MT_ && nt == NT_ && silu == E_) {                                                \
-    if (xsm) /* nt 4: the VALU sums (hipcc's AGPR-copy rewrite crashes on that form) */     \
-      hipLaunchKernelGGL((ft::w4_xr_kernel<MT_, NT_, E_, (NT_ <= 2)>), grid, block, 0, stream,\
-                         (const uint16_t*)x, x_stride, M, wq, (const float2*)sz, K, ws,      \
-                         (uint16_t*)out, out_stride, N, k_slice);                            \
-    else                                                                                     \
     hipLaunchKernelGGL((ft::w4_xr_kernel<MT_, NT_, E_>), grid, block, 0, stream,             \
                        (const uint16_t*)x, x_stride, M, wq, (const float2*)sz, K, ws,        \
                        (uint16_t*)out, out_stride, N, k_slice);                              \
@@ -659,31 +705,32 @@ extern "C" int ft_w4_gemm_xr(const void* x, int x_stride, int M, const uint32_t*
   return -5;
 }
 
-// "xr8" variant (33..64 rows): nt must be 1 (16 columns per wave), N % 64 == 0,
-// K % (512 * splits) == 0; silu: one split, gate / up tile pairs across waves.
-extern "C" int ft_w4_gemm_xr8(const void* x, int x_stride, int M, const uint32_t* wq,
-                              const void* sz, int N, int K, float* ws, void* out, int out_stride,
-                              int splits, int nt, int silu, hipStream_t stream) {
+// "mh" variant (33..64 rows; 17..32 run one row half): N % 32 == 0, K % (256 * splits)
+// == 0, K / splits <= 4096 (the x-sum table); ring 2 (two x chunks in flight too) or 3;
+// silu: one split, out [M, N/2].
+extern "C" int ft_w4_gemm_mh(const void* x, int x_stride, int M, const uint32_t* wq, const void* sz,
+                             int N, int K, float* ws, void* out, int out_stride, int splits, int ring,
+                             int silu, hipStream_t stream) {
   if (M <= 0) return 0;
   if (M > 64 || splits < 1) return -1;
-  if (nt != 1) return -7;
-  if (N % 64 != 0) return -2;
-  if (K % (512 * splits) != 0) return -3;
+  if (N % 32 != 0) return -2;
+  if (K % (256 * splits) != 0 || K / splits > 4096) return -3;
   if (splits > 1 && (ws == nullptr || silu)) return -4;
   if (ws == nullptr && out == nullptr) return -6;
-  const int mt = (M + 15) / 16;
-  dim3 grid(N / 64, splits), block(512);
+  if (ring != 2 && ring != 3) return -7;
+  const int mh = M > 32 ? 2 : 1;
+  dim3 grid((N / 16 + 7) / 8, splits), block(256 * mh);
   const int k_slice = K / splits;
-#define FT_W4X8(MT_, E_)                                                                     \
-  if (mt == MT_ && silu == E_) {                                                             \
-    hipLaunchKernelGGL((ft::w4_xr8_kernel<MT_, E_>), grid, block, 0, stream,                 \
-                       (const uint16_t*)x, x_stride, M, wq, (const float2*)sz, K, ws,        \
-                       (uint16_t*)out, out_stride, N, k_slice);                              \
-    return static_cast<int>(hipGetLastError());                                              \
+#define FT_W4MH(MH_, R_, E_)                                                                     \
+  if (mh == MH_ && ring == R_ && silu == E_) {                                                  \
+    hipLaunchKernelGGL((ft::w4_mh_kernel<MH_, R_, E_, R_ == 2 ? 2 : 1>), grid, block, 0, stream,\
+                       (const uint16_t*)x, x_stride, M, wq, (const float2*)sz, K, ws,           \
+                       (uint16_t*)out, out_stride, N, k_slice);                                 \
+    return static_cast<int>(hipGetLastError());                                                 \
   }
-  FT_W4X8(2, 0) FT_W4X8(3, 0) FT_W4X8(4, 0)
-  FT_W4X8(2, 1) FT_W4X8(3, 1) FT_W4X8(4, 1)
-#undef FT_W4X8
+  FT_W4MH(1, 2, 0) FT_W4MH(1, 3, 0) FT_W4MH(2, 2, 0) FT_W4MH(2, 3, 0)
+  FT_W4MH(1, 2, 1) FT_W4MH(1, 3, 1) FT_W4MH(2, 2, 1) FT_W4MH(2, 3, 1)
+#undef FT_W4MH
   return -5;
 }
 

@@ -325,9 +325,31 @@ W4_PLAN = {
 }
 
 
+# 49..64 rows: the "mh" kernel (w4a16.hip, xr 4 = weight ring 2 with two x chunks in
+# flight, 5 = ring 3) where it wins, cold-cache us at 50 / 64 rows on MI355X
+# (bench/w4mx_sweep.py, profiles/w4_mh_r06.log): qkv 12.2 / 12.7 (xr 13.9 / 14.6),
+# o 8.8 / 9.4 (9.2 / 9.6), gate_up + SiLU 38.5 / 38.9 (40.0 / 41.2); down keeps the
+# register kernel (19.7 vs 20.1).  At 33..48 rows the second row half is mostly
+# padding and xr stays ahead (gate_up 31.3 vs 39.0 at 33 rows).
+W4_PLAN_MH = {"qkv": (2, 4, 4), "o": (2, 8, 4), "gu": (2, 1, 5)}
+W4_MH_MIN_ROWS = 49
+
+
 def w4_cfg(proj: str, rows: int):
+    if rows >= W4_MH_MIN_ROWS and proj in W4_PLAN_MH:
+        return W4_PLAN_MH[proj]
     b = next(m for m in _M_BUCKETS if m >= rows)
     return W4_PLAN[proj][b]
+
+
+def w4_fits(xr: int, nt: int, sp: int, n: int, k: int) -> bool:
+    """Whether the W4 decode kernel ``xr`` (0 register, 1 xr, 4 / 5 mh) tiles [n, k]
+    at ``sp`` K splits (TP shards can break the plan's shapes)."""
+    if xr in (4, 5):
+        return n % 32 == 0 and k % (256 * sp) == 0 and k // sp <= 4096
+    if xr:
+        return n % (64 * nt) == 0 and k % (512 * sp) == 0
+    return n % (16 * nt) == 0 and k % (128 * sp) == 0
 
 
 # Projections of >= 64 M weights (Llama-3-70B at TP=1: qkv 10240 x 8192, o 8192 x 8192,
@@ -838,14 +860,14 @@ class LlamaModel:
             il = proj == "gu" and self.w4_gu_il
             if rows <= W4_ROWS:
                 nt, sp, xr = w4_cfg(proj, rows)
-                if xr and (q.n % (64 * nt) or q.k % (512 * sp)):
-                    nt, sp, xr = 1, 1, 0          # shape the xr tiles do not cover (TP shards)
-                if il and xr and nt == 2 and sp == 1 and q.n % 128 == 0:
-                    return 0, Q.w4_gemm(x, q, nt=2, xr=True, silu=True)
+                if xr and not w4_fits(xr, nt, sp, q.n, q.k):
+                    nt, sp, xr = 1, 1, 0          # shape the LDS kernels do not cover (TP shards)
+                if il and xr and nt == 2 and sp == 1 and q.n % (32 if xr in (4, 5) else 128) == 0:
+                    return 0, Q.w4_gemm(x, q, nt=2, xr=xr, silu=True)
                 if self.ws is not None and self.w4_slab.get(proj):
-                    Q.w4_gemm(x, q, ws=self.ws, splits=sp, nt=nt, xr=bool(xr))
+                    Q.w4_gemm(x, q, ws=self.ws, splits=sp, nt=nt, xr=xr)
                     return sp, None
-                y = Q.w4_gemm(x, q, nt=nt, xr=bool(xr))
+                y = Q.w4_gemm(x, q, nt=nt, xr=xr)
             else:
                 # the dequantized prefill image (_prepare_w4_prefill), or this
                 # projection dequantized and packed into a scratch when it is off

@@ -151,11 +151,13 @@ def w4_dequant(w: W4Weight, out: Optional[torch.Tensor] = None,
 
 
 def w4_gemm(x: torch.Tensor, w: W4Weight, out=None, ws=None, splits: int = 1, nt: int = 1,
-            xr: bool = False, silu: bool = False):
+            xr: int = 0, silu: bool = False):
     """y = x dequant(w)^T for M <= 64 rows.  With ``ws`` the kernel leaves fp32
     slabs ([splits, M, N]) for a fused epilogue; otherwise returns bf16 ``out``.
-    ``xr``: the x-in-LDS variant (17..64 rows; 2 = its 8-wave form); ``silu``: its SiLU epilogue on a
-    gate/up image interleaved in 16-row groups (returns h = silu(gate) * up)."""
+    ``xr`` picks the kernel (w4a16.hip): 0 the register kernel, 1 "xr" (x chunks in
+    LDS, 17..64 rows), 4 / 5 "mh" (two tiles per wave, rows over wave pairs; weight
+    ring 2 with two x chunks in flight / ring 3).  ``silu``: the LDS kernels' SiLU
+    epilogue on a gate/up image interleaved in 16-row groups (h = silu(gate) * up)."""
     if not x.is_cuda:
         y = x @ w4_dequant(w, dtype=x.dtype).t()
         if silu:

@@ -152,3 +152,21 @@ def test_decode_workspace_piece_mode_slots():
     assert n_out == 4 * 8 * 4 * 4 * 128 and n_ml == 4 * 8 * 4 * 4 * 2   # 128 tiles -> 4 pieces
     n0, _ = ops.decode_workspace(4, 32, 8, 128, waves=16)
     assert n0 == (4 * 8 + 16) * 4 * 128
+
+
+def test_w4_plan_uses_mh_above_48_rows():
+    """49..64 rows run the "mh" W4 kernel for qkv / o / gate_up (xr 4 / 5), down
+    and smaller batches keep the round-5 entries; every entry tiles the Llama-3-8B
+    shapes, and w4_fits rejects shapes a TP shard can break."""
+    assert llama.w4_cfg("qkv", 50) == (2, 4, 4)
+    assert llama.w4_cfg("gu", 64) == (2, 1, 5)
+    assert llama.w4_cfg("down", 50) == llama.W4_PLAN["down"][64]
+    assert llama.w4_cfg("qkv", 40) == llama.W4_PLAN["qkv"][64]
+    shapes = {"qkv": (6144, 4096), "o": (4096, 4096), "gu": (28672, 4096), "down": (4096, 14336)}
+    for proj, (n, k) in shapes.items():
+        for rows in (1, 8, 16, 20, 33, 48, 50, 64):
+            nt, sp, xr = llama.w4_cfg(proj, rows)
+            assert llama.w4_fits(xr, nt, sp, n, k), (proj, rows)
+    assert not llama.w4_fits(4, 2, 4, 6144 // 8 + 16, 4096)   # N % 32
+    assert not llama.w4_fits(4, 2, 1, 4096, 14336)            # K slice > 4096 (x-sum table)
+    assert not llama.w4_fits(1, 2, 1, 96, 4096)               # xr: N % 128
