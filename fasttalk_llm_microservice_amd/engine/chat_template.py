@@ -93,6 +93,29 @@ class ChatTemplate:
             self._msg_cache[key] = ids
         return list(ids)
 
+    def remember_assistant(self, ids: Sequence[int]) -> None:
+        """Token-exact history: the ids an assistant turn was GENERATED as, filed under the
+        text they decode to, so the next turn renders that message with the same ids and
+        the engine's prefix cache covers the whole reply.  This is the path of stateless
+        clients (the OpenAI facade, /v1/chat/completions, and any render after a history
+        window cut) that send the reply back as text; a WS session continues from its
+        own token state (NativeHandler).  Re-encoding a generated reply
+        rarely reproduces its ids (a sampled sequence is seldom the tokenizer's own
+        segmentation of its text: 40% of a random 128-token reply survived a round trip
+        on the synthetic tokenizer), and every token after the first mismatch is
+        prefilled again.  A message stored with any other text (stop-string cuts,
+        post-processing) simply misses the entry and is encoded as before."""
+        ids = list(ids)
+        if not ids or any(self.tok.is_special(t) for t in ids):
+            return
+        key = ("assistant", self.tok.decode(ids))
+        while len(self._msg_cache) >= self.MSG_CACHE:
+            try:
+                self._msg_cache.pop(next(iter(self._msg_cache)))
+            except (RuntimeError, KeyError, StopIteration):
+                self._msg_cache.clear()
+        self._msg_cache[key] = self._header("assistant") + ids + [self.tok.eot_id]
+
     def render(self, messages: Sequence[Dict[str, Any]], add_generation_prompt: bool = True,
                tools: Optional[Sequence[Dict[str, Any]]] = None) -> List[int]:
         msgs = list(messages)

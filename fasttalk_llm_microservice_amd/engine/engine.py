@@ -84,6 +84,9 @@ class LLMEngine:
         self.jump_forward = os.environ.get("ENGINE_JUMP_FORWARD", "1") != "0"
         # a grammar that is complete ends the sequence without decoding its EOS
         self.grammar_eos_shortcut = self.jump_forward
+        # token-exact assistant history (ChatTemplate.remember_assistant;
+        # ENGINE_TOKEN_HISTORY=0 re-encodes every reply from its text)
+        self.token_history = os.environ.get("ENGINE_TOKEN_HISTORY", "1") != "0"
         self._jf_cache: Dict[bytes, List[int]] = {}
         self._guided_lens = collections.deque(maxlen=4096)
         self.stats = collections.Counter()
@@ -785,6 +788,12 @@ class LLMEngine:
             seq.detok_stream = -1
         text = delta + (seq.stop_buf if reason != "stop" else "") + tail
         seq.stop_buf = ""
+        if self.token_history and reason in ("length", "stop") and seq.grammar is None \
+                and not seq.params.stop:
+            out_ids = seq.output_ids
+            while out_ids and self.tokenizer.is_special(out_ids[-1]):   # the EOS that ended it
+                out_ids.pop()
+            self.template.remember_assistant(out_ids)
         out = RequestOutput(seq.request_id, text, ids or [], finished=True, finish_reason=reason,
                             num_prompt_tokens=seq.prompt_len,
                             num_cached_tokens=seq.num_cached_tokens,

@@ -738,3 +738,48 @@ def test_guided_rows_cap_the_steps_prefill():
         else:
             assert max(g_steps) > 8
     assert outs[0] == outs[8]
+
+
+def _chat_turn(eng, prompt, sp, rid):
+    """One request through add_request / step: (streamed text, ids, cached prompt tokens)."""
+    eng.add_request(rid, prompt, sp)
+    text, ids, cached = "", [], None
+    while eng.has_work():
+        for o in eng.step():
+            if o.request_id != rid:
+                continue
+            text += o.text
+            ids += o.token_ids
+            if o.finished:
+                cached = o.num_cached_tokens
+    return text, ids, cached
+
+
+def test_token_exact_assistant_history_keeps_the_reply_in_the_prefix_cache(tiny_engine):
+    """A reply rendered back into the next turn's prompt keeps the ids it was generated
+    as (ChatTemplate.remember_assistant), so the prefix cache covers the whole reply;
+    the cached entry decodes to exactly the stored text."""
+    eng = tiny_engine
+    tpl = eng.template
+    msgs = [{"role": "system", "content": "You are a helpful voice assistant."},
+            {"role": "user", "content": "Tell me something about the weather on the coast today."}]
+    sp = SamplingParams(temperature=1.0, top_p=1.0, max_tokens=40, ignore_eos=True, seed=4)
+    p1 = tpl.render(msgs)
+    text, ids, _ = _chat_turn(eng, p1, sp, "tok-hist-1")
+    assert len(ids) == 40 and text == eng.tokenizer.decode(ids)
+    # (this sample is not the tokenizer's own segmentation of its text: re-encoding
+    # it breaks the prefix after two tokens)
+    assert eng.tokenizer.encode(text)[:len(ids)] != ids
+    msgs2 = msgs + [{"role": "assistant", "content": text},
+                    {"role": "user", "content": "And tomorrow?"}]
+    p2 = tpl.render(msgs2)
+    head = p1 + ids
+    assert p2[:len(head)] == head   # the reply kept its generated ids
+    assert eng.tokenizer.decode(tpl.message_ids(msgs2[2])) == \
+        eng.tokenizer.decode(tpl._header("assistant")) + text + eng.tokenizer.decode([eng.tokenizer.eot_id])
+    _, _, cached = _chat_turn(eng, p2, SamplingParams(temperature=0, max_tokens=2, ignore_eos=True),
+                              "tok-hist-2")
+    bs = eng.bm.block_size
+    # every full block of the first turn's prompt + reply (but the last sampled token,
+    # whose KV was never computed) comes from the cache
+    assert cached >= ((len(head) - 1) // bs) * bs
