@@ -370,6 +370,11 @@ def main():
     hb["done"] = True
     # sessions this worker (rank) holds: the front door's placement
     placed = int(board.get(rank, "active")) if door else a.sessions
+    if door and world > 1:
+        # every rank reads its worker's count before any rank's load client closes its
+        # sessions: the door places a rank's sessions on any worker, so a fast rank's
+        # close would otherwise show up as missing sessions on a slower rank's row
+        dist.barrier()
     if loop_prof is not None:
         dumped = threading.Event()
 
