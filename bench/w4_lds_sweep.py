@@ -44,7 +44,7 @@ def main():
             ref = x.float() @ wdq.t()
             out = torch.empty(m, n, device=dev).bfloat16()
             rows = []
-            cfgs = [("plan",) + tuple(w4_cfg(name, m))]
+            cfgs = [("plan",) + tuple(w4_cfg(name, m, n, k))]
             for sp in (1, 2, 4, 7, 8, 14):
                 cfgs += [("reg", 4, sp, 0), ("xr", 2, sp, 1), ("mh", 2, sp, 4), ("mh3", 2, sp, 5)]
             for kind, nt, sp, xr in cfgs:
@@ -65,6 +65,8 @@ def main():
                 href = (torch.nn.functional.silu(g_) * u_).reshape(m, -1)
                 hout = torch.empty(m, n // 2, device=dev).bfloat16()
                 for xr in (1, 4, 5):
+                    if not w4_fits(xr, 2, 1, n, k):
+                        continue
                     fn = lambda W, xr=xr: (lambda: Q.w4_gemm(x, W, out=hout, nt=2, xr=xr, silu=True))
                     fn(W0)()
                     err = (hout.float() - href).abs().max().item() / (href.abs().max().item() + 1e-6)

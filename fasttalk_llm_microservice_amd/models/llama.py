@@ -333,13 +333,30 @@ W4_PLAN = {
 # padding and xr stays ahead (gate_up 31.3 vs 39.0 at 33 rows).
 W4_PLAN_MH = {"qkv": (2, 4, 4), "o": (2, 8, 4), "gu": (2, 1, 5)}
 W4_MH_MIN_ROWS = 49
+# Llama-3-70B at TP=1 (>= 64 M-weight projections), 49..64 rows, cold-cache us at 50
+# rows (profiles/w4_70b_sweep_r06.log): qkv mh at 8 splits 33.2 (4 splits 40.3), o the
+# register kernel at 2 splits 22.7 (mh / 8: 25.6); gate_up (K 8192 > mh's K slice)
+# stays on the xr SiLU entry, down on the register kernel.
+W4_PLAN_WIDE = {"qkv": (2, 8, 4), "o": (4, 2, 0)}
 
 
-def w4_cfg(proj: str, rows: int):
-    if rows >= W4_MH_MIN_ROWS and proj in W4_PLAN_MH:
-        return W4_PLAN_MH[proj]
+def w4_cfg(proj: str, rows: int, n: int = 0, k: int = 0):
+    """(nt, splits, xr) of a W4 decode GEMM.  With the shape given, an entry whose
+    kernel cannot tile it (TP shards, Llama-3-70B's K 8192 gate_up / 28672 down for
+    mh's 4096-wide K slices) falls back to the bucket plan, then to the register
+    kernel at one split."""
     b = next(m for m in _M_BUCKETS if m >= rows)
-    return W4_PLAN[proj][b]
+    cands = [W4_PLAN[proj][b]]
+    if rows >= W4_MH_MIN_ROWS and proj in W4_PLAN_MH:
+        cands.insert(0, W4_PLAN_MH[proj])
+    if rows >= W4_MH_MIN_ROWS and n * k >= WIDE_ELEMS and proj in W4_PLAN_WIDE:
+        cands.insert(0, W4_PLAN_WIDE[proj])
+    if not n:
+        return cands[0]
+    for c in cands:
+        if w4_fits(c[2], c[0], c[1], n, k):
+            return c
+    return (1, 1, 0)
 
 
 def w4_fits(xr: int, nt: int, sp: int, n: int, k: int) -> bool:
@@ -859,9 +876,7 @@ class LlamaModel:
         if q is not None:  # W4A16
             il = proj == "gu" and self.w4_gu_il
             if rows <= W4_ROWS:
-                nt, sp, xr = w4_cfg(proj, rows)
-                if xr and not w4_fits(xr, nt, sp, q.n, q.k):
-                    nt, sp, xr = 1, 1, 0          # shape the LDS kernels do not cover (TP shards)
+                nt, sp, xr = w4_cfg(proj, rows, q.n, q.k)
                 if il and xr and nt == 2 and sp == 1 and q.n % (32 if xr in (4, 5) else 128) == 0:
                     return 0, Q.w4_gemm(x, q, nt=2, xr=xr, silu=True)
                 if self.ws is not None and self.w4_slab.get(proj):

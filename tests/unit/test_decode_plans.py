@@ -170,3 +170,10 @@ def test_w4_plan_uses_mh_above_48_rows():
     assert not llama.w4_fits(4, 2, 4, 6144 // 8 + 16, 4096)   # N % 32
     assert not llama.w4_fits(4, 2, 1, 4096, 14336)            # K slice > 4096 (x-sum table)
     assert not llama.w4_fits(1, 2, 1, 96, 4096)               # xr: N % 128
+    # Llama-3-70B (TP=1): gate_up's K 8192 is past mh's one-split K slice -> the xr
+    # SiLU entry of the bucket plan, not the register kernel
+    assert llama.w4_cfg("gu", 50, 57344, 8192) == llama.W4_PLAN["gu"][64]
+    assert llama.w4_cfg("qkv", 50, 10240, 8192) == (2, 8, 4)   # the wide (70B) entries
+    assert llama.w4_cfg("o", 50, 8192, 8192) == (4, 2, 0)
+    assert llama.w4_cfg("qkv", 50, 6144, 4096) == (2, 4, 4)
+    assert llama.w4_cfg("down", 50, 8192, 28672) == llama.W4_PLAN["down"][64]
