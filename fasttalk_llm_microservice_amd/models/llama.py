@@ -610,8 +610,11 @@ class LlamaModel:
         instead of dequantizing every layer's weight into a scratch and calling
         hipBLASLt on every mixed step (15 GB written and read again per step for an
         8B model).  Decode steps keep streaming the int4 image.  FT_W4_PREFILL_IMAGE:
-        auto (default: when the bf16 image is <= 15% of device memory -- 8B: 14 GB of
-        288; 70B at TP=1 is not), 1, 0."""
+        auto (default: when a quarter of device memory stays free for the KV cache
+        after the bf16 image -- 8B: 14 GB of 288; 70B at TP=1: 140 GB next to 35 GB of
+        int4, 50 sessions 1,006 -> 1,386 tok/s, p50 TTFT 449 -> 165 ms,
+        profiles/bench_70b_awq_image_s50_r06.log), 1, 0 (int4 only: the least memory,
+        prefill-size steps dequantize per projection)."""
         mode = os.environ.get("FT_W4_PREFILL_IMAGE", "auto")
         if self.quant is None or mode == "0" or self.device.type != "cuda" or not self.layers:
             return
@@ -620,8 +623,8 @@ class LlamaModel:
             return
         nbytes = sum(q.n * q.k * 2 for _, _, q in qs)
         if mode != "1":
-            _, total = torch.cuda.mem_get_info(self.device)
-            if nbytes > 0.15 * total:
+            free, total = torch.cuda.mem_get_info(self.device)
+            if free - nbytes < 0.25 * total:
                 return
         for L, p, q in qs:
             dense = self._w4_prefill_dense(p, Q.w4_dequant(q))
