@@ -166,6 +166,9 @@ def main():
     ap.add_argument("--device", default="cuda", help="cpu runs the same path over gloo (tests)")
     ap.add_argument("--quant", default="", choices=["", "w4", "awq"],
                     help="W4A16 layer weights (the reference's AWQ-INT4 model); default bf16")
+    ap.add_argument("--kv-cache-dtype", default="auto", choices=["auto", "fp8"],
+                    help="KV-cache storage (ENGINE_KV_CACHE_DTYPE): auto = bf16 (the headline), fp8 = "
+                         "e4m3 at scale 1 (vLLM's --kv-cache-dtype fp8); reported in the JSON")
     ap.add_argument("--serve", choices=["door", "rank"], default="door",
                     help="DP topology: 'door' (default) = the shipping ENGINE_DP_SIZE service: every "
                          "rank is a service worker behind ONE port whose front door (rank 0, "
@@ -183,6 +186,8 @@ def main():
         raise SystemExit(f"bench: --gpus {a.gpus} but WORLD_SIZE={os.environ['WORLD_SIZE']}")
     if a.quant:
         os.environ["ENGINE_QUANTIZATION"] = a.quant
+    if a.kv_cache_dtype != "auto":
+        os.environ["ENGINE_KV_CACHE_DTYPE"] = a.kv_cache_dtype
     if a.agent_tools >= 0:
         os.environ["AGENT_GUIDED_TOOL_CALLS"] = "true"
         os.environ.setdefault("WEB_SEARCH_BACKEND", "stub")
@@ -428,6 +433,7 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": ("w4a16 (bf16 compute)" if a.quant else "bf16") if not cpu else "fp32",
+            "kv_cache_dtype": "fp8 (e4m3)" if a.kv_cache_dtype == "fp8" else "same as dtype",
             "data": f"synthetic (random-init {mlabel} weights, synthetic English prompts, "
                     "synthetic Llama-3 tokenizer)",
             # which GPUs the ranks ran on and over what: an N-GPU record shows by itself
@@ -664,6 +670,7 @@ def bench_tp(a, rank: int, world: int, local_rank: int):
         "warmup": a.warmup, "ms_per_step": round(1e3 * elapsed / a.steps, 2),
         "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
         "dtype": ("w4a16 (bf16 compute)" if a.quant else "bf16") if a.device == "cuda" else "fp32",
+        "kv_cache_dtype": "fp8 (e4m3)" if a.kv_cache_dtype == "fp8" else "same as dtype",
         "data": "synthetic (random-init weights, synthetic English prompts, synthetic Llama-3 tokenizer)",
         "config": {"model": a.model, "global_batch": a.sessions,
                    "seq_len": ctx["ctx_mean"], "ctx_mean": ctx["ctx_mean"], "ctx_max": ctx["ctx_max"],

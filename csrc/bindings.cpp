@@ -16,7 +16,7 @@ int ft_fused_add_rmsnorm(void* out, const void* x, void* residual, const void* w
 int ft_silu_mul(void* out, const void* gu, int rows, int inter, int il, hipStream_t stream);
 int ft_rope_kv_write(void* qkv, int qkv_stride, const int* positions, const float* cos_sin,
                      const int* slot_mapping, void* k_cache, void* v_cache, int tokens, int nq,
-                     int nkv, int head_dim, int block_size, int cos_rows, int num_slots,
+                     int nkv, int head_dim, int block_size, int cos_rows, int num_slots, int kv8,
                      hipStream_t stream);
 int ft_decode_waves();
 int ft_decode_max_batch();
@@ -25,7 +25,7 @@ int ft_paged_decode_attention(void* out, int out_stride, float* tmp_out, float* 
                               const void* v_cache, const int* block_tables, int bt_stride,
                               const int* seq_lens, int batch, int nq, int nkv, int head_dim,
                               int block_size, float scale, int* counters, int piece,
-                              int slot_cap, int num_blocks, hipStream_t stream);
+                              int slot_cap, int num_blocks, int kv8, hipStream_t stream);
 int ft_prefill_tile_tokens(int nq, int nkv);
 int ft_prefill_attention(void* out, int out_stride, const void* q, int q_stride,
                          const void* k_cache, const void* v_cache, const int* block_tables,
@@ -33,7 +33,7 @@ int ft_prefill_attention(void* out, int out_stride, const void* q, int q_stride,
                          const int* tile_info, int num_tiles, int nq, int nkv, int head_dim,
                          int block_size, float scale, float* part_o, float* part_ml,
                          const int* combine, int num_combine, int invariant, int num_blocks,
-                         hipStream_t stream);
+                         int kv8, hipStream_t stream);
 int ft_sample(int* out_tokens, const void* logits, int logits_is_bf16, long logit_stride,
               int batch, int vocab, const float* temperature, const float* top_p,
               const int* top_k, const long long* seeds, const int* steps,
@@ -102,7 +102,7 @@ int ft_slab_rope_kv(const float* ws, int splits, int rows, int cols, void* q_out
                     const int* positions, const float* cos_sin, const int* slot_mapping,
                     void* k_cache, void* v_cache, int nq, int nkv, int head_dim, int block_size,
                     const void* residual, int hidden, float eps, int cos_rows, int num_slots,
-                    hipStream_t stream);
+                    int kv8, hipStream_t stream);
 }
 
 namespace {
@@ -132,16 +132,22 @@ void check_rows(const at::Tensor& t, const char* name) {
 // KV caches: K [blocks, nkv, block_size, D] (token rows), V [blocks, nkv, D,
 // block_size] (transposed, rope_kv.hip); a mismatched V layout would be read as
 // garbage by the attention kernels, so every op touching the caches checks both
-void check_kv_caches(const at::Tensor& k_cache, const at::Tensor& v_cache, int64_t nkv,
+// returns true for fp8 (e4m3) caches, false for bf16
+bool check_kv_caches(const at::Tensor& k_cache, const at::Tensor& v_cache, int64_t nkv,
                      int64_t head_dim) {
-  check_bf16(k_cache, "k_cache");
-  check_bf16(v_cache, "v_cache");
+  check_dev(k_cache, "k_cache");
+  check_dev(v_cache, "v_cache");
+  const bool kv8 = k_cache.scalar_type() == at::kFloat8_e4m3fn;
+  TORCH_CHECK(kv8 || k_cache.scalar_type() == at::kBFloat16, "KV caches must be bfloat16 or float8_e4m3fn");
+  TORCH_CHECK(v_cache.scalar_type() == k_cache.scalar_type(), "K and V caches must share a dtype");
+  TORCH_CHECK(!kv8 || k_cache.size(2) >= 16, "fp8 KV caches need block_size >= 16");
   TORCH_CHECK(k_cache.is_contiguous() && v_cache.is_contiguous(), "KV caches must be contiguous");
   TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(1) == nkv && k_cache.size(3) == head_dim,
               "k_cache must be [blocks, nkv, block_size, head_dim]");
   TORCH_CHECK(v_cache.dim() == 4 && v_cache.size(0) == k_cache.size(0) && v_cache.size(1) == nkv &&
                   v_cache.size(2) == head_dim && v_cache.size(3) == k_cache.size(2),
               "v_cache must be [blocks, nkv, head_dim, block_size] (transposed V blocks)");
+  return kv8;
 }
 
 void rmsnorm(at::Tensor out, at::Tensor x, at::Tensor w, double eps) {
@@ -198,7 +204,7 @@ void rope_kv_write(at::Tensor qkv, at::Tensor positions, at::Tensor cos_sin,
   TORCH_CHECK(cos_sin.scalar_type() == at::kFloat && cos_sin.is_contiguous() &&
                   cos_sin.size(1) == head_dim,
               "cos_sin must be fp32 [max_pos, head_dim]");
-  check_kv_caches(k_cache, v_cache, nkv, head_dim);
+  const bool kv8 = check_kv_caches(k_cache, v_cache, nkv, head_dim);
   TORCH_CHECK(qkv.size(1) >= (nq + 2 * nkv) * head_dim, "qkv width");
   const int tokens = (int)qkv.size(0);
   TORCH_CHECK(positions.numel() >= tokens && slot_mapping.numel() >= tokens, "metadata length");
@@ -206,7 +212,7 @@ void rope_kv_write(at::Tensor qkv, at::Tensor positions, at::Tensor cos_sin,
                             cos_sin.data_ptr<float>(), slot_mapping.data_ptr<int>(),
                             k_cache.data_ptr(), v_cache.data_ptr(), tokens, (int)nq, (int)nkv,
                             (int)head_dim, (int)k_cache.size(2), (int)cos_sin.size(0),
-                            (int)(k_cache.size(0) * k_cache.size(2)), cur_stream()),
+                            (int)(k_cache.size(0) * k_cache.size(2)), kv8 ? 1 : 0, cur_stream()),
            "rope_kv_write");
 }
 
@@ -218,7 +224,7 @@ void paged_decode_attention(at::Tensor out, at::Tensor q, at::Tensor k_cache, at
   check_bf16(q, "q");
   check_rows(out, "out");
   check_rows(q, "q");
-  check_kv_caches(k_cache, v_cache, nkv, head_dim);
+  const bool kv8 = check_kv_caches(k_cache, v_cache, nkv, head_dim);
   check_i32(block_tables, "block_tables");
   check_i32(seq_lens, "seq_lens");
   const int batch = (int)q.size(0);
@@ -253,7 +259,7 @@ void paged_decode_attention(at::Tensor out, at::Tensor q, at::Tensor k_cache, at
                                      seq_lens.data_ptr<int>(), batch, (int)nq, (int)nkv,
                                      (int)head_dim, (int)k_cache.size(2), (float)scale, cnt,
                                      (int)piece, (int)std::min<int64_t>(slot_cap, INT32_MAX),
-                                     (int)k_cache.size(0),
+                                     (int)k_cache.size(0), kv8 ? 1 : 0,
                                      cur_stream()),
            "paged_decode_attention");
 }
@@ -268,7 +274,7 @@ void prefill_attention(at::Tensor out, at::Tensor q, at::Tensor k_cache, at::Ten
   check_bf16(q, "q");
   check_rows(out, "out");
   check_rows(q, "q");
-  check_kv_caches(k_cache, v_cache, nkv, head_dim);
+  const bool kv8 = check_kv_caches(k_cache, v_cache, nkv, head_dim);
   check_i32(block_tables, "block_tables");
   check_i32(seq_lens, "seq_lens");
   check_i32(q_start_loc, "q_start_loc");
@@ -302,7 +308,8 @@ void prefill_attention(at::Tensor out, at::Tensor q, at::Tensor k_cache, at::Ten
                                 seq_lens.data_ptr<int>(), q_start_loc.data_ptr<int>(),
                                 tile_info.data_ptr<int>(), (int)num_tiles, (int)nq, (int)nkv,
                                 (int)head_dim, (int)k_cache.size(2), (float)scale, po, pml, cb,
-                                (int)num_combine, (int)invariant, (int)k_cache.size(0), cur_stream()),
+                                (int)num_combine, (int)invariant, (int)k_cache.size(0), kv8 ? 1 : 0,
+                                cur_stream()),
            "prefill_attention");
 }
 
@@ -350,12 +357,17 @@ void sample(at::Tensor out_tokens, at::Tensor logits, at::Tensor temperature, at
 }
 
 void kv_block_copy(at::Tensor k_cache, at::Tensor v_cache, at::Tensor src_dst) {
-  check_bf16(k_cache, "k_cache");
-  check_bf16(v_cache, "v_cache");
+  check_dev(k_cache, "k_cache");
+  check_dev(v_cache, "v_cache");
+  TORCH_CHECK(k_cache.scalar_type() == v_cache.scalar_type() &&
+                  (k_cache.scalar_type() == at::kBFloat16 || k_cache.scalar_type() == at::kFloat8_e4m3fn),
+              "KV caches bfloat16 or float8_e4m3fn");
   check_i32(src_dst, "src_dst");
   TORCH_CHECK(k_cache.is_contiguous() && v_cache.is_contiguous(), "caches contiguous");
-  const long block_elems = (long)(k_cache.numel() / k_cache.size(0));
-  TORCH_CHECK(block_elems % 8 == 0, "block size");
+  // the kernel copies 16-B words; it counts a block in 2-byte units
+  const long block_bytes = (long)(k_cache.numel() / k_cache.size(0)) * (long)k_cache.element_size();
+  TORCH_CHECK(block_bytes % 16 == 0, "block size");
+  const long block_elems = block_bytes / 2;
   check_rc(ft_kv_block_copy(k_cache.data_ptr(), v_cache.data_ptr(), src_dst.data_ptr<int>(),
                             (int)(src_dst.numel() / 2), block_elems, (int)k_cache.size(0),
                             cur_stream()),
@@ -370,12 +382,17 @@ void kv_swap(at::Tensor ptrs, at::Tensor ids, at::Tensor staging, int64_t block_
   check_dev(ptrs, "ptrs");
   TORCH_CHECK(ptrs.scalar_type() == at::kLong && ptrs.is_contiguous(), "ptrs int64");
   check_i32(ids, "ids");
-  check_bf16(staging, "staging");
+  check_dev(staging, "staging");
+  TORCH_CHECK(staging.scalar_type() == at::kBFloat16 || staging.scalar_type() == at::kFloat8_e4m3fn,
+              "staging in the caches' dtype (bfloat16 or float8_e4m3fn)");
   TORCH_CHECK(staging.is_contiguous(), "staging contiguous");
   const int n = (int)ids.numel();
   TORCH_CHECK(staging.numel() >= (int64_t)n * ptrs.numel() * block_elems, "staging too small");
+  // the kernel moves 16-B words and counts a block in 2-byte units
+  const int64_t block_bytes = block_elems * (int64_t)staging.element_size();
+  TORCH_CHECK(block_bytes % 16 == 0, "block bytes must be a multiple of 16");
   check_rc(ft_kv_swap(reinterpret_cast<const uint64_t*>(ptrs.data_ptr<int64_t>()),
-                      (int)ptrs.numel(), ids.data_ptr<int>(), n, staging.data_ptr(), block_elems,
+                      (int)ptrs.numel(), ids.data_ptr<int>(), n, staging.data_ptr(), block_bytes / 2,
                       to_staging ? 1 : 0, (int)num_blocks, cur_stream()),
            "kv_swap");
 }
@@ -845,7 +862,7 @@ void slab_rope_kv(at::Tensor ws, int64_t splits, int64_t rows, int64_t cols, at:
   TORCH_CHECK(cols == (nq + 2 * nkv) * head_dim, "cols");
   TORCH_CHECK(q_out.size(0) >= rows && q_out.size(1) >= nq * head_dim, "q_out shape");
   TORCH_CHECK(cos_sin.scalar_type() == at::kFloat && cos_sin.size(1) == head_dim, "cos_sin");
-  check_kv_caches(k_cache, v_cache, nkv, head_dim);
+  const bool kv8 = check_kv_caches(k_cache, v_cache, nkv, head_dim);
   TORCH_CHECK(positions.numel() >= rows && slot_mapping.numel() >= rows, "metadata length");
   check_rc(ft_slab_rope_kv(ws.data_ptr<float>(), (int)splits, (int)rows, (int)cols,
                            q_out.data_ptr(), (int)q_out.stride(0), positions.data_ptr<int>(),
@@ -853,7 +870,7 @@ void slab_rope_kv(at::Tensor ws, int64_t splits, int64_t rows, int64_t cols, at:
                            k_cache.data_ptr(), v_cache.data_ptr(), (int)nq, (int)nkv,
                            (int)head_dim, (int)k_cache.size(2), rp, hidden, (float)eps,
                            (int)cos_sin.size(0), (int)(k_cache.size(0) * k_cache.size(2)),
-                           cur_stream()), "slab_rope_kv");
+                           kv8 ? 1 : 0, cur_stream()), "slab_rope_kv");
 }
 
 #if defined(FT_KERNEL_CHECKS) && FT_KERNEL_CHECKS

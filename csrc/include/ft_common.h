@@ -60,6 +60,42 @@ __device__ __forceinline__ uint4 store8(const float (&f)[8]) {
   return v;
 }
 
+// fp8 KV cache (OCP e4m3, torch.float8_e4m3fn; ENGINE_KV_CACHE_DTYPE=fp8).  Stored
+// value = x at a per-tensor scale of 1 (vLLM's uncalibrated default), clamped to the
+// format's +-448 first: gfx950's v_cvt_pk_fp8_f32 turns an out-of-range value into
+// NaN, not the max (bench/probes/fp8_cvt_check.py, measured).  Reads widen straight
+// to bf16 MFMA operands with v_cvt_scalef32_pk_bf16_fp8 (2 values per op; its scale
+// operand is exact for powers of two only -- probe -- so it stays 1).
+constexpr float kFp8Max = 448.f;
+
+__device__ __forceinline__ uint32_t fp8x4_pack(float a, float b, float c, float d) {
+  a = fminf(fmaxf(a, -kFp8Max), kFp8Max);
+  b = fminf(fmaxf(b, -kFp8Max), kFp8Max);
+  c = fminf(fmaxf(c, -kFp8Max), kFp8Max);
+  d = fminf(fmaxf(d, -kFp8Max), kFp8Max);
+  int w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+  w = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);
+  return (uint32_t)w;
+}
+
+// 8 fp32 -> 8 fp8 (low element first)
+__device__ __forceinline__ uint2 fp8x8_pack(const float (&f)[8]) {
+  return make_uint2(fp8x4_pack(f[0], f[1], f[2], f[3]), fp8x4_pack(f[4], f[5], f[6], f[7]));
+}
+
+// 4 fp8 (one word, low byte first) -> 4 bf16 (two words)
+__device__ __forceinline__ uint2 fp8x4_to_bf16(uint32_t w) {
+  const ft_bf16x2_t lo = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w, 1.f, false);
+  const ft_bf16x2_t hi = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w, 1.f, true);
+  return make_uint2(__builtin_bit_cast(uint32_t, lo), __builtin_bit_cast(uint32_t, hi));
+}
+
+// 8 fp8 -> 8 bf16 (a 16-B MFMA fragment)
+__device__ __forceinline__ uint4 fp8x8_to_bf16(uint32_t w0, uint32_t w1) {
+  const uint2 a = fp8x4_to_bf16(w0), b = fp8x4_to_bf16(w1);
+  return make_uint4(a.x, a.y, b.x, b.y);
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -46,6 +46,8 @@
 
 #include <stdlib.h>
 
+#include <type_traits>
+
 namespace ft {
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
@@ -127,6 +129,34 @@ __device__ __forceinline__ void mt_load(MTile<D>& t, const uint16_t* __restrict_
 #pragma unroll
   for (int nd = 0; nd < D / 16; ++nd)
     t.v[nd] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(vr, voff_b, nd * vstep_b, 2));
+}
+
+// fp8 (e4m3) tile (KV8): 1-byte K rows and V^T rows.  Lane (g, n) loads 16
+// consecutive dims of K row n per 64-dim pair of k-steps (dims 64 p + 16 g + [0, 16):
+// the first 8 feed k-step 2p, the next 8 k-step 2p+1 -- the Q fragments use the same
+// dim permutation, so S is unchanged) and 4 tokens of each V^T dim row; both widen
+// to bf16 fragments in registers (ft_common.h fp8x8_to_bf16).  Half the bytes of
+// the bf16 tile per token.
+template <int D>
+struct MTile8 {
+  uint4 k[D / 64];
+  uint32_t v[D / 16];
+};
+
+template <int D>
+__device__ __forceinline__ void mt_load8(MTile8<D>& t, const uint8_t* __restrict__ k_cache,
+                                         const uint8_t* __restrict__ v_cache, size_t kbase,
+                                         size_t vbase, int koff_b, int voff_b, int vstep_b) {
+  const __amdgpu_buffer_rsrc_t kr = __builtin_amdgcn_make_buffer_rsrc(
+      uniform_ptr(k_cache + kbase), 0, 16 * D, 0x00020000);
+  const __amdgpu_buffer_rsrc_t vr = __builtin_amdgcn_make_buffer_rsrc(
+      uniform_ptr(v_cache + vbase), 0, 0x7fffffff, 0x00020000);
+#pragma unroll
+  for (int p = 0; p < D / 64; ++p)
+    t.k[p] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(kr, koff_b + p * 64, 0, 2));
+#pragma unroll
+  for (int nd = 0; nd < D / 16; ++nd)
+    t.v[nd] = __builtin_amdgcn_raw_buffer_load_b32(vr, voff_b, nd * vstep_b, 2);
 }
 
 // End of a wave's piece of segment (b, h): the whole segment -> bf16 output;
@@ -251,7 +281,7 @@ __device__ __forceinline__ void dec_finish(floatx4_t (&o)[ND], float l_run, floa
   }
 }
 
-template <int D, int G, int R, bool FC, int WPC, bool PIECE = false>
+template <int D, int G, int R, bool FC, int WPC, bool PIECE = false, bool KV8 = false>
 __global__ __launch_bounds__(256, WPC) void paged_decode_kernel(
     uint16_t* __restrict__ out, int out_stride, float* __restrict__ tmp_out,
     float* __restrict__ tmp_ml, const uint16_t* __restrict__ q, int q_stride,
@@ -291,10 +321,13 @@ __global__ __launch_bounds__(256, WPC) void paged_decode_kernel(
   const int bsz = 1 << bs_shift;
   const int bmask = bsz - 1;
   const size_t blk_stride = (size_t)nkv * bsz * D;
-  // per-lane offsets inside a 16-token tile
-  const int koff_b = 2 * (n * D + 8 * g);     // bytes: K row n, dims 8g.. (+32 kc)
-  const int voff_b = 2 * (n * bsz + 4 * g);   // bytes: V^T row n (+16 nd), tokens 4g..4g+3
-  const int vstep_b = 2 * 16 * bsz;           // bytes between the V^T dim tiles
+  // per-lane offsets inside a 16-token tile (element size EB)
+  constexpr int EB = KV8 ? 1 : 2;
+  // bytes: K row n, dims 8g.. (+32 kc); fp8: dims 16g.. (+64 p)
+  const int koff_b = KV8 ? (n * D + 16 * g) : 2 * (n * D + 8 * g);
+  const int voff_b = EB * (n * bsz + 4 * g);   // bytes: V^T row n (+16 nd), tokens 4g..4g+3
+  const int vstep_b = EB * 16 * bsz;           // bytes between the V^T dim tiles
+  using Tile = typename std::conditional<KV8, MTile8<D>, MTile<D>>::type;
 
   // tiles [t0, t0 + cnt) of segment (b, h), then dec_finish
   auto run = [&](int b, int h, int t0, int cnt, int nb, bool whole, int slot_i, int first, int np) {
@@ -303,10 +336,12 @@ __global__ __launch_bounds__(256, WPC) void paged_decode_kernel(
     // Q^T fragments (B operand): lane (g, n) = head n of this kv head, dims 8g.. (+32 kc)
     uint4 qb[KC];
 #pragma unroll
-    for (int kc = 0; kc < KC; ++kc)
-      qb[kc] = n < G ? *reinterpret_cast<const uint4*>(q + (size_t)b * q_stride +
-                                                       (h * G + n) * D + kc * 32 + 8 * g)
+    for (int kc = 0; kc < KC; ++kc) {
+      // fp8 tiles: k-step kc covers dims 64 (kc / 2) + 16 g + 8 (kc & 1) (MTile8)
+      const int d0 = KV8 ? 64 * (kc >> 1) + 16 * g + 8 * (kc & 1) : kc * 32 + 8 * g;
+      qb[kc] = n < G ? *reinterpret_cast<const uint4*>(q + (size_t)b * q_stride + (h * G + n) * D + d0)
                      : make_uint4(0, 0, 0, 0);
+    }
     floatx4_t o[ND];
 #pragma unroll
     for (int nd = 0; nd < ND; ++nd) o[nd] = floatx4_t{0.f, 0.f, 0.f, 0.f};
@@ -324,20 +359,32 @@ __global__ __launch_bounds__(256, WPC) void paged_decode_kernel(
         my_blk = FT_CHECK_IDX(bt[tok >> bs_shift], num_blocks, kCkBlockTable, b);
         my_off = tok & bmask;
       }
-      auto ld = [&](MTile<D>& t, int i) {
+      auto ld = [&](Tile& t, int i) {
         const int j = min(i, cc - 1);  // past the end: re-load the last tile (never consumed)
         const size_t blk = (size_t)(uint32_t)__builtin_amdgcn_readlane(my_blk, j);
         const int off = __builtin_amdgcn_readlane(my_off, j);
         const size_t hb = blk * blk_stride + (size_t)h * bsz * D;
-        mt_load<D>(t, k_cache, v_cache, hb + (size_t)off * D, hb + off, koff_b, voff_b, vstep_b);
+        if constexpr (KV8)
+          mt_load8<D>(t, reinterpret_cast<const uint8_t*>(k_cache), reinterpret_cast<const uint8_t*>(v_cache),
+                      hb + (size_t)off * D, hb + off, koff_b, voff_b, vstep_b);
+        else
+          mt_load<D>(t, k_cache, v_cache, hb + (size_t)off * D, hb + off, koff_b, voff_b, vstep_b);
       };
-      auto consume = [&](MTile<D>& t, int i) {
+      auto consume = [&](Tile& t, int i) {
         const int valid = L - ((t0 + c0 + i) << 4);   // tokens of this tile inside the sequence
         floatx4_t s = floatx4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int kc = 0; kc < KC; ++kc)
-          s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, t.k[kc]),
+        for (int kc = 0; kc < KC; ++kc) {
+          uint4 kf;
+          if constexpr (KV8) {
+            const uint4& w = t.k[kc >> 1];
+            kf = (kc & 1) ? fp8x8_to_bf16(w.z, w.w) : fp8x8_to_bf16(w.x, w.y);
+          } else {
+            kf = t.k[kc];
+          }
+          s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, kf),
                                                       __builtin_bit_cast(bf16x8_t, qb[kc]), s, 0, 0, 0);
+        }
         // only a sequence's last tile can be partial: a wave-uniform branch, so full
         // tiles carry no mask compares / selects
         if (valid < 16) {
@@ -373,11 +420,15 @@ __global__ __launch_bounds__(256, WPC) void paged_decode_kernel(
         const u32x2_t pw = {pack2(p[0], p[1]), pack2(p[2], p[3])};   // 2 x v_cvt_pk_bf16_f32
         const short4_t pa = __builtin_bit_cast(short4_t, pw);
 #pragma unroll
-        for (int nd = 0; nd < ND; ++nd)
-          o[nd] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(pa, __builtin_bit_cast(short4_t, t.v[nd]),
+        for (int nd = 0; nd < ND; ++nd) {
+          uint2 vf;
+          if constexpr (KV8) vf = fp8x4_to_bf16(t.v[nd]);
+          else vf = t.v[nd];
+          o[nd] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(pa, __builtin_bit_cast(short4_t, vf),
                                                            o[nd], 0, 0, 0);
+        }
       };
-      MTile<D> ring[R];
+      Tile ring[R];
 #pragma unroll
       for (int r = 0; r + 1 < R; ++r) ld(ring[r], r);
       for (int i = 0; i < cc; i += R) {
@@ -541,7 +592,7 @@ extern "C" int ft_paged_decode_attention(void* out, int out_stride, float* tmp_o
                                          int bt_stride, const int* seq_lens, int batch, int nq,
                                          int nkv, int head_dim, int block_size, float scale,
                                          int* counters, int piece, int slot_cap,
-                                         int num_blocks, hipStream_t stream) {
+                                         int num_blocks, int kv8, hipStream_t stream) {
   if (batch <= 0) return 0;
   if (nq % nkv != 0) return -1;
   if (piece < 0 || (piece > 0 && counters == nullptr)) return -6;  // pieces merge in-launch
@@ -574,6 +625,12 @@ extern "C" int ft_paged_decode_attention(void* out, int out_stride, float* tmp_o
     const int v = e ? atoi(e) : 2;
     return (v == 1 || v == 2 || v == 4) ? v : 2;
   }();
+  // fp8 tiles carry half the bytes: ring depth of the fp8 path (FT_DECODE_RING8, 2 / 3)
+  static const int ring8 = [] {
+    const char* e = getenv("FT_DECODE_RING8");
+    const int r = e ? atoi(e) : 3;
+    return (r == 2 || r == 3) ? r : 3;
+  }();
   int nwg = 0;
 #define FT_DEC_ARGS                                                                             \
   (uint16_t*)out, out_stride, tmp_out, tmp_ml, (const uint16_t*)q, q_stride, (uint16_t*)k_cache, \
@@ -589,6 +646,26 @@ extern "C" int ft_paged_decode_attention(void* out, int out_stride, float* tmp_o
 #define FT_DEC_CASE(DD, GG, RR)                                                                \
   if (head_dim == DD && G == GG) {                                                             \
     nwg = ft_num_cus() * wpc;                                                                  \
+    if (kv8) {  /* fp8 caches: one workgroup per CU, ring8 tiles deep */                       \
+      nwg = ft_num_cus();                                                                      \
+      if (piece > 0)                                                                           \
+        hipLaunchKernelGGL((ft::paged_decode_kernel<DD, GG, 2, true, 1, true, true>), dim3(nwg), \
+                           dim3(256), 0, stream, FT_DEC_ARGS);                                 \
+      else if (counters != nullptr && ring8 == 3)                                              \
+        hipLaunchKernelGGL((ft::paged_decode_kernel<DD, GG, 3, true, 1, false, true>), dim3(nwg), \
+                           dim3(64 * nwv), 0, stream, FT_DEC_ARGS);                            \
+      else if (counters != nullptr)                                                            \
+        hipLaunchKernelGGL((ft::paged_decode_kernel<DD, GG, 2, true, 1, false, true>), dim3(nwg), \
+                           dim3(64 * nwv), 0, stream, FT_DEC_ARGS);                            \
+      else {                                                                                   \
+        hipLaunchKernelGGL((ft::paged_decode_kernel<DD, GG, 2, false, 1, false, true>), dim3(nwg), \
+                           dim3(64 * nwv), 0, stream, FT_DEC_ARGS);                            \
+        hipLaunchKernelGGL((ft::paged_decode_combine_kernel<DD, GG>), dim3(batch * nkv), dim3(256),\
+                           0, stream, (uint16_t*)out, out_stride, tmp_out, tmp_ml, seq_lens, batch,\
+                           nkv, nwg * nwv, min_tiles);                                         \
+      }                                                                                        \
+      return static_cast<int>(hipGetLastError());                                              \
+    }                                                                                          \
     if (piece > 0) {                                                                           \
       nwg = ft_num_cus();                                                                      \
       hipLaunchKernelGGL((ft::paged_decode_kernel<DD, GG, 2, true, 1, true>), dim3(nwg),      \
@@ -605,8 +682,8 @@ extern "C" int ft_paged_decode_attention(void* out, int out_stride, float* tmp_o
   }
   // ring 2 at one workgroup per CU: full kernel 86 vs 92 us (ring 3) at 50 x 1.5-3k,
   // 125 vs 128 us at 50 x 2.2-4.5k (bench/attn_diag.py, profiles/attn_decode_w1_r02.log)
-  if (ring == 3) { FT_DEC_CASE(128, 4, 3) }
-  if (ring == 4) { FT_DEC_CASE(128, 4, 4) }
+  if (ring == 3 && !kv8) { FT_DEC_CASE(128, 4, 3) }
+  if (ring == 4 && !kv8) { FT_DEC_CASE(128, 4, 4) }
   FT_DEC_CASE(128, 1, 2)
   FT_DEC_CASE(128, 2, 2)
   FT_DEC_CASE(128, 3, 2)

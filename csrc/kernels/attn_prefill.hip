@@ -62,7 +62,14 @@ __device__ __forceinline__ float kgroup_sum(float v) { return kgroups_sum(v); }
 // INV (batch-invariant mode): the deferred rescale is decided per query row (lane)
 // instead of wave-wide, so a row's rounding never depends on the rows that share its
 // wave -- which change with chunking and prefix-cache hits.
-template <int D, int G, bool INV>
+//
+// KV8 (fp8 e4m3 caches): the LDS images stay bf16 -- the same swizzled layouts, so
+// tile_math is unchanged -- but they are filled through registers: every thread
+// loads one 16-B piece of fp8 K rows and one of V^T rows (16 elements each), widens
+// them to bf16 (ft_common.h fp8x8_to_bf16) and writes two 16-B chunks at their
+// swizzled slots.  Two tiles are in flight in registers (loaded two iterations ahead)
+// over two LDS slots; one barrier per tile.
+template <int D, int G, bool INV, bool KV8 = false>
 __global__ __launch_bounds__(512, 1) void prefill_attn_kernel(
     uint16_t* __restrict__ out, int out_stride, const uint16_t* __restrict__ q, int q_stride,
     const uint16_t* __restrict__ k_cache, const uint16_t* __restrict__ v_cache,
@@ -79,7 +86,7 @@ __global__ __launch_bounds__(512, 1) void prefill_attn_kernel(
   constexpr int SWZ = (NCH >= 16) ? 15 : (NCH - 1);
 
   // one LDS array (guide §5 item 4a): [NSLOT slots][K image | V^T image], then the table
-  constexpr int NSLOT = 4;
+  constexpr int NSLOT = KV8 ? 2 : 4;
   constexpr int KIMG = kPrefillBK * D, VIMG = D * kPrefillBK;   // bf16 elements
   constexpr int SLOT = KIMG + VIMG;
   __shared__ __attribute__((aligned(16))) uint16_t smem[NSLOT * SLOT + 2 * kPrefillMaxBlocks];
@@ -342,6 +349,63 @@ __global__ __launch_bounds__(512, 1) void prefill_attn_kernel(
     s_bt[i] = FT_CHECK_IDX(bt[i], num_blocks, kCkBlockTable, b);
   __syncthreads();
 
+  if constexpr (KV8) {
+    // ---- fp8 caches: register-staged tiles (see the comment above the kernel) ----
+    constexpr int NP = kPrefillBK * D / 16;   // 16-B fp8 pieces per image (K and V^T alike)
+    constexpr int KPR = D / 16;               // K pieces per row
+    const int tid = threadIdx.x;
+    const uint8_t* k8 = reinterpret_cast<const uint8_t*>(k_cache);
+    const uint8_t* v8 = reinterpret_cast<const uint8_t*>(v_cache);
+    auto load8t = [&](int kt, uint4& kr, uint4& vr) {
+      const int kbase = kt * kPrefillBK;
+      if (tid < NP) {
+        const int t = tid / KPR, j = tid - (tid / KPR) * KPR;
+        const int tok = min(kbase + t, kv_end - 1);   // past kv_end: a valid row (masked)
+        kr = *reinterpret_cast<const uint4*>(k8 + (size_t)s_bt[tok >> bs_shift] * blk_stride + head_off +
+                                             (size_t)(tok & bmask) * D + 16 * j);
+        const int d = tid >> 2, c = tid & 3;          // V^T: dim d, tokens 16 c .. 16 c + 15
+        const int p = min(kbase + 16 * c, (kv_end - 1) & ~15);
+        vr = *reinterpret_cast<const uint4*>(v8 + (size_t)s_bt[p >> bs_shift] * blk_stride + head_off +
+                                             (size_t)d * block_size + (p & bmask));
+      }
+    };
+    auto store8t = [&](int slot, const uint4& kr, const uint4& vr) {
+      if (tid < NP) {
+        const uint32_t kimg = lds0 + slot * SLOT * 2, vimg = kimg + KIMG * 2;
+        const int t = tid / KPR, j = tid - (tid / KPR) * KPR;
+        const uint32_t kr0 = kimg + t * D * 2;
+        ds_write16(kr0 + (((2 * j) ^ (t & SWZ)) << 4), fp8x8_to_bf16(kr.x, kr.y));
+        ds_write16(kr0 + (((2 * j + 1) ^ (t & SWZ)) << 4), fp8x8_to_bf16(kr.z, kr.w));
+        const int d = tid >> 2, c = tid & 3, sw = (d >> 1) & 7;
+        const uint32_t vr0 = vimg + d * kPrefillBK * 2;
+        ds_write16(vr0 + (((2 * c) ^ sw) << 4), fp8x8_to_bf16(vr.x, vr.y));
+        ds_write16(vr0 + (((2 * c + 1) ^ sw) << 4), fp8x8_to_bf16(vr.z, vr.w));
+      }
+    };
+    uint4 kr0 = make_uint4(0, 0, 0, 0), vr0 = kr0, kr1 = kr0, vr1 = kr0;
+    // register set (kt - kt_lo) & 1 holds tile kt; LDS slot kt & 1
+    if (kt_lo < ntiles) load8t(kt_lo, kr0, vr0);
+    if (kt_lo + 1 < ntiles) load8t(kt_lo + 1, kr1, vr1);
+    if (kt_lo < ntiles) store8t(kt_lo & 1, kr0, vr0);
+    if (kt_lo + 2 < ntiles) load8t(kt_lo + 2, kr0, vr0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    // one tile: math on slot kt & 1, then the next tile (registers `kn`, `vn`) into the
+    // other slot -- last read at tile kt - 1, before the previous barrier -- and the
+    // tile after next into the registers just freed
+    auto step = [&](int kt, uint4& kn, uint4& vn) {
+      kb = lds0 + (kt & 1) * SLOT * 2;
+      tile_math(kt);
+      if (kt + 1 < ntiles) store8t((kt + 1) & 1, kn, vn);
+      if (kt + 3 < ntiles) load8t(kt + 3, kn, vn);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    };
+    for (int kt = kt_lo; kt < ntiles; kt += 2) {
+      step(kt, kr1, vr1);
+      if (kt + 1 < ntiles) step(kt + 1, kr0, vr0);
+    }
+  } else {
 #pragma unroll
   for (int t = 0; t < NSLOT - 1; ++t)
     if (kt_lo + t < ntiles) issue_tile(kt_lo + t, (kt_lo + t) % NSLOT);
@@ -359,6 +423,7 @@ __global__ __launch_bounds__(512, 1) void prefill_attn_kernel(
     tile_math(kt);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();          // slot kt % NSLOT may be refilled
+  }
   }
 
   // ---- normalise + store: lane (l15 = query, lg) writes dims 16 nd + 4 lg .. +3 -------
@@ -452,7 +517,7 @@ extern "C" int ft_prefill_attention(void* out, int out_stride, const void* q, in
                                     const int* q_start_loc, const int* tile_info, int num_tiles,
                                     int nq, int nkv, int head_dim, int block_size, float scale,
                                     float* part_o, float* part_ml, const int* combine,
-                                    int num_combine, int invariant, int num_blocks,
+                                    int num_combine, int invariant, int num_blocks, int kv8,
                                     hipStream_t stream) {
   if (num_tiles <= 0) return 0;
   if (nq % nkv != 0) return -1;
@@ -462,7 +527,19 @@ extern "C" int ft_prefill_attention(void* out, int out_stride, const void* q, in
   dim3 grid(num_tiles, nkv), block(512);
 #define FT_PF_CASE(DD, GG)                                                                   \
   if (head_dim == DD && G == GG) {                                                           \
-    if (invariant)                                                                           \
+    if (kv8 && invariant)                                                                    \
+      hipLaunchKernelGGL((ft::prefill_attn_kernel<DD, GG, true, true>), grid, block, 0, stream, \
+                         (uint16_t*)out, out_stride, (const uint16_t*)q, q_stride,           \
+                         (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables,   \
+                         bt_stride, seq_lens, q_start_loc, tile_info, nkv, block_size,       \
+                         scale_log2, part_o, part_ml, num_blocks);                           \
+    else if (kv8)                                                                            \
+      hipLaunchKernelGGL((ft::prefill_attn_kernel<DD, GG, false, true>), grid, block, 0, stream, \
+                         (uint16_t*)out, out_stride, (const uint16_t*)q, q_stride,           \
+                         (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables,   \
+                         bt_stride, seq_lens, q_start_loc, tile_info, nkv, block_size,       \
+                         scale_log2, part_o, part_ml, num_blocks);                           \
+    else if (invariant)                                                                      \
       hipLaunchKernelGGL((ft::prefill_attn_kernel<DD, GG, true>), grid, block, 0, stream,    \
                          (uint16_t*)out, out_stride, (const uint16_t*)q, q_stride,           \
                          (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables,   \

@@ -27,6 +27,12 @@ __device__ __forceinline__ uint2 ds_read8(uint32_t a) {
   asm volatile("ds_read_b64 %0, %1" : "=v"(v) : "v"(a));
   return __builtin_bit_cast(uint2, v);
 }
+// LDS store in inline asm, ordered with the asm reads above ("memory": the compiler
+// keeps it between the surrounding waits and barriers)
+__device__ __forceinline__ void ds_write16(uint32_t a, const uint4& v) {
+  const u32x4_t w = __builtin_bit_cast(u32x4_t, v);
+  asm volatile("ds_write_b128 %0, %1" ::"v"(a), "v"(w) : "memory");
+}
 // the same with a compile-time immediate offset (the ds_read offset field, 0..65535):
 // per-lane base addresses computed once, per-fragment displacements as immediates
 template <int OFF>

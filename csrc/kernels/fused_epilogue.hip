@@ -142,11 +142,12 @@ __global__ __launch_bounds__(256) void slab_store_kernel(SrcSlab src, uint16_t* 
 // ---------------------------------------------------------------------------------
 // RoPE + paged KV write from split-K slabs of the QKV projection
 // ---------------------------------------------------------------------------------
-template <int D>
+// KV8: fp8 (e4m3) caches (ft_common.h fp8x*), same layouts with 1-byte elements
+template <int D, bool KV8>
 __global__ __launch_bounds__(256) void slab_rope_kv_kernel(
     SrcSlab src, uint16_t* __restrict__ q_out, int q_stride, const int* __restrict__ positions,
     const float* __restrict__ cos_sin, const int* __restrict__ slot_mapping,
-    uint16_t* __restrict__ k_cache, uint16_t* __restrict__ v_cache, int nq, int nkv,
+    void* __restrict__ k_cache, void* __restrict__ v_cache, int nq, int nkv,
     int block_size, const uint16_t* __restrict__ residual, int hidden, float eps, int cos_rows,
     int num_slots) {
   constexpr int HALF = D / 2;
@@ -198,9 +199,16 @@ __global__ __launch_bounds__(256) void slab_rope_kv_kernel(
       *reinterpret_cast<uint4*>(qp + c * 8) = store8(y1);
       *reinterpret_cast<uint4*>(qp + HALF + c * 8) = store8(y2);
     } else if (slot >= 0) {
-      uint16_t* kp = k_cache + (((size_t)blk * nkv + (head - nq)) * block_size + off) * D;
-      *reinterpret_cast<uint4*>(kp + c * 8) = store8(y1);
-      *reinterpret_cast<uint4*>(kp + HALF + c * 8) = store8(y2);
+      const size_t e = (((size_t)blk * nkv + (head - nq)) * block_size + off) * D;
+      if constexpr (KV8) {
+        uint8_t* kp = reinterpret_cast<uint8_t*>(k_cache) + e;
+        *reinterpret_cast<uint2*>(kp + c * 8) = fp8x8_pack(y1);
+        *reinterpret_cast<uint2*>(kp + HALF + c * 8) = fp8x8_pack(y2);
+      } else {
+        uint16_t* kp = reinterpret_cast<uint16_t*>(k_cache) + e;
+        *reinterpret_cast<uint4*>(kp + c * 8) = store8(y1);
+        *reinterpret_cast<uint4*>(kp + HALF + c * 8) = store8(y2);
+      }
     }
   }
   if (slot >= 0) {
@@ -212,9 +220,17 @@ __global__ __launch_bounds__(256) void slab_rope_kv_kernel(
 #pragma unroll
       for (int j = 0; j < 8; ++j) f[j] *= rs;
       // V blocks are transposed ([D][block_size], rope_kv.hip)
-      uint16_t* vp = v_cache + (((size_t)blk * nkv + kh) * D + c * 8) * block_size + off;
+      const size_t e = (((size_t)blk * nkv + kh) * D + c * 8) * block_size + off;
+      if constexpr (KV8) {
+        const uint2 q8 = fp8x8_pack(f);
+        uint8_t* vp = reinterpret_cast<uint8_t*>(v_cache) + e;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) vp[j * block_size] = f32_to_bf16(f[j]);
+        for (int j = 0; j < 8; ++j) vp[j * block_size] = (uint8_t)(((j < 4 ? q8.x : q8.y) >> (8 * (j & 3))) & 0xffu);
+      } else {
+        uint16_t* vp = reinterpret_cast<uint16_t*>(v_cache) + e;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) vp[j * block_size] = f32_to_bf16(f[j]);
+      }
     }
   }
 }
@@ -294,24 +310,24 @@ extern "C" int ft_slab_rope_kv(const float* ws, int splits, int rows, int cols, 
                                int q_stride, const int* positions, const float* cos_sin,
                                const int* slot_mapping, void* k_cache, void* v_cache, int nq,
                                int nkv, int head_dim, int block_size, const void* residual,
-                               int hidden, float eps, int cos_rows, int num_slots,
+                               int hidden, float eps, int cos_rows, int num_slots, int kv8,
                                hipStream_t stream) {
   if (rows <= 0) return 0;
   if (residual != nullptr && hidden % 8 != 0) return -2;
   ft::SrcSlab src{ws, splits, rows, cols};
+#define FT_SRK(DD, K8)                                                                          \
+  hipLaunchKernelGGL((ft::slab_rope_kv_kernel<DD, K8>), dim3(rows, 2), dim3(256), 0, stream, src, \
+                     (uint16_t*)q_out, q_stride, positions, cos_sin, slot_mapping, k_cache,       \
+                     v_cache, nq, nkv, block_size, (const uint16_t*)residual, hidden, eps,        \
+                     cos_rows, num_slots)
   if (head_dim == 128) {
-    hipLaunchKernelGGL(ft::slab_rope_kv_kernel<128>, dim3(rows, 2), dim3(256), 0, stream, src,
-                       (uint16_t*)q_out, q_stride, positions, cos_sin, slot_mapping,
-                       (uint16_t*)k_cache, (uint16_t*)v_cache, nq, nkv, block_size,
-                       (const uint16_t*)residual, hidden, eps, cos_rows, num_slots);
+    if (kv8) FT_SRK(128, true); else FT_SRK(128, false);
   } else if (head_dim == 64) {
-    hipLaunchKernelGGL(ft::slab_rope_kv_kernel<64>, dim3(rows, 2), dim3(256), 0, stream, src,
-                       (uint16_t*)q_out, q_stride, positions, cos_sin, slot_mapping,
-                       (uint16_t*)k_cache, (uint16_t*)v_cache, nq, nkv, block_size,
-                       (const uint16_t*)residual, hidden, eps, cos_rows, num_slots);
+    if (kv8) FT_SRK(64, true); else FT_SRK(64, false);
   } else {
     return -1;
   }
+#undef FT_SRK
   return static_cast<int>(hipGetLastError());
 }
 

@@ -18,13 +18,14 @@
 
 namespace ft {
 
-template <int D>
+// KV8: fp8 (e4m3) caches, same layouts with 1-byte elements (ft_common.h fp8x*)
+template <int D, bool KV8>
 __global__ __launch_bounds__(256) void rope_kv_kernel(uint16_t* __restrict__ qkv, int qkv_stride,
                                                       const int* __restrict__ positions,
                                                       const float* __restrict__ cos_sin,
                                                       const int* __restrict__ slot_mapping,
-                                                      uint16_t* __restrict__ k_cache,
-                                                      uint16_t* __restrict__ v_cache, int nq,
+                                                      void* __restrict__ k_cache,
+                                                      void* __restrict__ v_cache, int nq,
                                                       int nkv, int block_size, int cos_rows,
                                                       int num_slots) {
   constexpr int HALF = D / 2;
@@ -66,9 +67,16 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(uint16_t* __restrict__ qkv
     } else if (slot >= 0) {
       const int kh = head - nq;
       const int blk = slot / block_size, off = slot - blk * block_size;
-      uint16_t* kp = k_cache + (((size_t)blk * nkv + kh) * block_size + off) * D;
-      reinterpret_cast<uint4*>(kp + c * 8)[0] = o1;
-      reinterpret_cast<uint4*>(kp + HALF + c * 8)[0] = o2;
+      const size_t e = (((size_t)blk * nkv + kh) * block_size + off) * D;
+      if constexpr (KV8) {
+        uint8_t* kp = reinterpret_cast<uint8_t*>(k_cache) + e;
+        reinterpret_cast<uint2*>(kp + c * 8)[0] = fp8x8_pack(y1);
+        reinterpret_cast<uint2*>(kp + HALF + c * 8)[0] = fp8x8_pack(y2);
+      } else {
+        uint16_t* kp = reinterpret_cast<uint16_t*>(k_cache) + e;
+        reinterpret_cast<uint4*>(kp + c * 8)[0] = o1;
+        reinterpret_cast<uint4*>(kp + HALF + c * 8)[0] = o2;
+      }
     }
   }
   if (slot >= 0) {
@@ -78,13 +86,23 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(uint16_t* __restrict__ qkv
     for (int item = threadIdx.x; item < nv; item += blockDim.x) {
       const int kh = item / (D / 8), c = item - kh * (D / 8);
       // V blocks are transposed ([D][block_size]): dims c*8.. of this token
-      uint16_t* vp = v_cache + (((size_t)blk * nkv + kh) * D + c * 8) * block_size + off;
+      const size_t e = (((size_t)blk * nkv + kh) * D + c * 8) * block_size + off;
       const uint4 v = vsrc[item];
-      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+      if constexpr (KV8) {
+        float f[8];
+        load8(v, f);
+        const uint2 q8 = fp8x8_pack(f);
+        uint8_t* vp = reinterpret_cast<uint8_t*>(v_cache) + e;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        vp[(2 * j) * block_size] = (uint16_t)(w[j] & 0xffffu);
-        vp[(2 * j + 1) * block_size] = (uint16_t)(w[j] >> 16);
+        for (int j = 0; j < 8; ++j) vp[j * block_size] = (uint8_t)(((j < 4 ? q8.x : q8.y) >> (8 * (j & 3))) & 0xffu);
+      } else {
+        uint16_t* vp = reinterpret_cast<uint16_t*>(v_cache) + e;
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          vp[(2 * j) * block_size] = (uint16_t)(w[j] & 0xffffu);
+          vp[(2 * j + 1) * block_size] = (uint16_t)(w[j] >> 16);
+        }
       }
     }
   }
@@ -95,21 +113,22 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(uint16_t* __restrict__ qkv
 extern "C" int ft_rope_kv_write(void* qkv, int qkv_stride, const int* positions,
                                 const float* cos_sin, const int* slot_mapping, void* k_cache,
                                 void* v_cache, int tokens, int nq, int nkv, int head_dim,
-                                int block_size, int cos_rows, int num_slots,
+                                int block_size, int cos_rows, int num_slots, int kv8,
                                 hipStream_t stream) {
   if (tokens <= 0) return 0;
   dim3 grid(tokens), block(256);
+#define FT_ROPE(DD, K8)                                                                     \
+  hipLaunchKernelGGL((ft::rope_kv_kernel<DD, K8>), grid, block, 0, stream, (uint16_t*)qkv,  \
+                     qkv_stride, positions, cos_sin, slot_mapping, k_cache, v_cache, nq, nkv, \
+                     block_size, cos_rows, num_slots)
   if (head_dim == 128) {
-    hipLaunchKernelGGL(ft::rope_kv_kernel<128>, grid, block, 0, stream, (uint16_t*)qkv,
-                       qkv_stride, positions, cos_sin, slot_mapping, (uint16_t*)k_cache,
-                       (uint16_t*)v_cache, nq, nkv, block_size, cos_rows, num_slots);
+    if (kv8) FT_ROPE(128, true); else FT_ROPE(128, false);
   } else if (head_dim == 64) {
-    hipLaunchKernelGGL(ft::rope_kv_kernel<64>, grid, block, 0, stream, (uint16_t*)qkv,
-                       qkv_stride, positions, cos_sin, slot_mapping, (uint16_t*)k_cache,
-                       (uint16_t*)v_cache, nq, nkv, block_size, cos_rows, num_slots);
+    if (kv8) FT_ROPE(64, true); else FT_ROPE(64, false);
   } else {
     return -1;
   }
+#undef FT_ROPE
   return static_cast<int>(hipGetLastError());
 }
 

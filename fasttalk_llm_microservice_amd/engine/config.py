@@ -67,6 +67,20 @@ class EngineConfig:
     # a sequence's tokens independent of what else shares its steps (fixed GEMM splits,
     # fixed-piece attention partitions; TP=1, bf16; slower decode attention)
     batch_invariant: bool = False
+    # KV-cache storage: "auto" (the compute dtype) | "fp8" (OCP e4m3 at scale 1, vLLM's
+    # --kv-cache-dtype fp8 without calibration): half the cache bytes per token, so the
+    # decode attention stream halves and the pool holds twice the tokens
+    kv_cache_dtype: str = "auto"
+
+    def kv_torch_dtype(self, compute_dtype):
+        import torch
+
+        v = (self.kv_cache_dtype or "auto").lower()
+        if v in ("auto", "bf16", "bfloat16", "float32", "fp32"):
+            return compute_dtype
+        if v in ("fp8", "fp8_e4m3", "float8_e4m3fn", "e4m3"):
+            return torch.float8_e4m3fn
+        raise ValueError(f"kv_cache_dtype {self.kv_cache_dtype!r}: auto | fp8")
 
     def resolved_device(self) -> str:
         if self.device != "auto":
@@ -120,6 +134,7 @@ class EngineConfig:
             max_restarts=_env(["ENGINE_MAX_RESTARTS"], 3, int),
             quantization=_env(["ENGINE_QUANTIZATION", "VLLM_QUANTIZATION"], None) or None,
             batch_invariant=_env(["ENGINE_BATCH_INVARIANT", "VLLM_BATCH_INVARIANT"], False, _bool),
+            kv_cache_dtype=_env(["ENGINE_KV_CACHE_DTYPE", "VLLM_KV_CACHE_DTYPE"], "auto"),
         )
         for k, v in overrides.items():
             setattr(c, k, v)

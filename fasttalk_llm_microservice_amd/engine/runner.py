@@ -217,8 +217,9 @@ class ModelRunner:
         if self.invariant:
             self.model.set_batch_invariant(max(cfg.max_num_batched_tokens, cfg.max_num_seqs)
                                            + cfg.max_num_seqs)
+        self.kv_dtype = cfg.kv_torch_dtype(self.dtype)
         self.num_blocks = self._decide_num_blocks()
-        self.kv = self.model.allocate_kv_cache(self.num_blocks, self.bs)
+        self.kv = self.model.allocate_kv_cache(self.num_blocks, self.bs, self.kv_dtype)
         # FT_KERNEL_CHECKS=1: the bounds-checked kernel build validates every index it
         # is handed against the tensors of the launch (this pool's blocks, the rotary
         # table's rows, the vocab) and reports into this word, read after each step
@@ -394,9 +395,9 @@ class ModelRunner:
         be = self.kv_block_elems
         if self.host_kv is None:
             t0 = time.time()
-            self.host_kv = torch.empty(self.num_host_blocks, nl * be, dtype=self.dtype,
+            self.host_kv = torch.empty(self.num_host_blocks, nl * be, dtype=self.kv_dtype,
                                        pin_memory=self.is_gpu)
-            self.swap_staging = torch.empty(self.SWAP_CHUNK, nl * be, dtype=self.dtype,
+            self.swap_staging = torch.empty(self.SWAP_CHUNK, nl * be, dtype=self.kv_dtype,
                                             device=self.device)
             if self.is_gpu:
                 self.kv_ptrs = torch.tensor([c.data_ptr() for kv in self.kv for c in kv],
@@ -426,7 +427,7 @@ class ModelRunner:
     def _decide_num_blocks(self) -> int:
         cfg = self.cfg
         per_block = self.mcfg.num_layers * 2 * self.model.nkv * self.model.d * self.bs * \
-            torch.tensor([], dtype=self.dtype).element_size()
+            torch.tensor([], dtype=self.kv_dtype).element_size()
         if cfg.num_kv_blocks:
             n = cfg.num_kv_blocks
         elif self.is_gpu:
@@ -443,8 +444,8 @@ class ModelRunner:
         else:
             n = max(1024, (self.max_model_len // self.bs) * 4)
         n = self.comm.min_int(int(min(n, 4_000_000)))  # every TP rank holds the same pool
-        log.info("KV cache: %d blocks x %d tokens = %d tokens (%.1f GiB)", n, self.bs, n * self.bs,
-                 n * per_block / 2**30)
+        log.info("KV cache: %d blocks x %d tokens = %d tokens (%.1f GiB, %s)", n, self.bs, n * self.bs,
+                 n * per_block / 2**30, str(self.kv_dtype).replace("torch.", ""))
         return n
 
     # ------------------------------------------------------------------ helpers

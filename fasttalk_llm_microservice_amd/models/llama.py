@@ -951,11 +951,14 @@ class LlamaModel:
     def v_cache_shape(self, num_blocks: int, block_size: int) -> Tuple[int, ...]:
         return (num_blocks, self.nkv, self.d, block_size)
 
-    def allocate_kv_cache(self, num_blocks: int, block_size: int):
+    def allocate_kv_cache(self, num_blocks: int, block_size: int, dtype=None):
+        """[(K, V)] per layer in ``dtype`` (default: the compute dtype; fp8 =
+        torch.float8_e4m3fn, written and read by the same kernels' KV8 paths)."""
         ks = self.kv_cache_shape(num_blocks, block_size)
         vs = self.v_cache_shape(num_blocks, block_size)
-        return [(torch.zeros(ks, dtype=self.dtype, device=self.device),
-                 torch.zeros(vs, dtype=self.dtype, device=self.device))
+        dt = dtype or self.dtype
+        return [(torch.zeros(ks, dtype=dt, device=self.device),
+                 torch.zeros(vs, dtype=dt, device=self.device))
                 for _ in range(self.cfg.num_layers)]
 
     # ------------------------------------------------------------------ forward

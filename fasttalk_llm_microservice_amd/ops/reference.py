@@ -70,6 +70,17 @@ def apply_rope(x: torch.Tensor, positions: torch.Tensor, cos_sin: torch.Tensor) 
     return torch.cat([x1 * cos - x2 * sin, x2 * cos + x1 * sin], dim=-1).to(x.dtype)
 
 
+FP8_MAX = 448.0   # float8_e4m3fn's largest finite value
+
+
+def to_cache(x: torch.Tensor, cache: torch.Tensor) -> torch.Tensor:
+    """x in the cache's dtype; fp8 caches clamp to the format's range first (a plain
+    cast turns an out-of-range value into NaN, as gfx950's converter does)."""
+    if cache.dtype == torch.float8_e4m3fn:
+        return x.float().clamp(-FP8_MAX, FP8_MAX).to(cache.dtype)
+    return x.to(cache.dtype)
+
+
 def rope_kv_write(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, nq, nkv, head_dim):
     """In place: rotate q inside ``qkv``; write rotated k and v into the paged caches."""
     t = qkv.shape[0]
@@ -87,8 +98,8 @@ def rope_kv_write(qkv, positions, cos_sin, slot_mapping, k_cache, v_cache, nq, n
         bs = k_cache.shape[2]
         s = slots[keep]
         blk, off = s // bs, s % bs
-        k_cache[blk, :, off, :] = kr[keep]
-        v_cache[blk, :, :, off] = v[keep]   # V blocks are transposed: [blocks, nkv, D, bs]
+        k_cache[blk, :, off, :] = to_cache(kr[keep], k_cache)
+        v_cache[blk, :, :, off] = to_cache(v[keep], v_cache)   # V blocks transposed: [blocks, nkv, D, bs]
 
 
 def _gather_kv(cache, table_row, length, transposed: bool = False):

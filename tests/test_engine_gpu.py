@@ -257,6 +257,30 @@ def test_host_swap_roundtrip_and_engine():
     assert eng.bm.num_free() == eng.bm.num_blocks and s.host.num_free() == s.host.num_blocks
 
 
+def test_fp8_kv_engine_serves_graph_and_eager():
+    """ENGINE_KV_CACHE_DTYPE=fp8: the engine allocates e4m3 caches (half the bytes per
+    block, so twice the tokens for the same pool bytes), decodes from hipGraphs and
+    agrees with its eager run token for token.  A second turn continuing from the
+    cached fp8 prefix starts like a run that prefills the whole history afresh
+    (their K/V differ by e4m3 rounding of decode- vs prefill-computed rows, so only
+    the first token and a majority are asserted)."""
+    prompts = _prompts(5, [5, 17, 33, 64, 100])
+    sp = SamplingParams(temperature=0.0, max_tokens=24, ignore_eos=True)
+    e = _engine(model="tiny-2k", kv_cache_dtype="fp8")
+    assert e.runner.kv[0][0].dtype == torch.float8_e4m3fn
+    a = e.generate(prompts, sp)
+    b = _engine(model="tiny-2k", kv_cache_dtype="fp8", enforce_eager=True).generate(prompts, sp)
+    assert a == b and all(len(o) == 24 for o in a)
+    turn2 = prompts[4] + a[4] + [128009, 128006, 882, 128007, 271, 40, 41, 42]
+    hits0 = e.bm.hits
+    with_cache = e.generate([turn2], sp)[0]
+    assert e.bm.hits > hits0
+    no_cache = _engine(model="tiny-2k", kv_cache_dtype="fp8",
+                       enable_prefix_caching=False).generate([turn2], sp)[0]
+    agree = sum(x == y for x, y in zip(with_cache, no_cache)) / len(no_cache)
+    assert with_cache[0] == no_cache[0] and agree >= 0.5, (with_cache, no_cache)
+
+
 def test_w4_engine_graph_matches_eager():
     """W4A16 decode through hipGraphs equals eager W4A16 decode token for token."""
     prompts = _prompts(6, [9, 30, 65, 17, 80, 3], seed=9)
@@ -364,12 +388,16 @@ def test_single_weight_image_llama3_8b():
     torch.cuda.empty_cache()
 
 
-@pytest.mark.parametrize("model,rows,quant,block", [
-    ("llama3-8b", 1, None, False), ("llama3-8b", 20, None, False), ("llama3-8b", 50, None, False),
-    ("llama3-8b", 100, None, False), ("llama3-70b", 1, None, False), ("llama3-70b", 72, None, False),
-    ("llama3-8b", 50, "w4", False), ("llama3-8b", 64, "w4", False), ("llama3-8b", 8, "w4", False),
-    ("llama3-8b", 100, "w4", False), ("llama3-8b", 40, None, True), ("llama3-8b", 64, None, True)])
-def test_llama3_shape_decode_matches_cpu_fp32(model, rows, quant, block, monkeypatch):
+@pytest.mark.parametrize("model,rows,quant,block,kv8", [
+    ("llama3-8b", 1, None, False, False), ("llama3-8b", 20, None, False, False),
+    ("llama3-8b", 50, None, False, False), ("llama3-8b", 100, None, False, False),
+    ("llama3-70b", 1, None, False, False), ("llama3-70b", 72, None, False, False),
+    ("llama3-8b", 50, "w4", False, False), ("llama3-8b", 64, "w4", False, False),
+    ("llama3-8b", 8, "w4", False, False), ("llama3-8b", 100, "w4", False, False),
+    ("llama3-8b", 40, None, True, False), ("llama3-8b", 64, None, True, False),
+    ("llama3-8b", 1, None, False, True), ("llama3-8b", 20, None, False, True),
+    ("llama3-8b", 50, None, False, True), ("llama3-8b", 100, None, False, True)])
+def test_llama3_shape_decode_matches_cpu_fp32(model, rows, quant, block, kv8, monkeypatch):
     """a 2-layer Llama-3-8B-shaped model (H 4096, I 14336, GQA 4) -- and
     a 70B-shaped one (H 8192, I 28672, GQA 8) -- decoding `rows` sequences with ragged
     contexts up to 6k over random KV caches: the fused layer (1 / 20 rows), the
@@ -378,7 +406,8 @@ def test_llama3_shape_decode_matches_cpu_fp32(model, rows, quant, block, monkeyp
     same weights and cache contents.  ``quant="w4"``: the W4A16 (AWQ-format, group 128)
     decode GEMMs of the 8 / 64 row buckets -- the reference's default deployment
     precision -- against the fp32 model on the dequantized weights.
-    ``block``: the opt-in persistent post-attention block (FT_DECODE_BLOCK=1)."""
+    ``block``: the opt-in persistent post-attention block (FT_DECODE_BLOCK=1).  ``kv8``:
+    fp8 (e4m3) KV caches on both sides (the CPU reference reads the same bytes)."""
     import dataclasses as dc
 
     monkeypatch.setenv("FT_DECODE_BLOCK", "1" if block else "0")
@@ -406,9 +435,16 @@ def test_llama3_shape_decode_matches_cpu_fp32(model, rows, quant, block, monkeyp
         bt[i, :nb] = perm[o:o + nb]
         o += nb
     total = sum(nblk)
-    kv_g = g.allocate_kv_cache(total, bs)
-    kv_c = c.allocate_kv_cache(total, bs)
+    kvd = torch.float8_e4m3fn if kv8 else None
+    kv_g = g.allocate_kv_cache(total, bs, kvd)
+    kv_c = c.allocate_kv_cache(total, bs, kvd)
     for (kg, vg), (kc, vc) in zip(kv_g, kv_c):
+        if kv8:
+            kc.copy_(torch.randn(kc.shape).to(kvd))
+            vc.copy_(torch.randn(vc.shape).to(kvd))
+            kg.copy_(kc.to(kg.device))
+            vg.copy_(vc.to(vg.device))
+            continue
         kc.copy_(torch.randn(kc.shape).bfloat16().float())
         vc.copy_(torch.randn(vc.shape).bfloat16().float())
         kg.copy_(kc.bfloat16())
