@@ -46,6 +46,24 @@ def test_tp_generation_matches_tp1(tp):
     assert out2 == LLMEngine(_cfg()).generate(prompts[:1], sp2)
 
 
+def test_tp2_fp8_kv_matches_tp1():
+    """fp8 KV caches under TP: each rank stores its kv heads in e4m3 and the tokens
+    match the single-rank fp8 engine."""
+    from fasttalk_llm_microservice_amd.parallel.tp import spawn_tp_engine
+
+    rng = np.random.default_rng(1)
+    prompts = [rng.integers(0, 120000, n).tolist() for n in (12, 40)]
+    sp = SamplingParams(temperature=0, max_tokens=6, ignore_eos=True)
+    ref = LLMEngine(_cfg(kv_cache_dtype="fp8")).generate(prompts, sp)
+    eng = spawn_tp_engine(_cfg(tp_size=2, kv_cache_dtype="fp8"))
+    try:
+        assert str(eng.runner.kv[0][0].dtype) == "torch.float8_e4m3fn"
+        out = eng.generate(prompts, sp)
+    finally:
+        eng.shutdown()
+    assert out == ref
+
+
 def _reader(name, idx, q):
     b = ShmBroadcast(2, name=name, create=False, reader_index=idx, num_slots=4, slot_bytes=1 << 12)
     total = 0
