@@ -625,11 +625,21 @@ extern "C" int ft_paged_decode_attention(void* out, int out_stride, float* tmp_o
     const int v = e ? atoi(e) : 2;
     return (v == 1 || v == 2 || v == 4) ? v : 2;
   }();
-  // fp8 tiles carry half the bytes: ring depth of the fp8 path (FT_DECODE_RING8, 2 / 3)
+  // ring depth of the fp8 path (FT_DECODE_RING8, 2 / 3).  bench/attn_fp8_bench.py,
+  // 50 x 1.5-3k / 50 x 2.2-4.5k / 64 x 4k (profiles/attn_fp8_r06.log): 2 waves per
+  // workgroup 68.7 / 98.6 / 131.5 us (ring 3), 4 waves 56.7 / 77.7 / 106.8 (ring 3) and
+  // 55.3 / 74.4 / 102.6 (ring 2) -- against 84.8 / 120.1 / 170.6 us on bf16 caches
   static const int ring8 = [] {
     const char* e = getenv("FT_DECODE_RING8");
-    const int r = e ? atoi(e) : 3;
-    return (r == 2 || r == 3) ? r : 3;
+    const int r = e ? atoi(e) : 2;
+    return (r == 2 || r == 3) ? r : 2;
+  }();
+  // waves per workgroup of the fp8 path (FT_DECODE_WAVES8, 2 / 4): the widening
+  // conversions double the VALU work per byte, so the fp8 stream wants every SIMD
+  static const int nwv8 = [] {
+    const char* e = getenv("FT_DECODE_WAVES8");
+    const int v = e ? atoi(e) : 4;
+    return (v == 2 || v == 4) ? v : 4;
   }();
   int nwg = 0;
 #define FT_DEC_ARGS                                                                             \
@@ -653,16 +663,16 @@ extern "C" int ft_paged_decode_attention(void* out, int out_stride, float* tmp_o
                            dim3(256), 0, stream, FT_DEC_ARGS);                                 \
       else if (counters != nullptr && ring8 == 3)                                              \
         hipLaunchKernelGGL((ft::paged_decode_kernel<DD, GG, 3, true, 1, false, true>), dim3(nwg), \
-                           dim3(64 * nwv), 0, stream, FT_DEC_ARGS);                            \
+                           dim3(64 * nwv8), 0, stream, FT_DEC_ARGS);                            \
       else if (counters != nullptr)                                                            \
         hipLaunchKernelGGL((ft::paged_decode_kernel<DD, GG, 2, true, 1, false, true>), dim3(nwg), \
-                           dim3(64 * nwv), 0, stream, FT_DEC_ARGS);                            \
+                           dim3(64 * nwv8), 0, stream, FT_DEC_ARGS);                            \
       else {                                                                                   \
         hipLaunchKernelGGL((ft::paged_decode_kernel<DD, GG, 2, false, 1, false, true>), dim3(nwg), \
-                           dim3(64 * nwv), 0, stream, FT_DEC_ARGS);                            \
+                           dim3(64 * nwv8), 0, stream, FT_DEC_ARGS);                            \
         hipLaunchKernelGGL((ft::paged_decode_combine_kernel<DD, GG>), dim3(batch * nkv), dim3(256),\
                            0, stream, (uint16_t*)out, out_stride, tmp_out, tmp_ml, seq_lens, batch,\
-                           nkv, nwg * nwv, min_tiles);                                         \
+                           nkv, nwg * nwv8, min_tiles);                                         \
       }                                                                                        \
       return static_cast<int>(hipGetLastError());                                              \
     }                                                                                          \
