@@ -54,7 +54,7 @@ def main():
             del kvs, fns
             torch.cuda.empty_cache()
         print(f"B={B} ctx {lo}-{hi}: fp8 / bf16 = {res['fp8'] / res['bf16']:.3f} "
-              f"(ring8 {os.environ.get('FT_DECODE_RING8', '3')})", flush=True)
+              f"(ring8 {os.environ.get('FT_DECODE_RING8', '2')}, wpc8 {os.environ.get('FT_DECODE_WPC8', '1')})", flush=True)
 
 
 if __name__ == "__main__":

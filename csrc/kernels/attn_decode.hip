@@ -641,6 +641,12 @@ extern "C" int ft_paged_decode_attention(void* out, int out_stride, float* tmp_o
     const int v = e ? atoi(e) : 4;
     return (v == 2 || v == 4) ? v : 4;
   }();
+  // FT_DECODE_WPC8=2: two fp8 workgroups per CU -- measured 61.8 / 81.1 / 105.8 us against
+  // 55.5 / 74.1 / 100.0 at one (profiles/attn_fp8_r06.log), kept for sweeps
+  static const int wpc8 = [] {
+    const char* e = getenv("FT_DECODE_WPC8");
+    return e && atoi(e) == 2 ? 2 : 1;
+  }();
   int nwg = 0;
 #define FT_DEC_ARGS                                                                             \
   (uint16_t*)out, out_stride, tmp_out, tmp_ml, (const uint16_t*)q, q_stride, (uint16_t*)k_cache, \
@@ -661,6 +667,9 @@ extern "C" int ft_paged_decode_attention(void* out, int out_stride, float* tmp_o
       if (piece > 0)                                                                           \
         hipLaunchKernelGGL((ft::paged_decode_kernel<DD, GG, 2, true, 1, true, true>), dim3(nwg), \
                            dim3(256), 0, stream, FT_DEC_ARGS);                                 \
+      else if (counters != nullptr && wpc8 == 2)                                               \
+        hipLaunchKernelGGL((ft::paged_decode_kernel<DD, GG, 2, true, 2, false, true>),          \
+                           dim3(2 * nwg), dim3(64 * nwv8), 0, stream, FT_DEC_ARGS);              \
       else if (counters != nullptr && ring8 == 3)                                              \
         hipLaunchKernelGGL((ft::paged_decode_kernel<DD, GG, 3, true, 1, false, true>), dim3(nwg), \
                            dim3(64 * nwv8), 0, stream, FT_DEC_ARGS);                            \
