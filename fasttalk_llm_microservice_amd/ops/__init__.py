@@ -361,6 +361,8 @@ def kv_swap(caches, ptrs, ids: torch.Tensor, staging: torch.Tensor, to_staging: 
     if n == 0:
         return
     flat = [c for kv in caches for c in kv]
+    if staging.dtype != flat[0].dtype:   # the kernel sizes a block by the staging dtype
+        raise ValueError(f"kv_swap: staging {staging.dtype} vs caches {flat[0].dtype}")
     if staging.is_cuda:
         nblk = flat[0].shape[0]
         native().kv_swap(ptrs, ids, staging, flat[0].numel() // nblk, to_staging, nblk)

@@ -281,6 +281,36 @@ def test_fp8_kv_engine_serves_graph_and_eager():
     assert with_cache[0] == no_cache[0] and agree >= 0.5, (with_cache, no_cache)
 
 
+def test_fp8_kv_host_swap_roundtrip():
+    """fp8 caches through the host swap pool (pinned e4m3 host blocks, gather / scatter
+    kernels sized in bytes): blocks come back bit-exact, and a pool too small for the
+    batch finishes every request through swaps."""
+    eng = _engine(num_kv_blocks=20, swap_space_gb=0.5, enable_prefix_caching=False,
+                  kv_cache_dtype="fp8")
+    r = eng.runner
+    assert r.kv[0][0].dtype == torch.float8_e4m3fn
+    for k, v in r.kv:
+        k.copy_(torch.randn(k.shape, device=k.device).to(k.dtype))
+        v.copy_(torch.randn(v.shape, device=v.device).to(v.dtype))
+    before = [(k[[3, 7, 11]].view(torch.uint8).clone(), v[[3, 7, 11]].view(torch.uint8).clone())
+              for k, v in r.kv]
+    r.swap([(3, 0), (7, 5), (11, 2)], [])
+    for k, v in r.kv:
+        k[[3, 7, 11]] = torch.zeros_like(k[[3, 7, 11]])
+    r.swap([], [(0, 14), (5, 1), (2, 9)])
+    torch.cuda.synchronize()
+    for (k, v), (k0, v0) in zip(r.kv, before):
+        assert torch.equal(k[[14, 1, 9]].view(torch.uint8), k0)
+        assert torch.equal(v[[14, 1, 9]].view(torch.uint8), v0)
+    prompts = _prompts(6, [40 + 9 * i for i in range(6)], seed=5)
+    sp = SamplingParams(temperature=0.8, top_p=0.9, seed=21, max_tokens=48, ignore_eos=True)
+    got = eng.generate(prompts, sp)
+    s = eng.scheduler
+    assert s.num_swap_out > 0 and s.num_swap_in == s.num_swap_out
+    assert all(len(o) == 48 for o in got)
+    assert eng.bm.num_free() == eng.bm.num_blocks and s.host.num_free() == s.host.num_blocks
+
+
 def test_w4_engine_graph_matches_eager():
     """W4A16 decode through hipGraphs equals eager W4A16 decode token for token."""
     prompts = _prompts(6, [9, 30, 65, 17, 80, 3], seed=9)
