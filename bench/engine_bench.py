@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--temperature", type=float, default=0.7)
     ap.add_argument("--kv-blocks", type=int, default=None)
     ap.add_argument("--batch-invariant", action="store_true")
+    ap.add_argument("--kv-cache-dtype", default="auto", choices=["auto", "fp8"])
     a = ap.parse_args()
 
     import numpy as np
@@ -35,7 +36,7 @@ def main():
     from fasttalk_llm_microservice_amd.engine.sampling_params import SamplingParams
 
     cfg = EngineConfig(model=a.model, enforce_eager=a.eager, num_kv_blocks=a.kv_blocks,
-                       batch_invariant=a.batch_invariant)
+                       batch_invariant=a.batch_invariant, kv_cache_dtype=a.kv_cache_dtype)
     t0 = time.time()
     eng = LLMEngine(cfg)
     print(f"engine up in {time.time() - t0:.1f}s", flush=True)
