@@ -75,3 +75,13 @@ def test_eight_ranks_through_the_front_door():
     spw = out["serve"]["sessions_per_worker"]
     assert len(spw) == 8 and sum(spw) == 24 and max(spw) - min(spw) <= 1, spw
     assert sorted(d["rank"] for d in out["rank_devices"]) == list(range(8))
+
+
+def test_fp8_kv_cache_flag_reaches_the_engine_and_the_json():
+    """--kv-cache-dtype fp8 sets ENGINE_KV_CACHE_DTYPE for the service the bench drives
+    (one rank here), the run completes on the fp8 pool and the JSON line says so."""
+    r = _run(["--device", "cpu", "--model", "tiny", "--sessions", "2", "--steps", "1", "--warmup", "1",
+              "--gen", "4", "--words", "6", "--kv-cache-dtype", "fp8"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = _json_lines(r.stdout)[0]
+    assert out["kv_cache_dtype"] == "fp8 (e4m3)" and out["value"] > 0
