@@ -16,7 +16,8 @@ import torch  # noqa: E402
 from fasttalk_llm_microservice_amd import ops  # noqa: E402
 from gemm_sweep import graph_time  # noqa: E402
 
-nq, nkv, d, bs = 32, 8, 128, 16
+nq, nkv, d = 32, 8, 128
+bs = int(os.environ.get("BS", "16"))   # KV block size (tokens)
 
 
 def main():
