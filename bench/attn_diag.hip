@@ -16,7 +16,7 @@ __global__ __launch_bounds__(256, 2) void attn_loads(const uint16_t* __restrict_
                                                      const int* __restrict__ seq_lens, int batch, int nkv,
                                                      int bs_shift, unsigned* __restrict__ sink) {
   __shared__ int s_pre[kDecMaxBatch + 1];
-  if (wave_id() == 0) dec_prefix(s_pre, seq_lens, batch);
+  if (wave_id() == 0) dec_prefix(s_pre, seq_lens, batch, 1);
   __syncthreads();
   const int total = nkv * s_pre[batch];
   const int nw = dec_num_waves(total, gridDim.x * 4, kDecMinTiles);
